@@ -1,0 +1,354 @@
+"""Pure-Python CPU restatement of the reference CBF hot path.
+
+TEST INFRASTRUCTURE ONLY.  This module is the *checker*: it may be imported by
+``tests/``, ``__graft_entry__.smoke()`` and the ``cpu_baseline`` leg of
+``bench.py`` and nothing else.  The product path (``cbf_amd``) never imports it
+and fails loudly when its HIP library is missing.
+
+Parity pinning: the row assembly, box rows, de-bias and clip below are checked
+bit-for-bit against golden vectors captured from the reference's own
+``cbf.py`` (see ``tests/golden/make_golden.py``).  The QP minimiser is
+checked against an independent brute-force enumerator and KKT certificates;
+cvxopt itself is absent from this image, so "within 1e-5 of cvxopt" is
+*unpinned* ("Oracle").
+
+Every function cites the reference line(s) it restates.  All arithmetic is
+IEEE fp64 in the exact evaluation order the reference's numpy expressions use
+(orders were probed against numpy 2.2 / OpenBLAS 0.3.29 and are pinned by the
+golden fixtures):
+
+* ``hs_p @ d``             -> fma chain fma(h3,d3,fma(h2,d2,fma(h1,d1,h0*d0)))  (cbf.py:58)
+* ``-hs_p @ g``            -> pairwise (t0+t1)+(t2+t3); pinned for exact products
+                              (k a power of two or g the callers' g), else unpinned (cbf.py:56)
+* ``g @ u0`` (gemv)        -> fma(g[r,0], u0x, g[r,1]*u0y)         (cbf.py:59)
+* ``np.dot(hs_p, g@u0)``   -> fma chain as hs_p @ d                (cbf.py:59)
+* ``f @ d`` (gemv 4x4)     -> OpenBLAS-kernel dependent: pinned only for the callers'
+                              f = 0 (every product is a signed zero); plain order otherwise
+* ``np.sum(X[:,j]-X[:,i,None], 1)`` -> sequential from +0.0        (cross_and_rescue.py:118,125)
+* ``v @ rotation``         -> fma(v1, R[1,c], v0*R[0,c])           (cross_and_rescue.py:118)
+"""
+from __future__ import annotations
+
+import math
+from fractions import Fraction
+
+import numpy as np
+
+GAMMA = 0.5  # cbf.py:16 (hard-coded, not a constructor argument)
+
+# per-agent status codes (low byte); bits 8.. hold the relaxation count
+STATUS_IDLE = 0            # no neighbour: filter not called, u = u0 unclipped (cross_and_rescue.py:153)
+STATUS_OPTIMAL = 1         # exact minimiser of the QP of cbf.py:62-81
+STATUS_RELAXED = 2         # CBF rows relaxed k times by +1 (cbf.py:84-87 rule), then optimal
+STATUS_BOX_INFEASIBLE = 3  # the 8 box rows alone are infeasible; x = 0
+STATUS_RELAX_CAP = 4       # relaxation cap hit; x = 0
+
+FEAS_TOL = 1e-12   # a.x - b <= FEAS_TOL*max(1,|b|) counts as feasible
+ACTIVE_TOL = 1e-12  # a.x >= b - ACTIVE_TOL*max(1,|b|) counts as active
+RELAX_CAP = 1 << 16
+
+# cbf.py:66 -- G rows in reference order (rows 1 and 2 are the "mismatched" pair)
+BOX_G = ((1.0, 0.0), (0.0, 1.0), (-1.0, 0.0), (0.0, -1.0),
+         (1.0, 0.0), (-1.0, 0.0), (0.0, 1.0), (0.0, -1.0))
+
+
+def fma(a: float, b: float, c: float) -> float:
+    """Correctly rounded a*b+c (math.fma is not in Python 3.10)."""
+    a = float(a); b = float(b); c = float(c)
+    p = a * b
+    if c == 0.0 or a == 0.0 or b == 0.0:
+        return p + c
+    return float(Fraction(a) * Fraction(b) + Fraction(c))
+
+
+def dot4(h, v):
+    """numpy int(4,) @ float(4,[1]) as measured: a sequential fma chain."""
+    return fma(h[3], v[3], fma(h[2], v[2], fma(h[1], v[1], h[0] * v[0])))
+
+
+def cull_threshold(safety_distance: float) -> float:
+    """Smallest t with sqrt(t) >= safety_distance, so that
+    ``sqrt(s) < safety_distance  <=>  s < t`` for every double s >= 0
+    (cross_and_rescue.py:142-143; for 0.2 this is the double 0.04, *not* 0.2*0.2)."""
+    d = float(safety_distance)
+    t = d * d
+    while t > 0.0 and math.sqrt(np.nextafter(t, 0.0)) >= d:
+        t = float(np.nextafter(t, 0.0))
+    while math.sqrt(t) < d:
+        t = float(np.nextafter(t, math.inf))
+    return t
+
+
+class Params:
+    """ControlBarrierFunction(max_speed, dmin=0.2, k=1) state (cbf.py:6-16) plus
+    the callers' dynamics f, g (cross_and_rescue.py:31-32) and cull radius (:134)."""
+
+    def __init__(self, max_speed, dmin=0.2, k=1, f=None, g=None, safety_distance=0.2, gamma=GAMMA):
+        self.max_speed = float(max_speed)
+        self.dmin = float(dmin)
+        self.k = float(k)
+        self.gamma = float(gamma)
+        self.f = np.zeros((4, 4)) if f is None else np.asarray(f, dtype=np.float64).reshape(4, 4)
+        self.g = (0.1 * np.array([[1, 0], [0, 1], [0, 0], [0, 0]])) if g is None else \
+            np.asarray(g, dtype=np.float64).reshape(4, 2)
+        self.safety_distance = float(safety_distance)
+        self.cull_t = cull_threshold(safety_distance)
+
+
+def _hs(p: Params, d0: float, d1: float):
+    # cbf.py:47-53 : +1 unless strictly negative (so -0.0 -> +1)
+    sx = -1.0 if d0 < 0 else 1.0
+    sy = -1.0 if d1 < 0 else 1.0
+    return (sx, sy, p.k * sx, p.k * sy), (1 if sx < 0 else 0) | (2 if sy < 0 else 0)
+
+
+def quadrant_normal(p: Params, q: int):
+    """L_g = -hs_p @ g for sign quadrant q (cbf.py:56); pairwise order."""
+    sx = -1.0 if (q & 1) else 1.0
+    sy = -1.0 if (q & 2) else 1.0
+    nh = (-sx, -sy, -(p.k * sx), -(p.k * sy))
+    g = p.g
+    return tuple((nh[0] * g[0, c] + nh[1] * g[1, c]) + (nh[2] * g[2, c] + nh[3] * g[3, c]) for c in range(2))
+
+
+def assemble_row(p: Params, r, o, u0):
+    """One barrier row (cbf.py:38-59). Returns (a0, a1, b, quadrant)."""
+    d = [float(r[i]) - float(o[i]) for i in range(4)]                 # cbf.py:39
+    hs, q = _hs(p, d[0], d[1])                                          # cbf.py:47-53
+    H = dot4(hs, d)                                                     # hs_p @ d
+    f = p.f
+    fd = [((f[i, 0] * d[0] + f[i, 1] * d[1]) + f[i, 2] * d[2]) + f[i, 3] * d[3] for i in range(4)]
+    L_f = dot4(hs, fd)                                                  # cbf.py:55
+    a0, a1 = quadrant_normal(p, q)                                       # cbf.py:56
+    g = p.g
+    gu = [fma(g[i, 0], u0[0], g[i, 1] * u0[1]) for i in range(4)]        # g @ u0
+    c = dot4(hs, gu)
+    b = (p.gamma * (H - p.dmin) + L_f) + c                               # cbf.py:58-59
+    return a0, a1, b, q
+
+
+def box_rhs(p: Params, r, u0):
+    """S_saturated (cbf.py:67-70), reference row order."""
+    ms = p.max_speed
+    u0x, u0y = float(u0[0]), float(u0[1])
+    rvx, rvy = float(r[2]), float(r[3])
+    return [ms - u0x, ms + u0x, ms - u0y, ms + u0y,
+            (ms - rvx) - u0x, (ms + rvx) + u0x, (ms - rvy) - u0y, (ms + rvy) + u0y]
+
+
+def assemble(p: Params, r, obs, u0):
+    """A = vstack(L_gs, G), b = vstack(rhs, S) exactly as handed to cvxopt (cbf.py:72-80)."""
+    rows = [assemble_row(p, r, o, u0) for o in obs]
+    A = [(a0, a1) for a0, a1, _, _ in rows] + list(BOX_G)
+    b = [bb for _, _, bb, _ in rows] + box_rhs(p, r, u0)
+    return np.array(A, dtype=np.float64).reshape(-1, 2), np.array(b, dtype=np.float64)
+
+
+# --------------------------------------------------------------------------------------
+# exact 2-variable QP:  min 1/2|x|^2  s.t.  a_h . x <= b_h   (cbf.py:62-81, Q=I, p=0)
+# --------------------------------------------------------------------------------------
+def _feasible(planes, x0, x1):
+    for (a0, a1, b) in planes:
+        lhs = a0 * x0 + a1 * x1
+        if lhs - b > FEAS_TOL * max(1.0, abs(b)):
+            return False
+    return True
+
+
+def solve_halfplanes(planes):
+    """planes: list of (a0, a1, b) in the fixed order [box+x, box+y, box-x, box-y, cbf q0..q3].
+    Returns (feasible, x0, x1).  Enumeration: origin, then single projections of planes
+    violated at the origin, then pair vertices with >=1 plane violated at the origin;
+    the first non-empty phase's min-norm feasible candidate (ties -> first) is the optimum."""
+    if _feasible(planes, 0.0, 0.0):
+        return True, 0.0, 0.0
+    best = None
+    for (a0, a1, b) in planes:
+        if not (b < 0):
+            continue
+        n2 = a0 * a0 + a1 * a1
+        if not (n2 > 0):
+            continue
+        t = b / n2
+        x0, x1 = t * a0, t * a1
+        if _feasible(planes, x0, x1):
+            nn = x0 * x0 + x1 * x1
+            if best is None or nn < best[0]:
+                best = (nn, x0, x1)
+    if best is not None:
+        return True, best[1], best[2]
+    n = len(planes)
+    for i in range(n):
+        a0, a1, b = planes[i]
+        for j in range(i + 1, n):
+            c0, c1, e = planes[j]
+            if not (b < 0 or e < 0):
+                continue
+            det = a0 * c1 - a1 * c0
+            if det == 0:
+                continue
+            x0 = (b * c1 - e * a1) / det
+            x1 = (a0 * e - c0 * b) / det
+            if _feasible(planes, x0, x1):
+                nn = x0 * x0 + x1 * x1
+                if best is None or nn < best[0]:
+                    best = (nn, x0, x1)
+    if best is not None:
+        return True, best[1], best[2]
+    return False, 0.0, 0.0
+
+
+def _box_planes(S):
+    return [(1.0, 0.0, min(S[0], S[4])), (0.0, 1.0, min(S[1], S[6])),
+            (-1.0, 0.0, min(S[2], S[5])), (0.0, -1.0, min(S[3], S[7]))]
+
+
+def _py_min(a, b):
+    return b if b < a else a
+
+
+def _py_max(a, b):
+    return b if b > a else a
+
+
+def clip(p: Params, x0, x1, u0):
+    """cbf.py:89-91 -- u = x + u0, then Python max(min(u, ms), -ms) per component."""
+    ms = p.max_speed
+    u = [x0 + float(u0[0]), x1 + float(u0[1])]
+    return [_py_max(_py_min(v, ms), -ms) for v in u]
+
+
+def filter_one(p: Params, r, obs, u0):
+    """get_safe_control (cbf.py:18-92) for one ego with its culled neighbour list.
+    Returns dict(u, x, status, iters, rows=(A,b) of the final (possibly relaxed) QP)."""
+    u0 = [float(u0[0]), float(u0[1])]
+    bq = [None] * 4
+    for o in obs:
+        _, _, b, q = assemble_row(p, r, o, u0)
+        bq[q] = b if bq[q] is None else _py_min(bq[q], b)
+    S = box_rhs(p, r, u0)
+    box = _box_planes(S)
+    normals = [quadrant_normal(p, q) for q in range(4)]
+
+    def planes_for(bqv):
+        return box + [(normals[q][0], normals[q][1], bqv[q]) for q in range(4) if bqv[q] is not None]
+
+    ok, x0, x1 = solve_halfplanes(planes_for(bq))
+    status, iters = STATUS_OPTIMAL, 0
+    if not ok:
+        okb, _, _ = solve_halfplanes(box)
+        if not okb:
+            status, x0, x1 = STATUS_BOX_INFEASIBLE, 0.0, 0.0
+        else:
+            while True:
+                bq = [None if v is None else v + 1.0 for v in bq]   # cbf.py:85-87
+                iters += 1
+                ok, x0, x1 = solve_halfplanes(planes_for(bq))
+                if ok:
+                    status = STATUS_RELAXED
+                    break
+                if iters >= RELAX_CAP:
+                    status, x0, x1 = STATUS_RELAX_CAP, 0.0, 0.0
+                    break
+    u = clip(p, x0, x1, u0)
+    return dict(u=u, x=[x0, x1], status=status, iters=iters)
+
+
+def relaxed_b(b: float, iters: int) -> float:
+    for _ in range(iters):
+        b = b + 1.0
+    return b
+
+
+def diagnose(p: Params, r, obs, u0, x, iters):
+    """Active set and violation of the final QP at x (SURVEY 8d correctness gates)."""
+    A, b = assemble(p, r, obs, u0)
+    m = len(obs)
+    active, viol = [], 0.0
+    for i in range(A.shape[0]):
+        bi = relaxed_b(float(b[i]), iters) if i < m else float(b[i])
+        lhs = A[i, 0] * x[0] + A[i, 1] * x[1]
+        active.append(bool(lhs >= bi - ACTIVE_TOL * max(1.0, abs(bi))))
+        viol = max(viol, lhs - bi)
+    return active, max(viol, 0.0)
+
+
+# --------------------------------------------------------------------------------------
+# callers: cull, nominal control, Euler  (cross_and_rescue.py / meet_at_center.py)
+# --------------------------------------------------------------------------------------
+def cull_one(p: Params, pos, n_obs, ego):
+    """Neighbour indices of ego (cross_and_rescue.py:141-150): every obstacle with
+    dist < 0.2 (index order), then every agent with 0 < dist < 0.2 (index order)."""
+    r0, r1 = float(pos[ego][0]), float(pos[ego][1])
+    out = []
+    for j in range(len(pos)):
+        e0 = float(pos[j][0]) - r0
+        e1 = float(pos[j][1]) - r1
+        s = (0 + e0 * e0) + e1 * e1       # builtin sum over (o-r)**2
+        if s < p.cull_t and (j < n_obs or s > 0):
+            out.append(j)
+    return out
+
+
+def filter_swarm(p: Params, pos, vel, n_obs, ego_begin, ego_end):
+    """The per-agent loop of cross_and_rescue.py:135-160 (Jacobi: every ego sees the
+    nominal states packed before the loop, :133).  Ego state = [pos, vel] with
+    vel = its nominal control u0 (:133,155)."""
+    pos = np.asarray(pos, dtype=np.float64)
+    vel = np.asarray(vel, dtype=np.float64)
+    n = ego_end - ego_begin
+    u = np.zeros((n, 2)); status = np.zeros(n, np.int32); cnt = np.zeros(n, np.int32)
+    nbrs = []
+    for e in range(ego_begin, ego_end):
+        nb = cull_one(p, pos, n_obs, e)
+        nbrs.append(nb)
+        k = e - ego_begin
+        cnt[k] = len(nb)
+        if not nb:
+            u[k] = vel[e]                 # not filtered, not clipped (cross_and_rescue.py:153)
+            status[k] = STATUS_IDLE
+            continue
+        r = [pos[e, 0], pos[e, 1], vel[e, 0], vel[e, 1]]
+        obs = [[pos[j, 0], pos[j, 1], vel[j, 0], vel[j, 1]] for j in nb]
+        res = filter_one(p, r, obs, vel[e])
+        u[k] = res["u"]
+        status[k] = res["status"] | (min(res["iters"], (1 << 23) - 1) << 8)
+    return u, status, cnt, nbrs
+
+
+def consensus_csr(src, row_ptr, col, self_idx, n_group, anchors=None, scale=1.0, rot=None):
+    """Nominal control by graph Laplacian (cross_and_rescue.py:108-125,
+    meet_at_center.py:86-103):  v_i = (sum_j (x_j - x_i)) [@ R(theta)] * scale.
+    col >= n_group refers to anchors[col - n_group] (the goal column, cross_and_rescue.py:102)."""
+    out = np.zeros((len(self_idx), 2))
+    for k, i in enumerate(self_idx):
+        xi = src[i]
+        acc = [0.0, 0.0]
+        for jj in range(row_ptr[k], row_ptr[k + 1]):
+            j = col[jj]
+            xj = src[j] if j < n_group else anchors[j - n_group]
+            acc[0] = acc[0] + (float(xj[0]) - float(xi[0]))
+            acc[1] = acc[1] + (float(xj[1]) - float(xi[1]))
+        if rot is not None:
+            c, s = rot
+            v = [fma(acc[1], -s, acc[0] * c), fma(acc[1], c, acc[0] * s)]
+        else:
+            v = acc
+        out[k] = [v[0] * scale, v[1] * scale]
+    return out
+
+
+def lattice_neighbors(i, W, H):
+    """4-neighbour lattice Laplacian row, ascending index (np.where order)."""
+    r, c = divmod(i, W)
+    out = []
+    if r > 0: out.append(i - W)
+    if c > 0: out.append(i - 1)
+    if c < W - 1: out.append(i + 1)
+    if r < H - 1: out.append(i + W)
+    return out
+
+
+def euler(pos, vel, T):
+    """p <- p + T*v (cross_and_rescue.py:173)."""
+    return np.asarray(pos) + T * np.asarray(vel)
