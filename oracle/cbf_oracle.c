@@ -103,67 +103,41 @@ typedef struct {
     double a0[8], a1[8], b[8];
 } planes_t;
 
-static int feasible(const planes_t* P, double x0, double x1) {
-    for (int h = 0; h < P->n; ++h) {
-        double lhs = P->a0[h] * x0 + P->a1[h] * x1;
-        if (lhs - P->b[h] > FEAS_TOL * py_max(1.0, fabs(P->b[h]))) return 0;
-    }
-    return 1;
-}
-
+/* Incremental (Seidel) exact min-norm solve over the planes in order; returns -1 when
+ * feasible (x set) or the index of the plane at which the prefix became infeasible. */
 static int solve_planes(const planes_t* P, double* x0o, double* x1o) {
-    if (feasible(P, 0.0, 0.0)) {
-        *x0o = 0.0;
-        *x1o = 0.0;
-        return 1;
-    }
-    int found = 0;
-    double bn = 0, bx0 = 0, bx1 = 0;
+    double tb[8];
+    for (int h = 0; h < P->n; ++h) tb[h] = FEAS_TOL * py_max(1.0, fabs(P->b[h]));
+    double x0 = 0.0, x1 = 0.0;
     for (int h = 0; h < P->n; ++h) {
         double a0 = P->a0[h], a1 = P->a1[h], b = P->b[h];
-        if (!(b < 0)) continue;
+        if ((a0 * x0 + a1 * x1) - b <= tb[h]) continue;
         double n2 = a0 * a0 + a1 * a1;
-        if (!(n2 > 0)) continue;
+        if (!(n2 > 0)) return h;
         double t = b / n2;
-        double x0 = t * a0, x1 = t * a1;
-        if (feasible(P, x0, x1)) {
-            double nn = x0 * x0 + x1 * x1;
-            if (!found || nn < bn) {
-                found = 1;
-                bn = nn;
-                bx0 = x0;
-                bx1 = x1;
-            }
-        }
-    }
-    if (found) {
-        *x0o = bx0;
-        *x1o = bx1;
-        return 1;
-    }
-    for (int i = 0; i < P->n; ++i) {
-        double a0 = P->a0[i], a1 = P->a1[i], b = P->b[i];
-        for (int j = i + 1; j < P->n; ++j) {
+        double p0 = t * a0, p1 = t * a1;
+        double d0 = -a1, d1 = a0;
+        double lo = -INFINITY, hi = INFINITY;
+        for (int j = 0; j < h; ++j) {
             double c0 = P->a0[j], c1 = P->a1[j], e = P->b[j];
-            if (!(b < 0 || e < 0)) continue;
-            double det = a0 * c1 - a1 * c0;
-            if (det == 0) continue;
-            double x0 = (b * c1 - e * a1) / det;
-            double x1 = (a0 * e - c0 * b) / det;
-            if (feasible(P, x0, x1)) {
-                double nn = x0 * x0 + x1 * x1;
-                if (!found || nn < bn) {
-                    found = 1;
-                    bn = nn;
-                    bx0 = x0;
-                    bx1 = x1;
-                }
-            }
+            double ad = c0 * d0 + c1 * d1;
+            double r = e - (c0 * p0 + c1 * p1);
+            if (ad > 0)
+                hi = py_min(hi, r / ad);
+            else if (ad < 0)
+                lo = py_max(lo, r / ad);
         }
+        double s = 0.0;
+        if (s > hi) s = hi;
+        if (s < lo) s = lo;
+        x0 = p0 + s * d0;
+        x1 = p1 + s * d1;
+        for (int j = 0; j <= h; ++j)
+            if (!((P->a0[j] * x0 + P->a1[j] * x1) - P->b[j] <= tb[j])) return h;
     }
-    *x0o = bx0;
-    *x1o = bx1;
-    return found;
+    *x0o = x0;
+    *x1o = x1;
+    return -1;
 }
 
 static void box_planes(const double S[8], planes_t* P) {
@@ -194,14 +168,12 @@ static int solve_ego(const orc_params* p, const double r[4], const double u0[2],
                 P.b[P.n] = bq[q];
                 P.n++;
             }
-        if (solve_planes(&P, &x[0], &x[1])) break;
-        if (iters == 0) {
-            double t0, t1;
-            if (!solve_planes(&B, &t0, &t1)) {
-                status = ST_BOX_INFEASIBLE;
-                x[0] = x[1] = 0.0;
-                break;
-            }
+        int fail = solve_planes(&P, &x[0], &x[1]);
+        if (fail < 0) break;
+        if (fail < 4) { /* box rows alone infeasible */
+            status = ST_BOX_INFEASIBLE;
+            x[0] = x[1] = 0.0;
+            break;
         }
         if (iters >= RELAX_CAP) {
             status = ST_RELAX_CAP;

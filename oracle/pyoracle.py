@@ -147,55 +147,56 @@ def assemble(p: Params, r, obs, u0):
 # --------------------------------------------------------------------------------------
 # exact 2-variable QP:  min 1/2|x|^2  s.t.  a_h . x <= b_h   (cbf.py:62-81, Q=I, p=0)
 # --------------------------------------------------------------------------------------
-def _feasible(planes, x0, x1):
-    for (a0, a1, b) in planes:
-        lhs = a0 * x0 + a1 * x1
-        if lhs - b > FEAS_TOL * max(1.0, abs(b)):
-            return False
-    return True
+def _viol_ok(a0, a1, b, tb, x0, x1):
+    return (a0 * x0 + a1 * x1) - b <= tb
 
 
 def solve_halfplanes(planes):
-    """planes: list of (a0, a1, b) in the fixed order [box+x, box+y, box-x, box-y, cbf q0..q3].
-    Returns (feasible, x0, x1).  Enumeration: origin, then single projections of planes
-    violated at the origin, then pair vertices with >=1 plane violated at the origin;
-    the first non-empty phase's min-norm feasible candidate (ties -> first) is the optimum."""
-    if _feasible(planes, 0.0, 0.0):
-        return True, 0.0, 0.0
-    best = None
-    for (a0, a1, b) in planes:
-        if not (b < 0):
+    """Exact min-norm point of a list of half-planes a.x <= b (<= 8, fixed order
+    [box+x, box+y, box-x, box-y, cbf q0..q3 present]).  Incremental (Seidel) method:
+    keep the optimum of the prefix; when plane h is violated the new optimum lies on its
+    line, found by clamping t=0 (the origin's projection) to the interval cut out by the
+    earlier planes.  Feasibility tolerance FEAS_TOL*max(1,|b|) in b-units.
+    Returns (fail_index, x0, x1): fail_index = -1 when feasible, else the plane index at which
+    the prefix became infeasible (< 4 means the box rows alone are infeasible)."""
+    n = len(planes)
+    tb = [FEAS_TOL * _py_max(1.0, abs(b)) for (_, _, b) in planes]
+    x0 = 0.0
+    x1 = 0.0
+    for h in range(n):
+        a0, a1, b = planes[h]
+        if _viol_ok(a0, a1, b, tb[h], x0, x1):
             continue
         n2 = a0 * a0 + a1 * a1
         if not (n2 > 0):
-            continue
+            return h, 0.0, 0.0
         t = b / n2
-        x0, x1 = t * a0, t * a1
-        if _feasible(planes, x0, x1):
-            nn = x0 * x0 + x1 * x1
-            if best is None or nn < best[0]:
-                best = (nn, x0, x1)
-    if best is not None:
-        return True, best[1], best[2]
-    n = len(planes)
-    for i in range(n):
-        a0, a1, b = planes[i]
-        for j in range(i + 1, n):
+        p0 = t * a0
+        p1 = t * a1
+        d0 = -a1
+        d1 = a0
+        lo = -math.inf
+        hi = math.inf
+        for j in range(h):
             c0, c1, e = planes[j]
-            if not (b < 0 or e < 0):
-                continue
-            det = a0 * c1 - a1 * c0
-            if det == 0:
-                continue
-            x0 = (b * c1 - e * a1) / det
-            x1 = (a0 * e - c0 * b) / det
-            if _feasible(planes, x0, x1):
-                nn = x0 * x0 + x1 * x1
-                if best is None or nn < best[0]:
-                    best = (nn, x0, x1)
-    if best is not None:
-        return True, best[1], best[2]
-    return False, 0.0, 0.0
+            ad = c0 * d0 + c1 * d1
+            r = e - (c0 * p0 + c1 * p1)
+            if ad > 0:
+                hi = _py_min(hi, r / ad)
+            elif ad < 0:
+                lo = _py_max(lo, r / ad)
+        s = 0.0
+        if s > hi:
+            s = hi
+        if s < lo:
+            s = lo
+        x0 = p0 + s * d0
+        x1 = p1 + s * d1
+        for j in range(h + 1):
+            c0, c1, e = planes[j]
+            if not _viol_ok(c0, c1, e, tb[j], x0, x1):
+                return h, 0.0, 0.0
+    return -1, x0, x1
 
 
 def _box_planes(S):
@@ -233,18 +234,17 @@ def filter_one(p: Params, r, obs, u0):
     def planes_for(bqv):
         return box + [(normals[q][0], normals[q][1], bqv[q]) for q in range(4) if bqv[q] is not None]
 
-    ok, x0, x1 = solve_halfplanes(planes_for(bq))
+    fail, x0, x1 = solve_halfplanes(planes_for(bq))
     status, iters = STATUS_OPTIMAL, 0
-    if not ok:
-        okb, _, _ = solve_halfplanes(box)
-        if not okb:
+    if fail >= 0:
+        if fail < 4:                                   # box rows alone infeasible
             status, x0, x1 = STATUS_BOX_INFEASIBLE, 0.0, 0.0
         else:
             while True:
                 bq = [None if v is None else v + 1.0 for v in bq]   # cbf.py:85-87
                 iters += 1
-                ok, x0, x1 = solve_halfplanes(planes_for(bq))
-                if ok:
+                fail, x0, x1 = solve_halfplanes(planes_for(bq))
+                if fail < 0:
                     status = STATUS_RELAXED
                     break
                 if iters >= RELAX_CAP:
