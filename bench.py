@@ -1,0 +1,197 @@
+"""Benchmark of the CBF safety-filter hot path on MI355X (BASELINE.json metric).
+
+Default workload (cfg4): a 1024 x 1024 jittered lattice swarm per GPU, one fused timestep
+(lattice-Laplacian nominal control + cell-list cull + barrier assembly + exact QP + clip + Euler)
+per step, captured in a hipGraph.  value = agent-QP solves/s over the whole job (agents whose
+filter ran, counted on device).  With --gpus N (torchrun, one rank per GPU) the lattice is
+1024 x 1024 N rows, sharded in row stripes, with one RCCL all-gather of halo slabs per step
+(weak scaling).  Prints ONE JSON line on rank 0.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "agent-QP solves/sec (whole node) at N=1M; timesteps/sec; % HBM roofline"
+HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
+FILTER_BYTES_PER_AGENT = 64    # 32 B state in (p, u0) + 16 B u out + 16 B p_new out
+STEP_BYTES_PER_AGENT = 80      # + 16 B nominal control out
+
+
+def _dist_env():
+    ws = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    return ws, rank, local
+
+
+def load_pmc_traffic(kernel="k_lattice_filter"):
+    """HBM bytes per launch of the dominant kernel from the committed PMC summary, if any."""
+    path = os.path.join(ROOT, "profiles", "pmc_summary.json")
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        return d.get(kernel, {}).get("hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        return None
+
+
+def cpu_baseline_lattice(W, H, seed, budget_s=12.0):
+    """The oracle restating the reference's per-agent loop (O(N) cull per ego, cbf.py QP) on one
+    host core, over a bounded sample of egos of the same workload."""
+    from cbf_amd import scenarios
+    from oracle import coracle, pyoracle as po
+    pos = scenarios.lattice(W, H, seed=seed)
+    vel = coracle.consensus_lattice(W, H, 0, H, pos, scenarios.LATTICE_GAIN)
+    p = po.Params(15)
+    rng = np.random.default_rng(123)
+    order = rng.permutation(W * H)
+    t0 = time.perf_counter()
+    done = solves = 0
+    while time.perf_counter() - t0 < budget_s and done < len(order):
+        e = int(order[done])
+        o = coracle.filter_swarm(p, pos, vel, 0, e, e + 1)
+        solves += int(o["cnt"][0] > 0)
+        done += 1
+    dt = time.perf_counter() - t0
+    return {"value": solves / dt, "unit": "agent-QP solves/s", "cores": 1, "kind": "port",
+            "sample": f"{done} random egos of cfg4 (N={W * H}), each culled against all N agents as the reference "
+                      f"loop does (cross_and_rescue.py:141-150), then assembled + solved + clipped; "
+                      f"{dt:.1f} s single-threaded C oracle"}
+
+
+def bench_lattice(args, ws, rank, local):
+    import torch
+    from cbf_amd import scenarios, swarm
+    W = args.width
+    rows = args.rows
+    if ws > 1:
+        from cbf_amd.shard import ShardedLattice
+        S = ShardedLattice(W, rows, seed=args.seed)
+    else:
+        pos = scenarios.lattice(W, rows, seed=args.seed)
+        S = swarm.LatticeSwarm(pos, W, rows, gain=scenarios.LATTICE_GAIN)
+    use_graph = not args.eager
+    if use_graph:
+        S.capture()
+    for _ in range(args.warmup):
+        S.step()
+    torch.cuda.synchronize()
+    S.reset_solves()
+    if ws > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev1 = torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record()
+    for _ in range(args.steps):
+        S.step()
+    ev1.record()
+    torch.cuda.synchronize()
+    if ws > 1:
+        torch.distributed.barrier()
+    t1 = time.perf_counter()
+    elapsed = t1 - t0
+    solves = S.solves_total()
+    n_local = S.n_owned if ws > 1 else S.n
+    if ws > 1:
+        t = torch.tensor([elapsed, float(solves), float(n_local)], dtype=torch.float64, device="cuda")
+        mx = t.clone()
+        torch.distributed.all_reduce(mx[:1], op=torch.distributed.ReduceOp.MAX)
+        torch.distributed.all_reduce(t[1:], op=torch.distributed.ReduceOp.SUM)
+        elapsed = float(mx[0]); solves = int(t[1]); n_total = int(t[2])
+        S.check_guard()
+    else:
+        n_total = n_local
+    # dominant kernel (filter + clip + Euler) timed alone with HIP events on the launch stream
+    kt = []
+    for _ in range(args.kernel_iters):
+        S.build_phase()
+        a = torch.cuda.Event(enable_timing=True)
+        b = torch.cuda.Event(enable_timing=True)
+        a.record()
+        S.advance_phase()
+        b.record()
+        kt.append((a, b))
+    torch.cuda.synchronize()
+    k_ms = float(np.mean([a.elapsed_time(b) for a, b in kt]))
+    status = S.status.cpu().numpy()
+    codes = np.bincount(status & 0xFF, minlength=5)
+    achieved = FILTER_BYTES_PER_AGENT * n_local / (k_ms * 1e-3) / 1e9
+    traffic = load_pmc_traffic()
+    res = {
+        "metric": METRIC,
+        "value": solves / elapsed,
+        "unit": "agent-QP solves/s",
+        "n_gpus": ws,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic",
+        "config": {"workload": f"cfg4: {W}x{rows * ws} jittered lattice swarm (spacing 0.145), lattice-Laplacian "
+                               "consensus + radius-0.2 cell-list cull + CBF QP + clip + Euler, one fused timestep "
+                               "per step",
+                   "agents_total": n_total, "agents_per_gpu": n_local,
+                   "parallelism": f"row-stripe shards x{ws}, 1 RCCL all-gather of halo slabs / step" if ws > 1
+                   else "single GPU", "graph": use_graph},
+        "timesteps_per_s": args.steps / elapsed,
+        "solves_per_step": solves / args.steps,
+        "status_fraction_last_step": {"idle": codes[0] / len(status), "optimal": codes[1] / len(status),
+                                      "relaxed": codes[2] / len(status),
+                                      "box_infeasible": codes[3] / len(status)},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS,
+                     "traffic": traffic, "kernel": "k_lattice_filter", "kernel_ms": k_ms,
+                     "algorithmic_bytes_per_launch": FILTER_BYTES_PER_AGENT * n_local,
+                     "step_algorithmic_GBps": STEP_BYTES_PER_AGENT * n_local * args.steps / elapsed / 1e9 / ws},
+    }
+    return res
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--width", type=int, default=1024)
+    ap.add_argument("--rows", type=int, default=1024, help="lattice rows per GPU")
+    ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--eager", action="store_true", help="no hipGraph capture")
+    ap.add_argument("--kernel-iters", type=int, default=20)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-budget", type=float, default=12.0)
+    args = ap.parse_args()
+    ws, rank, local = _dist_env()
+    import torch
+    if ws > 1:
+        torch.cuda.set_device(local)
+        os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        torch.distributed.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    res = bench_lattice(args, ws, rank, local)
+    if rank == 0:
+        if ws == 1 and not args.no_cpu_baseline:
+            res["cpu_baseline"] = cpu_baseline_lattice(args.width, args.rows, args.seed, args.cpu_budget)
+        else:
+            res["cpu_baseline"] = None
+        print(json.dumps(res), flush=True)
+    if ws > 1:
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

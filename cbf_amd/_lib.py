@@ -1,0 +1,106 @@
+"""ctypes binding of libcbf_amd.so (include/cbf_amd.h).
+
+The HIP library is the only compute path: there is no CPU fallback.  Importing this module
+fails loudly when the library is missing, and every compute call raises when no ROCm GPU is
+visible.  torch supplies device memory and the current HIP stream (plumbing only).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(PKG, "libcbf_amd.so")
+
+CBF_EINVAL = -1
+STATUS_IDLE, STATUS_OPTIMAL, STATUS_RELAXED, STATUS_BOX_INFEASIBLE, STATUS_RELAX_CAP = 0, 1, 2, 3, 4
+
+
+class CbfParams(C.Structure):
+    _fields_ = [("max_speed", C.c_double), ("dmin", C.c_double), ("k", C.c_double), ("gamma", C.c_double),
+                ("f", C.c_double * 16), ("g", C.c_double * 8), ("cull_t", C.c_double),
+                ("nrm", (C.c_double * 2) * 4), ("f_is_zero", C.c_int32), ("relax_cap", C.c_int32)]
+
+
+class CbfGrid(C.Structure):
+    _fields_ = [("x0", C.c_double), ("y0", C.c_double), ("inv_h", C.c_double), ("nx", C.c_int32),
+                ("ny", C.c_int32)]
+
+
+class CbfDiag(C.Structure):
+    _fields_ = [("kmax", C.c_int32), ("nbr_idx", C.c_void_p), ("nbr_active", C.c_void_p),
+                ("box_active", C.c_void_p), ("x", C.c_void_p), ("viol", C.c_void_p)]
+
+
+# symbol -> (restype, argtypes); kept in sync with include/cbf_amd.h (tests check every export)
+_vp, _i32, _d, _sz = C.c_void_p, C.c_int32, C.c_double, C.c_size_t
+_P, _G, _D = C.POINTER(CbfParams), C.POINTER(CbfGrid), C.POINTER(CbfDiag)
+SIGNATURES = {
+    "cbf_abi_version": (C.c_int, []),
+    "cbf_params_init": (C.c_int, [_P, _d, _d, _d, _vp, _vp, _d]),
+    "cbf_get_safe_control_batch": (C.c_int, [_P, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "cbf_assemble_rows": (C.c_int, [_P, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "cbf_filter_allpairs": (C.c_int, [_P, _i32, _i32, _vp, _vp, _i32, _i32, _vp, _vp, _vp, _D, _vp]),
+    "cbf_cells_workspace_size": (_sz, [_i32, _G]),
+    "cbf_filter_cells": (C.c_int, [_P, _G, _i32, _i32, _vp, _vp, _i32, _i32, _vp, _vp, _vp, _D, _vp, _sz, _vp]),
+    "cbf_consensus_csr": (C.c_int, [_i32, _i32, _i32, _vp, _vp, _vp, _vp, _i32, _d, _d, _d, _vp, _vp]),
+    "cbf_consensus_lattice": (C.c_int, [_i32, _i32, _i32, _i32, _i32, _vp, _d, _vp, _vp]),
+    "cbf_euler": (C.c_int, [_i32, _vp, _vp, _d, _vp]),
+    "cbf_lattice_workspace_size": (_sz, [_i32, _i32, _G]),
+    "cbf_lattice_step": (C.c_int, [_P, _G, _i32, _i32, _i32, _i32, _i32, _i32, _vp, _d, _d, _vp, _vp, _vp, _vp,
+                                   _vp, _i32, _vp, _vp, _vp, _sz, _vp]),
+    "cbf_lattice_build": (C.c_int, [_P, _G, _i32, _i32, _i32, _i32, _i32, _i32, _vp, _d, _vp, _vp, _sz, _vp]),
+    "cbf_lattice_advance": (C.c_int, [_P, _G, _i32, _i32, _i32, _i32, _i32, _i32, _vp, _d, _vp, _vp, _vp, _vp,
+                                      _i32, _vp, _vp, _vp, _sz, _vp]),
+    "cbf_mc_rollout": (C.c_int, [_P, _i32, _i32, _i32, _i32, _d, _d, _d, _d, _d, _vp, _vp, _vp, _vp]),
+}
+
+if not os.path.exists(LIB_PATH):
+    raise ImportError(f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
+                      "(there is no CPU fallback)")
+
+lib = C.CDLL(LIB_PATH)
+for _name, (_res, _args) in SIGNATURES.items():
+    _fn = getattr(lib, _name)
+    _fn.restype = _res
+    _fn.argtypes = _args
+
+
+class CbfError(RuntimeError):
+    pass
+
+
+def check(rc: int, what: str) -> None:
+    if rc == CBF_EINVAL:
+        raise CbfError(f"{what}: invalid argument (CBF_EINVAL)")
+    if rc != 0:
+        raise CbfError(f"{what}: HIP error {rc}")
+
+
+def make_params(max_speed, dmin=0.2, k=1.0, f=None, g=None, safety_distance=0.2) -> CbfParams:
+    p = CbfParams()
+    fa = None if f is None else np.ascontiguousarray(np.asarray(f, dtype=np.float64).reshape(16))
+    ga = None if g is None else np.ascontiguousarray(np.asarray(g, dtype=np.float64).reshape(8))
+    rc = lib.cbf_params_init(C.byref(p), float(max_speed), float(dmin), float(k),
+                             None if fa is None else fa.ctypes.data, None if ga is None else ga.ctypes.data,
+                             float(safety_distance))
+    check(rc, "cbf_params_init")
+    return p
+
+
+def require_gpu():
+    import torch
+    if not torch.cuda.is_available():
+        raise CbfError("cbf_amd runs only on a ROCm GPU (MI355X); no GPU is visible and there is no CPU fallback")
+    return torch
+
+
+def stream_handle():
+    import torch
+    return C.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def ptr(t) -> C.c_void_p:
+    return C.c_void_p(0 if t is None else t.data_ptr())

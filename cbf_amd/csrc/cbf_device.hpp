@@ -1,0 +1,294 @@
+// cbf_device.hpp -- device-side building blocks of the CBF safety filter (gfx950).
+//
+// Everything here is IEEE fp64 with no contraction (built with -ffp-contract=off); the only
+// fused multiply-adds are the explicit fma() calls that reproduce the evaluation order numpy
+// uses in the reference (probed, pinned by tests/golden):
+//   hs_p @ d, np.dot(hs_p, g@u0)  -> fma chain     (cbf.py:55-59)
+//   g @ u0                        -> fma(g[r,0], u0x, g[r,1]*u0y)
+//   v @ rotation                  -> fma(v1, R[1,c], v0*R[0,c])  (cross_and_rescue.py:118)
+// so that results are bit-identical to the CPU oracle (oracle/cbf_oracle.c).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdint.h>
+
+#include "cbf_amd.h"
+
+namespace cbf {
+
+constexpr double FEAS_TOL = 1e-12;
+constexpr double ACTIVE_TOL = 1e-12;
+constexpr int kBlock = 256;
+
+// Kernel-argument copy of cbf_params (passed by value: lives in the kernarg segment / SGPRs).
+struct KP {
+    double ms, dmin, k, gamma;
+    double f[16];
+    double g[8];
+    double cull_t;
+    double n0[4], n1[4];  // quadrant normals L_g (host-computed with the reference's order)
+    int f_zero;
+    int relax_cap;
+};
+
+inline KP make_kp(const cbf_params* p) {
+    KP k;
+    k.ms = p->max_speed;
+    k.dmin = p->dmin;
+    k.k = p->k;
+    k.gamma = p->gamma;
+    for (int i = 0; i < 16; ++i) k.f[i] = p->f[i];
+    for (int i = 0; i < 8; ++i) k.g[i] = p->g[i];
+    k.cull_t = p->cull_t;
+    for (int q = 0; q < 4; ++q) {
+        k.n0[q] = p->nrm[q][0];
+        k.n1[q] = p->nrm[q][1];
+    }
+    k.f_zero = p->f_is_zero;
+    k.relax_cap = p->relax_cap;
+    return k;
+}
+
+__device__ __forceinline__ double pmin(double a, double b) { return (b < a) ? b : a; }  // Python min(a, b)
+__device__ __forceinline__ double pmax(double a, double b) { return (b > a) ? b : a; }  // Python max(a, b)
+
+// One ego's accumulated QP: its state, g@u0, and the per-sign-quadrant minimum barrier rhs.
+struct Ego {
+    double r0, r1, r2, r3;  // robot_state (x, y, vx, vy)
+    double u0x, u0y;        // nominal control
+    double gu0, gu1, gu2, gu3;
+    double bq0, bq1, bq2, bq3;
+    unsigned present;  // bit q: quadrant q has >= 1 neighbour
+    int count;         // neighbours
+};
+
+__device__ __forceinline__ void ego_init(const KP& P, Ego& E, double px, double py, double vx, double vy, double ux,
+                                         double uy) {
+    E.r0 = px;
+    E.r1 = py;
+    E.r2 = vx;
+    E.r3 = vy;
+    E.u0x = ux;
+    E.u0y = uy;
+    E.gu0 = fma(P.g[0], ux, P.g[1] * uy);
+    E.gu1 = fma(P.g[2], ux, P.g[3] * uy);
+    E.gu2 = fma(P.g[4], ux, P.g[5] * uy);
+    E.gu3 = fma(P.g[6], ux, P.g[7] * uy);
+    E.bq0 = E.bq1 = E.bq2 = E.bq3 = INFINITY;
+    E.present = 0u;
+    E.count = 0;
+}
+
+// Barrier row rhs for neighbour o (cbf.py:38-59); q = sign quadrant (cbf.py:47-53, -0.0 -> +1).
+__device__ __forceinline__ double row_b(const KP& P, const Ego& E, double o0, double o1, double o2, double o3,
+                                        int& q) {
+    const double d0 = E.r0 - o0, d1 = E.r1 - o1, d2 = E.r2 - o2, d3 = E.r3 - o3;
+    const bool nx = d0 < 0, ny = d1 < 0;
+    const double sx = nx ? -1.0 : 1.0, sy = ny ? -1.0 : 1.0;
+    const double ksx = P.k * sx, ksy = P.k * sy;
+    const double H = fma(ksy, d3, fma(ksx, d2, fma(sy, d1, sx * d0)));
+    double Lf = 0.0;
+    if (!P.f_zero) {
+        double fd[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+            fd[i] = ((P.f[4 * i] * d0 + P.f[4 * i + 1] * d1) + P.f[4 * i + 2] * d2) + P.f[4 * i + 3] * d3;
+        Lf = fma(ksy, fd[3], fma(ksx, fd[2], fma(sy, fd[1], sx * fd[0])));
+    }
+    const double c = fma(ksy, E.gu3, fma(ksx, E.gu2, fma(sy, E.gu1, sx * E.gu0)));
+    q = (nx ? 1 : 0) | (ny ? 2 : 0);
+    return (P.gamma * (H - P.dmin) + Lf) + c;
+}
+
+__device__ __forceinline__ void ego_add(const KP& P, Ego& E, double o0, double o1, double o2, double o3) {
+    int q;
+    const double b = row_b(P, E, o0, o1, o2, o3, q);
+    E.bq0 = (q == 0 && b < E.bq0) ? b : E.bq0;
+    E.bq1 = (q == 1 && b < E.bq1) ? b : E.bq1;
+    E.bq2 = (q == 2 && b < E.bq2) ? b : E.bq2;
+    E.bq3 = (q == 3 && b < E.bq3) ? b : E.bq3;
+    E.present |= 1u << q;
+    E.count++;
+}
+
+// Cull test (cross_and_rescue.py:141-150): sqrt(s) < d <=> s < cull_t; agents also need s > 0.
+__device__ __forceinline__ bool cull_keep(const KP& P, double r0, double r1, double p0, double p1, bool is_obstacle,
+                                          double& s) {
+    const double e0 = p0 - r0, e1 = p1 - r1;
+    s = e0 * e0 + e1 * e1;
+    return s < P.cull_t && (is_obstacle || s > 0);
+}
+
+// Box rows S_saturated (cbf.py:67-70), reference row order.
+struct Box {
+    double S[8];
+};
+__device__ __forceinline__ Box box_rhs(const KP& P, const Ego& E) {
+    Box B;
+    const double ms = P.ms;
+    B.S[0] = ms - E.u0x;
+    B.S[1] = ms + E.u0x;
+    B.S[2] = ms - E.u0y;
+    B.S[3] = ms + E.u0y;
+    B.S[4] = (ms - E.r2) - E.u0x;
+    B.S[5] = (ms + E.r2) + E.u0x;
+    B.S[6] = (ms - E.r3) - E.u0y;
+    B.S[7] = (ms + E.r3) + E.u0y;
+    return B;
+}
+
+// Exact min-norm point of the (<= 8) half-planes a.x <= b whose slot bit is set in mask;
+// slots 0..3 are the merged box rows, 4..7 the CBF quadrants.  Incremental (Seidel) method,
+// identical arithmetic to oracle/cbf_oracle.c:solve_planes.  Returns -1 (feasible) or the slot
+// at which the prefix became infeasible.
+__device__ __forceinline__ int solve8(const double (&a0)[8], const double (&a1)[8], const double (&b)[8],
+                                      unsigned mask, double& xo0, double& xo1) {
+    double tb[8];
+#pragma unroll
+    for (int h = 0; h < 8; ++h) tb[h] = FEAS_TOL * pmax(1.0, fabs(b[h]));
+    double x0 = 0.0, x1 = 0.0;
+#pragma unroll
+    for (int h = 0; h < 8; ++h) {
+        if (!((mask >> h) & 1u)) continue;
+        if ((a0[h] * x0 + a1[h] * x1) - b[h] <= tb[h]) continue;
+        const double n2 = a0[h] * a0[h] + a1[h] * a1[h];
+        if (!(n2 > 0)) return h;
+        const double t = b[h] / n2;
+        const double p0 = t * a0[h], p1 = t * a1[h];
+        const double d0 = -a1[h], d1 = a0[h];
+        double lo = -INFINITY, hi = INFINITY;
+#pragma unroll
+        for (int j = 0; j < h; ++j) {
+            if (!((mask >> j) & 1u)) continue;
+            const double ad = a0[j] * d0 + a1[j] * d1;
+            const double r = b[j] - (a0[j] * p0 + a1[j] * p1);
+            const double qv = r / ad;
+            if (ad > 0)
+                hi = pmin(hi, qv);
+            else if (ad < 0)
+                lo = pmax(lo, qv);
+        }
+        double s = 0.0;
+        if (s > hi) s = hi;
+        if (s < lo) s = lo;
+        x0 = p0 + s * d0;
+        x1 = p1 + s * d1;
+        bool ok = true;
+#pragma unroll
+        for (int j = 0; j <= h; ++j)
+            if ((mask >> j) & 1u) ok = ok && ((a0[j] * x0 + a1[j] * x1) - b[j] <= tb[j]);
+        if (!ok) return h;
+    }
+    xo0 = x0;
+    xo1 = x1;
+    return -1;
+}
+
+struct Sol {
+    double x0, x1;
+    int status;
+    int iters;
+    double viol;
+};
+
+// The QP of cbf.py:62-87 for an ego: merged box rows + per-quadrant CBF rows, with the
+// reference's +1 relaxation (cbf.py:84-87) applied while infeasible.
+__device__ __forceinline__ Sol solve_ego(const KP& P, const Ego& E) {
+    const Box B = box_rhs(P, E);
+    double a0[8] = {1.0, 0.0, -1.0, 0.0, P.n0[0], P.n0[1], P.n0[2], P.n0[3]};
+    double a1[8] = {0.0, 1.0, 0.0, -1.0, P.n1[0], P.n1[1], P.n1[2], P.n1[3]};
+    double b[8] = {pmin(B.S[0], B.S[4]), pmin(B.S[1], B.S[6]), pmin(B.S[2], B.S[5]), pmin(B.S[3], B.S[7]),
+                   E.bq0, E.bq1, E.bq2, E.bq3};
+    const unsigned mask = 0xFu | (E.present << 4);
+    Sol S;
+    S.status = CBF_STATUS_OPTIMAL;
+    S.iters = 0;
+    S.x0 = S.x1 = 0.0;
+    for (;;) {
+        const int fail = solve8(a0, a1, b, mask, S.x0, S.x1);
+        if (fail < 0) break;
+        if (fail < 4) {
+            S.status = CBF_STATUS_BOX_INFEASIBLE;
+            S.x0 = S.x1 = 0.0;
+            break;
+        }
+        if (S.iters >= P.relax_cap) {
+            S.status = CBF_STATUS_RELAX_CAP;
+            S.x0 = S.x1 = 0.0;
+            break;
+        }
+        b[4] = b[4] + 1.0;
+        b[5] = b[5] + 1.0;
+        b[6] = b[6] + 1.0;
+        b[7] = b[7] + 1.0;
+        S.iters++;
+        S.status = CBF_STATUS_RELAXED;
+    }
+    double v = 0.0;
+#pragma unroll
+    for (int h = 0; h < 8; ++h)
+        if ((mask >> h) & 1u) {
+            const double d = (a0[h] * S.x0 + a1[h] * S.x1) - b[h];
+            if (d > v) v = d;
+        }
+    S.viol = v;
+    return S;
+}
+
+// cbf.py:89-91
+__device__ __forceinline__ void clip_u(const KP& P, const Sol& S, const Ego& E, double& ux, double& uy) {
+    ux = pmax(pmin(S.x0 + E.u0x, P.ms), -P.ms);
+    uy = pmax(pmin(S.x1 + E.u0y, P.ms), -P.ms);
+}
+
+__device__ __forceinline__ int32_t pack_status(const Sol& S) {
+    const int it = S.iters < (1 << 23) ? S.iters : (1 << 23) - 1;
+    return S.status | (it << 8);
+}
+
+// Active-row test at x for a neighbour row after `iters` relaxations (SURVEY 8d gate).
+__device__ __forceinline__ uint8_t row_active(const KP& P, const Ego& E, const Sol& S, double o0, double o1,
+                                              double o2, double o3) {
+    int q;
+    double b = row_b(P, E, o0, o1, o2, o3, q);
+    for (int i = 0; i < S.iters; ++i) b = b + 1.0;
+    double a0 = 0, a1 = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+        if (q == k) {
+            a0 = P.n0[k];
+            a1 = P.n1[k];
+        }
+    const double lhs = a0 * S.x0 + a1 * S.x1;
+    return lhs >= b - ACTIVE_TOL * pmax(1.0, fabs(b)) ? 1 : 0;
+}
+
+__device__ __forceinline__ uint8_t box_active_bits(const KP& P, const Ego& E, const Sol& S) {
+    const Box B = box_rhs(P, E);
+    const double g0[8] = {1.0, 0.0, -1.0, 0.0, 1.0, -1.0, 0.0, 0.0};
+    const double g1[8] = {0.0, 1.0, 0.0, -1.0, 0.0, 0.0, 1.0, -1.0};
+    uint8_t bits = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const double lhs = g0[i] * S.x0 + g1[i] * S.x1;
+        if (lhs >= B.S[i] - ACTIVE_TOL * pmax(1.0, fabs(B.S[i]))) bits |= (uint8_t)(1u << i);
+    }
+    return bits;
+}
+
+// Uniform-grid cell coordinate with clamping (exact for any input; NaN -> 0).
+__device__ __forceinline__ int cell_coord(double v, double o, double inv_h, int n) {
+    double f = floor((v - o) * inv_h);
+    if (!(f >= 0.0)) f = 0.0;
+    if (f > (double)(n - 1)) f = (double)(n - 1);
+    return (int)f;
+}
+
+// Monotone u64 key of a double (for atomicMin/Max extents).
+__device__ __forceinline__ unsigned long long dkey(double v) {
+    unsigned long long u = (unsigned long long)__double_as_longlong(v);
+    return (u >> 63) ? ~u : (u | 0x8000000000000000ull);
+}
+
+}  // namespace cbf

@@ -1,0 +1,82 @@
+// cells.hpp -- uniform cell list (counting sort by cell) shared by the swarm kernels.
+//
+// Build = bin (cell id + per-cell atomic slot) -> per-tile reduce -> tile scan -> scatter into
+// cell-sorted SoA copies.  Slot order inside a cell depends on atomic arrival, which is harmless:
+// the filter's per-quadrant minimum is order-independent, so results stay deterministic.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "cbf_amd.h"
+
+namespace cbf {
+
+constexpr int kScanTile = 2048;  // 256 threads x 8 cells
+
+struct CellGrid {
+    double x0, y0, inv_h;
+    int nx, ny;
+};
+
+inline CellGrid make_grid(const cbf_grid* g) {
+    CellGrid G;
+    G.x0 = g->x0;
+    G.y0 = g->y0;
+    G.inv_h = g->inv_h;
+    G.nx = g->nx;
+    G.ny = g->ny;
+    return G;
+}
+
+inline size_t align256(size_t b) { return (b + 255) & ~size_t(255); }
+
+// Workspace carve-up (all segments 256-byte aligned).
+struct CellWs {
+    int32_t* count;   // [ncell]
+    int32_t* start;   // [ncell + 1]
+    int32_t* tilesum; // [ntiles]
+    int2* cs;         // [n] (cell, slot); cell < 0: not binned
+    double2* spos;    // [n] cell-sorted positions
+    double2* svel;    // [n] cell-sorted velocities / nominal controls
+    int32_t* sidx;    // [n] entity index of each sorted slot
+    double2* wvel;    // [n] scratch velocities (lattice step: nominal of window agents)
+    unsigned long long* ext;  // [4] extents keys (lattice step)
+    long ncell;
+    int ntiles;
+
+    static int tiles(long ncell) { return (int)((ncell + kScanTile - 1) / kScanTile); }
+    static size_t bytes(long n, long ncell) {
+        return align256(4 * ncell) + align256(4 * (ncell + 1)) + align256(4 * (size_t)tiles(ncell)) +
+               align256(8 * n) + 2 * align256(16 * n) + align256(4 * n) + align256(16 * n) + 256;
+    }
+    CellWs(void* base, long n, long nc) : ncell(nc), ntiles(tiles(nc)) {
+        char* p = (char*)base;
+        count = (int32_t*)p;
+        p += align256(4 * nc);
+        start = (int32_t*)p;
+        p += align256(4 * (nc + 1));
+        tilesum = (int32_t*)p;
+        p += align256(4 * (size_t)ntiles);
+        cs = (int2*)p;
+        p += align256(8 * n);
+        spos = (double2*)p;
+        p += align256(16 * n);
+        svel = (double2*)p;
+        p += align256(16 * n);
+        sidx = (int32_t*)p;
+        p += align256(4 * n);
+        wvel = (double2*)p;
+        p += align256(16 * n);
+        ext = (unsigned long long*)p;
+    }
+};
+
+// Full build from positions: memset counts, bin, scan, scatter (vel copied alongside).
+// When `skip_bin` is set the caller already binned (count / cs filled by its own kernel).
+int build_cells(const CellGrid& G, const CellWs& W, int n, const double2* pos, const double2* vel,
+                const int32_t* unused, hipStream_t s);
+int scan_and_scatter(const CellGrid& G, const CellWs& W, int n, const double2* pos, const double2* vel,
+                     hipStream_t s);
+
+}  // namespace cbf

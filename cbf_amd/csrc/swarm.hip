@@ -1,0 +1,377 @@
+// swarm.hip -- nominal control, Euler, and the fused lattice-swarm timestep (gfx950).
+//   graph-Laplacian consensus / cyclic pursuit   cross_and_rescue.py:108-125, meet_at_center.py:86-103
+//   Euler                                        cross_and_rescue.py:173
+//   whole timestep of a lattice swarm            SURVEY cfg3/cfg4 (cross_and_rescue.py:97-175 shape)
+#include "cbf_device.hpp"
+#include "cells.hpp"
+
+using namespace cbf;
+
+namespace {
+
+inline int nblk(long n) { return (int)((n + kBlock - 1) / kBlock); }
+
+__global__ void __launch_bounds__(kBlock) k_consensus_csr(int n_dst, int self_offset, int n_group,
+                                                          const double2* __restrict__ src,
+                                                          const double2* __restrict__ anchors,
+                                                          const int32_t* __restrict__ row_ptr,
+                                                          const int32_t* __restrict__ col, int rotate, double rc,
+                                                          double rs, double scale, double2* __restrict__ out) {
+    const int k = blockIdx.x * kBlock + threadIdx.x;
+    if (k >= n_dst) return;
+    const double2 xi = src[self_offset + k];
+    double a0 = 0.0, a1 = 0.0;
+    for (int t = row_ptr[k]; t < row_ptr[k + 1]; ++t) {
+        const int j = col[t];
+        const double2 xj = (j < n_group) ? src[j] : anchors[j - n_group];
+        a0 = a0 + (xj.x - xi.x);
+        a1 = a1 + (xj.y - xi.y);
+    }
+    double v0 = a0, v1 = a1;
+    if (rotate) {  // (sum) @ [[rc, rs], [-rs, rc]] as OpenBLAS gemv evaluates it
+        v0 = fma(a1, -rs, a0 * rc);
+        v1 = fma(a1, rc, a0 * rs);
+    }
+    out[k] = make_double2(v0 * scale, v1 * scale);
+}
+
+// Lattice Laplacian sum for window agent w (neighbours in ascending index order).
+__device__ __forceinline__ double2 lattice_sum(const double2* __restrict__ pos, long w, int r, int c, int W, int H) {
+    const double2 pi = pos[w];
+    double a0 = 0.0, a1 = 0.0;
+    if (r > 0) {
+        const double2 q = pos[w - W];
+        a0 = a0 + (q.x - pi.x);
+        a1 = a1 + (q.y - pi.y);
+    }
+    if (c > 0) {
+        const double2 q = pos[w - 1];
+        a0 = a0 + (q.x - pi.x);
+        a1 = a1 + (q.y - pi.y);
+    }
+    if (c < W - 1) {
+        const double2 q = pos[w + 1];
+        a0 = a0 + (q.x - pi.x);
+        a1 = a1 + (q.y - pi.y);
+    }
+    if (r < H - 1) {
+        const double2 q = pos[w + W];
+        a0 = a0 + (q.x - pi.x);
+        a1 = a1 + (q.y - pi.y);
+    }
+    return make_double2(a0, a1);
+}
+
+__global__ void __launch_bounds__(kBlock) k_consensus_lattice(int W, int H, int row_begin, int row_end, int pos_row0,
+                                                              const double2* __restrict__ pos, double scale,
+                                                              double2* __restrict__ out) {
+    const long k = (long)blockIdx.x * kBlock + threadIdx.x;
+    const long nk = (long)(row_end - row_begin) * W;
+    if (k >= nk) return;
+    const int r = row_begin + (int)(k / W), c = (int)(k % W);
+    const long w = (long)(r - pos_row0) * W + c;
+    const double2 a = lattice_sum(pos, w, r, c, W, H);
+    out[k] = make_double2(a.x * scale, a.y * scale);
+}
+
+__global__ void __launch_bounds__(kBlock) k_euler(int n, double2* __restrict__ pos, const double2* __restrict__ vel,
+                                                  double T) {
+    const int i = blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    const double2 p = pos[i], v = vel[i];
+    pos[i] = make_double2(p.x + T * v.x, p.y + T * v.y);
+}
+
+// Lattice step K1: nominal control of every window agent whose lattice neighbours are all in the
+// window, + cell binning of those agents.  Owned agents also get vel_out.
+__global__ void __launch_bounds__(kBlock) k_lattice_nominal_bin(CellGrid G, int W, int H, int row_begin, int row_end,
+                                                                int win_row0, int win_rows,
+                                                                const double2* __restrict__ pos, double gain,
+                                                                double2* __restrict__ wvel,
+                                                                double2* __restrict__ vel_out,
+                                                                int32_t* __restrict__ count, int2* __restrict__ cs,
+                                                                unsigned long long* __restrict__ ext) {
+    const long w = (long)blockIdx.x * kBlock + threadIdx.x;
+    if (w == 0 && ext) {
+        ext[0] = dkey(INFINITY);
+        ext[1] = dkey(-INFINITY);
+        ext[2] = dkey(-INFINITY);
+        ext[3] = dkey(INFINITY);
+    }
+    if (w >= (long)win_rows * W) return;
+    const int r = win_row0 + (int)(w / W), c = (int)(w % W);
+    const bool ok = (r == 0 || r - 1 >= win_row0) && (r == H - 1 || r + 1 < win_row0 + win_rows);
+    if (!ok) {
+        cs[w] = make_int2(-1, 0);
+        return;
+    }
+    const double2 a = lattice_sum(pos, w, r, c, W, H);
+    const double2 u0 = make_double2(a.x * gain, a.y * gain);
+    wvel[w] = u0;
+    if (r >= row_begin && r < row_end) vel_out[(long)(r - row_begin) * W + c] = u0;
+    const double2 p = pos[w];
+    const int cell = cell_coord(p.y, G.y0, G.inv_h, G.ny) * G.nx + cell_coord(p.x, G.x0, G.inv_h, G.nx);
+    const int slot = atomicAdd(&count[cell], 1);
+    cs[w] = make_int2(cell, slot);
+}
+
+__device__ __forceinline__ double wave_min(double v) {
+    for (int o = 32; o > 0; o >>= 1) v = pmin(v, __shfl_xor(v, o, 64));
+    return v;
+}
+__device__ __forceinline__ double wave_max(double v) {
+    for (int o = 32; o > 0; o >>= 1) v = pmax(v, __shfl_xor(v, o, 64));
+    return v;
+}
+
+// Lattice step K4: filter + clip + Euler for the owned agents, lane = cell-sorted slot.
+__global__ void __launch_bounds__(kBlock) k_lattice_filter(KP P, CellGrid G, int W, int row_begin, int row_end,
+                                                           int win_row0, long ncell, const double2* __restrict__ spos,
+                                                           const double2* __restrict__ svel,
+                                                           const int32_t* __restrict__ sidx,
+                                                           const int32_t* __restrict__ start, double T,
+                                                           double2* __restrict__ pos_out, double2* __restrict__ u,
+                                                           int32_t* __restrict__ status, int32_t* __restrict__ cnt,
+                                                           int guard_rows, double* __restrict__ ext_part,
+                                                           unsigned long long* __restrict__ solves) {
+    const int slot = blockIdx.x * kBlock + threadIdx.x;
+    bool solved = false;
+    const int total = start[ncell];
+    bool own = false;
+    double ny = 0.0;
+    int r = 0;
+    if (slot < total) {
+        const int w = sidx[slot];
+        r = win_row0 + w / W;
+        const int c = w % W;
+        own = r >= row_begin && r < row_end;
+        if (own) {
+            const double2 pe = spos[slot], ve = svel[slot];
+            Ego E;
+            ego_init(P, E, pe.x, pe.y, ve.x, ve.y, ve.x, ve.y);
+            const int cx = cell_coord(pe.x, G.x0, G.inv_h, G.nx);
+            const int cy = cell_coord(pe.y, G.y0, G.inv_h, G.ny);
+            const int xa = cx > 0 ? cx - 1 : 0;
+            const int xb = cx < G.nx - 1 ? cx + 1 : G.nx - 1;
+            for (int dy = -1; dy <= 1; ++dy) {
+                const int yy = cy + dy;
+                if (yy < 0 || yy >= G.ny) continue;
+                const int t0 = start[yy * G.nx + xa], t1 = start[yy * G.nx + xb + 1];
+                for (int t = t0; t < t1; ++t) {
+                    const double2 pj = spos[t];
+                    const double e0 = pj.x - E.r0, e1 = pj.y - E.r1;
+                    const double s = e0 * e0 + e1 * e1;
+                    if (!(s < P.cull_t && s > 0)) continue;
+                    const double2 vj = svel[t];
+                    ego_add(P, E, pj.x, pj.y, vj.x, vj.y);
+                }
+            }
+            const long k = (long)(r - row_begin) * W + c;
+            double ux, uy;
+            int32_t st;
+            if (E.count == 0) {
+                ux = E.u0x;
+                uy = E.u0y;
+                st = CBF_STATUS_IDLE;
+            } else {
+                const Sol S = solve_ego(P, E);
+                clip_u(P, S, E, ux, uy);
+                st = pack_status(S);
+            }
+            const double2 pn = make_double2(pe.x + T * ux, pe.y + T * uy);
+            pos_out[k] = pn;
+            u[k] = make_double2(ux, uy);
+            status[k] = st;
+            if (cnt) cnt[k] = E.count;
+            ny = pn.y;
+            solved = E.count > 0;
+        }
+    }
+    if (solves) {  // wave-aggregated, spread over 64 counters on separate 128-B lines
+        const unsigned long long m = __ballot(solved);
+        if ((threadIdx.x & 63) == 0 && m)
+            atomicAdd(&solves[16 * ((blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6)) & 63)],
+                      (unsigned long long)__popcll(m));
+    }
+    if (!ext_part) return;
+    // per-block extents of the new owned positions (halo guard for the sharded step)
+    __shared__ double red[4][kBlock / 64];
+    const double v0 = own ? ny : INFINITY, v1 = own ? ny : -INFINITY;
+    const double v2 = (own && r < row_end - guard_rows) ? ny : -INFINITY;
+    const double v3 = (own && r >= row_begin + guard_rows) ? ny : INFINITY;
+    const double m0 = wave_min(v0), m1 = wave_max(v1), m2 = wave_max(v2), m3 = wave_min(v3);
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    if (lane == 0) {
+        red[0][wid] = m0;
+        red[1][wid] = m1;
+        red[2][wid] = m2;
+        red[3][wid] = m3;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double a = red[0][0], b = red[1][0], c2 = red[2][0], d = red[3][0];
+        for (int q = 1; q < kBlock / 64; ++q) {
+            a = pmin(a, red[0][q]);
+            b = pmax(b, red[1][q]);
+            c2 = pmax(c2, red[2][q]);
+            d = pmin(d, red[3][q]);
+        }
+        double* o = ext_part + 4l * blockIdx.x;
+        o[0] = a;
+        o[1] = b;
+        o[2] = c2;
+        o[3] = d;
+    }
+}
+
+__global__ void __launch_bounds__(kBlock) k_extents_finalize(int nparts, const double* __restrict__ part,
+                                                             double* __restrict__ out) {
+    double a = INFINITY, b = -INFINITY, c = -INFINITY, d = INFINITY;
+    for (int i = threadIdx.x; i < nparts; i += kBlock) {
+        a = pmin(a, part[4 * i]);
+        b = pmax(b, part[4 * i + 1]);
+        c = pmax(c, part[4 * i + 2]);
+        d = pmin(d, part[4 * i + 3]);
+    }
+    a = wave_min(a);
+    b = wave_max(b);
+    c = wave_max(c);
+    d = wave_min(d);
+    __shared__ double red[4][kBlock / 64];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    if (lane == 0) {
+        red[0][wid] = a;
+        red[1][wid] = b;
+        red[2][wid] = c;
+        red[3][wid] = d;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int q = 1; q < kBlock / 64; ++q) {
+            red[0][0] = pmin(red[0][0], red[0][q]);
+            red[1][0] = pmax(red[1][0], red[1][q]);
+            red[2][0] = pmax(red[2][0], red[2][q]);
+            red[3][0] = pmin(red[3][0], red[3][q]);
+        }
+        out[0] = red[0][0];
+        out[1] = red[1][0];
+        out[2] = red[2][0];
+        out[3] = red[3][0];
+    }
+}
+
+}  // namespace
+
+extern "C" int cbf_consensus_csr(int32_t n_dst, int32_t self_offset, int32_t n_group, const double* src,
+                                 const double* anchors, const int32_t* row_ptr, const int32_t* col, int32_t rotate,
+                                 double rc, double rs, double scale, double* out, void* stream) {
+    if (n_dst < 0 || self_offset < 0 || n_group < 0 || self_offset + n_dst > n_group) return CBF_EINVAL;
+    if (n_dst == 0) return 0;
+    if (!src || !row_ptr || !out) return CBF_EINVAL;
+    hipLaunchKernelGGL(k_consensus_csr, dim3(nblk(n_dst)), dim3(kBlock), 0, (hipStream_t)stream, n_dst, self_offset,
+                       n_group, reinterpret_cast<const double2*>(src), reinterpret_cast<const double2*>(anchors),
+                       row_ptr, col, rotate, rc, rs, scale, reinterpret_cast<double2*>(out));
+    return (int)hipGetLastError();
+}
+
+extern "C" int cbf_consensus_lattice(int32_t W, int32_t H, int32_t row_begin, int32_t row_end, int32_t pos_row0,
+                                     const double* pos, double scale, double* out, void* stream) {
+    if (W <= 0 || H <= 0 || row_begin < 0 || row_end > H || row_begin > row_end) return CBF_EINVAL;
+    if (pos_row0 > (row_begin > 0 ? row_begin - 1 : 0)) return CBF_EINVAL;
+    if (row_end == row_begin) return 0;
+    if (!pos || !out) return CBF_EINVAL;
+    const long nk = (long)(row_end - row_begin) * W;
+    hipLaunchKernelGGL(k_consensus_lattice, dim3(nblk(nk)), dim3(kBlock), 0, (hipStream_t)stream, W, H, row_begin,
+                       row_end, pos_row0, reinterpret_cast<const double2*>(pos), scale,
+                       reinterpret_cast<double2*>(out));
+    return (int)hipGetLastError();
+}
+
+extern "C" int cbf_euler(int32_t n, double* pos, const double* vel, double T, void* stream) {
+    if (n < 0) return CBF_EINVAL;
+    if (n == 0) return 0;
+    if (!pos || !vel) return CBF_EINVAL;
+    hipLaunchKernelGGL(k_euler, dim3(nblk(n)), dim3(kBlock), 0, (hipStream_t)stream, n,
+                       reinterpret_cast<double2*>(pos), reinterpret_cast<const double2*>(vel), T);
+    return (int)hipGetLastError();
+}
+
+static size_t lattice_ext_bytes(long win_n) { return align256(32 * (size_t)((win_n + kBlock - 1) / kBlock)); }
+
+extern "C" size_t cbf_lattice_workspace_size(int32_t W, int32_t win_rows, const cbf_grid* grid) {
+    if (!grid || W <= 0 || win_rows <= 0 || grid->nx <= 0 || grid->ny <= 0) return 0;
+    const long n = (long)W * win_rows;
+    return CellWs::bytes(n, (long)grid->nx * grid->ny) + lattice_ext_bytes(n);
+}
+
+static int check_lattice(const cbf_params* p, const cbf_grid* grid, int32_t W, int32_t H, int32_t row_begin,
+                         int32_t row_end, int32_t win_row0, int32_t win_rows, const double* pos, void* workspace,
+                         size_t workspace_bytes) {
+    if (!p || !grid || W <= 0 || H <= 0) return CBF_EINVAL;
+    if (row_begin < 0 || row_end > H || row_begin >= row_end) return CBF_EINVAL;
+    if (win_row0 < 0 || win_rows <= 0 || win_row0 + win_rows > H) return CBF_EINVAL;
+    // owned rows plus one neighbour row on each side (where it exists) must be in the window
+    if (win_row0 > (row_begin > 0 ? row_begin - 1 : 0)) return CBF_EINVAL;
+    if (win_row0 + win_rows < (row_end < H ? row_end + 1 : H)) return CBF_EINVAL;
+    if ((long)W * win_rows >= (1l << 31)) return CBF_EINVAL;
+    if (!pos || !workspace) return CBF_EINVAL;
+    if (grid->nx <= 0 || grid->ny <= 0 || !(grid->inv_h > 0) || !(1.0 / grid->inv_h >= sqrt(p->cull_t)))
+        return CBF_EINVAL;
+    if ((long)grid->nx * grid->ny > (1l << 30)) return CBF_EINVAL;
+    if (workspace_bytes < cbf_lattice_workspace_size(W, win_rows, grid)) return CBF_EINVAL;
+    return 0;
+}
+
+extern "C" int cbf_lattice_build(const cbf_params* p, const cbf_grid* grid, int32_t W, int32_t H, int32_t row_begin,
+                                 int32_t row_end, int32_t win_row0, int32_t win_rows, const double* pos, double gain,
+                                 double* vel_out, void* workspace, size_t workspace_bytes, void* stream) {
+    int rc = check_lattice(p, grid, W, H, row_begin, row_end, win_row0, win_rows, pos, workspace, workspace_bytes);
+    if (rc) return rc;
+    if (!vel_out) return CBF_EINVAL;
+    hipStream_t s = (hipStream_t)stream;
+    const long n = (long)W * win_rows;
+    const CellGrid G = make_grid(grid);
+    CellWs Wk(workspace, n, (long)G.nx * G.ny);
+    hipError_t e = hipMemsetAsync(Wk.count, 0, sizeof(int32_t) * Wk.ncell, s);
+    if (e != hipSuccess) return (int)e;
+    const double2* p2 = reinterpret_cast<const double2*>(pos);
+    hipLaunchKernelGGL(k_lattice_nominal_bin, dim3(nblk(n)), dim3(kBlock), 0, s, G, W, H, row_begin, row_end, win_row0,
+                       win_rows, p2, gain, Wk.wvel, reinterpret_cast<double2*>(vel_out), Wk.count, Wk.cs,
+                       (unsigned long long*)nullptr);
+    return scan_and_scatter(G, Wk, (int)n, p2, Wk.wvel, s);
+}
+
+extern "C" int cbf_lattice_advance(const cbf_params* p, const cbf_grid* grid, int32_t W, int32_t H,
+                                   int32_t row_begin, int32_t row_end, int32_t win_row0, int32_t win_rows,
+                                   const double* pos, double T, double* pos_out, double* u, int32_t* status,
+                                   int32_t* nbr_count, int32_t guard_rows, double* extents, uint64_t* solves,
+                                   void* workspace, size_t workspace_bytes, void* stream) {
+    int rc = check_lattice(p, grid, W, H, row_begin, row_end, win_row0, win_rows, pos, workspace, workspace_bytes);
+    if (rc) return rc;
+    if (!pos_out || !u || !status) return CBF_EINVAL;
+    if (pos_out == pos && (win_row0 != row_begin || win_rows != row_end - row_begin)) return CBF_EINVAL;
+    hipStream_t s = (hipStream_t)stream;
+    const long n = (long)W * win_rows;
+    const CellGrid G = make_grid(grid);
+    CellWs Wk(workspace, n, (long)G.nx * G.ny);
+    double* ext_part = extents ? (double*)((char*)workspace + CellWs::bytes(n, Wk.ncell)) : nullptr;
+    const int nb = nblk(n);
+    hipLaunchKernelGGL(k_lattice_filter, dim3(nb), dim3(kBlock), 0, s, make_kp(p), G, W, row_begin, row_end, win_row0,
+                       Wk.ncell, Wk.spos, Wk.svel, Wk.sidx, Wk.start, T, reinterpret_cast<double2*>(pos_out),
+                       reinterpret_cast<double2*>(u), status, nbr_count, guard_rows, ext_part,
+                       reinterpret_cast<unsigned long long*>(solves));
+    if (extents) hipLaunchKernelGGL(k_extents_finalize, dim3(1), dim3(kBlock), 0, s, nb, ext_part, extents);
+    return (int)hipGetLastError();
+}
+
+extern "C" int cbf_lattice_step(const cbf_params* p, const cbf_grid* grid, int32_t W, int32_t H, int32_t row_begin,
+                                int32_t row_end, int32_t win_row0, int32_t win_rows, const double* pos, double gain,
+                                double T, double* pos_out, double* vel_out, double* u, int32_t* status,
+                                int32_t* nbr_count, int32_t guard_rows, double* extents, uint64_t* solves,
+                                void* workspace, size_t workspace_bytes, void* stream) {
+    int rc = cbf_lattice_build(p, grid, W, H, row_begin, row_end, win_row0, win_rows, pos, gain, vel_out, workspace,
+                               workspace_bytes, stream);
+    if (rc) return rc;
+    return cbf_lattice_advance(p, grid, W, H, row_begin, row_end, win_row0, win_rows, pos, T, pos_out, u, status,
+                               nbr_count, guard_rows, extents, solves, workspace, workspace_bytes, stream);
+}

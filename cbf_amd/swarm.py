@@ -1,0 +1,268 @@
+"""Batched swarm API over the HIP library: the per-agent loop of the reference callers
+(cross_and_rescue.py:97-175, meet_at_center.py:76-153) as device-resident batched steps.
+
+Entity layout: one (n, 2) float64 CUDA tensor of positions and one of velocities; entities
+[0, n_obs) are obstacles, [n_obs, n) agents.  An agent's "velocity" slot is its nominal control
+u0 (cross_and_rescue.py:133) -- exactly the reference's packing, kept as SoA-of-pairs so every
+lane loads 16 contiguous bytes.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, field
+
+import numpy as np
+
+from . import _lib
+from ._lib import CbfDiag, CbfGrid, check, lib, ptr, stream_handle
+
+
+@dataclass
+class FilterParams:
+    """ControlBarrierFunction(max_speed, dmin, k) + the callers' f, g and cull radius."""
+    max_speed: float = 15.0              # cross_and_rescue.py:30
+    dmin: float = 0.2                    # cbf.py:6
+    k: float = 1.0                       # cbf.py:6
+    safety_distance: float = 0.2         # cross_and_rescue.py:134
+    f: np.ndarray = field(default_factory=lambda: np.zeros((4, 4)))                                  # :31
+    g: np.ndarray = field(default_factory=lambda: 0.1 * np.array([[1, 0], [0, 1], [0, 0], [0, 0]]))  # :32
+
+    def c(self):
+        return _lib.make_params(self.max_speed, self.dmin, self.k, self.f, self.g, self.safety_distance)
+
+
+def make_grid(xmin, ymin, xmax, ymax, cell):
+    g = CbfGrid()
+    g.x0, g.y0, g.inv_h = float(xmin), float(ymin), 1.0 / float(cell)
+    g.nx = max(1, int(math.ceil((xmax - xmin) / cell)))
+    g.ny = max(1, int(math.ceil((ymax - ymin) / cell)))
+    return g
+
+
+def grid_for_points(pos_np, cull_radius, margin=1.0, cell_factor=1.02):
+    lo = pos_np.min(axis=0) - margin
+    hi = pos_np.max(axis=0) + margin
+    return make_grid(lo[0], lo[1], hi[0], hi[1], cull_radius * cell_factor)
+
+
+def filter_swarm(params, pos, vel, n_obs, ego_begin=None, ego_end=None, method="auto", grid=None, kmax=0,
+                 diag=False, workspace=None):
+    """cross_and_rescue.py:135-160 for every ego in [ego_begin, ego_end).  Returns a dict of
+    CUDA tensors: u (n_ego,2), status, nbr_count [, nbr_idx, nbr_active, box_active, x, viol]."""
+    torch = _lib.require_gpu()
+    n = pos.shape[0]
+    eb = n_obs if ego_begin is None else ego_begin
+    ee = n if ego_end is None else ego_end
+    ne = ee - eb
+    dev = pos.device
+    pos = pos.contiguous()
+    vel = vel.contiguous()
+    assert pos.dtype == torch.float64 and vel.dtype == torch.float64 and pos.shape == vel.shape == (n, 2)
+    cp = params.c() if isinstance(params, FilterParams) else params
+    out = {"u": torch.empty((ne, 2), dtype=torch.float64, device=dev),
+           "status": torch.empty((ne,), dtype=torch.int32, device=dev),
+           "nbr_count": torch.empty((ne,), dtype=torch.int32, device=dev)}
+    D = None
+    if kmax or diag:
+        D = CbfDiag()
+        D.kmax = kmax
+        if kmax:
+            out["nbr_idx"] = torch.empty((ne, kmax), dtype=torch.int32, device=dev)
+            D.nbr_idx = out["nbr_idx"].data_ptr()
+            if diag:
+                out["nbr_active"] = torch.empty((ne, kmax), dtype=torch.uint8, device=dev)
+                D.nbr_active = out["nbr_active"].data_ptr()
+        if diag:
+            out["box_active"] = torch.empty((ne,), dtype=torch.uint8, device=dev)
+            out["x"] = torch.empty((ne, 2), dtype=torch.float64, device=dev)
+            out["viol"] = torch.empty((ne,), dtype=torch.float64, device=dev)
+            D.box_active = out["box_active"].data_ptr()
+            D.x = out["x"].data_ptr()
+            D.viol = out["viol"].data_ptr()
+    if method == "auto":
+        method = "allpairs" if n <= 8192 else "cells"
+    Dp = None if D is None else _lib.C.byref(D)
+    if method == "allpairs":
+        check(lib.cbf_filter_allpairs(cp, n, n_obs, ptr(pos), ptr(vel), eb, ee, ptr(out["u"]), ptr(out["status"]),
+                                      ptr(out["nbr_count"]), Dp, stream_handle()), "cbf_filter_allpairs")
+    elif method == "cells":
+        if grid is None:
+            grid = grid_for_points(pos.cpu().numpy(), params.safety_distance if isinstance(params, FilterParams)
+                                   else math.sqrt(cp.cull_t))
+        need = lib.cbf_cells_workspace_size(n, _lib.C.byref(grid))
+        if workspace is None or workspace.numel() < need:
+            workspace = torch.empty((need,), dtype=torch.uint8, device=dev)
+        check(lib.cbf_filter_cells(cp, _lib.C.byref(grid), n, n_obs, ptr(pos), ptr(vel), eb, ee, ptr(out["u"]),
+                                   ptr(out["status"]), ptr(out["nbr_count"]), Dp, ptr(workspace), need,
+                                   stream_handle()), "cbf_filter_cells")
+    else:
+        raise ValueError(method)
+    return out
+
+
+def consensus_csr(src, row_ptr, col, self_offset=0, anchors=None, rot=None, scale=1.0, out=None):
+    """Laplacian nominal control (cross_and_rescue.py:108-125): out[k] = (sum_j (x_j - x_k)) [@ R] * scale."""
+    torch = _lib.require_gpu()
+    n_dst = row_ptr.shape[0] - 1
+    if out is None:
+        out = torch.empty((n_dst, 2), dtype=torch.float64, device=src.device)
+    rc, rs = (1.0, 0.0) if rot is None else rot
+    check(lib.cbf_consensus_csr(n_dst, self_offset, src.shape[0], ptr(src), ptr(anchors), ptr(row_ptr), ptr(col),
+                                0 if rot is None else 1, float(rc), float(rs), float(scale), ptr(out),
+                                stream_handle()), "cbf_consensus_csr")
+    return out
+
+
+def consensus_lattice(pos, W, H, gain, row_begin=0, row_end=None, pos_row0=0, out=None):
+    torch = _lib.require_gpu()
+    row_end = H if row_end is None else row_end
+    if out is None:
+        out = torch.empty(((row_end - row_begin) * W, 2), dtype=torch.float64, device=pos.device)
+    check(lib.cbf_consensus_lattice(W, H, row_begin, row_end, pos_row0, ptr(pos), float(gain), ptr(out),
+                                    stream_handle()), "cbf_consensus_lattice")
+    return out
+
+
+def euler(pos, vel, T):
+    """In place: pos <- pos + T*vel (cross_and_rescue.py:173)."""
+    _lib.require_gpu()
+    check(lib.cbf_euler(pos.shape[0], ptr(pos), ptr(vel), float(T), stream_handle()), "cbf_euler")
+    return pos
+
+
+def csr_from_rows(rows, device):
+    import torch
+    rp = np.concatenate([[0], np.cumsum([len(r) for r in rows])]).astype(np.int32)
+    col = np.array([j for r in rows for j in r] or [0], dtype=np.int32)
+    return torch.tensor(rp, device=device), torch.tensor(col, device=device)
+
+
+class GroupSwarm:
+    """A swarm of entity groups with graph-Laplacian nominal controls (cfg1/cfg2 shape):
+    each group = (begin, end, rows [list of neighbour lists, indices relative to begin;
+    >= size -> anchors], anchors, rotation (c, s) or None, scale).  One step = nominal control
+    per group, per-agent cull + filter (all-pairs) for egos [n_obs, n), Euler for every entity
+    (obstacles with their nominal velocity, agents with the filtered control)."""
+
+    def __init__(self, pos, n_obs, groups, params: FilterParams = None, T=1 / 30, method="auto"):
+        torch = _lib.require_gpu()
+        self.dev = torch.device("cuda")
+        self.pos = torch.as_tensor(np.asarray(pos, dtype=np.float64), device=self.dev).contiguous()
+        self.n = self.pos.shape[0]
+        self.n_obs = n_obs
+        self.T = T
+        self.params = params or FilterParams()
+        self.cp = self.params.c()
+        self.method = method
+        self.vel = torch.zeros_like(self.pos)
+        self.groups = []
+        for (b, e, rows, anchors, rot, scale) in groups:
+            rp, col = csr_from_rows(rows, self.dev)
+            anc = None if anchors is None else torch.as_tensor(np.asarray(anchors, np.float64).reshape(-1, 2),
+                                                               device=self.dev).contiguous()
+            self.groups.append((b, e, rp, col, anc, rot, scale))
+        self.last = None
+
+    def nominal(self):
+        for (b, e, rp, col, anc, rot, scale) in self.groups:
+            consensus_csr(self.pos[b:e], rp, col, 0, anc, rot, scale, out=self.vel[b:e])
+        return self.vel
+
+    def step(self, kmax=0, diag=False):
+        self.nominal()
+        out = filter_swarm(self.cp, self.pos, self.vel, self.n_obs, method=self.method, kmax=kmax, diag=diag)
+        u = self.vel.clone()
+        u[self.n_obs:] = out["u"]
+        out["nominal"] = self.vel.clone()
+        out["u_all"] = u
+        euler(self.pos, u, self.T)
+        self.last = out
+        return out
+
+
+class LatticeSwarm:
+    """SURVEY cfg3/cfg4: a W x H lattice swarm, one fused timestep per `step()` through
+    cbf_lattice_step (nominal + cell list + filter + clip + Euler); optionally captured in a
+    hipGraph.  Single-GPU: the window is the whole lattice."""
+
+    def __init__(self, pos, W, H, gain=0.25, params: FilterParams = None, T=1 / 30, grid=None, margin=1.0):
+        torch = _lib.require_gpu()
+        self.dev = torch.device("cuda")
+        pos = np.asarray(pos, dtype=np.float64).reshape(W * H, 2)
+        self.W, self.H, self.gain, self.T = W, H, float(gain), float(T)
+        self.params = params or FilterParams()
+        self.cp = self.params.c()
+        self.grid = grid or grid_for_points(pos, self.params.safety_distance, margin=margin)
+        n = W * H
+        self.n = n
+        self.pos = torch.tensor(pos, device=self.dev)
+        self.vel = torch.empty((n, 2), dtype=torch.float64, device=self.dev)
+        self.u = torch.empty((n, 2), dtype=torch.float64, device=self.dev)
+        self.status = torch.empty((n,), dtype=torch.int32, device=self.dev)
+        self.nbr_count = torch.empty((n,), dtype=torch.int32, device=self.dev)
+        self.ws_bytes = lib.cbf_lattice_workspace_size(W, H, _lib.C.byref(self.grid))
+        self.ws = torch.zeros((self.ws_bytes,), dtype=torch.uint8, device=self.dev)
+        self.solves = torch.zeros((1024,), dtype=torch.int64, device=self.dev)
+        self.graph = None
+
+    def _launch(self):
+        check(lib.cbf_lattice_step(self.cp, _lib.C.byref(self.grid), self.W, self.H, 0, self.H, 0, self.H,
+                                   ptr(self.pos), self.gain, self.T, ptr(self.pos), ptr(self.vel), ptr(self.u),
+                                   ptr(self.status), ptr(self.nbr_count), 0, None, ptr(self.solves), ptr(self.ws),
+                                   self.ws_bytes, stream_handle()), "cbf_lattice_step")
+
+    def build_phase(self):
+        """nominal control + cell list only (K1-K3)."""
+        check(lib.cbf_lattice_build(self.cp, _lib.C.byref(self.grid), self.W, self.H, 0, self.H, 0, self.H,
+                                    ptr(self.pos), self.gain, ptr(self.vel), ptr(self.ws), self.ws_bytes,
+                                    stream_handle()), "cbf_lattice_build")
+
+    def advance_phase(self):
+        """filter + clip + Euler only (the dominant kernel, K4)."""
+        check(lib.cbf_lattice_advance(self.cp, _lib.C.byref(self.grid), self.W, self.H, 0, self.H, 0, self.H,
+                                      ptr(self.pos), self.T, ptr(self.pos), ptr(self.u), ptr(self.status),
+                                      ptr(self.nbr_count), 0, None, ptr(self.solves), ptr(self.ws), self.ws_bytes,
+                                      stream_handle()), "cbf_lattice_advance")
+
+    def solves_total(self) -> int:
+        return int(self.solves.view(64, 16)[:, 0].sum().item())
+
+    def reset_solves(self):
+        self.solves.zero_()
+
+    def capture(self):
+        """Capture one step into a hipGraph (replayed by step())."""
+        import torch
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            self._launch()  # warm-up outside capture
+        torch.cuda.current_stream().wait_stream(s)
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            self._launch()
+        self.graph = g
+        return g
+
+    def step(self):
+        if self.graph is not None:
+            self.graph.replay()
+        else:
+            self._launch()
+
+
+def mc_rollout(params, pos, n_o, n_a, steps, T=1 / 30, theta=None, so=1.0, ga=1.0):
+    """SURVEY cfg5: pos (n_scen, n_o+n_a, 2) CUDA float64, advanced in place by `steps` steps.
+    Returns (counters int64 (n_scen,4), maxviol (n_scen,))."""
+    torch = _lib.require_gpu()
+    theta = -math.pi / n_o if theta is None else theta
+    rc, rs = float(np.cos(theta)), float(np.sin(theta))
+    n_scen = pos.shape[0]
+    assert pos.is_contiguous() and pos.dtype == torch.float64 and pos.shape[1] == n_o + n_a
+    cnt = torch.empty((n_scen, 4), dtype=torch.int64, device=pos.device)
+    mv = torch.empty((n_scen,), dtype=torch.float64, device=pos.device)
+    cp = params.c() if isinstance(params, FilterParams) else params
+    check(lib.cbf_mc_rollout(cp, n_scen, n_o, n_a, steps, float(T), rc, rs, float(so), float(ga), ptr(pos), ptr(cnt),
+                             ptr(mv), stream_handle()), "cbf_mc_rollout")
+    return cnt, mv

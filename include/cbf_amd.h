@@ -1,0 +1,198 @@
+/*
+ * cbf_amd.h -- C ABI of the MI355X-native CBF safety filter (libcbf_amd.so).
+ *
+ * Drop-in boundary for the reference's hot path (YilunAllenChen/CBF):
+ *   ControlBarrierFunction.__init__        cbf.py:6-16            -> cbf_params_init
+ *   ControlBarrierFunction.get_safe_control cbf.py:18-92          -> cbf_get_safe_control_batch
+ *   (A, b) handed to cvxopt.solvers.qp     cbf.py:64-81           -> cbf_assemble_rows
+ *   per-agent cull + filter loop           cross_and_rescue.py:135-160,
+ *                                          meet_at_center.py:118-143 -> cbf_filter_allpairs / cbf_filter_cells
+ *   Laplacian consensus / cyclic pursuit   cross_and_rescue.py:108-125,
+ *                                          meet_at_center.py:86-103 -> cbf_consensus_csr / cbf_consensus_lattice
+ *   Euler integration                      cross_and_rescue.py:173 -> cbf_euler
+ *   whole timestep (large swarm)           cross_and_rescue.py:97-175 -> cbf_lattice_step
+ *   batched Monte-Carlo rendezvous         meet_at_center.py:76-153 (x n_scen) -> cbf_mc_rollout
+ *
+ * Conventions
+ *  - All arrays are caller-owned DEVICE pointers (hipMalloc / torch CUDA tensors), fp64,
+ *    row-major, contiguous: positions / velocities / controls are [n][2] (x, y), states [n][4]
+ *    = (x, y, vx, vy) as in the reference's packed rows (cross_and_rescue.py:132-133).
+ *  - Parameter structs (cbf_params, cbf_grid, cbf_diag) live in HOST memory.
+ *  - `stream` is a hipStream_t (NULL = default stream).  Every call is asynchronous and
+ *    stream-ordered; no call allocates, synchronises or keeps global state, so any sequence
+ *    may be captured into a hipGraph.  Calls are re-entrant.
+ *  - Return value: 0 on success, CBF_EINVAL (<0) on a bad argument (nothing launched),
+ *    or a positive hipError_t from the launch.  No exception crosses the ABI.
+ *  - Results are deterministic (no float atomics on any result path) and bit-identical to
+ *    the CPU oracle in oracle/ for the same inputs.
+ */
+#ifndef CBF_AMD_H
+#define CBF_AMD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CBF_ABI_VERSION 1
+
+#define CBF_EINVAL (-1)
+
+/* per-ego status (low byte); bits 8..30 hold the number of +1 relaxations applied */
+#define CBF_STATUS_IDLE 0           /* no neighbour: filter not run, u = u0 unclipped (cross_and_rescue.py:153) */
+#define CBF_STATUS_OPTIMAL 1        /* exact minimiser of the QP of cbf.py:62-81 */
+#define CBF_STATUS_RELAXED 2        /* infeasible; CBF rows relaxed by the cbf.py:84-87 rule, then optimal */
+#define CBF_STATUS_BOX_INFEASIBLE 3 /* the 8 box rows alone are infeasible; x = 0 */
+#define CBF_STATUS_RELAX_CAP 4      /* relaxation cap reached; x = 0 */
+
+/* ControlBarrierFunction state (cbf.py:6-16) + the callers' dynamics and cull radius. */
+typedef struct cbf_params {
+    double max_speed; /* cbf.py:15 */
+    double dmin;      /* cbf.py:12 (default 0.2) */
+    double k;         /* cbf.py:13 (default 1) */
+    double gamma;     /* cbf.py:16 (0.5, not a constructor argument in the reference) */
+    double f[16];     /* dynamics f, row-major 4x4 (cross_and_rescue.py:31) */
+    double g[8];      /* dynamics g, row-major 4x2 (cross_and_rescue.py:32) */
+    double cull_t;    /* keep j iff |p_j - p_i|^2 < cull_t  <=>  sqrt(.) < safety_distance (:134,143) */
+    double nrm[4][2]; /* derived: L_g = -hs_p @ g per sign quadrant q = (dx<0) | (dy<0)<<1 (cbf.py:56) */
+    int32_t f_is_zero;/* derived */
+    int32_t relax_cap;/* max +1 relaxations before CBF_STATUS_RELAX_CAP (default 65536) */
+} cbf_params;
+
+/* Fill *p (host).  f16 / g8 may be NULL for the callers' f = 0, g = 0.1 [I2; 0]. */
+int cbf_params_init(cbf_params* p, double max_speed, double dmin, double k, const double* f16, const double* g8,
+                    double safety_distance);
+
+/* Optional per-ego diagnostics (device pointers; any may be NULL).  Neighbour lists are
+ * truncated at kmax entries (the count in nbr_count is never truncated). */
+typedef struct cbf_diag {
+    int32_t kmax;
+    int32_t* nbr_idx;    /* [n_ego][kmax] entity indices, -1 padded */
+    uint8_t* nbr_active; /* [n_ego][kmax] 1 if that neighbour's row is active at x */
+    uint8_t* box_active; /* [n_ego] bit i = box row i (cbf.py:66 order) active */
+    double* x;           /* [n_ego][2] QP deviation x (u = clip(x + u0)) */
+    double* viol;        /* [n_ego] max_i (a_i.x - b_i), clipped at 0, over the final QP's rows */
+} cbf_diag;
+
+/*
+ * get_safe_control (cbf.py:18-92) for a batch of independent egos with explicit
+ * neighbour lists (CSR): ego i's neighbours are obs_states[nbr_off[i] .. nbr_off[i+1]).
+ * robot_state [n][4], u0 [n][2], obs_states [M][4], u [n][2], status [n], x_out [n][2] (nullable).
+ * An ego with zero neighbours still solves the 8-row box QP and is clipped.
+ */
+int cbf_get_safe_control_batch(const cbf_params* p, int32_t n_ego, const double* robot_state, const double* u0,
+                               const int32_t* nbr_off, const double* obs_states, double* u, int32_t* status,
+                               double* x_out, void* stream);
+
+/* The (A, b) of cbf.py:72-80 per ego: rows [nbr_off[i] + 8 i, nbr_off[i+1] + 8 (i+1)) of
+ * A [M + 8n][2] and b [M + 8n]: the ego's barrier rows in list order, then the 8 box rows. */
+int cbf_assemble_rows(const cbf_params* p, int32_t n_ego, const double* robot_state, const double* u0,
+                      const int32_t* nbr_off, const double* obs_states, double* A, double* b, void* stream);
+
+/*
+ * The per-agent loop of cross_and_rescue.py:135-160 over a swarm of n entities:
+ * entities [0, n_obs) are obstacles, [n_obs, n) agents.  Egos are [ego_begin, ego_end)
+ * (agents).  Ego e's state is (pos[e], vel[e]) and its nominal control is vel[e] (:133,155).
+ * Neighbours: every obstacle with |dp|^2 < cull_t, every agent with 0 < |dp|^2 < cull_t.
+ * Outputs are indexed e - ego_begin: u [n_ego][2] (= vel[e] unclipped if no neighbour),
+ * status [n_ego], nbr_count [n_ego] (nullable).
+ * _allpairs tests every entity (LDS-tiled); _cells uses a uniform cell list (grid below).
+ */
+int cbf_filter_allpairs(const cbf_params* p, int32_t n, int32_t n_obs, const double* pos, const double* vel,
+                        int32_t ego_begin, int32_t ego_end, double* u, int32_t* status, int32_t* nbr_count,
+                        const cbf_diag* diag, void* stream);
+
+/* Uniform cell grid: cell (cx, cy) = clamp(floor((p - origin) * inv_h), 0, n-1).  The cell
+ * edge 1/inv_h must be >= the cull radius (checked).  Clamping keeps results exact for
+ * entities outside the grid (only speed suffers). */
+typedef struct cbf_grid {
+    double x0, y0;  /* origin */
+    double inv_h;   /* 1 / cell edge */
+    int32_t nx, ny; /* cells per axis */
+} cbf_grid;
+
+size_t cbf_cells_workspace_size(int32_t n, const cbf_grid* grid);
+
+int cbf_filter_cells(const cbf_params* p, const cbf_grid* grid, int32_t n, int32_t n_obs, const double* pos,
+                     const double* vel, int32_t ego_begin, int32_t ego_end, double* u, int32_t* status,
+                     int32_t* nbr_count, const cbf_diag* diag, void* workspace, size_t workspace_bytes,
+                     void* stream);
+
+/*
+ * Graph-Laplacian nominal control (cross_and_rescue.py:108-125, meet_at_center.py:86-103):
+ *   out[k] = ( (sum_{t in row k} (src[col[t]] - src[self_offset + k])) [@ R] ) * scale
+ * sum sequential from +0.0 in CSR order; R = [[rc, rs], [-rs, rc]] applied as the reference's
+ * row-vector product when rotate != 0.  col[t] >= n_group addresses anchors[col[t] - n_group]
+ * (the goal column of cross_and_rescue.py:102).  src [n_group][2], out [n_dst][2].
+ */
+int cbf_consensus_csr(int32_t n_dst, int32_t self_offset, int32_t n_group, const double* src, const double* anchors,
+                      const int32_t* row_ptr, const int32_t* col, int32_t rotate, double rc, double rs,
+                      double scale, double* out, void* stream);
+
+/* 4-neighbour lattice Laplacian of a W x H lattice (ascending-index neighbour order),
+ * rows [row_begin, row_end); pos holds lattice rows [pos_row0, ...) so that agent (r, c) is
+ * pos[(r - pos_row0) W + c] (rows row_begin-1 .. row_end must be present where they exist);
+ * out[(r - row_begin) W + c] = scale * sum. */
+int cbf_consensus_lattice(int32_t W, int32_t H, int32_t row_begin, int32_t row_end, int32_t pos_row0,
+                          const double* pos, double scale, double* out, void* stream);
+
+/* pos <- pos + T * vel over n entities (cross_and_rescue.py:173). */
+int cbf_euler(int32_t n, double* pos, const double* vel, double T, void* stream);
+
+/*
+ * One full timestep of a lattice swarm (SURVEY cfg3/cfg4): nominal control by the lattice
+ * Laplacian (scale gain), cell-list cull, barrier assembly, exact QP, clip and Euler, for the
+ * agents of rows [row_begin, row_end) of a W x H lattice (cross_and_rescue.py:97-175 shape).
+ * pos holds rows [win_row0, win_row0 + win_rows) (a halo window when sharded; the window must
+ * contain the owned rows plus one lattice row on each side where it exists).  Only owned rows
+ * are written (index (r - row_begin) W + c): pos_out = p + T u (may alias pos only when the
+ * window is exactly the owned rows), vel_out = nominal control, u = filtered control, status,
+ * nbr_count (nullable).  Window agents whose nominal control cannot be formed (first / last
+ * window row unless it is a lattice edge) are not candidates; callers size the halo so that
+ * they are out of cull range and check it with `extents` (nullable, device double[4]):
+ * {min y, max y} of the new owned positions, {max y over owned rows < row_end - guard_rows,
+ * min y over owned rows >= row_begin + guard_rows}.  solves (nullable, device uint64[1024])
+ * accumulates the number of agent-QP solves (egos with >= 1 neighbour) in slots [16 i], i < 64.
+ *
+ * cbf_lattice_step = cbf_lattice_build (nominal control + cell list) then cbf_lattice_advance
+ * (filter + clip + Euler, the dominant kernel), with the same arguments and workspace.
+ */
+size_t cbf_lattice_workspace_size(int32_t W, int32_t win_rows, const cbf_grid* grid);
+
+int cbf_lattice_step(const cbf_params* p, const cbf_grid* grid, int32_t W, int32_t H, int32_t row_begin,
+                     int32_t row_end, int32_t win_row0, int32_t win_rows, const double* pos, double gain, double T,
+                     double* pos_out, double* vel_out, double* u, int32_t* status, int32_t* nbr_count,
+                     int32_t guard_rows, double* extents, uint64_t* solves, void* workspace, size_t workspace_bytes,
+                     void* stream);
+
+int cbf_lattice_build(const cbf_params* p, const cbf_grid* grid, int32_t W, int32_t H, int32_t row_begin,
+                      int32_t row_end, int32_t win_row0, int32_t win_rows, const double* pos, double gain,
+                      double* vel_out, void* workspace, size_t workspace_bytes, void* stream);
+
+int cbf_lattice_advance(const cbf_params* p, const cbf_grid* grid, int32_t W, int32_t H, int32_t row_begin,
+                        int32_t row_end, int32_t win_row0, int32_t win_rows, const double* pos, double T,
+                        double* pos_out, double* u, int32_t* status, int32_t* nbr_count, int32_t guard_rows,
+                        double* extents, uint64_t* solves, void* workspace, size_t workspace_bytes, void* stream);
+
+/*
+ * Batched Monte-Carlo rendezvous (SURVEY cfg5): n_scen independent scenarios, each with
+ * n_o pursuit obstacles (ring i -> i+1, rotation (rc, rs), scale so) then n_a free agents
+ * (complete-graph consensus, gain ga; only they are filtered), `steps` Euler steps of T.
+ * pos [n_scen][n_o + n_a][2] is updated in place.  counters [n_scen][4] int64 = {filter calls,
+ * relaxed, box-infeasible, relax-cap}; maxviol [n_scen] = max row violation over feasible
+ * solves.  One workgroup runs several scenarios for all steps with the state in LDS.
+ * Requires 1 <= n_o, n_a and n_o + n_a <= 256.
+ */
+int cbf_mc_rollout(const cbf_params* p, int32_t n_scen, int32_t n_o, int32_t n_a, int32_t steps, double T, double rc,
+                   double rs, double so, double ga, double* pos, int64_t* counters, double* maxviol, void* stream);
+
+/* ABI version of the loaded library (== CBF_ABI_VERSION). */
+int cbf_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* CBF_AMD_H */

@@ -1,0 +1,104 @@
+"""C-ABI library: loads, exports every symbol include/cbf_amd.h declares, host-side parameter
+setup matches the oracle, and argument validation rejects bad calls before any launch.
+CPU only (no compute calls)."""
+import ctypes as C
+import os
+import re
+
+import numpy as np
+import pytest
+
+from oracle import pyoracle as po
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _declared():
+    src = open(os.path.join(ROOT, "include", "cbf_amd.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"^\s*(?:int|size_t)\s+(cbf_\w+)\s*\(", src, flags=re.M)))
+
+
+def test_library_loads_and_exports_every_declared_symbol():
+    from cbf_amd import _lib
+    names = _declared()
+    assert len(names) >= 14
+    for n in names:
+        assert hasattr(_lib.lib, n), n
+        assert n in _lib.SIGNATURES, n
+    assert set(_lib.SIGNATURES) == set(names)
+    assert _lib.lib.cbf_abi_version() == 1
+
+
+def test_library_is_gfx950_code_object():
+    from cbf_amd import _lib
+    data = open(_lib.LIB_PATH, "rb").read()
+    assert b"gfx950" in data
+
+
+@pytest.mark.parametrize("k", [1, 2, 0.5, 3])
+def test_params_init_matches_oracle(k):
+    from cbf_amd import _lib
+    rng = np.random.default_rng(int(k * 10))
+    for trial in range(20):
+        g = None if trial == 0 else rng.normal(0, 0.3, (4, 2))
+        f = None if trial < 10 else rng.normal(0, 0.1, (4, 4))
+        d = float(rng.choice([0.2, 0.12, 0.3]))
+        cp = _lib.make_params(15, 0.2, k, f, g, d)
+        pp = po.Params(15, 0.2, k, f=f, g=g, safety_distance=d)
+        assert cp.cull_t == pp.cull_t
+        assert cp.gamma == 0.5 and cp.relax_cap == 1 << 16
+        assert cp.f_is_zero == (1 if f is None else 0)
+        for q in range(4):
+            assert tuple(cp.nrm[q]) == po.quadrant_normal(pp, q)
+    cp = _lib.make_params(15)
+    assert cp.cull_t == 0.04 and list(cp.g) == [0.1, 0, 0, 0.1, 0, 0, 0, 0]
+
+
+def test_argument_validation_without_launch():
+    from cbf_amd import _lib
+    L = _lib.lib
+    cp = _lib.make_params(15)
+    null = None
+    # n_obs > n
+    assert L.cbf_filter_allpairs(cp, 4, 5, 1, 1, 5, 4, 1, 1, null, null, null) == _lib.CBF_EINVAL
+    # ego range outside the agents
+    assert L.cbf_filter_allpairs(cp, 10, 5, 1, 1, 2, 10, 1, 1, null, null, null) == _lib.CBF_EINVAL
+    # cell edge below the cull radius
+    g = _lib.CbfGrid(); g.x0 = g.y0 = 0.0; g.inv_h = 10.0; g.nx = g.ny = 4
+    assert L.cbf_filter_cells(cp, C.byref(g), 8, 0, 1, 1, 0, 8, 1, 1, null, null, 1, 1 << 20,
+                              null) == _lib.CBF_EINVAL
+    # lattice window missing the neighbour row
+    g.inv_h = 4.0
+    assert L.cbf_lattice_step(cp, C.byref(g), 8, 8, 2, 4, 2, 2, 1, 0.25, 0.1, 1, 1, 1, 1, null, 0, null, null, 1,
+                              1 << 24, null) == _lib.CBF_EINVAL
+    # mc: too many entities per scenario
+    assert L.cbf_mc_rollout(cp, 4, 200, 100, 1, 0.1, 1.0, 0.0, 1.0, 1.0, 1, 1, 1, null) == _lib.CBF_EINVAL
+    # zero-size calls are no-ops
+    assert L.cbf_euler(0, null, null, 0.1, null) == 0
+    assert L.cbf_get_safe_control_batch(cp, 0, null, null, null, null, null, null, null, null) == 0
+
+
+def test_workspace_sizes():
+    from cbf_amd import _lib, swarm
+    g = swarm.make_grid(-1, -1, 150, 150, 0.204)
+    n = 1 << 20
+    ws = _lib.lib.cbf_lattice_workspace_size(1024, 1024, C.byref(g))
+    cells = _lib.lib.cbf_cells_workspace_size(n, C.byref(g))
+    assert cells > 60 * n and ws > cells
+    assert ws < 200 * n   # stays well inside 288 GB HBM even at 1e9 agents / 8 GPUs
+
+
+def test_product_path_has_no_cpu_fallback():
+    """The package never imports the oracle, and compute calls refuse to run without a GPU."""
+    import cbf_amd
+    pkg = os.path.dirname(cbf_amd.__file__)
+    for fn in os.listdir(pkg):
+        if fn.endswith(".py"):
+            txt = open(os.path.join(pkg, fn)).read()
+            assert "oracle" not in re.sub(r'""".*?"""|#.*', "", txt, flags=re.S), fn
+    import torch
+    if not torch.cuda.is_available():
+        with pytest.raises(cbf_amd.CbfError):
+            cbf_amd.ControlBarrierFunction(15).get_safe_control(np.zeros(4), np.zeros((1, 4)), np.zeros((4, 4)),
+                                                                0.1 * np.eye(4, 2), [0.0, 0.0])
