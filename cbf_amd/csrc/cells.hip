@@ -40,7 +40,7 @@ __global__ void __launch_bounds__(kBlock) k_tile_reduce(const int32_t* __restric
 
 // Exclusive scan: each tile adds the sum of all previous tiles (summed redundantly per block:
 // a few hundred ints) to its own block-local scan.
-__global__ void __launch_bounds__(kBlock) k_tile_scan(const int32_t* __restrict__ count, long ncell,
+__global__ void __launch_bounds__(kBlock) k_tile_scan(int32_t* __restrict__ count, long ncell,
                                                       const int32_t* __restrict__ tilesum,
                                                       int32_t* __restrict__ start) {
     __shared__ int red[kBlock / 64];
@@ -58,6 +58,10 @@ __global__ void __launch_bounds__(kBlock) k_tile_scan(const int32_t* __restrict_
         c[k] = (base + k < ncell) ? count[base + k] : 0;
         tot += c[k];
     }
+    // leave the counts zeroed for the next build (no memset node needed in a captured step)
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+        if (base + k < ncell) count[base + k] = 0;
     // inclusive wave scan of thread totals
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     int inc = tot;
@@ -108,8 +112,6 @@ int scan_and_scatter(const CellGrid& G, const CellWs& W, int n, const double2* p
 
 int build_cells(const CellGrid& G, const CellWs& W, int n, const double2* pos, const double2* vel, const int32_t*,
                 hipStream_t s) {
-    hipError_t e = hipMemsetAsync(W.count, 0, sizeof(int32_t) * W.ncell, s);
-    if (e != hipSuccess) return (int)e;
     hipLaunchKernelGGL(k_bin, dim3(nblk(n)), dim3(kBlock), 0, s, G, n, pos, W.count, W.cs);
     return scan_and_scatter(G, W, n, pos, vel, s);
 }

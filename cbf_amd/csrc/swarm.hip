@@ -332,8 +332,6 @@ extern "C" int cbf_lattice_build(const cbf_params* p, const cbf_grid* grid, int3
     const long n = (long)W * win_rows;
     const CellGrid G = make_grid(grid);
     CellWs Wk(workspace, n, (long)G.nx * G.ny);
-    hipError_t e = hipMemsetAsync(Wk.count, 0, sizeof(int32_t) * Wk.ncell, s);
-    if (e != hipSuccess) return (int)e;
     const double2* p2 = reinterpret_cast<const double2*>(pos);
     hipLaunchKernelGGL(k_lattice_nominal_bin, dim3(nblk(n)), dim3(kBlock), 0, s, G, W, H, row_begin, row_end, win_row0,
                        win_rows, p2, gain, Wk.wvel, reinterpret_cast<double2*>(vel_out), Wk.count, Wk.cs,
@@ -349,7 +347,6 @@ extern "C" int cbf_lattice_advance(const cbf_params* p, const cbf_grid* grid, in
     int rc = check_lattice(p, grid, W, H, row_begin, row_end, win_row0, win_rows, pos, workspace, workspace_bytes);
     if (rc) return rc;
     if (!pos_out || !u || !status) return CBF_EINVAL;
-    if (pos_out == pos && (win_row0 != row_begin || win_rows != row_end - row_begin)) return CBF_EINVAL;
     hipStream_t s = (hipStream_t)stream;
     const long n = (long)W * win_rows;
     const CellGrid G = make_grid(grid);

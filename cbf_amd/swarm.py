@@ -54,6 +54,9 @@ def filter_swarm(params, pos, vel, n_obs, ego_begin=None, ego_end=None, method="
     eb = n_obs if ego_begin is None else ego_begin
     ee = n if ego_end is None else ego_end
     ne = ee - eb
+    if not (0 <= n_obs <= eb <= ee <= n):
+        raise _lib.CbfError(f"filter_swarm: need 0 <= n_obs <= ego_begin <= ego_end <= n, got "
+                            f"{n_obs}, {eb}, {ee}, {n}")
     dev = pos.device
     pos = pos.contiguous()
     vel = vel.contiguous()
@@ -91,7 +94,7 @@ def filter_swarm(params, pos, vel, n_obs, ego_begin=None, ego_end=None, method="
                                    else math.sqrt(cp.cull_t))
         need = lib.cbf_cells_workspace_size(n, _lib.C.byref(grid))
         if workspace is None or workspace.numel() < need:
-            workspace = torch.empty((need,), dtype=torch.uint8, device=dev)
+            workspace = torch.zeros((need,), dtype=torch.uint8, device=dev)
         check(lib.cbf_filter_cells(cp, _lib.C.byref(grid), n, n_obs, ptr(pos), ptr(vel), eb, ee, ptr(out["u"]),
                                    ptr(out["status"]), ptr(out["nbr_count"]), Dp, ptr(workspace), need,
                                    stream_handle()), "cbf_filter_cells")

@@ -113,6 +113,8 @@ typedef struct cbf_grid {
     int32_t nx, ny; /* cells per axis */
 } cbf_grid;
 
+/* Workspaces (cells and lattice) must be zero-filled before their first use; every call leaves
+ * them zero-filled again, so one workspace can be reused by any sequence of calls on a stream. */
 size_t cbf_cells_workspace_size(int32_t n, const cbf_grid* grid);
 
 int cbf_filter_cells(const cbf_params* p, const cbf_grid* grid, int32_t n, int32_t n_obs, const double* pos,
@@ -147,8 +149,8 @@ int cbf_euler(int32_t n, double* pos, const double* vel, double T, void* stream)
  * agents of rows [row_begin, row_end) of a W x H lattice (cross_and_rescue.py:97-175 shape).
  * pos holds rows [win_row0, win_row0 + win_rows) (a halo window when sharded; the window must
  * contain the owned rows plus one lattice row on each side where it exists).  Only owned rows
- * are written (index (r - row_begin) W + c): pos_out = p + T u (may alias pos only when the
- * window is exactly the owned rows), vel_out = nominal control, u = filtered control, status,
+ * are written (index (r - row_begin) W + c): pos_out = p + T u (may alias or overlap pos: the
+ * advance phase reads only cell-sorted copies), vel_out = nominal control, u = filtered control, status,
  * nbr_count (nullable).  Window agents whose nominal control cannot be formed (first / last
  * window row unless it is a lattice edge) are not candidates; callers size the halo so that
  * they are out of cull range and check it with `extents` (nullable, device double[4]):
