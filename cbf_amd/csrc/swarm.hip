@@ -260,7 +260,35 @@ __global__ void __launch_bounds__(kBlock) k_extents_finalize(int nparts, const d
     }
 }
 
+__global__ void k_halo_guard(const double* __restrict__ E, long stride, int ws, int rank, double radius,
+                             int32_t* __restrict__ flag) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    const double rm = radius * (1.0 + 1e-9) + 1e-12;
+    const double* me = E + (long)rank * stride;
+    const double ymin = me[0], ymax = me[1];
+    int bad = 0;
+    for (int q = 0; q < ws; ++q) {
+        const double* o = E + (long)q * stride;
+        if (q < rank) {  // rows below: rank-1's rows outside our halo, everything of lower ranks
+            const double lim = (q == rank - 1) ? o[2] : o[1];
+            if (!(ymin - lim > rm)) bad = 1;
+        } else if (q > rank) {
+            const double lim = (q == rank + 1) ? o[3] : o[0];
+            if (!(lim - ymax > rm)) bad = 1;
+        }
+    }
+    if (bad) flag[0] |= 1;
+}
+
 }  // namespace
+
+extern "C" int cbf_halo_guard(const double* ext_all, int64_t stride, int32_t world_size, int32_t rank, double radius,
+                              int32_t* flag, void* stream) {
+    if (!ext_all || !flag || world_size < 1 || rank < 0 || rank >= world_size || stride < 4) return CBF_EINVAL;
+    hipLaunchKernelGGL(k_halo_guard, dim3(1), dim3(64), 0, (hipStream_t)stream, ext_all, (long)stride, world_size,
+                       rank, radius, flag);
+    return (int)hipGetLastError();
+}
 
 extern "C" int cbf_consensus_csr(int32_t n_dst, int32_t self_offset, int32_t n_group, const double* src,
                                  const double* anchors, const int32_t* row_ptr, const int32_t* col, int32_t rotate,

@@ -179,6 +179,16 @@ int cbf_lattice_advance(const cbf_params* p, const cbf_grid* grid, int32_t W, in
                         double* extents, uint64_t* solves, void* workspace, size_t workspace_bytes, void* stream);
 
 /*
+ * Halo guard of the row-sharded lattice step.  ext_all holds world_size records of 4 doubles
+ * (record q at ext_all + q * stride) as produced by cbf_lattice_step's `extents` with
+ * guard_rows = halo - 1.  Sets *flag |= 1 (device int32) unless every agent outside rank's
+ * candidate rows is farther than `radius` (in y) from every agent rank owns, i.e. unless the
+ * halo exchange provably contained every neighbour.  One lane; stream-ordered.
+ */
+int cbf_halo_guard(const double* ext_all, int64_t stride, int32_t world_size, int32_t rank, double radius,
+                   int32_t* flag, void* stream);
+
+/*
  * Batched Monte-Carlo rendezvous (SURVEY cfg5): n_scen independent scenarios, each with
  * n_o pursuit obstacles (ring i -> i+1, rotation (rc, rs), scale so) then n_a free agents
  * (complete-graph consensus, gain ga; only they are filtered), `steps` Euler steps of T.

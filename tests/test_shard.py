@@ -1,0 +1,119 @@
+"""Row-stripe sharding (cbf_amd/shard.py) on CPU with the gloo backend, world_size 2 and 3.
+The device work is done by an oracle backend (test infrastructure), so this checks the
+exchange / window / guard logic: the sharded rollout must equal the single-lattice oracle
+rollout bit for bit."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from cbf_amd import scenarios
+from cbf_amd.shard import ShardedLattice, guard_ok, stripe_extents
+from oracle import coracle, pyoracle as po
+
+
+class OracleBackend:
+    def __init__(self, W, H, gain, T, radius):
+        self.W, self.H, self.gain, self.T, self.radius = W, H, gain, T, radius
+        self.p = po.Params(15)
+        self.flag = 0
+
+    def tensor(self, a):
+        return torch.as_tensor(np.ascontiguousarray(a)).clone()
+
+    def lattice_step(self, S, ext_out):
+        W, H = self.W, self.H
+        full = np.zeros((W * H, 2))
+        full[S.w0 * W:S.w1 * W] = S.wpos.numpy()
+        lo = S.w0 if S.w0 == 0 else S.w0 + 1
+        hi = S.w1 if S.w1 == H else S.w1 - 1
+        vel = coracle.consensus_lattice(W, H, lo, hi, full, self.gain)
+        cand = full[lo * W:hi * W]
+        eb, ee = (S.rb - lo) * W, (S.re - lo) * W
+        out = coracle.filter_swarm(self.p, cand, vel, 0, eb, ee)
+        new = coracle.euler(cand[eb:ee], out["u"], self.T)
+        S.own.copy_(torch.as_tensor(new))
+        S.vel.copy_(torch.as_tensor(vel[eb:ee])); S.u.copy_(torch.as_tensor(out["u"]))
+        S.status.copy_(torch.as_tensor(out["status"])); S.nbr_count.copy_(torch.as_tensor(out["cnt"]))
+        ext_out.copy_(torch.as_tensor(stripe_extents(new, W, S.halo - 1)))
+        S.solves[0] += int((out["cnt"] > 0).sum())
+
+    def guard(self, recv_ext, stride, ws, rank):
+        ext = np.stack([recv_ext[q * stride:q * stride + 4].numpy() for q in range(ws)])
+        if not guard_ok(ext, rank, self.radius):
+            self.flag = 1
+
+    def guard_failed(self):
+        return bool(self.flag)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _worker(rank, ws, port, W, R, steps, halo, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=ws)
+    H = R * ws
+    be = OracleBackend(W, H, scenarios.LATTICE_GAIN, scenarios.T, 0.2)
+    S = ShardedLattice(W, R, seed=2, halo=halo, backend=be)
+    for _ in range(steps):
+        S.step()
+    S.check_guard()
+    q.put((rank, S.own.numpy().copy(), S.u.numpy().copy(), S.status.numpy().copy(), int(S.solves[0])))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("ws", [2, 3])
+def test_sharded_rollout_equals_single_lattice(ws):
+    W, R, steps, halo = 20, 8, 4, 4
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, ws, port, W, R, steps, halo, q)) for r in range(ws)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=300) for _ in range(ws)], key=lambda t: t[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    H = R * ws
+    pos = scenarios.lattice(W, H, seed=2)
+    p = po.Params(15)
+    solves = 0
+    for _ in range(steps):
+        vel = coracle.consensus_lattice(W, H, 0, H, pos, scenarios.LATTICE_GAIN)
+        out = coracle.filter_swarm(p, pos, vel, 0)
+        solves += int((out["cnt"] > 0).sum())
+        pos = coracle.euler(pos, out["u"], scenarios.T)
+    got = np.concatenate([r[1] for r in res])
+    assert np.array_equal(got, pos)
+    assert np.array_equal(np.concatenate([r[2] for r in res]), out["u"])
+    assert np.array_equal(np.concatenate([r[3] for r in res]), out["status"])
+    assert sum(r[4] for r in res) == solves
+
+
+def test_guard_logic():
+    W, halo = 10, 4
+    a = scenarios.LATTICE_SPACING
+    pos = scenarios.lattice(W, 30, seed=0)
+    ext = np.stack([stripe_extents(pos[r * 10 * W:(r + 1) * 10 * W], W, halo - 1) for r in range(3)])
+    for r in range(3):
+        assert guard_ok(ext, r, 0.2)
+    bad = ext.copy()
+    bad[0, 2] = ext[1, 0] - 0.1            # rank 0's non-halo rows reach into rank 1's range
+    assert not guard_ok(bad, 1, 0.2)
+    assert guard_ok(bad, 2, 0.2)
+    bad = ext.copy()
+    bad[2, 0] = ext[0, 1] + 0.05           # rank 2 reaches down to rank 0
+    assert not guard_ok(bad, 0, 0.2)
+    assert a * (halo - 2) > 0.2            # default halo leaves slack for the jittered lattice
