@@ -161,8 +161,108 @@ def bench_lattice(args, ws, rank, local):
     return res
 
 
+def bench_allpairs(args, ws, rank, local):
+    """cfg3: N = width x rows jittered lattice, every pair tested (FP64-VALU bound); replicas for N > 1."""
+    import torch
+    from cbf_amd import scenarios, swarm
+    W, H = args.width, args.rows
+    L = swarm.LatticeSwarm(scenarios.lattice(W, H, seed=args.seed + rank), W, H, gain=scenarios.LATTICE_GAIN,
+                           method="allpairs")
+    L.capture()
+    for _ in range(args.warmup):
+        L.step()
+    L.reset_solves()
+    if ws > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        L.step()
+    torch.cuda.synchronize()
+    if ws > 1:
+        torch.distributed.barrier()
+    elapsed = time.perf_counter() - t0
+    solves = int(L.solves[0].item())
+    elapsed, solves = _reduce(elapsed, solves, ws)
+    n = W * H
+    pairs = float(n) * n * args.steps * ws / elapsed
+    return {"metric": METRIC, "value": solves / elapsed, "unit": "agent-QP solves/s", "n_gpus": ws,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
+            "config": {"workload": f"cfg3: {W}x{H} jittered lattice, all-pairs cull (every pair tested)",
+                       "agents_per_gpu": n, "parallelism": "replicas" if ws > 1 else "single GPU"},
+            "timesteps_per_s": args.steps / elapsed, "pair_tests_per_s": pairs,
+            "roofline": {"bound": "valu-fp64", "achieved": pairs * 6 / 1e12, "peak": 78.6, "unit": "TFLOP/s",
+                         "frac": pairs * 6 / 1e12 / 78.6, "traffic": None,
+                         "note": "6 fp64 ops per pair test (2 sub, 2 mul, 1 add, 1 cmp) vs the MI355X FP64 vector "
+                                 "peak (spec, FMA counted as 2)"}}
+
+
+def bench_mc(args, ws, rank, local):
+    """cfg5: batched Monte-Carlo rendezvous, scenarios sharded across ranks (strong scaling),
+    counters combined with one all_reduce at the end."""
+    import torch
+    from cbf_amd import scenarios, swarm
+    n_o = n_a = 16
+    per = (args.mc_scenarios + ws - 1) // ws
+    lo = rank * per
+    hi = min(args.mc_scenarios, lo + per)
+    pos0 = scenarios.mc_scenarios(args.mc_scenarios, n_o, n_a, seed=args.seed)[lo:hi]
+    P = torch.tensor(pos0, device="cuda")
+    fp = swarm.FilterParams()
+    for _ in range(args.warmup):
+        swarm.mc_rollout(fp, P, n_o, n_a, args.mc_inner, ga=scenarios.MC_GAIN)
+    if ws > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    tot = torch.zeros(4, dtype=torch.int64, device="cuda")
+    mv = torch.zeros(1, dtype=torch.float64, device="cuda")
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        cnt, m = swarm.mc_rollout(fp, P, n_o, n_a, args.mc_inner, ga=scenarios.MC_GAIN)
+        tot += cnt.sum(0)
+        mv = torch.maximum(mv, m.max().reshape(1))
+    torch.cuda.synchronize()
+    if ws > 1:
+        torch.distributed.barrier()
+    elapsed = time.perf_counter() - t0
+    if ws > 1:
+        torch.distributed.all_reduce(tot)
+        torch.distributed.all_reduce(mv, op=torch.distributed.ReduceOp.MAX)
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        elapsed = float(t[0])
+    c = tot.cpu().numpy()
+    return {"metric": METRIC, "value": c[0] / elapsed, "unit": "agent-QP solves/s", "n_gpus": ws,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
+            "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f64",
+            "data": "synthetic",
+            "config": {"workload": f"cfg5: {args.mc_scenarios} independent 16+16 rendezvous scenarios, "
+                                   f"{args.mc_inner} timesteps per step, scenario-sharded",
+                       "parallelism": f"scenario shards x{ws}" if ws > 1 else "single GPU"},
+            "scenario_timesteps_per_s": args.mc_scenarios * args.mc_inner * args.steps / elapsed,
+            "relaxed_fraction": c[1] / max(c[0], 1), "box_infeasible": int(c[2]), "relax_cap": int(c[3]),
+            "max_violation": float(mv.item()),
+            "roofline": {"bound": "valu-fp64", "achieved": None, "peak": 78.6, "unit": "TFLOP/s", "frac": None,
+                         "traffic": None, "note": "state lives in LDS for the whole rollout; no HBM traffic per step"}}
+
+
+def _reduce(elapsed, solves, ws):
+    if ws == 1:
+        return elapsed, solves
+    import torch
+    t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+    s = torch.tensor([solves], dtype=torch.int64, device="cuda")
+    torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+    torch.distributed.all_reduce(s)
+    return float(t[0]), int(s[0])
+
+
 def main():
     ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="cfg4", choices=["cfg4", "cfg3", "cfg5"])
+    ap.add_argument("--mc-scenarios", type=int, default=100000)
+    ap.add_argument("--mc-inner", type=int, default=10, help="cfg5: timesteps per bench step")
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
@@ -182,9 +282,16 @@ def main():
         torch.distributed.init_process_group("nccl", device_id=torch.device("cuda", local))
     else:
         torch.cuda.set_device(0)
-    res = bench_lattice(args, ws, rank, local)
+    if args.config == "cfg3":
+        if args.rows == 1024 and args.width == 1024:
+            args.width = args.rows = 256
+        res = bench_allpairs(args, ws, rank, local)
+    elif args.config == "cfg5":
+        res = bench_mc(args, ws, rank, local)
+    else:
+        res = bench_lattice(args, ws, rank, local)
     if rank == 0:
-        if ws == 1 and not args.no_cpu_baseline:
+        if ws == 1 and not args.no_cpu_baseline and args.config == "cfg4":
             res["cpu_baseline"] = cpu_baseline_lattice(args.width, args.rows, args.seed, args.cpu_budget)
         else:
             res["cpu_baseline"] = None

@@ -81,6 +81,9 @@ __device__ __forceinline__ void ego_init(const KP& P, Ego& E, double px, double 
 }
 
 // Barrier row rhs for neighbour o (cbf.py:38-59); q = sign quadrant (cbf.py:47-53, -0.0 -> +1).
+// FZ: compile-time "f == 0" (the callers' dynamics, cross_and_rescue.py:31) -> L_f = 0 with f
+// never read; otherwise the runtime flag decides.
+template <bool FZ = false>
 __device__ __forceinline__ double row_b(const KP& P, const Ego& E, double o0, double o1, double o2, double o3,
                                         int& q) {
     const double d0 = E.r0 - o0, d1 = E.r1 - o1, d2 = E.r2 - o2, d3 = E.r3 - o3;
@@ -89,7 +92,7 @@ __device__ __forceinline__ double row_b(const KP& P, const Ego& E, double o0, do
     const double ksx = P.k * sx, ksy = P.k * sy;
     const double H = fma(ksy, d3, fma(ksx, d2, fma(sy, d1, sx * d0)));
     double Lf = 0.0;
-    if (!P.f_zero) {
+    if (!FZ && !P.f_zero) {
         double fd[4];
 #pragma unroll
         for (int i = 0; i < 4; ++i)
@@ -101,9 +104,10 @@ __device__ __forceinline__ double row_b(const KP& P, const Ego& E, double o0, do
     return (P.gamma * (H - P.dmin) + Lf) + c;
 }
 
+template <bool FZ = false>
 __device__ __forceinline__ void ego_add(const KP& P, Ego& E, double o0, double o1, double o2, double o3) {
     int q;
-    const double b = row_b(P, E, o0, o1, o2, o3, q);
+    const double b = row_b<FZ>(P, E, o0, o1, o2, o3, q);
     E.bq0 = (q == 0 && b < E.bq0) ? b : E.bq0;
     E.bq1 = (q == 1 && b < E.bq1) ? b : E.bq1;
     E.bq2 = (q == 2 && b < E.bq2) ? b : E.bq2;
@@ -111,6 +115,27 @@ __device__ __forceinline__ void ego_add(const KP& P, Ego& E, double o0, double o
     E.present |= 1u << q;
     E.count++;
 }
+
+// Per-lane list of cull hits in LDS (column per lane: conflict-free), flushed into the ego's QP.
+constexpr int kHitCap = 16;
+struct HitList {
+    int n = 0;
+    // returns true when full (caller flushes)
+    __device__ __forceinline__ bool push(int* lds, int t) {
+        lds[n * kBlock + threadIdx.x] = t;
+        return ++n == kHitCap;
+    }
+    template <bool FZ = false>
+    __device__ __forceinline__ void flush(const int* lds, const KP& P, Ego& E, const double2* __restrict__ pos,
+                                          const double2* __restrict__ vel) {
+        for (int i = 0; i < n; ++i) {
+            const int t = lds[i * kBlock + threadIdx.x];
+            const double2 pj = pos[t], vj = vel[t];
+            ego_add<FZ>(P, E, pj.x, pj.y, vj.x, vj.y);
+        }
+        n = 0;
+    }
+};
 
 // Cull test (cross_and_rescue.py:141-150): sqrt(s) < d <=> s < cull_t; agents also need s > 0.
 __device__ __forceinline__ bool cull_keep(const KP& P, double r0, double r1, double p0, double p1, bool is_obstacle,
@@ -157,21 +182,37 @@ __device__ __forceinline__ int solve8(const double (&a0)[8], const double (&a1)[
         const double t = b[h] / n2;
         const double p0 = t * a0[h], p1 = t * a1[h];
         const double d0 = -a1[h], d1 = a0[h];
-        double lo = -INFINITY, hi = INFINITY;
+        // 1-D interval on the line: upper bounds r/ad (ad > 0), lower bounds r/ad (ad < 0),
+        // compared by cross-multiplication; only the binding bound is divided out.
+        double rh = 0.0, ah = 0.0, rl = 0.0, al = 0.0;
+        bool has_hi = false, has_lo = false;
 #pragma unroll
         for (int j = 0; j < h; ++j) {
             if (!((mask >> j) & 1u)) continue;
             const double ad = a0[j] * d0 + a1[j] * d1;
             const double r = b[j] - (a0[j] * p0 + a1[j] * p1);
-            const double qv = r / ad;
-            if (ad > 0)
-                hi = pmin(hi, qv);
-            else if (ad < 0)
-                lo = pmax(lo, qv);
+            if (ad > 0) {
+                if (!has_hi || r * ah < rh * ad) {
+                    rh = r;
+                    ah = ad;
+                }
+                has_hi = true;
+            } else if (ad < 0) {
+                if (!has_lo || r * al > rl * ad) {
+                    rl = r;
+                    al = ad;
+                }
+                has_lo = true;
+            }
         }
         double s = 0.0;
-        if (s > hi) s = hi;
-        if (s < lo) s = lo;
+        bool s_hi = false;
+        if (has_hi && rh < 0) {  // hi = rh/ah < 0
+            s = rh / ah;
+            s_hi = true;
+        }
+        if (has_lo && (s_hi ? (rh * al > rl * ah) : (rl < 0)))  // s < lo = rl/al
+            s = rl / al;
         x0 = p0 + s * d0;
         x1 = p1 + s * d1;
         bool ok = true;
@@ -205,12 +246,43 @@ __device__ __forceinline__ Sol solve_ego(const KP& P, const Ego& E) {
     S.status = CBF_STATUS_OPTIMAL;
     S.iters = 0;
     S.x0 = S.x1 = 0.0;
+    // Strip pre-check: quadrants q and 3-q have exactly opposite normals (negation is exact in
+    // IEEE), so both rows can hold within tolerance only if b_q + b_{3-q} >= -(tb_q + tb_{3-q}).
+    // While that is violated by a clear margin the exact solve below is certain to fail at a CBF
+    // plane, so skip it and apply the +1 relaxation directly -- same iterates, same result as
+    // solving at every count (the oracle does; tests check bit-equality).
+    if ((E.present & 9u) == 9u || (E.present & 6u) == 6u) {
+        for (;;) {
+            bool dead = false;
+            if ((E.present & 9u) == 9u) {
+                const double s = b[4] + b[7];
+                const double tb = FEAS_TOL * (pmax(1.0, fabs(b[4])) + pmax(1.0, fabs(b[7])));
+                dead = dead || (s < -tb - 1e-9 * (1.0 + fabs(b[4]) + fabs(b[7])));
+            }
+            if ((E.present & 6u) == 6u) {
+                const double s = b[5] + b[6];
+                const double tb = FEAS_TOL * (pmax(1.0, fabs(b[5])) + pmax(1.0, fabs(b[6])));
+                dead = dead || (s < -tb - 1e-9 * (1.0 + fabs(b[5]) + fabs(b[6])));
+            }
+            if (!dead || S.iters >= P.relax_cap) break;
+            b[4] = b[4] + 1.0;
+            b[5] = b[5] + 1.0;
+            b[6] = b[6] + 1.0;
+            b[7] = b[7] + 1.0;
+            S.iters++;
+        }
+    }
     for (;;) {
         const int fail = solve8(a0, a1, b, mask, S.x0, S.x1);
         if (fail < 0) break;
-        if (fail < 4) {
+        if (fail < 4) {  // reported as at the first solve: no relaxation applied
             S.status = CBF_STATUS_BOX_INFEASIBLE;
+            S.iters = 0;
             S.x0 = S.x1 = 0.0;
+            b[4] = E.bq0;
+            b[5] = E.bq1;
+            b[6] = E.bq2;
+            b[7] = E.bq3;
             break;
         }
         if (S.iters >= P.relax_cap) {
@@ -223,8 +295,8 @@ __device__ __forceinline__ Sol solve_ego(const KP& P, const Ego& E) {
         b[6] = b[6] + 1.0;
         b[7] = b[7] + 1.0;
         S.iters++;
-        S.status = CBF_STATUS_RELAXED;
     }
+    if (S.status == CBF_STATUS_OPTIMAL && S.iters > 0) S.status = CBF_STATUS_RELAXED;
     double v = 0.0;
 #pragma unroll
     for (int h = 0; h < 8; ++h)

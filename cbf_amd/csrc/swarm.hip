@@ -105,13 +105,13 @@ __global__ void __launch_bounds__(kBlock) k_lattice_nominal_bin(CellGrid G, int 
         cs[w] = make_int2(-1, 0);
         return;
     }
+    const double2 p = pos[w];
+    const int cell = cell_coord(p.y, G.y0, G.inv_h, G.ny) * G.nx + cell_coord(p.x, G.x0, G.inv_h, G.nx);
+    const int slot = atomicAdd(&count[cell], 1);  // issued first: its return latency hides under the sum
     const double2 a = lattice_sum(pos, w, r, c, W, H);
     const double2 u0 = make_double2(a.x * gain, a.y * gain);
     wvel[w] = u0;
-    if (r >= row_begin && r < row_end) vel_out[(long)(r - row_begin) * W + c] = u0;
-    const double2 p = pos[w];
-    const int cell = cell_coord(p.y, G.y0, G.inv_h, G.ny) * G.nx + cell_coord(p.x, G.x0, G.inv_h, G.nx);
-    const int slot = atomicAdd(&count[cell], 1);
+    if (vel_out != wvel && r >= row_begin && r < row_end) vel_out[(long)(r - row_begin) * W + c] = u0;
     cs[w] = make_int2(cell, slot);
 }
 
@@ -125,6 +125,7 @@ __device__ __forceinline__ double wave_max(double v) {
 }
 
 // Lattice step K4: filter + clip + Euler for the owned agents, lane = cell-sorted slot.
+template <bool FZ>
 __global__ void __launch_bounds__(kBlock) k_lattice_filter(KP P, CellGrid G, int W, int row_begin, int row_end,
                                                            int win_row0, long ncell, const double2* __restrict__ spos,
                                                            const double2* __restrict__ svel,
@@ -134,6 +135,7 @@ __global__ void __launch_bounds__(kBlock) k_lattice_filter(KP P, CellGrid G, int
                                                            int32_t* __restrict__ status, int32_t* __restrict__ cnt,
                                                            int guard_rows, double* __restrict__ ext_part,
                                                            unsigned long long* __restrict__ solves) {
+    __shared__ int hit_lds[kHitCap * kBlock];
     const int slot = blockIdx.x * kBlock + threadIdx.x;
     bool solved = false;
     const int total = start[ncell];
@@ -153,6 +155,10 @@ __global__ void __launch_bounds__(kBlock) k_lattice_filter(KP P, CellGrid G, int
             const int cy = cell_coord(pe.y, G.y0, G.inv_h, G.ny);
             const int xa = cx > 0 ? cx - 1 : 0;
             const int xb = cx < G.nx - 1 ? cx + 1 : G.nx - 1;
+            // pass 1: cheap cull test over the 3x3 cells, hits compacted into a per-lane LDS list;
+            // pass 2: row assembly only for hits (keeps divergent lanes from paying assembly for
+            // every candidate iteration of the wave)
+            HitList H;
             for (int dy = -1; dy <= 1; ++dy) {
                 const int yy = cy + dy;
                 if (yy < 0 || yy >= G.ny) continue;
@@ -162,10 +168,10 @@ __global__ void __launch_bounds__(kBlock) k_lattice_filter(KP P, CellGrid G, int
                     const double e0 = pj.x - E.r0, e1 = pj.y - E.r1;
                     const double s = e0 * e0 + e1 * e1;
                     if (!(s < P.cull_t && s > 0)) continue;
-                    const double2 vj = svel[t];
-                    ego_add(P, E, pj.x, pj.y, vj.x, vj.y);
+                    if (H.push(hit_lds, t)) H.template flush<FZ>(hit_lds, P, E, spos, svel);
                 }
             }
+            H.template flush<FZ>(hit_lds, P, E, spos, svel);
             const long k = (long)(r - row_begin) * W + c;
             double ux, uy;
             int32_t st;
@@ -361,10 +367,13 @@ extern "C" int cbf_lattice_build(const cbf_params* p, const cbf_grid* grid, int3
     const CellGrid G = make_grid(grid);
     CellWs Wk(workspace, n, (long)G.nx * G.ny);
     const double2* p2 = reinterpret_cast<const double2*>(pos);
+    // unsharded: the window is the owned rows, so the nominal controls go straight to vel_out
+    double2* wv = (win_row0 == row_begin && win_rows == row_end - row_begin) ? reinterpret_cast<double2*>(vel_out)
+                                                                              : Wk.wvel;
     hipLaunchKernelGGL(k_lattice_nominal_bin, dim3(nblk(n)), dim3(kBlock), 0, s, G, W, H, row_begin, row_end, win_row0,
-                       win_rows, p2, gain, Wk.wvel, reinterpret_cast<double2*>(vel_out), Wk.count, Wk.cs,
+                       win_rows, p2, gain, wv, reinterpret_cast<double2*>(vel_out), Wk.count, Wk.cs,
                        (unsigned long long*)nullptr);
-    return scan_and_scatter(G, Wk, (int)n, p2, Wk.wvel, s);
+    return scan_and_scatter(G, Wk, (int)n, p2, wv, s);
 }
 
 extern "C" int cbf_lattice_advance(const cbf_params* p, const cbf_grid* grid, int32_t W, int32_t H,
@@ -381,7 +390,8 @@ extern "C" int cbf_lattice_advance(const cbf_params* p, const cbf_grid* grid, in
     CellWs Wk(workspace, n, (long)G.nx * G.ny);
     double* ext_part = extents ? (double*)((char*)workspace + CellWs::bytes(n, Wk.ncell)) : nullptr;
     const int nb = nblk(n);
-    hipLaunchKernelGGL(k_lattice_filter, dim3(nb), dim3(kBlock), 0, s, make_kp(p), G, W, row_begin, row_end, win_row0,
+    hipLaunchKernelGGL(p->f_is_zero ? k_lattice_filter<true> : k_lattice_filter<false>, dim3(nb), dim3(kBlock), 0, s,
+                       make_kp(p), G, W, row_begin, row_end, win_row0,
                        Wk.ncell, Wk.spos, Wk.svel, Wk.sidx, Wk.start, T, reinterpret_cast<double2*>(pos_out),
                        reinterpret_cast<double2*>(u), status, nbr_count, guard_rows, ext_part,
                        reinterpret_cast<unsigned long long*>(solves));

@@ -188,11 +188,13 @@ class LatticeSwarm:
     cbf_lattice_step (nominal + cell list + filter + clip + Euler); optionally captured in a
     hipGraph.  Single-GPU: the window is the whole lattice."""
 
-    def __init__(self, pos, W, H, gain=0.25, params: FilterParams = None, T=1 / 30, grid=None, margin=1.0):
+    def __init__(self, pos, W, H, gain=0.25, params: FilterParams = None, T=1 / 30, grid=None, margin=1.0,
+                 method="cells"):
         torch = _lib.require_gpu()
         self.dev = torch.device("cuda")
         pos = np.asarray(pos, dtype=np.float64).reshape(W * H, 2)
         self.W, self.H, self.gain, self.T = W, H, float(gain), float(T)
+        self.method = method  # "cells" (fused cbf_lattice_step) or "allpairs" (cfg3: every pair tested)
         self.params = params or FilterParams()
         self.cp = self.params.c()
         self.grid = grid or grid_for_points(pos, self.params.safety_distance, margin=margin)
@@ -209,6 +211,14 @@ class LatticeSwarm:
         self.graph = None
 
     def _launch(self):
+        if self.method == "allpairs":
+            consensus_lattice(self.pos, self.W, self.H, self.gain, out=self.vel)
+            check(lib.cbf_filter_allpairs(self.cp, self.n, 0, ptr(self.pos), ptr(self.vel), 0, self.n, ptr(self.u),
+                                          ptr(self.status), ptr(self.nbr_count), None, stream_handle()),
+                  "cbf_filter_allpairs")
+            euler(self.pos, self.u, self.T)
+            self.solves[0] += (self.nbr_count > 0).sum()
+            return
         check(lib.cbf_lattice_step(self.cp, _lib.C.byref(self.grid), self.W, self.H, 0, self.H, 0, self.H,
                                    ptr(self.pos), self.gain, self.T, ptr(self.pos), ptr(self.vel), ptr(self.u),
                                    ptr(self.status), ptr(self.nbr_count), 0, None, ptr(self.solves), ptr(self.ws),

@@ -117,19 +117,35 @@ static int solve_planes(const planes_t* P, double* x0o, double* x1o) {
         double t = b / n2;
         double p0 = t * a0, p1 = t * a1;
         double d0 = -a1, d1 = a0;
-        double lo = -INFINITY, hi = INFINITY;
+        /* interval of t on the line: bounds r/ad compared by cross-multiplication, only the
+         * binding one divided out */
+        double rh = 0.0, ah = 0.0, rl = 0.0, al = 0.0;
+        int has_hi = 0, has_lo = 0;
         for (int j = 0; j < h; ++j) {
             double c0 = P->a0[j], c1 = P->a1[j], e = P->b[j];
             double ad = c0 * d0 + c1 * d1;
             double r = e - (c0 * p0 + c1 * p1);
-            if (ad > 0)
-                hi = py_min(hi, r / ad);
-            else if (ad < 0)
-                lo = py_max(lo, r / ad);
+            if (ad > 0) {
+                if (!has_hi || r * ah < rh * ad) {
+                    rh = r;
+                    ah = ad;
+                }
+                has_hi = 1;
+            } else if (ad < 0) {
+                if (!has_lo || r * al > rl * ad) {
+                    rl = r;
+                    al = ad;
+                }
+                has_lo = 1;
+            }
         }
         double s = 0.0;
-        if (s > hi) s = hi;
-        if (s < lo) s = lo;
+        int s_hi = 0;
+        if (has_hi && rh < 0) {
+            s = rh / ah;
+            s_hi = 1;
+        }
+        if (has_lo && (s_hi ? (rh * al > rl * ah) : (rl < 0))) s = rl / al;
         x0 = p0 + s * d0;
         x1 = p1 + s * d1;
         for (int j = 0; j <= h; ++j)

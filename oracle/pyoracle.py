@@ -175,21 +175,26 @@ def solve_halfplanes(planes):
         p1 = t * a1
         d0 = -a1
         d1 = a0
-        lo = -math.inf
-        hi = math.inf
+        # interval of s on the line: bounds r/ad compared by cross-multiplication,
+        # only the binding one divided out
+        hi = lo = None              # (r, ad) of the binding upper / lower bound
         for j in range(h):
             c0, c1, e = planes[j]
             ad = c0 * d0 + c1 * d1
             r = e - (c0 * p0 + c1 * p1)
             if ad > 0:
-                hi = _py_min(hi, r / ad)
+                if hi is None or r * hi[1] < hi[0] * ad:
+                    hi = (r, ad)
             elif ad < 0:
-                lo = _py_max(lo, r / ad)
+                if lo is None or r * lo[1] > lo[0] * ad:
+                    lo = (r, ad)
         s = 0.0
-        if s > hi:
-            s = hi
-        if s < lo:
-            s = lo
+        s_hi = False
+        if hi is not None and hi[0] < 0:
+            s = hi[0] / hi[1]
+            s_hi = True
+        if lo is not None and ((hi[0] * lo[1] > lo[0] * hi[1]) if s_hi else (lo[0] < 0)):
+            s = lo[0] / lo[1]
         x0 = p0 + s * d0
         x1 = p1 + s * d1
         for j in range(h + 1):
