@@ -15,6 +15,12 @@
 
 #include "cbf_amd.h"
 
+// Ablation builds only (tools/ablate.py): 1 = skip the QP, 2 = also skip row assembly,
+// 3 = also skip the candidate scan.  The shipped library is built with 0.
+#ifndef CBF_ABLATE
+#define CBF_ABLATE 0
+#endif
+
 namespace cbf {
 
 constexpr double FEAS_TOL = 1e-12;
@@ -116,15 +122,16 @@ __device__ __forceinline__ void ego_add(const KP& P, Ego& E, double o0, double o
     E.count++;
 }
 
-// Per-lane list of cull hits in LDS (column per lane: conflict-free), flushed into the ego's QP.
+// Per-lane list of cull hits in LDS (column per lane: conflict-free), flushed into the ego's QP
+// after the scan.  More than kHitCap hits -> the caller rescans with direct assembly.
 constexpr int kHitCap = 16;
 struct HitList {
     int n = 0;
-    // returns true when full (caller flushes)
-    __device__ __forceinline__ bool push(int* lds, int t) {
-        lds[n * kBlock + threadIdx.x] = t;
-        return ++n == kHitCap;
+    __device__ __forceinline__ void push(int* lds, int t) {
+        if (n < kHitCap) lds[n * kBlock + threadIdx.x] = t;
+        ++n;
     }
+    __device__ __forceinline__ bool overflowed() const { return n > kHitCap; }
     template <bool FZ = false>
     __device__ __forceinline__ void flush(const int* lds, const KP& P, Ego& E, const double2* __restrict__ pos,
                                           const double2* __restrict__ vel) {
@@ -136,6 +143,45 @@ struct HitList {
         n = 0;
     }
 };
+
+// Cull test over cell-sorted candidate slots [t0, t1) for an agent ego (0 < s < cull_t),
+// 4 candidates' loads in flight per lane.
+__device__ __forceinline__ void scan_range(int t0, int t1, const KP& P, const Ego& E, HitList& H, int* lds,
+                                           const double2* __restrict__ spos) {
+    int t = t0;
+    for (; t + 4 <= t1; t += 4) {
+        double2 p[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) p[u] = spos[t + u];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const double e0 = p[u].x - E.r0, e1 = p[u].y - E.r1;
+            const double s = e0 * e0 + e1 * e1;
+            if (s < P.cull_t && s > 0) H.push(lds, t + u);
+        }
+    }
+    for (; t < t1; ++t) {
+        const double2 pj = spos[t];
+        const double e0 = pj.x - E.r0, e1 = pj.y - E.r1;
+        const double s = e0 * e0 + e1 * e1;
+        if (s < P.cull_t && s > 0) H.push(lds, t);
+    }
+}
+
+// Direct (uncompacted) cull + assembly over [t0, t1): the overflow path.
+template <bool FZ = false>
+__device__ __forceinline__ void scan_range_direct(int t0, int t1, const KP& P, Ego& E,
+                                                  const double2* __restrict__ spos,
+                                                  const double2* __restrict__ svel) {
+    for (int t = t0; t < t1; ++t) {
+        const double2 pj = spos[t];
+        const double e0 = pj.x - E.r0, e1 = pj.y - E.r1;
+        const double s = e0 * e0 + e1 * e1;
+        if (!(s < P.cull_t && s > 0)) continue;
+        const double2 vj = svel[t];
+        ego_add<FZ>(P, E, pj.x, pj.y, vj.x, vj.y);
+    }
+}
 
 // Cull test (cross_and_rescue.py:141-150): sqrt(s) < d <=> s < cull_t; agents also need s > 0.
 __device__ __forceinline__ bool cull_keep(const KP& P, double r0, double r1, double p0, double p1, bool is_obstacle,

@@ -158,20 +158,30 @@ __global__ void __launch_bounds__(kBlock) k_lattice_filter(KP P, CellGrid G, int
             // pass 1: cheap cull test over the 3x3 cells, hits compacted into a per-lane LDS list;
             // pass 2: row assembly only for hits (keeps divergent lanes from paying assembly for
             // every candidate iteration of the wave)
-            HitList H;
-            for (int dy = -1; dy <= 1; ++dy) {
-                const int yy = cy + dy;
-                if (yy < 0 || yy >= G.ny) continue;
-                const int t0 = start[yy * G.nx + xa], t1 = start[yy * G.nx + xb + 1];
-                for (int t = t0; t < t1; ++t) {
-                    const double2 pj = spos[t];
-                    const double e0 = pj.x - E.r0, e1 = pj.y - E.r1;
-                    const double s = e0 * e0 + e1 * e1;
-                    if (!(s < P.cull_t && s > 0)) continue;
-                    if (H.push(hit_lds, t)) H.template flush<FZ>(hit_lds, P, E, spos, svel);
-                }
+            int rt0[3], rt1[3];
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+                const int yy = cy + k - 1;
+                const bool in = yy >= 0 && yy < G.ny;
+                rt0[k] = in ? start[yy * G.nx + xa] : 0;
+                rt1[k] = in ? start[yy * G.nx + xb + 1] : 0;
             }
-            H.template flush<FZ>(hit_lds, P, E, spos, svel);
+#if CBF_ABLATE < 3
+            HitList H;
+#pragma unroll
+            for (int k = 0; k < 3; ++k) scan_range(rt0[k], rt1[k], P, E, H, hit_lds, spos);
+#if CBF_ABLATE < 2
+            if (!H.overflowed()) {
+                H.template flush<FZ>(hit_lds, P, E, spos, svel);
+            } else {
+#pragma unroll
+                for (int k = 0; k < 3; ++k) scan_range_direct<FZ>(rt0[k], rt1[k], P, E, spos, svel);
+            }
+#else
+            E.count = H.n;
+            asm volatile("" ::"v"(E.count));
+#endif
+#endif
             const long k = (long)(r - row_begin) * W + c;
             double ux, uy;
             int32_t st;
@@ -180,7 +190,16 @@ __global__ void __launch_bounds__(kBlock) k_lattice_filter(KP P, CellGrid G, int
                 uy = E.u0y;
                 st = CBF_STATUS_IDLE;
             } else {
+#if CBF_ABLATE >= 1
+                Sol S;
+                S.x0 = S.x1 = 0.0;
+                S.status = CBF_STATUS_OPTIMAL;
+                S.iters = 0;
+                S.viol = E.bq0 + E.bq1 + E.bq2 + E.bq3;
+                asm volatile("" ::"v"(S.viol));
+#else
                 const Sol S = solve_ego(P, E);
+#endif
                 clip_u(P, S, E, ux, uy);
                 st = pack_status(S);
             }

@@ -1,0 +1,103 @@
+"""A/B harness for the lattice step kernels: builds variants of libcbf_amd.so with compile-time
+switches and times cbf_lattice_build / cbf_lattice_advance of each, interleaved in one process
+(HIP events on the launch stream).
+
+  python tools/ablate.py build            # in the build container (hipcc)
+  python tools/ablate.py run [--rounds R] # on the GPU box
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes as C
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+OUT = os.path.join(ROOT, "tools", "_ablate")
+VARIANTS = {
+    "full": [],
+    "no_qp": ["-DCBF_ABLATE=1"],
+    "no_qp_no_rows": ["-DCBF_ABLATE=2"],
+    "no_scan": ["-DCBF_ABLATE=3"],
+}
+
+
+def build():
+    from cbf_amd import build as B
+    os.makedirs(OUT, exist_ok=True)
+    for name, defs in VARIANTS.items():
+        objs = []
+        for src in B.SOURCES:
+            o = os.path.join(OUT, f"{name}_{os.path.splitext(src)[0]}.o")
+            lang = ["-x", "hip"] if src.endswith(".hip") else []
+            subprocess.run([B.HIPCC] + B.FLAGS + defs + lang + ["-c", os.path.join(B.CSRC, src), "-o", o], check=True)
+            objs.append(o)
+        subprocess.run([B.HIPCC, "-shared", f"--offload-arch={B.ARCH}", "-o", os.path.join(OUT, f"lib_{name}.so")]
+                       + objs, check=True)
+        print("built", name)
+
+
+def run(rounds, iters, W, H):
+    import numpy as np
+    import torch
+    from cbf_amd import _lib, scenarios, swarm
+    torch.cuda.set_device(0)
+    libs = {}
+    for name in VARIANTS:
+        L = C.CDLL(os.path.join(OUT, f"lib_{name}.so"))
+        for fn, (res, args) in _lib.SIGNATURES.items():
+            getattr(L, fn).restype = res
+            getattr(L, fn).argtypes = args
+        libs[name] = L
+    pos0 = scenarios.lattice(W, H, seed=0)
+    grid = swarm.grid_for_points(pos0, 0.2)
+    cp = _lib.make_params(15)
+    ws_bytes = _lib.lib.cbf_lattice_workspace_size(W, H, C.byref(grid))
+    st = {}
+    for name in VARIANTS:
+        st[name] = dict(pos=torch.tensor(pos0, device="cuda"), vel=torch.empty((W * H, 2), dtype=torch.float64,
+                                                                                device="cuda"),
+                        u=torch.empty((W * H, 2), dtype=torch.float64, device="cuda"),
+                        status=torch.empty(W * H, dtype=torch.int32, device="cuda"),
+                        cnt=torch.empty(W * H, dtype=torch.int32, device="cuda"),
+                        ws=torch.zeros(ws_bytes, dtype=torch.uint8, device="cuda"))
+    P = _lib.ptr
+    times = {n: {"build": [], "advance": []} for n in VARIANTS}
+    for r in range(rounds):
+        for name, L in libs.items():
+            s = st[name]
+            for _ in range(iters):
+                e0, e1, e2 = (torch.cuda.Event(enable_timing=True) for _ in range(3))
+                e0.record()
+                _lib.check(L.cbf_lattice_build(cp, C.byref(grid), W, H, 0, H, 0, H, P(s["pos"]), 0.25, P(s["vel"]),
+                                               P(s["ws"]), ws_bytes, _lib.stream_handle()), "build")
+                e1.record()
+                _lib.check(L.cbf_lattice_advance(cp, C.byref(grid), W, H, 0, H, 0, H, P(s["pos"]), 1 / 30,
+                                                 P(s["pos"]), P(s["u"]), P(s["status"]), P(s["cnt"]), 0, None, None,
+                                                 P(s["ws"]), ws_bytes, _lib.stream_handle()), "advance")
+                e2.record()
+                torch.cuda.synchronize()
+                if r > 0:
+                    times[name]["build"].append(e0.elapsed_time(e1))
+                    times[name]["advance"].append(e1.elapsed_time(e2))
+    res = {n: {k: {"median_us": float(np.median(v)) * 1e3, "min_us": float(np.min(v)) * 1e3}
+               for k, v in t.items()} for n, t in times.items()}
+    print(json.dumps(res, indent=1))
+    return res
+
+
+if __name__ == "__main__":
+    ap = argparse.ArgumentParser()
+    ap.add_argument("cmd", choices=["build", "run"])
+    ap.add_argument("--rounds", type=int, default=6)
+    ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--W", type=int, default=1024)
+    ap.add_argument("--H", type=int, default=1024)
+    a = ap.parse_args()
+    if a.cmd == "build":
+        build()
+    else:
+        run(a.rounds, a.iters, a.W, a.H)
