@@ -26,13 +26,8 @@ __device__ __forceinline__ int block_sum(int v, int* red) {
     return t;  // valid in thread 0
 }
 
-__device__ __forceinline__ bool gate_closed(const int32_t* gate) {
-    return gate && !(gate[0] == 0 || gate[1] != 0);
-}
-
 __global__ void __launch_bounds__(kBlock) k_tile_reduce(const int32_t* __restrict__ count, long ncell,
-                                                        int32_t* __restrict__ tilesum, const int32_t* gate) {
-    if (gate_closed(gate)) return;
+                                                        int32_t* __restrict__ tilesum) {
     __shared__ int red[kBlock / 64];
     const long base = (long)blockIdx.x * kScanTile + threadIdx.x * 8;
     int v = 0;
@@ -47,8 +42,7 @@ __global__ void __launch_bounds__(kBlock) k_tile_reduce(const int32_t* __restric
 // a few hundred ints) to its own block-local scan.
 __global__ void __launch_bounds__(kBlock) k_tile_scan(int32_t* __restrict__ count, long ncell,
                                                       const int32_t* __restrict__ tilesum,
-                                                      int32_t* __restrict__ start, const int32_t* gate) {
-    if (gate_closed(gate)) return;
+                                                      int32_t* __restrict__ start) {
     __shared__ int red[kBlock / 64];
     __shared__ int wtot[kBlock / 64];
     __shared__ int s_off;
@@ -107,14 +101,10 @@ inline int nblk(long n) { return (int)((n + kBlock - 1) / kBlock); }
 
 }  // namespace
 
-void launch_scan(const CellWs& W, const int32_t* gate, hipStream_t s) {
-    hipLaunchKernelGGL(k_tile_reduce, dim3(W.ntiles), dim3(kBlock), 0, s, W.count, W.ncell, W.tilesum, gate);
-    hipLaunchKernelGGL(k_tile_scan, dim3(W.ntiles), dim3(kBlock), 0, s, W.count, W.ncell, W.tilesum, W.start, gate);
-}
-
 int scan_and_scatter(const CellGrid& G, const CellWs& W, int n, const double2* pos, const double2* vel,
                      hipStream_t s) {
-    launch_scan(W, nullptr, s);
+    hipLaunchKernelGGL(k_tile_reduce, dim3(W.ntiles), dim3(kBlock), 0, s, W.count, W.ncell, W.tilesum);
+    hipLaunchKernelGGL(k_tile_scan, dim3(W.ntiles), dim3(kBlock), 0, s, W.count, W.ncell, W.tilesum, W.start);
     hipLaunchKernelGGL(k_scatter, dim3(nblk(n)), dim3(kBlock), 0, s, n, W.cs, W.start, pos, vel, W.spos, W.svel,
                        W.sidx);
     return (int)hipGetLastError();

@@ -41,17 +41,14 @@ struct CellWs {
     double2* svel;    // [n] cell-sorted velocities / nominal controls
     int32_t* sidx;    // [n] entity index of each sorted slot
     double2* wvel;    // [n] scratch velocities (lattice step: nominal of window agents)
-    double2* bpos;    // [n] positions at the last rebuild, per sorted slot (lattice step skin)
-    int32_t* slot_of; // [n] sorted slot of each window agent (lattice step)
-    int32_t* state;   // [8] lattice step: [0] list valid, [1] drift beyond the skin this step
+    unsigned long long* ext;  // [4] extents keys (lattice step)
     long ncell;
     int ntiles;
 
     static int tiles(long ncell) { return (int)((ncell + kScanTile - 1) / kScanTile); }
     static size_t bytes(long n, long ncell) {
         return align256(4 * ncell) + align256(4 * (ncell + 1)) + align256(4 * (size_t)tiles(ncell)) +
-               align256(8 * n) + 2 * align256(16 * n) + align256(4 * n) + align256(16 * n) + align256(16 * n) +
-               align256(4 * n) + 256;
+               align256(8 * n) + 2 * align256(16 * n) + align256(4 * n) + align256(16 * n) + 256;
     }
     CellWs(void* base, long n, long nc) : ncell(nc), ntiles(tiles(nc)) {
         char* p = (char*)base;
@@ -71,17 +68,9 @@ struct CellWs {
         p += align256(4 * n);
         wvel = (double2*)p;
         p += align256(16 * n);
-        bpos = (double2*)p;
-        p += align256(16 * n);
-        slot_of = (int32_t*)p;
-        p += align256(4 * n);
-        state = (int32_t*)p;
+        ext = (unsigned long long*)p;
     }
 };
-
-// Scan kernels, optionally gated: they do nothing unless gate == nullptr or gate[0] == 0 or
-// gate[1] != 0 (the lattice step's "list invalid / drift beyond skin" condition).
-void launch_scan(const CellWs& W, const int32_t* gate, hipStream_t s);
 
 // Full build from positions: memset counts, bin, scan, scatter (vel copied alongside).
 // When `skip_bin` is set the caller already binned (count / cs filled by its own kernel).

@@ -82,96 +82,37 @@ __global__ void __launch_bounds__(kBlock) k_euler(int n, double2* __restrict__ p
     pos[i] = make_double2(p.x + T * v.x, p.y + T * v.y);
 }
 
-// The lattice step keeps its cell list in the workspace between calls ("skin" list): it is
-// rebuilt only when some candidate has drifted more than `skin` (per axis) from where it was
-// binned.  With cell edge h >= r + 2 skin, any pair within the cull radius r now was within
-// r + 2 skin < h per axis at binning time, so the 3x3 stencil around the ego's binning cell
-// still holds every neighbour: the candidate set, and every result, are exact.
-struct LatticeCfg {
-    int W, H, row_begin, row_end, win_row0, win_rows;
-};
-
-__device__ __forceinline__ bool lattice_computable(const LatticeCfg& L, int r) {
-    return (r == 0 || r - 1 >= L.win_row0) && (r == L.H - 1 || r + 1 < L.win_row0 + L.win_rows);
-}
-
-// state[2..7] = signature of the configuration the list was built for
-__device__ __forceinline__ bool same_config(const int32_t* st, const LatticeCfg& L, const CellGrid& G) {
-    return st[2] == L.W && st[3] == L.win_row0 && st[4] == L.win_rows && st[5] == L.H && st[6] == G.nx &&
-           st[7] == G.ny;
-}
-
-__device__ __forceinline__ bool gate_open(const int32_t* st) { return st[0] == 0 || st[1] != 0; }
-
-// Lattice step K1 (every step): nominal control of every computable window agent (lattice
-// neighbours all in the window), written in agent order (vel_out for owned agents) and gathered,
-// with the current position, into the agent's cell-sorted slot; drift beyond the skin flags a
-// rebuild of the list for this very step.
-__global__ void __launch_bounds__(kBlock) k_lattice_nominal_gather(LatticeCfg L, CellGrid G, double skin,
-                                                                   const double2* __restrict__ pos, double gain,
-                                                                   double2* __restrict__ wvel,
-                                                                   double2* __restrict__ vel_out,
-                                                                   const int32_t* __restrict__ slot_of,
-                                                                   const double2* __restrict__ bpos,
-                                                                   double2* __restrict__ spos,
-                                                                   double2* __restrict__ svel, int32_t* state) {
+// Lattice step K1: nominal control of every window agent whose lattice neighbours are all in the
+// window, + cell binning of those agents.  Owned agents also get vel_out.
+__global__ void __launch_bounds__(kBlock) k_lattice_nominal_bin(CellGrid G, int W, int H, int row_begin, int row_end,
+                                                                int win_row0, int win_rows,
+                                                                const double2* __restrict__ pos, double gain,
+                                                                double2* __restrict__ wvel,
+                                                                double2* __restrict__ vel_out,
+                                                                int32_t* __restrict__ count, int2* __restrict__ cs,
+                                                                unsigned long long* __restrict__ ext) {
     const long w = (long)blockIdx.x * kBlock + threadIdx.x;
-    if (w >= (long)L.win_rows * L.W) return;
-    const int r = L.win_row0 + (int)(w / L.W), c = (int)(w % L.W);
-    if (!lattice_computable(L, r)) return;
-    const double2 p = pos[w];
-    const double2 a = lattice_sum(pos, w, r, c, L.W, L.H);
-    const double2 u0 = make_double2(a.x * gain, a.y * gain);
-    wvel[w] = u0;
-    if (vel_out != wvel && r >= L.row_begin && r < L.row_end) vel_out[(long)(r - L.row_begin) * L.W + c] = u0;
-    if (state[0] == 0 || !same_config(state, L, G)) {
-        if (state[1] == 0) state[1] = 1;  // benign race: every writer stores 1
-        return;
+    if (w == 0 && ext) {
+        ext[0] = dkey(INFINITY);
+        ext[1] = dkey(-INFINITY);
+        ext[2] = dkey(-INFINITY);
+        ext[3] = dkey(INFINITY);
     }
-    const int t = slot_of[w];
-    const double2 b = bpos[t];
-    if (fabs(p.x - b.x) > skin || fabs(p.y - b.y) > skin) state[1] = 1;
-    spos[t] = p;
-    svel[t] = u0;
-}
-
-// Rebuild (only when the gate is open): bin, scan, scatter.
-__global__ void __launch_bounds__(kBlock) k_lattice_rebin(LatticeCfg L, CellGrid G, const double2* __restrict__ pos,
-                                                          int32_t* __restrict__ count, int2* __restrict__ cs,
-                                                          const int32_t* state) {
-    if (!gate_open(state)) return;
-    const long w = (long)blockIdx.x * kBlock + threadIdx.x;
-    if (w >= (long)L.win_rows * L.W) return;
-    const int r = L.win_row0 + (int)(w / L.W);
-    if (!lattice_computable(L, r)) {
+    if (w >= (long)win_rows * W) return;
+    const int r = win_row0 + (int)(w / W), c = (int)(w % W);
+    const bool ok = (r == 0 || r - 1 >= win_row0) && (r == H - 1 || r + 1 < win_row0 + win_rows);
+    if (!ok) {
         cs[w] = make_int2(-1, 0);
         return;
     }
     const double2 p = pos[w];
     const int cell = cell_coord(p.y, G.y0, G.inv_h, G.ny) * G.nx + cell_coord(p.x, G.x0, G.inv_h, G.nx);
-    cs[w] = make_int2(cell, atomicAdd(&count[cell], 1));
-}
-
-__global__ void __launch_bounds__(kBlock) k_lattice_rescatter(LatticeCfg L, const double2* __restrict__ pos,
-                                                              const double2* __restrict__ wvel,
-                                                              const int2* __restrict__ cs,
-                                                              const int32_t* __restrict__ start,
-                                                              int32_t* __restrict__ sidx,
-                                                              int32_t* __restrict__ slot_of,
-                                                              double2* __restrict__ bpos, double2* __restrict__ spos,
-                                                              double2* __restrict__ svel, const int32_t* state) {
-    if (!gate_open(state)) return;
-    const long w = (long)blockIdx.x * kBlock + threadIdx.x;
-    if (w >= (long)L.win_rows * L.W) return;
-    const int2 c = cs[w];
-    if (c.x < 0) return;
-    const int d = start[c.x] + c.y;
-    const double2 p = pos[w];
-    sidx[d] = (int)w;
-    slot_of[w] = d;
-    bpos[d] = p;
-    spos[d] = p;
-    svel[d] = wvel[w];
+    const int slot = atomicAdd(&count[cell], 1);  // issued first: its return latency hides under the sum
+    const double2 a = lattice_sum(pos, w, r, c, W, H);
+    const double2 u0 = make_double2(a.x * gain, a.y * gain);
+    wvel[w] = u0;
+    if (vel_out != wvel && r >= row_begin && r < row_end) vel_out[(long)(r - row_begin) * W + c] = u0;
+    cs[w] = make_int2(cell, slot);
 }
 
 __device__ __forceinline__ double wave_min(double v) {
@@ -193,21 +134,9 @@ __global__ void __launch_bounds__(kBlock) k_lattice_filter(KP P, CellGrid G, int
                                                            double2* __restrict__ pos_out, double2* __restrict__ u,
                                                            int32_t* __restrict__ status, int32_t* __restrict__ cnt,
                                                            int guard_rows, double* __restrict__ ext_part,
-                                                           unsigned long long* __restrict__ solves,
-                                                           const double2* __restrict__ bpos, int32_t* state,
-                                                           LatticeCfg L) {
+                                                           unsigned long long* __restrict__ solves) {
     __shared__ int hit_lds[kHitCap * kBlock];
     const int slot = blockIdx.x * kBlock + threadIdx.x;
-    if (slot == 0) {  // the list (rebuilt or not) is valid for this configuration from here on
-        state[0] = 1;
-        state[1] = 0;
-        state[2] = L.W;
-        state[3] = L.win_row0;
-        state[4] = L.win_rows;
-        state[5] = L.H;
-        state[6] = G.nx;
-        state[7] = G.ny;
-    }
     bool solved = false;
     const int total = start[ncell];
     bool own = false;
@@ -222,9 +151,8 @@ __global__ void __launch_bounds__(kBlock) k_lattice_filter(KP P, CellGrid G, int
             const double2 pe = spos[slot], ve = svel[slot];
             Ego E;
             ego_init(P, E, pe.x, pe.y, ve.x, ve.y, ve.x, ve.y);
-            const double2 be = bpos[slot];  // stencil centred on the cell the ego was binned in
-            const int cx = cell_coord(be.x, G.x0, G.inv_h, G.nx);
-            const int cy = cell_coord(be.y, G.y0, G.inv_h, G.ny);
+            const int cx = cell_coord(pe.x, G.x0, G.inv_h, G.nx);
+            const int cy = cell_coord(pe.y, G.y0, G.inv_h, G.ny);
             const int xa = cx > 0 ? cx - 1 : 0;
             const int xb = cx < G.nx - 1 ? cx + 1 : G.nx - 1;
             // pass 1: cheap cull test over the 3x3 cells, hits compacted into a per-lane LDS list;
@@ -461,18 +389,10 @@ extern "C" int cbf_lattice_build(const cbf_params* p, const cbf_grid* grid, int3
     // unsharded: the window is the owned rows, so the nominal controls go straight to vel_out
     double2* wv = (win_row0 == row_begin && win_rows == row_end - row_begin) ? reinterpret_cast<double2*>(vel_out)
                                                                               : Wk.wvel;
-    const LatticeCfg L{W, H, row_begin, row_end, win_row0, win_rows};
-    const double h = 1.0 / grid->inv_h, r = sqrt(p->cull_t);
-    double skin = 0.5 * (h - r) * (1.0 - 1e-9) - 1e-12;  // h >= r + 2 skin with rounding slack
-    if (!(skin > 0)) skin = -1.0;                         // no slack: rebuild every step
-    const int nb = nblk(n);
-    hipLaunchKernelGGL(k_lattice_nominal_gather, dim3(nb), dim3(kBlock), 0, s, L, G, skin, p2, gain, wv,
-                       reinterpret_cast<double2*>(vel_out), Wk.slot_of, Wk.bpos, Wk.spos, Wk.svel, Wk.state);
-    hipLaunchKernelGGL(k_lattice_rebin, dim3(nb), dim3(kBlock), 0, s, L, G, p2, Wk.count, Wk.cs, Wk.state);
-    launch_scan(Wk, Wk.state, s);
-    hipLaunchKernelGGL(k_lattice_rescatter, dim3(nb), dim3(kBlock), 0, s, L, p2, wv, Wk.cs, Wk.start, Wk.sidx,
-                       Wk.slot_of, Wk.bpos, Wk.spos, Wk.svel, Wk.state);
-    return (int)hipGetLastError();
+    hipLaunchKernelGGL(k_lattice_nominal_bin, dim3(nblk(n)), dim3(kBlock), 0, s, G, W, H, row_begin, row_end, win_row0,
+                       win_rows, p2, gain, wv, reinterpret_cast<double2*>(vel_out), Wk.count, Wk.cs,
+                       (unsigned long long*)nullptr);
+    return scan_and_scatter(G, Wk, (int)n, p2, wv, s);
 }
 
 extern "C" int cbf_lattice_advance(const cbf_params* p, const cbf_grid* grid, int32_t W, int32_t H,
@@ -493,8 +413,7 @@ extern "C" int cbf_lattice_advance(const cbf_params* p, const cbf_grid* grid, in
                        make_kp(p), G, W, row_begin, row_end, win_row0,
                        Wk.ncell, Wk.spos, Wk.svel, Wk.sidx, Wk.start, T, reinterpret_cast<double2*>(pos_out),
                        reinterpret_cast<double2*>(u), status, nbr_count, guard_rows, ext_part,
-                       reinterpret_cast<unsigned long long*>(solves), Wk.bpos, Wk.state,
-                       LatticeCfg{W, H, row_begin, row_end, win_row0, win_rows});
+                       reinterpret_cast<unsigned long long*>(solves));
     if (extents) hipLaunchKernelGGL(k_extents_finalize, dim3(1), dim3(kBlock), 0, s, nb, ext_part, extents);
     return (int)hipGetLastError();
 }

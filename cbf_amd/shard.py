@@ -126,7 +126,7 @@ class ShardedLattice:
         win = pos_global[self.w0 * W:self.w1 * W]
         a = scenarios.LATTICE_SPACING
         grid = make_grid(-1.0 - a, self.w0 * a - 1.0 - a, W * a + 1.0, self.w1 * a + 1.0,
-                         self.params.safety_distance * 1.1)
+                         self.params.safety_distance * 1.02)
         if backend is None:
             backend = HipBackend(W, self.H, gain, T, self.params, grid, self.win_rows)
         self.be = backend

@@ -189,7 +189,6 @@ class LatticeSwarm:
     hipGraph.  Single-GPU: the window is the whole lattice."""
 
     def __init__(self, pos, W, H, gain=0.25, params: FilterParams = None, T=1 / 30, grid=None, margin=1.0,
-                 cell_factor=1.1,
                  method="cells"):
         torch = _lib.require_gpu()
         self.dev = torch.device("cuda")
@@ -198,7 +197,7 @@ class LatticeSwarm:
         self.method = method  # "cells" (fused cbf_lattice_step) or "allpairs" (cfg3: every pair tested)
         self.params = params or FilterParams()
         self.cp = self.params.c()
-        self.grid = grid or grid_for_points(pos, self.params.safety_distance, margin=margin, cell_factor=cell_factor)
+        self.grid = grid or grid_for_points(pos, self.params.safety_distance, margin=margin)
         n = W * H
         self.n = n
         self.pos = torch.tensor(pos, device=self.dev)
