@@ -354,6 +354,57 @@ __device__ __forceinline__ Sol solve_ego(const KP& P, const Ego& E) {
     return S;
 }
 
+// The common case of solve_ego without the Seidel machinery: after the strip pre-relaxation the
+// origin satisfies every plane, so solve8 would return x = 0 at its first call.  Same arithmetic
+// as solve_ego on that path (bit-identical Sol); returns false when the full solve is needed.
+__device__ __forceinline__ bool solve_easy(const KP& P, const Ego& E, Sol& S) {
+    const Box B = box_rhs(P, E);
+    const double a0[8] = {1.0, 0.0, -1.0, 0.0, P.n0[0], P.n0[1], P.n0[2], P.n0[3]};
+    const double a1[8] = {0.0, 1.0, 0.0, -1.0, P.n1[0], P.n1[1], P.n1[2], P.n1[3]};
+    double b[8] = {pmin(B.S[0], B.S[4]), pmin(B.S[1], B.S[6]), pmin(B.S[2], B.S[5]), pmin(B.S[3], B.S[7]),
+                   E.bq0, E.bq1, E.bq2, E.bq3};
+    const unsigned mask = 0xFu | (E.present << 4);
+    int iters = 0;
+    if ((E.present & 9u) == 9u || (E.present & 6u) == 6u) {
+        for (;;) {
+            bool dead = false;
+            if ((E.present & 9u) == 9u) {
+                const double s = b[4] + b[7];
+                const double tb = FEAS_TOL * (pmax(1.0, fabs(b[4])) + pmax(1.0, fabs(b[7])));
+                dead = dead || (s < -tb - 1e-9 * (1.0 + fabs(b[4]) + fabs(b[7])));
+            }
+            if ((E.present & 6u) == 6u) {
+                const double s = b[5] + b[6];
+                const double tb = FEAS_TOL * (pmax(1.0, fabs(b[5])) + pmax(1.0, fabs(b[6])));
+                dead = dead || (s < -tb - 1e-9 * (1.0 + fabs(b[5]) + fabs(b[6])));
+            }
+            if (!dead || iters >= P.relax_cap) break;
+            b[4] = b[4] + 1.0;
+            b[5] = b[5] + 1.0;
+            b[6] = b[6] + 1.0;
+            b[7] = b[7] + 1.0;
+            iters++;
+        }
+    }
+    const double x0 = 0.0, x1 = 0.0;
+    bool ok = true;
+    double v = 0.0;
+#pragma unroll
+    for (int h = 0; h < 8; ++h)
+        if ((mask >> h) & 1u) {
+            const double d = (a0[h] * x0 + a1[h] * x1) - b[h];
+            ok = ok && (d <= FEAS_TOL * pmax(1.0, fabs(b[h])));
+            if (d > v) v = d;
+        }
+    if (!ok) return false;
+    S.x0 = x0;
+    S.x1 = x1;
+    S.iters = iters;
+    S.status = iters > 0 ? CBF_STATUS_RELAXED : CBF_STATUS_OPTIMAL;
+    S.viol = v;
+    return true;
+}
+
 // cbf.py:89-91
 __device__ __forceinline__ void clip_u(const KP& P, const Sol& S, const Ego& E, double& ux, double& uy) {
     ux = pmax(pmin(S.x0 + E.u0x, P.ms), -P.ms);

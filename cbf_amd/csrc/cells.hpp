@@ -13,6 +13,7 @@
 namespace cbf {
 
 constexpr int kScanTile = 2048;  // 256 threads x 8 cells
+constexpr int kHardBlocks = 256; // grid of the hard-QP kernel of the lattice step
 
 struct CellGrid {
     double x0, y0, inv_h;
@@ -41,14 +42,14 @@ struct CellWs {
     double2* svel;    // [n] cell-sorted velocities / nominal controls
     int32_t* sidx;    // [n] entity index of each sorted slot
     double2* wvel;    // [n] scratch velocities (lattice step: nominal of window agents)
-    unsigned long long* ext;  // [4] extents keys (lattice step)
+    int32_t* hardq;   // [1 + n] lattice step: count, then the cell-sorted slots of queued hard QPs
     long ncell;
     int ntiles;
 
     static int tiles(long ncell) { return (int)((ncell + kScanTile - 1) / kScanTile); }
     static size_t bytes(long n, long ncell) {
         return align256(4 * ncell) + align256(4 * (ncell + 1)) + align256(4 * (size_t)tiles(ncell)) +
-               align256(8 * n) + 2 * align256(16 * n) + align256(4 * n) + align256(16 * n) + 256;
+               align256(8 * n) + 2 * align256(16 * n) + align256(4 * n) + align256(16 * n) + align256(4 * (n + 1));
     }
     CellWs(void* base, long n, long nc) : ncell(nc), ntiles(tiles(nc)) {
         char* p = (char*)base;
@@ -68,7 +69,7 @@ struct CellWs {
         p += align256(4 * n);
         wvel = (double2*)p;
         p += align256(16 * n);
-        ext = (unsigned long long*)p;
+        hardq = (int32_t*)p;
     }
 };
 

@@ -90,14 +90,9 @@ __global__ void __launch_bounds__(kBlock) k_lattice_nominal_bin(CellGrid G, int 
                                                                 double2* __restrict__ wvel,
                                                                 double2* __restrict__ vel_out,
                                                                 int32_t* __restrict__ count, int2* __restrict__ cs,
-                                                                unsigned long long* __restrict__ ext) {
+                                                                int32_t* __restrict__ hardq) {
     const long w = (long)blockIdx.x * kBlock + threadIdx.x;
-    if (w == 0 && ext) {
-        ext[0] = dkey(INFINITY);
-        ext[1] = dkey(-INFINITY);
-        ext[2] = dkey(-INFINITY);
-        ext[3] = dkey(INFINITY);
-    }
+    if (w == 0) hardq[0] = 0;  // hard-QP queue of this step's advance phase starts empty
     if (w >= (long)win_rows * W) return;
     const int r = win_row0 + (int)(w / W), c = (int)(w % W);
     const bool ok = (r == 0 || r - 1 >= win_row0) && (r == H - 1 || r + 1 < win_row0 + win_rows);
@@ -124,107 +119,99 @@ __device__ __forceinline__ double wave_max(double v) {
     return v;
 }
 
-// Lattice step K4: filter + clip + Euler for the owned agents, lane = cell-sorted slot.
-template <bool FZ>
-__global__ void __launch_bounds__(kBlock) k_lattice_filter(KP P, CellGrid G, int W, int row_begin, int row_end,
-                                                           int win_row0, long ncell, const double2* __restrict__ spos,
-                                                           const double2* __restrict__ svel,
-                                                           const int32_t* __restrict__ sidx,
-                                                           const int32_t* __restrict__ start, double T,
-                                                           double2* __restrict__ pos_out, double2* __restrict__ u,
-                                                           int32_t* __restrict__ status, int32_t* __restrict__ cnt,
-                                                           int guard_rows, double* __restrict__ ext_part,
-                                                           unsigned long long* __restrict__ solves) {
-    __shared__ int hit_lds[kHitCap * kBlock];
-    const int slot = blockIdx.x * kBlock + threadIdx.x;
-    bool solved = false;
-    const int total = start[ncell];
-    bool own = false;
-    double ny = 0.0;
-    int r = 0;
-    if (slot < total) {
-        const int w = sidx[slot];
-        r = win_row0 + w / W;
-        const int c = w % W;
-        own = r >= row_begin && r < row_end;
-        if (own) {
-            const double2 pe = spos[slot], ve = svel[slot];
-            Ego E;
-            ego_init(P, E, pe.x, pe.y, ve.x, ve.y, ve.x, ve.y);
-            const int cx = cell_coord(pe.x, G.x0, G.inv_h, G.nx);
-            const int cy = cell_coord(pe.y, G.y0, G.inv_h, G.ny);
-            const int xa = cx > 0 ? cx - 1 : 0;
-            const int xb = cx < G.nx - 1 ? cx + 1 : G.nx - 1;
-            // pass 1: cheap cull test over the 3x3 cells, hits compacted into a per-lane LDS list;
-            // pass 2: row assembly only for hits (keeps divergent lanes from paying assembly for
-            // every candidate iteration of the wave)
-            int rt0[3], rt1[3];
+// Lattice step K4: filter + clip + Euler for one owned agent at cell-sorted slot `slot`.
+// FULL = false: QPs that the origin does not solve (after the strip pre-relaxation) are not
+// solved here but appended to the hard queue -- one such lane would otherwise make its whole
+// wave run the Seidel path.  FULL = true: the second kernel solves the queued egos.
+// Returns 0 (not an owned agent), 1 (done: outputs written, *ny = new y), 2 (queued).
+template <bool FZ, bool FULL>
+__device__ __forceinline__ int lattice_ego(const KP& P, const CellGrid& G, int W, int row_begin, int row_end,
+                                           int win_row0, int slot, const double2* __restrict__ spos,
+                                           const double2* __restrict__ svel, const int32_t* __restrict__ sidx,
+                                           const int32_t* __restrict__ start, double T, double2* __restrict__ pos_out,
+                                           double2* __restrict__ u, int32_t* __restrict__ status,
+                                           int32_t* __restrict__ cnt, int32_t* __restrict__ hardq, int* hit_lds,
+                                           double* ny, int* row, int* nbrs) {
+    const int w = sidx[slot];
+    const int r = win_row0 + w / W;
+    const int c = w % W;
+    *row = r;
+    if (!(r >= row_begin && r < row_end)) return 0;
+    const double2 pe = spos[slot], ve = svel[slot];
+    Ego E;
+    ego_init(P, E, pe.x, pe.y, ve.x, ve.y, ve.x, ve.y);
+    const int cx = cell_coord(pe.x, G.x0, G.inv_h, G.nx);
+    const int cy = cell_coord(pe.y, G.y0, G.inv_h, G.ny);
+    const int xa = cx > 0 ? cx - 1 : 0;
+    const int xb = cx < G.nx - 1 ? cx + 1 : G.nx - 1;
+    // pass 1: cheap cull test over the 3x3 cells, hits compacted into a per-lane LDS list;
+    // pass 2: row assembly only for hits (keeps divergent lanes from paying assembly for
+    // every candidate iteration of the wave)
+    int rt0[3], rt1[3];
 #pragma unroll
-            for (int k = 0; k < 3; ++k) {
-                const int yy = cy + k - 1;
-                const bool in = yy >= 0 && yy < G.ny;
-                rt0[k] = in ? start[yy * G.nx + xa] : 0;
-                rt1[k] = in ? start[yy * G.nx + xb + 1] : 0;
-            }
+    for (int k = 0; k < 3; ++k) {
+        const int yy = cy + k - 1;
+        const bool in = yy >= 0 && yy < G.ny;
+        rt0[k] = in ? start[yy * G.nx + xa] : 0;
+        rt1[k] = in ? start[yy * G.nx + xb + 1] : 0;
+    }
 #if CBF_ABLATE < 3
-            HitList H;
+    HitList Hl;
 #pragma unroll
-            for (int k = 0; k < 3; ++k) scan_range(rt0[k], rt1[k], P, E, H, hit_lds, spos);
+    for (int k = 0; k < 3; ++k) scan_range(rt0[k], rt1[k], P, E, Hl, hit_lds, spos);
 #if CBF_ABLATE < 2
-            if (!H.overflowed()) {
-                H.template flush<FZ>(hit_lds, P, E, spos, svel);
-            } else {
+    if (!Hl.overflowed()) {
+        Hl.template flush<FZ>(hit_lds, P, E, spos, svel);
+    } else {
 #pragma unroll
-                for (int k = 0; k < 3; ++k) scan_range_direct<FZ>(rt0[k], rt1[k], P, E, spos, svel);
-            }
+        for (int k = 0; k < 3; ++k) scan_range_direct<FZ>(rt0[k], rt1[k], P, E, spos, svel);
+    }
 #else
-            E.count = H.n;
-            asm volatile("" ::"v"(E.count));
+    E.count = Hl.n;
+    asm volatile("" ::"v"(E.count));
 #endif
 #endif
-            const long k = (long)(r - row_begin) * W + c;
-            double ux, uy;
-            int32_t st;
-            if (E.count == 0) {
-                ux = E.u0x;
-                uy = E.u0y;
-                st = CBF_STATUS_IDLE;
-            } else {
+    *nbrs = E.count;
+    const long k = (long)(r - row_begin) * W + c;
+    double ux, uy;
+    int32_t st;
+    if (E.count == 0) {
+        ux = E.u0x;
+        uy = E.u0y;
+        st = CBF_STATUS_IDLE;
+    } else {
+        Sol S;
 #if CBF_ABLATE >= 1
-                Sol S;
-                S.x0 = S.x1 = 0.0;
-                S.status = CBF_STATUS_OPTIMAL;
-                S.iters = 0;
-                S.viol = E.bq0 + E.bq1 + E.bq2 + E.bq3;
-                asm volatile("" ::"v"(S.viol));
+        S.x0 = S.x1 = 0.0;
+        S.status = CBF_STATUS_OPTIMAL;
+        S.iters = 0;
+        S.viol = E.bq0 + E.bq1 + E.bq2 + E.bq3;
+        asm volatile("" ::"v"(S.viol));
 #else
-                const Sol S = solve_ego(P, E);
-#endif
-                clip_u(P, S, E, ux, uy);
-                st = pack_status(S);
-            }
-            const double2 pn = make_double2(pe.x + T * ux, pe.y + T * uy);
-            pos_out[k] = pn;
-            u[k] = make_double2(ux, uy);
-            status[k] = st;
-            if (cnt) cnt[k] = E.count;
-            ny = pn.y;
-            solved = E.count > 0;
+        if (FULL) {
+            S = solve_ego(P, E);
+        } else if (!solve_easy(P, E, S)) {
+            hardq[1 + atomicAdd(&hardq[0], 1)] = slot;
+            return 2;
         }
+#endif
+        clip_u(P, S, E, ux, uy);
+        st = pack_status(S);
     }
-    if (solves) {  // wave-aggregated, spread over 64 counters on separate 128-B lines
-        const unsigned long long m = __ballot(solved);
-        if ((threadIdx.x & 63) == 0 && m)
-            atomicAdd(&solves[16 * ((blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6)) & 63)],
-                      (unsigned long long)__popcll(m));
-    }
-    if (!ext_part) return;
-    // per-block extents of the new owned positions (halo guard for the sharded step)
+    const double2 pn = make_double2(pe.x + T * ux, pe.y + T * uy);
+    pos_out[k] = pn;
+    u[k] = make_double2(ux, uy);
+    status[k] = st;
+    if (cnt) cnt[k] = E.count;
+    *ny = pn.y;
+    return 1;
+}
+
+// Per-block extents of the new owned y (halo guard of the sharded step): {min, max, max over rows
+// < row_end - guard, min over rows >= row_begin + guard}.
+__device__ __forceinline__ void block_extents(double e0, double e1, double e2, double e3, double* out) {
     __shared__ double red[4][kBlock / 64];
-    const double v0 = own ? ny : INFINITY, v1 = own ? ny : -INFINITY;
-    const double v2 = (own && r < row_end - guard_rows) ? ny : -INFINITY;
-    const double v3 = (own && r >= row_begin + guard_rows) ? ny : INFINITY;
-    const double m0 = wave_min(v0), m1 = wave_max(v1), m2 = wave_max(v2), m3 = wave_min(v3);
+    const double m0 = wave_min(e0), m1 = wave_max(e1), m2 = wave_max(e2), m3 = wave_min(e3);
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     if (lane == 0) {
         red[0][wid] = m0;
@@ -241,12 +228,78 @@ __global__ void __launch_bounds__(kBlock) k_lattice_filter(KP P, CellGrid G, int
             c2 = pmax(c2, red[2][q]);
             d = pmin(d, red[3][q]);
         }
-        double* o = ext_part + 4l * blockIdx.x;
-        o[0] = a;
-        o[1] = b;
-        o[2] = c2;
-        o[3] = d;
+        out[0] = a;
+        out[1] = b;
+        out[2] = c2;
+        out[3] = d;
     }
+}
+
+__device__ __forceinline__ void ext_accumulate(int r, int row_begin, int row_end, int guard_rows, double ny,
+                                               double& e0, double& e1, double& e2, double& e3) {
+    e0 = pmin(e0, ny);
+    e1 = pmax(e1, ny);
+    if (r < row_end - guard_rows) e2 = pmax(e2, ny);
+    if (r >= row_begin + guard_rows) e3 = pmin(e3, ny);
+}
+
+// K4: one lane per cell-sorted slot; easy QPs solved in place, hard ones queued.
+template <bool FZ>
+__global__ void __launch_bounds__(kBlock) k_lattice_filter(KP P, CellGrid G, int W, int row_begin, int row_end,
+                                                           int win_row0, long ncell, const double2* __restrict__ spos,
+                                                           const double2* __restrict__ svel,
+                                                           const int32_t* __restrict__ sidx,
+                                                           const int32_t* __restrict__ start, double T,
+                                                           double2* __restrict__ pos_out, double2* __restrict__ u,
+                                                           int32_t* __restrict__ status, int32_t* __restrict__ cnt,
+                                                           int guard_rows, double* __restrict__ ext_part,
+                                                           unsigned long long* __restrict__ solves,
+                                                           int32_t* __restrict__ hardq) {
+    __shared__ int hit_lds[kHitCap * kBlock];
+    const int slot = blockIdx.x * kBlock + threadIdx.x;
+    const int total = start[ncell];
+    double e0 = INFINITY, e1 = -INFINITY, e2 = -INFINITY, e3 = INFINITY;
+    bool solved = false;
+    if (slot < total) {
+        double ny;
+        int r, nb = 0;
+        const int res = lattice_ego<FZ, false>(P, G, W, row_begin, row_end, win_row0, slot, spos, svel, sidx, start,
+                                               T, pos_out, u, status, cnt, hardq, hit_lds, &ny, &r, &nb);
+        solved = res != 0 && nb > 0;
+        if (res == 1) ext_accumulate(r, row_begin, row_end, guard_rows, ny, e0, e1, e2, e3);
+    }
+    if (solves) {  // wave-aggregated, spread over 64 counters on separate 128-B lines
+        const unsigned long long m = __ballot(solved);
+        if ((threadIdx.x & 63) == 0 && m)
+            atomicAdd(&solves[16 * ((blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6)) & 63)],
+                      (unsigned long long)__popcll(m));
+    }
+    if (ext_part) block_extents(e0, e1, e2, e3, ext_part + 4l * blockIdx.x);
+}
+
+// K5: the queued hard QPs, full waves of them (grid-stride over the queue).
+template <bool FZ>
+__global__ void __launch_bounds__(kBlock) k_lattice_filter_hard(KP P, CellGrid G, int W, int row_begin, int row_end,
+                                                                int win_row0, const double2* __restrict__ spos,
+                                                                const double2* __restrict__ svel,
+                                                                const int32_t* __restrict__ sidx,
+                                                                const int32_t* __restrict__ start, double T,
+                                                                double2* __restrict__ pos_out,
+                                                                double2* __restrict__ u, int32_t* __restrict__ status,
+                                                                int32_t* __restrict__ cnt, int guard_rows,
+                                                                double* __restrict__ ext_part,
+                                                                int32_t* __restrict__ hardq) {
+    __shared__ int hit_lds[kHitCap * kBlock];
+    const int nq = hardq[0];
+    double e0 = INFINITY, e1 = -INFINITY, e2 = -INFINITY, e3 = INFINITY;
+    for (int q = blockIdx.x * kBlock + threadIdx.x; q < nq; q += gridDim.x * kBlock) {
+        double ny;
+        int r, nb;
+        if (lattice_ego<FZ, true>(P, G, W, row_begin, row_end, win_row0, hardq[1 + q], spos, svel, sidx, start, T,
+                                  pos_out, u, status, cnt, hardq, hit_lds, &ny, &r, &nb) == 1)
+            ext_accumulate(r, row_begin, row_end, guard_rows, ny, e0, e1, e2, e3);
+    }
+    if (ext_part) block_extents(e0, e1, e2, e3, ext_part + 4l * blockIdx.x);
 }
 
 __global__ void __launch_bounds__(kBlock) k_extents_finalize(int nparts, const double* __restrict__ part,
@@ -349,7 +402,9 @@ extern "C" int cbf_euler(int32_t n, double* pos, const double* vel, double T, vo
     return (int)hipGetLastError();
 }
 
-static size_t lattice_ext_bytes(long win_n) { return align256(32 * (size_t)((win_n + kBlock - 1) / kBlock)); }
+static size_t lattice_ext_bytes(long win_n) {
+    return align256(32 * (size_t)((win_n + kBlock - 1) / kBlock + kHardBlocks));
+}
 
 extern "C" size_t cbf_lattice_workspace_size(int32_t W, int32_t win_rows, const cbf_grid* grid) {
     if (!grid || W <= 0 || win_rows <= 0 || grid->nx <= 0 || grid->ny <= 0) return 0;
@@ -390,8 +445,7 @@ extern "C" int cbf_lattice_build(const cbf_params* p, const cbf_grid* grid, int3
     double2* wv = (win_row0 == row_begin && win_rows == row_end - row_begin) ? reinterpret_cast<double2*>(vel_out)
                                                                               : Wk.wvel;
     hipLaunchKernelGGL(k_lattice_nominal_bin, dim3(nblk(n)), dim3(kBlock), 0, s, G, W, H, row_begin, row_end, win_row0,
-                       win_rows, p2, gain, wv, reinterpret_cast<double2*>(vel_out), Wk.count, Wk.cs,
-                       (unsigned long long*)nullptr);
+                       win_rows, p2, gain, wv, reinterpret_cast<double2*>(vel_out), Wk.count, Wk.cs, Wk.hardq);
     return scan_and_scatter(G, Wk, (int)n, p2, wv, s);
 }
 
@@ -409,12 +463,18 @@ extern "C" int cbf_lattice_advance(const cbf_params* p, const cbf_grid* grid, in
     CellWs Wk(workspace, n, (long)G.nx * G.ny);
     double* ext_part = extents ? (double*)((char*)workspace + CellWs::bytes(n, Wk.ncell)) : nullptr;
     const int nb = nblk(n);
+    const int hb = nb < kHardBlocks ? nb : kHardBlocks;
+    const KP kp = make_kp(p);
+    double2* po = reinterpret_cast<double2*>(pos_out);
+    double2* uo = reinterpret_cast<double2*>(u);
     hipLaunchKernelGGL(p->f_is_zero ? k_lattice_filter<true> : k_lattice_filter<false>, dim3(nb), dim3(kBlock), 0, s,
-                       make_kp(p), G, W, row_begin, row_end, win_row0,
-                       Wk.ncell, Wk.spos, Wk.svel, Wk.sidx, Wk.start, T, reinterpret_cast<double2*>(pos_out),
-                       reinterpret_cast<double2*>(u), status, nbr_count, guard_rows, ext_part,
-                       reinterpret_cast<unsigned long long*>(solves));
-    if (extents) hipLaunchKernelGGL(k_extents_finalize, dim3(1), dim3(kBlock), 0, s, nb, ext_part, extents);
+                       kp, G, W, row_begin, row_end, win_row0, Wk.ncell, Wk.spos, Wk.svel, Wk.sidx, Wk.start, T, po, uo,
+                       status, nbr_count, guard_rows, ext_part, reinterpret_cast<unsigned long long*>(solves),
+                       Wk.hardq);
+    hipLaunchKernelGGL(p->f_is_zero ? k_lattice_filter_hard<true> : k_lattice_filter_hard<false>, dim3(hb),
+                       dim3(kBlock), 0, s, kp, G, W, row_begin, row_end, win_row0, Wk.spos, Wk.svel, Wk.sidx, Wk.start,
+                       T, po, uo, status, nbr_count, guard_rows, ext_part ? ext_part + 4l * nb : nullptr, Wk.hardq);
+    if (extents) hipLaunchKernelGGL(k_extents_finalize, dim3(1), dim3(kBlock), 0, s, nb + hb, ext_part, extents);
     return (int)hipGetLastError();
 }
 
