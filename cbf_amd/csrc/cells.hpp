@@ -13,7 +13,14 @@
 namespace cbf {
 
 constexpr int kScanTile = 2048;  // 256 threads x 8 cells
-constexpr int kHardBlocks = 256; // grid of the hard-QP kernel of the lattice step
+constexpr int kHardBlocks = 256; // grid (64-lane blocks) of the hard-QP kernel of the lattice step
+constexpr int kHardHeader = 16;  // int32 words ahead of the hard-QP records (count + padding)
+
+// A QP the filter kernel could not solve at the origin, queued with its assembled state.
+struct HardRec {
+    double r0, r1, r2, r3, u0x, u0y, bq0, bq1, bq2, bq3;
+    int present, count, k, row;
+};
 
 struct CellGrid {
     double x0, y0, inv_h;
@@ -42,14 +49,15 @@ struct CellWs {
     double2* svel;    // [n] cell-sorted velocities / nominal controls
     int32_t* sidx;    // [n] entity index of each sorted slot
     double2* wvel;    // [n] scratch velocities (lattice step: nominal of window agents)
-    int32_t* hardq;   // [1 + n] lattice step: count, then the cell-sorted slots of queued hard QPs
+    int32_t* hardq;   // lattice step: [0] = count, records (HardRec) from word kHardHeader
     long ncell;
     int ntiles;
 
     static int tiles(long ncell) { return (int)((ncell + kScanTile - 1) / kScanTile); }
     static size_t bytes(long n, long ncell) {
         return align256(4 * ncell) + align256(4 * (ncell + 1)) + align256(4 * (size_t)tiles(ncell)) +
-               align256(8 * n) + 2 * align256(16 * n) + align256(4 * n) + align256(16 * n) + align256(4 * (n + 1));
+               align256(8 * n) + 2 * align256(16 * n) + align256(4 * n) + align256(16 * n) +
+               align256(4 * kHardHeader + sizeof(HardRec) * (size_t)n);
     }
     CellWs(void* base, long n, long nc) : ncell(nc), ntiles(tiles(nc)) {
         char* p = (char*)base;

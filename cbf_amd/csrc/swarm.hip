@@ -120,11 +120,11 @@ __device__ __forceinline__ double wave_max(double v) {
 }
 
 // Lattice step K4: filter + clip + Euler for one owned agent at cell-sorted slot `slot`.
-// FULL = false: QPs that the origin does not solve (after the strip pre-relaxation) are not
-// solved here but appended to the hard queue -- one such lane would otherwise make its whole
-// wave run the Seidel path.  FULL = true: the second kernel solves the queued egos.
+// QPs that the origin does not solve (after the strip pre-relaxation) are not solved here but
+// appended, with their assembled state, to the hard queue: one such lane would otherwise make
+// its whole wave run the Seidel path (and hold the registers for it); K5 solves them.
 // Returns 0 (not an owned agent), 1 (done: outputs written, *ny = new y), 2 (queued).
-template <bool FZ, bool FULL>
+template <bool FZ>
 __device__ __forceinline__ int lattice_ego(const KP& P, const CellGrid& G, int W, int row_begin, int row_end,
                                            int win_row0, int slot, const double2* __restrict__ spos,
                                            const double2* __restrict__ svel, const int32_t* __restrict__ sidx,
@@ -188,10 +188,23 @@ __device__ __forceinline__ int lattice_ego(const KP& P, const CellGrid& G, int W
         S.viol = E.bq0 + E.bq1 + E.bq2 + E.bq3;
         asm volatile("" ::"v"(S.viol));
 #else
-        if (FULL) {
-            S = solve_ego(P, E);
-        } else if (!solve_easy(P, E, S)) {
-            hardq[1 + atomicAdd(&hardq[0], 1)] = slot;
+        if (!solve_easy(P, E, S)) {
+            HardRec* q = reinterpret_cast<HardRec*>(hardq + kHardHeader);
+            HardRec& h = q[atomicAdd(&hardq[0], 1)];
+            h.r0 = E.r0;
+            h.r1 = E.r1;
+            h.r2 = E.r2;
+            h.r3 = E.r3;
+            h.u0x = E.u0x;
+            h.u0y = E.u0y;
+            h.bq0 = E.bq0;
+            h.bq1 = E.bq1;
+            h.bq2 = E.bq2;
+            h.bq3 = E.bq3;
+            h.present = (int)E.present;
+            h.count = E.count;
+            h.k = (int)k;
+            h.row = r;
             return 2;
         }
 #endif
@@ -263,7 +276,7 @@ __global__ void __launch_bounds__(kBlock) k_lattice_filter(KP P, CellGrid G, int
     if (slot < total) {
         double ny;
         int r, nb = 0;
-        const int res = lattice_ego<FZ, false>(P, G, W, row_begin, row_end, win_row0, slot, spos, svel, sidx, start,
+        const int res = lattice_ego<FZ>(P, G, W, row_begin, row_end, win_row0, slot, spos, svel, sidx, start,
                                                T, pos_out, u, status, cnt, hardq, hit_lds, &ny, &r, &nb);
         solved = res != 0 && nb > 0;
         if (res == 1) ext_accumulate(r, row_begin, row_end, guard_rows, ny, e0, e1, e2, e3);
@@ -277,29 +290,49 @@ __global__ void __launch_bounds__(kBlock) k_lattice_filter(KP P, CellGrid G, int
     if (ext_part) block_extents(e0, e1, e2, e3, ext_part + 4l * blockIdx.x);
 }
 
-// K5: the queued hard QPs, full waves of them (grid-stride over the queue).
-template <bool FZ>
-__global__ void __launch_bounds__(kBlock) k_lattice_filter_hard(KP P, CellGrid G, int W, int row_begin, int row_end,
-                                                                int win_row0, const double2* __restrict__ spos,
-                                                                const double2* __restrict__ svel,
-                                                                const int32_t* __restrict__ sidx,
-                                                                const int32_t* __restrict__ start, double T,
-                                                                double2* __restrict__ pos_out,
-                                                                double2* __restrict__ u, int32_t* __restrict__ status,
-                                                                int32_t* __restrict__ cnt, int guard_rows,
-                                                                double* __restrict__ ext_part,
-                                                                int32_t* __restrict__ hardq) {
-    __shared__ int hit_lds[kHitCap * kBlock];
+// K5: the queued hard QPs (state assembled by K4), 64-lane blocks spread over the CUs.
+__global__ void __launch_bounds__(64) k_lattice_filter_hard(KP P, int row_begin, int row_end, double T,
+                                                            double2* __restrict__ pos_out, double2* __restrict__ u,
+                                                            int32_t* __restrict__ status, int32_t* __restrict__ cnt,
+                                                            int guard_rows, double* __restrict__ ext_part,
+                                                            const int32_t* __restrict__ hardq) {
     const int nq = hardq[0];
+    const HardRec* q = reinterpret_cast<const HardRec*>(hardq + kHardHeader);
     double e0 = INFINITY, e1 = -INFINITY, e2 = -INFINITY, e3 = INFINITY;
-    for (int q = blockIdx.x * kBlock + threadIdx.x; q < nq; q += gridDim.x * kBlock) {
-        double ny;
-        int r, nb;
-        if (lattice_ego<FZ, true>(P, G, W, row_begin, row_end, win_row0, hardq[1 + q], spos, svel, sidx, start, T,
-                                  pos_out, u, status, cnt, hardq, hit_lds, &ny, &r, &nb) == 1)
-            ext_accumulate(r, row_begin, row_end, guard_rows, ny, e0, e1, e2, e3);
+    for (int i = blockIdx.x * 64 + threadIdx.x; i < nq; i += gridDim.x * 64) {
+        const HardRec& h = q[i];
+        Ego E;
+        E.r0 = h.r0;
+        E.r1 = h.r1;
+        E.r2 = h.r2;
+        E.r3 = h.r3;
+        E.u0x = h.u0x;
+        E.u0y = h.u0y;
+        E.bq0 = h.bq0;
+        E.bq1 = h.bq1;
+        E.bq2 = h.bq2;
+        E.bq3 = h.bq3;
+        E.present = (unsigned)h.present;
+        E.count = h.count;
+        const Sol S = solve_ego(P, E);
+        double ux, uy;
+        clip_u(P, S, E, ux, uy);
+        const double2 pn = make_double2(E.r0 + T * ux, E.r1 + T * uy);
+        pos_out[h.k] = pn;
+        u[h.k] = make_double2(ux, uy);
+        status[h.k] = pack_status(S);
+        if (cnt) cnt[h.k] = E.count;
+        ext_accumulate(h.row, row_begin, row_end, guard_rows, pn.y, e0, e1, e2, e3);
     }
-    if (ext_part) block_extents(e0, e1, e2, e3, ext_part + 4l * blockIdx.x);
+    if (!ext_part) return;
+    const double m0 = wave_min(e0), m1 = wave_max(e1), m2 = wave_max(e2), m3 = wave_min(e3);
+    if (threadIdx.x == 0) {
+        double* o = ext_part + 4l * blockIdx.x;
+        o[0] = m0;
+        o[1] = m1;
+        o[2] = m2;
+        o[3] = m3;
+    }
 }
 
 __global__ void __launch_bounds__(kBlock) k_extents_finalize(int nparts, const double* __restrict__ part,
@@ -471,9 +504,8 @@ extern "C" int cbf_lattice_advance(const cbf_params* p, const cbf_grid* grid, in
                        kp, G, W, row_begin, row_end, win_row0, Wk.ncell, Wk.spos, Wk.svel, Wk.sidx, Wk.start, T, po, uo,
                        status, nbr_count, guard_rows, ext_part, reinterpret_cast<unsigned long long*>(solves),
                        Wk.hardq);
-    hipLaunchKernelGGL(p->f_is_zero ? k_lattice_filter_hard<true> : k_lattice_filter_hard<false>, dim3(hb),
-                       dim3(kBlock), 0, s, kp, G, W, row_begin, row_end, win_row0, Wk.spos, Wk.svel, Wk.sidx, Wk.start,
-                       T, po, uo, status, nbr_count, guard_rows, ext_part ? ext_part + 4l * nb : nullptr, Wk.hardq);
+    hipLaunchKernelGGL(k_lattice_filter_hard, dim3(hb), dim3(64), 0, s, kp, row_begin, row_end, T, po, uo, status,
+                       nbr_count, guard_rows, ext_part ? ext_part + 4l * nb : nullptr, Wk.hardq);
     if (extents) hipLaunchKernelGGL(k_extents_finalize, dim3(1), dim3(kBlock), 0, s, nb + hb, ext_part, extents);
     return (int)hipGetLastError();
 }
