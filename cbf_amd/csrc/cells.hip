@@ -101,10 +101,14 @@ inline int nblk(long n) { return (int)((n + kBlock - 1) / kBlock); }
 
 }  // namespace
 
-int scan_and_scatter(const CellGrid& G, const CellWs& W, int n, const double2* pos, const double2* vel,
-                     hipStream_t s) {
+void launch_scan(const CellWs& W, hipStream_t s) {
     hipLaunchKernelGGL(k_tile_reduce, dim3(W.ntiles), dim3(kBlock), 0, s, W.count, W.ncell, W.tilesum);
     hipLaunchKernelGGL(k_tile_scan, dim3(W.ntiles), dim3(kBlock), 0, s, W.count, W.ncell, W.tilesum, W.start);
+}
+
+int scan_and_scatter(const CellGrid& G, const CellWs& W, int n, const double2* pos, const double2* vel,
+                     hipStream_t s) {
+    launch_scan(W, s);
     hipLaunchKernelGGL(k_scatter, dim3(nblk(n)), dim3(kBlock), 0, s, n, W.cs, W.start, pos, vel, W.spos, W.svel,
                        W.sidx);
     return (int)hipGetLastError();

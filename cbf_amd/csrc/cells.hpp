@@ -44,7 +44,7 @@ struct CellWs {
     int32_t* count;   // [ncell]
     int32_t* start;   // [ncell + 1]
     int32_t* tilesum; // [ntiles]
-    int2* cs;         // [n] (cell, slot); cell < 0: not binned
+    int2* cs;         // [n] (cell, slot), cell < 0: not binned; 16 B/entry reserved (lattice: int4)
     double2* spos;    // [n] cell-sorted positions
     double2* svel;    // [n] cell-sorted velocities / nominal controls
     int32_t* sidx;    // [n] entity index of each sorted slot
@@ -56,7 +56,7 @@ struct CellWs {
     static int tiles(long ncell) { return (int)((ncell + kScanTile - 1) / kScanTile); }
     static size_t bytes(long n, long ncell) {
         return align256(4 * ncell) + align256(4 * (ncell + 1)) + align256(4 * (size_t)tiles(ncell)) +
-               align256(8 * n) + 2 * align256(16 * n) + align256(4 * n) + align256(16 * n) +
+               align256(16 * n) + 2 * align256(16 * n) + align256(4 * n) + align256(16 * n) +
                align256(4 * kHardHeader + sizeof(HardRec) * (size_t)n);
     }
     CellWs(void* base, long n, long nc) : ncell(nc), ntiles(tiles(nc)) {
@@ -68,7 +68,7 @@ struct CellWs {
         tilesum = (int32_t*)p;
         p += align256(4 * (size_t)ntiles);
         cs = (int2*)p;
-        p += align256(8 * n);
+        p += align256(16 * n);
         spos = (double2*)p;
         p += align256(16 * n);
         svel = (double2*)p;
@@ -87,5 +87,7 @@ int build_cells(const CellGrid& G, const CellWs& W, int n, const double2* pos, c
                 const int32_t* unused, hipStream_t s);
 int scan_and_scatter(const CellGrid& G, const CellWs& W, int n, const double2* pos, const double2* vel,
                      hipStream_t s);
+// Exclusive scan of W.count into W.start (and re-zeroes W.count).
+void launch_scan(const CellWs& W, hipStream_t s);
 
 }  // namespace cbf

@@ -82,32 +82,79 @@ __global__ void __launch_bounds__(kBlock) k_euler(int n, double2* __restrict__ p
     pos[i] = make_double2(p.x + T * v.x, p.y + T * v.y);
 }
 
-// Lattice step K1: nominal control of every window agent whose lattice neighbours are all in the
-// window, + cell binning of those agents.  Owned agents also get vel_out.
-__global__ void __launch_bounds__(kBlock) k_lattice_nominal_bin(CellGrid G, int W, int H, int row_begin, int row_end,
-                                                                int win_row0, int win_rows,
-                                                                const double2* __restrict__ pos, double gain,
-                                                                double2* __restrict__ wvel,
-                                                                double2* __restrict__ vel_out,
-                                                                int32_t* __restrict__ count, int2* __restrict__ cs,
-                                                                int32_t* __restrict__ hardq) {
-    const long w = (long)blockIdx.x * kBlock + threadIdx.x;
-    if (w == 0) hardq[0] = 0;  // hard-QP queue of this step's advance phase starts empty
-    if (w >= (long)win_rows * W) return;
-    const int r = win_row0 + (int)(w / W), c = (int)(w % W);
-    const bool ok = (r == 0 || r - 1 >= win_row0) && (r == H - 1 || r + 1 < win_row0 + win_rows);
-    if (!ok) {
-        cs[w] = make_int2(-1, 0);
+// Lattice step K1, temporally coherent form: lanes walk the window agents in the previous step's
+// cell order (identity on the first call), so consecutive lanes mostly share a cell; each run of
+// equal cells in a wave takes its slots with ONE atomic (run length), and the later scatter
+// writes nearly sequential slots.  Per-lane result bcs[t] = {cell, slot, agent, -}.
+__global__ void __launch_bounds__(kBlock) k_lattice_nominal_bin_ordered(
+    CellGrid G, int W, int H, int row_begin, int row_end, int win_row0, int win_rows, const double2* __restrict__ pos,
+    double gain, double2* __restrict__ wvel, double2* __restrict__ vel_out, int32_t* __restrict__ count,
+    const int32_t* __restrict__ order, const int32_t* __restrict__ start, long ncell, int4* __restrict__ bcs,
+    int32_t* __restrict__ hardq) {
+    const long t = (long)blockIdx.x * kBlock + threadIdx.x;
+    const long nwin = (long)win_rows * W;
+    // hardq[2..3]: the previous build left a cell order for this window size (else identity)
+    const bool ordered = hardq[2] == 1 && hardq[3] == (int)nwin;
+    const int n_order = ordered ? start[ncell] : 0;
+    if (t == 0) hardq[0] = 0;  // hard-QP queue of this step's advance phase starts empty
+    int cell = -1;
+    long w = -1;
+    double2 p = make_double2(0.0, 0.0);
+    if (t < nwin) {
+        w = ordered ? (t < n_order ? order[t] : -1) : t;
+        if (w >= 0) {
+            const int r = win_row0 + (int)(w / W);
+            if ((r == 0 || r - 1 >= win_row0) && (r == H - 1 || r + 1 < win_row0 + win_rows)) {
+                p = pos[w];
+                cell = cell_coord(p.y, G.y0, G.inv_h, G.ny) * G.nx + cell_coord(p.x, G.x0, G.inv_h, G.nx);
+            }
+        }
+    }
+    // runs of equal cells inside the wave: one atomic per run
+    const int lane = threadIdx.x & 63;
+    int cprev = __shfl_up(cell, 1, 64);
+    const bool leader = lane == 0 || cell != cprev;
+    const unsigned long long lm = __ballot(leader);
+    const unsigned long long upto = (lane == 63) ? ~0ull : ((2ull << lane) - 1ull);
+    const int my_leader = 63 - __clzll(lm & upto);
+    const unsigned long long above = lm & ~upto;
+    const int next = above ? __ffsll((long long)above) - 1 : 64;
+    int base = 0;
+    if (leader && cell >= 0) base = atomicAdd(&count[cell], next - lane);
+    base = __shfl(base, my_leader, 64);
+    if (t >= nwin) return;
+    if (cell < 0) {
+        bcs[t] = make_int4(-1, 0, (int)w, 0);
         return;
     }
-    const double2 p = pos[w];
-    const int cell = cell_coord(p.y, G.y0, G.inv_h, G.ny) * G.nx + cell_coord(p.x, G.x0, G.inv_h, G.nx);
-    const int slot = atomicAdd(&count[cell], 1);  // issued first: its return latency hides under the sum
+    const int r = win_row0 + (int)(w / W), c = (int)(w % W);
     const double2 a = lattice_sum(pos, w, r, c, W, H);
     const double2 u0 = make_double2(a.x * gain, a.y * gain);
     wvel[w] = u0;
     if (vel_out != wvel && r >= row_begin && r < row_end) vel_out[(long)(r - row_begin) * W + c] = u0;
-    cs[w] = make_int2(cell, slot);
+    bcs[t] = make_int4(cell, base + lane - my_leader, (int)w, 0);
+}
+
+__global__ void __launch_bounds__(kBlock) k_lattice_scatter_ordered(long nwin, const int4* __restrict__ bcs,
+                                                                    const int32_t* __restrict__ start,
+                                                                    const double2* __restrict__ pos,
+                                                                    const double2* __restrict__ wvel,
+                                                                    double2* __restrict__ spos,
+                                                                    double2* __restrict__ svel,
+                                                                    int32_t* __restrict__ sidx,
+                                                                    int32_t* __restrict__ order_state, long n) {
+    const long t = (long)blockIdx.x * kBlock + threadIdx.x;
+    if (t == 0) {  // the cell order now exists for this window size: next build walks it
+        order_state[0] = 1;
+        order_state[1] = (int)n;
+    }
+    if (t >= nwin) return;
+    const int4 b = bcs[t];
+    if (b.x < 0) return;
+    const int d = start[b.x] + b.y;
+    spos[d] = pos[b.z];
+    svel[d] = wvel[b.z];
+    sidx[d] = b.z;
 }
 
 __device__ __forceinline__ double wave_min(double v) {
@@ -477,9 +524,14 @@ extern "C" int cbf_lattice_build(const cbf_params* p, const cbf_grid* grid, int3
     // unsharded: the window is the owned rows, so the nominal controls go straight to vel_out
     double2* wv = (win_row0 == row_begin && win_rows == row_end - row_begin) ? reinterpret_cast<double2*>(vel_out)
                                                                               : Wk.wvel;
-    hipLaunchKernelGGL(k_lattice_nominal_bin, dim3(nblk(n)), dim3(kBlock), 0, s, G, W, H, row_begin, row_end, win_row0,
-                       win_rows, p2, gain, wv, reinterpret_cast<double2*>(vel_out), Wk.count, Wk.cs, Wk.hardq);
-    return scan_and_scatter(G, Wk, (int)n, p2, wv, s);
+    int4* bcs = reinterpret_cast<int4*>(Wk.cs);
+    hipLaunchKernelGGL(k_lattice_nominal_bin_ordered, dim3(nblk(n)), dim3(kBlock), 0, s, G, W, H, row_begin, row_end,
+                       win_row0, win_rows, p2, gain, wv, reinterpret_cast<double2*>(vel_out), Wk.count, Wk.sidx,
+                       Wk.start, Wk.ncell, bcs, Wk.hardq);
+    launch_scan(Wk, s);
+    hipLaunchKernelGGL(k_lattice_scatter_ordered, dim3(nblk(n)), dim3(kBlock), 0, s, n, bcs, Wk.start, p2, wv, Wk.spos,
+                       Wk.svel, Wk.sidx, Wk.hardq + 2, n);
+    return (int)hipGetLastError();
 }
 
 extern "C" int cbf_lattice_advance(const cbf_params* p, const cbf_grid* grid, int32_t W, int32_t H,
