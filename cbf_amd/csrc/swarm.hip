@@ -93,16 +93,19 @@ __global__ void __launch_bounds__(kBlock) k_lattice_nominal_bin_ordered(
     int32_t* __restrict__ hardq) {
     const long t = (long)blockIdx.x * kBlock + threadIdx.x;
     const long nwin = (long)win_rows * W;
-    // hardq[2..3]: the previous build left a cell order for this window size (else identity)
-    const bool ordered = hardq[2] == 1 && hardq[3] == (int)nwin;
-    const int n_order = ordered ? start[ncell] : 0;
+    // hardq[2..4]: the previous build left a cell order for this window size and grid (else
+    // identity); the order only permutes the work, so a stale one costs speed, never results
+    const bool ordered = hardq[2] == 1 && hardq[3] == (int)nwin && hardq[4] == (int)ncell && hardq[5] == win_row0 &&
+                         hardq[6] == H;
+    int n_order = ordered ? start[ncell] : 0;
+    n_order = n_order < 0 ? 0 : (n_order > nwin ? (int)nwin : n_order);
     if (t == 0) hardq[0] = 0;  // hard-QP queue of this step's advance phase starts empty
     int cell = -1;
     long w = -1;
     double2 p = make_double2(0.0, 0.0);
     if (t < nwin) {
         w = ordered ? (t < n_order ? order[t] : -1) : t;
-        if (w >= 0) {
+        if (w >= 0 && w < nwin) {
             const int r = win_row0 + (int)(w / W);
             if ((r == 0 || r - 1 >= win_row0) && (r == H - 1 || r + 1 < win_row0 + win_rows)) {
                 p = pos[w];
@@ -142,11 +145,15 @@ __global__ void __launch_bounds__(kBlock) k_lattice_scatter_ordered(long nwin, c
                                                                     double2* __restrict__ spos,
                                                                     double2* __restrict__ svel,
                                                                     int32_t* __restrict__ sidx,
-                                                                    int32_t* __restrict__ order_state, long n) {
+                                                                    int32_t* __restrict__ order_state, long n,
+                                                                    long ncell, int win_row0, int H) {
     const long t = (long)blockIdx.x * kBlock + threadIdx.x;
-    if (t == 0) {  // the cell order now exists for this window size: next build walks it
+    if (t == 0) {  // the cell order now exists for this window and grid: the next build walks it
         order_state[0] = 1;
         order_state[1] = (int)n;
+        order_state[2] = (int)ncell;
+        order_state[3] = win_row0;
+        order_state[4] = H;
     }
     if (t >= nwin) return;
     const int4 b = bcs[t];
@@ -530,7 +537,7 @@ extern "C" int cbf_lattice_build(const cbf_params* p, const cbf_grid* grid, int3
                        Wk.start, Wk.ncell, bcs, Wk.hardq);
     launch_scan(Wk, s);
     hipLaunchKernelGGL(k_lattice_scatter_ordered, dim3(nblk(n)), dim3(kBlock), 0, s, n, bcs, Wk.start, p2, wv, Wk.spos,
-                       Wk.svel, Wk.sidx, Wk.hardq + 2, n);
+                       Wk.svel, Wk.sidx, Wk.hardq + 2, n, Wk.ncell, win_row0, H);
     return (int)hipGetLastError();
 }
 
