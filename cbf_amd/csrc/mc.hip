@@ -10,11 +10,13 @@ using namespace cbf;
 
 namespace {
 
+template <bool FZ>
 __global__ void __launch_bounds__(kBlock) k_mc_rollout(KP P, int n_scen, int n_o, int n_a, int steps, double T,
                                                        double rc, double rs, double so, double ga,
                                                        double2* __restrict__ pos, long long* __restrict__ counters,
                                                        double* __restrict__ maxviol) {
     extern __shared__ double2 lds[];
+    __shared__ int hit_lds[kHitCap * kBlock];
     const int tps = n_o > n_a ? n_o : n_a;
     const int S = kBlock / tps;
     const int n = n_o + n_a;
@@ -55,12 +57,30 @@ __global__ void __launch_bounds__(kBlock) k_mc_rollout(KP P, int n_scen, int n_o
             const double2 pe = sp[n_o + k], ve = sv[n_o + k];
             Ego E;
             ego_init(P, E, pe.x, pe.y, ve.x, ve.y, ve.x, ve.y);
+            // cull pass with hits compacted into a per-lane LDS list, then assembly over hits only
+            int nh = 0;
             for (int j = 0; j < n; ++j) {
                 const double2 pj = sp[j];
                 double s;
                 if (cull_keep(P, E.r0, E.r1, pj.x, pj.y, j < n_o, s)) {
-                    const double2 vj = sv[j];
-                    ego_add(P, E, pj.x, pj.y, vj.x, vj.y);
+                    if (nh < kHitCap) hit_lds[nh * kBlock + threadIdx.x] = j;
+                    ++nh;
+                }
+            }
+            if (nh <= kHitCap) {
+                for (int i = 0; i < nh; ++i) {
+                    const int j = hit_lds[i * kBlock + threadIdx.x];
+                    const double2 pj = sp[j], vj = sv[j];
+                    ego_add<FZ>(P, E, pj.x, pj.y, vj.x, vj.y);
+                }
+            } else {
+                for (int j = 0; j < n; ++j) {
+                    const double2 pj = sp[j];
+                    double s;
+                    if (cull_keep(P, E.r0, E.r1, pj.x, pj.y, j < n_o, s)) {
+                        const double2 vj = sv[j];
+                        ego_add<FZ>(P, E, pj.x, pj.y, vj.x, vj.y);
+                    }
                 }
             }
             if (E.count == 0) {
@@ -132,7 +152,7 @@ extern "C" int cbf_mc_rollout(const cbf_params* p, int32_t n_scen, int32_t n_o, 
     const int stride = n_o + n_a + 1;
     const size_t lds = sizeof(double2) * 2 * S * stride + (sizeof(long long) * 4 + sizeof(double)) * kBlock;
     const int blocks = (n_scen + S - 1) / S;
-    hipLaunchKernelGGL(k_mc_rollout, dim3(blocks), dim3(kBlock), lds, (hipStream_t)stream, make_kp(p), n_scen, n_o,
+    hipLaunchKernelGGL(p->f_is_zero ? k_mc_rollout<true> : k_mc_rollout<false>, dim3(blocks), dim3(kBlock), lds, (hipStream_t)stream, make_kp(p), n_scen, n_o,
                        n_a, steps, T, rc, rs, so, ga, reinterpret_cast<double2*>(pos),
                        reinterpret_cast<long long*>(counters), maxviol);
     return (int)hipGetLastError();
