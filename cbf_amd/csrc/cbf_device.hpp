@@ -107,6 +107,9 @@ __device__ __forceinline__ double row_b(const KP& P, const Ego& E, double o0, do
     }
     const double c = fma(ksy, E.gu3, fma(ksx, E.gu2, fma(sy, E.gu1, sx * E.gu0)));
     q = (nx ? 1 : 0) | (ny ? 2 : 0);
+    // with f == 0 the reference adds L_f = +-0, which leaves every nonzero value unchanged
+    // (only the sign of an exactly-zero sum can differ); the compile-time path drops the add
+    if (FZ) return P.gamma * (H - P.dmin) + c;
     return (P.gamma * (H - P.dmin) + Lf) + c;
 }
 
@@ -114,10 +117,14 @@ template <bool FZ = false>
 __device__ __forceinline__ void ego_add(const KP& P, Ego& E, double o0, double o1, double o2, double o3) {
     int q;
     const double b = row_b<FZ>(P, E, o0, o1, o2, o3, q);
-    E.bq0 = (q == 0 && b < E.bq0) ? b : E.bq0;
-    E.bq1 = (q == 1 && b < E.bq1) ? b : E.bq1;
-    E.bq2 = (q == 2 && b < E.bq2) ? b : E.bq2;
-    E.bq3 = (q == 3 && b < E.bq3) ? b : E.bq3;
+    // select the quadrant's current minimum, Python-min it, write it back (3 + 1 + 4 selects)
+    const bool q1 = q & 1, q2 = q & 2;
+    const double cur = q2 ? (q1 ? E.bq3 : E.bq2) : (q1 ? E.bq1 : E.bq0);
+    const double m = (b < cur) ? b : cur;
+    E.bq0 = (q == 0) ? m : E.bq0;
+    E.bq1 = (q == 1) ? m : E.bq1;
+    E.bq2 = (q == 2) ? m : E.bq2;
+    E.bq3 = (q == 3) ? m : E.bq3;
     E.present |= 1u << q;
     E.count++;
 }

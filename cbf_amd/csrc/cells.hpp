@@ -43,8 +43,9 @@ inline size_t align256(size_t b) { return (b + 255) & ~size_t(255); }
 struct CellWs {
     int32_t* count;   // [ncell]
     int32_t* start;   // [ncell + 1]
-    int32_t* tilesum; // [ntiles]
-    int2* cs;         // [n] (cell, slot), cell < 0: not binned; 16 B/entry reserved (lattice: int4)
+    unsigned long long* tstate;  // [ntiles] scan tile status {epoch:30 | flag:2 | value:32}
+    int32_t* sctl;    // [64] scan control: [0] tile ticket, [1] epoch, [2] error flag
+    int2* cs;        // [n] (cell, slot), cell < 0: not binned; 16 B/entry reserved (lattice: int4)
     double2* spos;    // [n] cell-sorted positions
     double2* svel;    // [n] cell-sorted velocities / nominal controls
     int32_t* sidx;    // [n] entity index of each sorted slot
@@ -55,7 +56,7 @@ struct CellWs {
 
     static int tiles(long ncell) { return (int)((ncell + kScanTile - 1) / kScanTile); }
     static size_t bytes(long n, long ncell) {
-        return align256(4 * ncell) + align256(4 * (ncell + 1)) + align256(4 * (size_t)tiles(ncell)) +
+        return align256(4 * ncell) + align256(4 * (ncell + 1)) + align256(8 * (size_t)tiles(ncell)) + 256 +
                align256(16 * n) + 2 * align256(16 * n) + align256(4 * n) + align256(16 * n) +
                align256(4 * kHardHeader + sizeof(HardRec) * (size_t)n);
     }
@@ -65,8 +66,10 @@ struct CellWs {
         p += align256(4 * nc);
         start = (int32_t*)p;
         p += align256(4 * (nc + 1));
-        tilesum = (int32_t*)p;
-        p += align256(4 * (size_t)ntiles);
+        tstate = (unsigned long long*)p;
+        p += align256(8 * (size_t)ntiles);
+        sctl = (int32_t*)p;
+        p += 256;
         cs = (int2*)p;
         p += align256(16 * n);
         spos = (double2*)p;
