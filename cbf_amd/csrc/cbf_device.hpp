@@ -117,14 +117,12 @@ template <bool FZ = false>
 __device__ __forceinline__ void ego_add(const KP& P, Ego& E, double o0, double o1, double o2, double o3) {
     int q;
     const double b = row_b<FZ>(P, E, o0, o1, o2, o3, q);
-    // select the quadrant's current minimum, Python-min it, write it back (3 + 1 + 4 selects)
-    const bool q1 = q & 1, q2 = q & 2;
-    const double cur = q2 ? (q1 ? E.bq3 : E.bq2) : (q1 ? E.bq1 : E.bq0);
-    const double m = (b < cur) ? b : cur;
-    E.bq0 = (q == 0) ? m : E.bq0;
-    E.bq1 = (q == 1) ? m : E.bq1;
-    E.bq2 = (q == 2) ? m : E.bq2;
-    E.bq3 = (q == 3) ? m : E.bq3;
+    // four predicated compare-selects: keeps bq0..3 in registers (a select-then-write-back form
+    // gets lowered to a dynamically indexed private array, i.e. scratch)
+    E.bq0 = (q == 0 && b < E.bq0) ? b : E.bq0;
+    E.bq1 = (q == 1 && b < E.bq1) ? b : E.bq1;
+    E.bq2 = (q == 2 && b < E.bq2) ? b : E.bq2;
+    E.bq3 = (q == 3 && b < E.bq3) ? b : E.bq3;
     E.present |= 1u << q;
     E.count++;
 }

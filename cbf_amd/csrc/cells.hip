@@ -15,12 +15,14 @@ __global__ void __launch_bounds__(kBlock) k_bin(CellGrid G, int n, const double2
     cs[i] = make_int2(c, slot);
 }
 
-// Single-pass exclusive scan of the cell counts (decoupled look-back).  Tiles are taken in
-// ticket order, so a tile only waits on tiles whose blocks are already running.  Tile status is
-// one 64-bit word {epoch:30 | flag:2 | value:32} written and read with agent-scope relaxed
-// atomics (the payload travels inside the flag word, so no fence is needed); the epoch (bumped
-// by the last tile) makes words of earlier launches invisible without any reset pass.  The
-// kernel re-zeroes the counts it consumed.  Spins are bounded; a timeout sets sctl[2].
+// Single-pass exclusive scan of the cell counts (decoupled look-back).  Tile = block index: the
+// dispatcher hands out workgroups in increasing order, so a tile only waits on tiles whose blocks
+// are already resident.  Tile status is one 64-bit word {epoch:30 | flag:2 | value:32} written
+// and read with agent-scope relaxed atomics (the payload travels inside the flag word, so no
+// fence is needed); the epoch (bumped by the last tile to finish) makes words of earlier
+// launches invisible without a reset pass.  The epoch load and the count loads are independent,
+// so the critical path is load -> publish/look-back -> store.  The kernel re-zeroes the counts it
+// consumed.  Spins are bounded; a timeout sets sctl[2].
 constexpr unsigned long long kFlagAgg = 1ull << 32, kFlagInc = 2ull << 32;
 
 __device__ __forceinline__ unsigned long long ld_state(const unsigned long long* p) {
@@ -34,27 +36,29 @@ __global__ void __launch_bounds__(kBlock) k_scan_onepass(int32_t* __restrict__ c
                                                          int32_t* __restrict__ start,
                                                          unsigned long long* __restrict__ tstate,
                                                          int32_t* __restrict__ sctl) {
-    __shared__ int s_tile, s_excl;
-    __shared__ unsigned s_epoch;
+    __shared__ int s_excl;
     __shared__ int wtot[kBlock / 64];
-    if (threadIdx.x == 0) {
-        s_tile = atomicAdd(&sctl[0], 1);
-        s_epoch = (unsigned)__hip_atomic_load(&sctl[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    __syncthreads();
-    const int tile = s_tile;
-    const unsigned long long ep = (unsigned long long)(s_epoch & 0x3FFFFFFFu) << 34;
+    const int tile = blockIdx.x;
+    const unsigned epoch = (unsigned)__hip_atomic_load(&sctl[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned long long ep = (unsigned long long)(epoch & 0x3FFFFFFFu) << 34;
     const long base = (long)tile * kScanTile + threadIdx.x * 8;
     int c[8];
     int tot = 0;
+    if (base + 8 <= ncell) {  // 2 x 16-B loads (base is a multiple of 8 ints)
+        const int4 a = *reinterpret_cast<const int4*>(count + base);
+        const int4 b = *reinterpret_cast<const int4*>(count + base + 4);
+        c[0] = a.x, c[1] = a.y, c[2] = a.z, c[3] = a.w, c[4] = b.x, c[5] = b.y, c[6] = b.z, c[7] = b.w;
+        *reinterpret_cast<int4*>(count + base) = make_int4(0, 0, 0, 0);  // zeroed for the next build
+        *reinterpret_cast<int4*>(count + base + 4) = make_int4(0, 0, 0, 0);
+    } else {
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-        c[k] = (base + k < ncell) ? count[base + k] : 0;
-        tot += c[k];
+        for (int k = 0; k < 8; ++k) {
+            c[k] = (base + k < ncell) ? count[base + k] : 0;
+            if (base + k < ncell) count[base + k] = 0;
+        }
     }
 #pragma unroll
-    for (int k = 0; k < 8; ++k)
-        if (base + k < ncell) count[base + k] = 0;  // leave the counts zeroed for the next build
+    for (int k = 0; k < 8; ++k) tot += c[k];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     int inc = tot;
     for (int o = 1; o < 64; o <<= 1) {
@@ -63,39 +67,51 @@ __global__ void __launch_bounds__(kBlock) k_scan_onepass(int32_t* __restrict__ c
     }
     if (lane == 63) wtot[wid] = inc;
     __syncthreads();
-    if (threadIdx.x == 0) {
+    if (wid == 0) {
+        // wave-parallel look-back: lane l reads the status of tile (top - l), 64 predecessors per
+        // round trip; the window is summed down to its nearest inclusive entry
         int agg = 0;
         for (int w = 0; w < kBlock / 64; ++w) agg += wtot[w];
         int excl = 0;
         if (tile == 0) {
-            st_state(&tstate[0], ep | kFlagInc | (unsigned)agg);
+            if (lane == 0) st_state(&tstate[0], ep | kFlagInc | (unsigned)agg);
         } else {
-            st_state(&tstate[tile], ep | kFlagAgg | (unsigned)agg);
-            int j = tile - 1;
+            if (lane == 0) st_state(&tstate[tile], ep | kFlagAgg | (unsigned)agg);
+            int top = tile - 1;
             long spins = 0;
-            while (j >= 0) {
-                const unsigned long long v = ld_state(&tstate[j]);
-                const bool mine = (v & ~((1ull << 34) - 1)) == ep;
-                const unsigned long long fl = v & (3ull << 32);
-                if (mine && fl != 0) {
-                    excl += (int)(unsigned)(v & 0xFFFFFFFFull);
-                    if (fl == kFlagInc) break;
-                    --j;
-                } else if (++spins > (1l << 26)) {
-                    sctl[2] = 1;
-                    break;
-                } else {
+            while (true) {
+                const int idx = top - lane;
+                const unsigned long long v = idx >= 0 ? ld_state(&tstate[idx]) : (ep | kFlagInc);
+                const bool ready = (v & ~((1ull << 34) - 1)) == ep && (v & (3ull << 32)) != 0;
+                const bool incl = ready && (v & (3ull << 32)) == kFlagInc;
+                const unsigned long long im = __ballot(incl), nr = __ballot(!ready);
+                const int stop = im ? __ffsll((long long)im) - 1 : 63;  // lanes 0..stop are needed
+                const unsigned long long need = stop == 63 ? ~0ull : ((1ull << (stop + 1)) - 1);
+                if (nr & need) {
+                    if (++spins > (1l << 24)) {
+                        if (lane == 0) sctl[2] = 1;
+                        break;
+                    }
                     __builtin_amdgcn_s_sleep(1);
+                    continue;
                 }
+                int part = lane <= stop ? (int)(unsigned)(v & 0xFFFFFFFFull) : 0;
+                for (int o = 32; o > 0; o >>= 1) part += __shfl_xor(part, o, 64);
+                excl += part;
+                if (im) break;
+                top -= 64;
             }
-            st_state(&tstate[tile], ep | kFlagInc | (unsigned)(excl + agg));
+            if (lane == 0) st_state(&tstate[tile], ep | kFlagInc | (unsigned)(excl + agg));
         }
-        s_excl = excl;
-        if (tile == ntiles - 1) {  // last ticket: every other block has read the epoch already
-            start[ncell] = excl + agg;
-            sctl[0] = 0;
-            __hip_atomic_store(&sctl[1], (int)((s_epoch + 1) & 0x3FFFFFFFu), __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
+        if (lane == 0) {
+            s_excl = excl;
+            if (tile == ntiles - 1) start[ncell] = excl + agg;
+            // the last block to finish bumps the epoch: every block has read it by then
+            if (atomicAdd(&sctl[0], 1) == ntiles - 1) {
+                sctl[0] = 0;
+                __hip_atomic_store(&sctl[1], (int)((epoch + 1) & 0x3FFFFFFFu), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+            }
         }
     }
     __syncthreads();

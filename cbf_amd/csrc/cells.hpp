@@ -44,7 +44,7 @@ struct CellWs {
     int32_t* count;   // [ncell]
     int32_t* start;   // [ncell + 1]
     unsigned long long* tstate;  // [ntiles] scan tile status {epoch:30 | flag:2 | value:32}
-    int32_t* sctl;    // [64] scan control: [0] tile ticket, [1] epoch, [2] error flag
+    int32_t* sctl;    // [64] scan control: [0] finished-tile counter, [1] epoch, [2] error flag
     int2* cs;        // [n] (cell, slot), cell < 0: not binned; 16 B/entry reserved (lattice: int4)
     double2* spos;    // [n] cell-sorted positions
     double2* svel;    // [n] cell-sorted velocities / nominal controls

@@ -25,15 +25,39 @@ VARIANTS = {
 }
 
 
-def build():
+def _variants():
+    """Compile-time ablations of the working tree plus `rev_<git rev>` builds listed in
+    tools/_ablate/revs (one revision per line), so a change can be A/B-timed against an
+    earlier commit in the same process."""
+    v = {k: (None, d) for k, d in VARIANTS.items()}
+    rf = os.path.join(OUT, "revs")
+    if os.path.exists(rf):
+        for rev in open(rf).read().split():
+            v[f"rev_{rev}"] = (rev, [])
+    return v
+
+
+def build(revs=()):
     from cbf_amd import build as B
     os.makedirs(OUT, exist_ok=True)
-    for name, defs in VARIANTS.items():
+    with open(os.path.join(OUT, "revs"), "w") as f:
+        f.write("\n".join(revs))
+    for name, (rev, defs) in _variants().items():
+        csrc, inc = B.CSRC, os.path.join(ROOT, "include")
+        if rev is not None:
+            src_root = os.path.join(OUT, f"src_{rev}")
+            os.makedirs(src_root, exist_ok=True)
+            arc = subprocess.run(["git", "-C", ROOT, "archive", rev, "cbf_amd/csrc", "include"], check=True,
+                                 capture_output=True).stdout
+            subprocess.run(["tar", "-x", "-C", src_root], input=arc, check=True)
+            csrc, inc = os.path.join(src_root, "cbf_amd", "csrc"), os.path.join(src_root, "include")
+        flags = [f for f in B.FLAGS if f not in (B.CSRC, os.path.join(ROOT, "include"))]
+        flags = [x for x in flags if x != "-I"] + ["-I", inc, "-I", csrc]
         objs = []
         for src in B.SOURCES:
             o = os.path.join(OUT, f"{name}_{os.path.splitext(src)[0]}.o")
             lang = ["-x", "hip"] if src.endswith(".hip") else []
-            subprocess.run([B.HIPCC] + B.FLAGS + defs + lang + ["-c", os.path.join(B.CSRC, src), "-o", o], check=True)
+            subprocess.run([B.HIPCC] + flags + defs + lang + ["-c", os.path.join(csrc, src), "-o", o], check=True)
             objs.append(o)
         subprocess.run([B.HIPCC, "-shared", f"--offload-arch={B.ARCH}", "-o", os.path.join(OUT, f"lib_{name}.so")]
                        + objs, check=True)
@@ -46,7 +70,8 @@ def run(rounds, iters, W, H):
     from cbf_amd import _lib, scenarios, swarm
     torch.cuda.set_device(0)
     libs = {}
-    for name in VARIANTS:
+    names = list(_variants())
+    for name in names:
         L = C.CDLL(os.path.join(OUT, f"lib_{name}.so"))
         for fn, (res, args) in _lib.SIGNATURES.items():
             getattr(L, fn).restype = res
@@ -57,7 +82,7 @@ def run(rounds, iters, W, H):
     cp = _lib.make_params(15)
     ws_bytes = _lib.lib.cbf_lattice_workspace_size(W, H, C.byref(grid))
     st = {}
-    for name in VARIANTS:
+    for name in names:
         st[name] = dict(pos=torch.tensor(pos0, device="cuda"), vel=torch.empty((W * H, 2), dtype=torch.float64,
                                                                                 device="cuda"),
                         u=torch.empty((W * H, 2), dtype=torch.float64, device="cuda"),
@@ -65,7 +90,7 @@ def run(rounds, iters, W, H):
                         cnt=torch.empty(W * H, dtype=torch.int32, device="cuda"),
                         ws=torch.zeros(ws_bytes, dtype=torch.uint8, device="cuda"))
     P = _lib.ptr
-    times = {n: {"build": [], "advance": []} for n in VARIANTS}
+    times = {n: {"build": [], "advance": []} for n in names}
     for r in range(rounds):
         for name, L in libs.items():
             s = st[name]
@@ -96,8 +121,9 @@ if __name__ == "__main__":
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--W", type=int, default=1024)
     ap.add_argument("--H", type=int, default=1024)
+    ap.add_argument("--revs", nargs="*", default=[], help="build: also build these git revisions")
     a = ap.parse_args()
     if a.cmd == "build":
-        build()
+        build(a.revs)
     else:
         run(a.rounds, a.iters, a.W, a.H)
