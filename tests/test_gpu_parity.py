@@ -325,3 +325,31 @@ def test_invalid_arguments_raise():
     bad = swarm.make_grid(0, 0, 1, 1, 0.1)   # cell edge smaller than the cull radius
     with pytest.raises(cbf_amd.CbfError):
         swarm.filter_swarm(fp, pos, pos, 0, method="cells", grid=bad)
+
+
+def test_gpu_vs_restated_cvxopt_feasible(golden):
+    """North-star gate "controls within 1e-5 of cvxopt", against the restatement of cvxopt's coneqp
+    (oracle/cvxqp.py; the binary is absent, so parity vs cvxopt itself stays unpinned): every
+    feasible golden QP within the IPM's own certified distance sqrt(2 gap), >= 98 % within 1e-5."""
+    from oracle import cvxqp
+    F = golden("golden_filter.npz")
+    errs = []
+    for (ms, dmin, k, gb), idx in _golden_groups(F).items():
+        g = np.frombuffer(gb, dtype=np.float64).reshape(4, 2)
+        c = cbf_amd.ControlBarrierFunction(ms, dmin=dmin, k=k)
+        obs = [F["obs"][F["obs_off"][i]:F["obs_off"][i + 1]] for i in idx]
+        off = np.concatenate([[0], np.cumsum([len(o) for o in obs])]).astype(np.int32)
+        u, st, x = c.get_safe_control_batch(_t(F["r"][idx]), (_t(off, torch.int32), _t(np.vstack(obs))),
+                                            _t(F["u0"][idx]), f=np.zeros((4, 4)), g=g, return_x=True)
+        u, x = u.cpu().numpy(), x.cpu().numpy()
+        for t, i in enumerate(idx):
+            if int(F["relax_iters"][i]) != 0:
+                continue
+            A = F["A"][F["ab_off"][i]:F["ab_off"][i + 1]]
+            b = F["b"][F["ab_off"][i]:F["ab_off"][i + 1]]
+            uc, sol = cvxqp.get_safe_control(A, b, len(b) - 8, F["u0"][i], ms)
+            assert sol["status"] == "optimal", i
+            assert np.linalg.norm(x[t] - sol["x"]) <= np.sqrt(2 * max(sol["gap"], 0.0)) + 1e-9, i
+            errs.append(float(np.abs(u[t] - uc).max()))
+    errs = np.array(errs)
+    assert len(errs) > 700 and (errs <= 1e-5).mean() >= 0.98
