@@ -20,6 +20,14 @@
 #ifndef CBF_ABLATE
 #define CBF_ABLATE 0
 #endif
+// Loads in flight per lane in the lattice filter's hit flush and joint candidate scan
+// (tools/ablate.py times the choices).
+#ifndef CBF_FLUSH_U
+#define CBF_FLUSH_U 4
+#endif
+#ifndef CBF_SCAN_U
+#define CBF_SCAN_U 6
+#endif
 
 namespace cbf {
 
@@ -140,10 +148,20 @@ struct HitList {
     template <bool FZ = false>
     __device__ __forceinline__ void flush(const int* lds, const KP& P, Ego& E, const double2* __restrict__ pos,
                                           const double2* __restrict__ vel) {
-        for (int i = 0; i < n; ++i) {
-            const int t = lds[i * kBlock + threadIdx.x];
-            const double2 pj = pos[t], vj = vel[t];
-            ego_add<FZ>(P, E, pj.x, pj.y, vj.x, vj.y);
+        // CBF_FLUSH_U hits' loads in flight per lane (same assembly order as one at a time)
+        for (int i = 0; i < n; i += CBF_FLUSH_U) {
+            double2 pj[CBF_FLUSH_U], vj[CBF_FLUSH_U];
+#pragma unroll
+            for (int q = 0; q < CBF_FLUSH_U; ++q) {
+                if (i + q < n) {
+                    const int t = lds[(i + q) * kBlock + threadIdx.x];
+                    pj[q] = pos[t];
+                    vj[q] = vel[t];
+                }
+            }
+#pragma unroll
+            for (int q = 0; q < CBF_FLUSH_U; ++q)
+                if (i + q < n) ego_add<FZ>(P, E, pj[q].x, pj[q].y, vj[q].x, vj[q].y);
         }
         n = 0;
     }
@@ -172,6 +190,34 @@ __device__ __forceinline__ void scan_range(int t0, int t1, const KP& P, const Eg
         if (s < P.cull_t && s > 0) H.push(lds, t);
     }
 }
+
+#if CBF_SCAN_U > 0
+// The three cell-row ranges of an ego scanned as one sequence, CBF_SCAN_U candidates' loads in
+// flight per lane (pushes in the same order as three scan_range calls).
+__device__ __forceinline__ void scan_rows_joint(const int (&t0)[3], const int (&t1)[3], const KP& P, const Ego& E,
+                                                HitList& H, int* lds, const double2* __restrict__ spos) {
+    const int l0 = t1[0] - t0[0], l01 = l0 + (t1[1] - t0[1]);
+    const int L = l01 + (t1[2] - t0[2]);
+    for (int v = 0; v < L; v += CBF_SCAN_U) {
+        double2 p[CBF_SCAN_U];
+        int tt[CBF_SCAN_U];
+#pragma unroll
+        for (int q = 0; q < CBF_SCAN_U; ++q) {
+            const int vv = v + q;
+            tt[q] = vv < l0 ? t0[0] + vv : (vv < l01 ? t0[1] + (vv - l0) : t0[2] + (vv - l01));
+            if (vv < L) p[q] = spos[tt[q]];
+        }
+#pragma unroll
+        for (int q = 0; q < CBF_SCAN_U; ++q) {
+            if (v + q < L) {
+                const double e0 = p[q].x - E.r0, e1 = p[q].y - E.r1;
+                const double s = e0 * e0 + e1 * e1;
+                if (s < P.cull_t && s > 0) H.push(lds, tt[q]);
+            }
+        }
+    }
+}
+#endif
 
 // Direct (uncompacted) cull + assembly over [t0, t1): the overflow path.
 template <bool FZ = false>

@@ -211,8 +211,12 @@ __device__ __forceinline__ int lattice_ego(const KP& P, const CellGrid& G, int W
     }
 #if CBF_ABLATE < 3
     HitList Hl;
+#if CBF_SCAN_U > 0
+    scan_rows_joint(rt0, rt1, P, E, Hl, hit_lds, spos);
+#else
 #pragma unroll
     for (int k = 0; k < 3; ++k) scan_range(rt0[k], rt1[k], P, E, Hl, hit_lds, spos);
+#endif
 #if CBF_ABLATE < 2
     if (!Hl.overflowed()) {
         Hl.template flush<FZ>(hit_lds, P, E, spos, svel);

@@ -19,9 +19,12 @@ sys.path.insert(0, ROOT)
 OUT = os.path.join(ROOT, "tools", "_ablate")
 VARIANTS = {
     "full": [],
-    "no_qp": ["-DCBF_ABLATE=1"],
-    "no_qp_no_rows": ["-DCBF_ABLATE=2"],
-    "no_scan": ["-DCBF_ABLATE=3"],
+    "flush2": ["-DCBF_FLUSH_U=2"],
+    "flush4": ["-DCBF_FLUSH_U=4"],
+    "scan6": ["-DCBF_SCAN_U=6"],
+    "scan8": ["-DCBF_SCAN_U=8"],
+    "scan8_flush2": ["-DCBF_SCAN_U=8", "-DCBF_FLUSH_U=2"],
+    "scan6_flush4": ["-DCBF_SCAN_U=6", "-DCBF_FLUSH_U=4"],
 }
 
 
