@@ -43,6 +43,8 @@ SIGNATURES = {
     "cbf_get_safe_control_batch": (C.c_int, [_P, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "cbf_assemble_rows": (C.c_int, [_P, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "cbf_filter_allpairs": (C.c_int, [_P, _i32, _i32, _vp, _vp, _i32, _i32, _vp, _vp, _vp, _D, _vp]),
+    "cbf_allpairs_workspace_size": (_sz, [_i32, _i32]),
+    "cbf_filter_allpairs_split": (C.c_int, [_P, _i32, _i32, _vp, _vp, _i32, _i32, _vp, _vp, _vp, _vp, _sz, _vp]),
     "cbf_cells_workspace_size": (_sz, [_i32, _G]),
     "cbf_filter_cells": (C.c_int, [_P, _G, _i32, _i32, _vp, _vp, _i32, _i32, _vp, _vp, _vp, _D, _vp, _sz, _vp]),
     "cbf_consensus_csr": (C.c_int, [_i32, _i32, _i32, _vp, _vp, _vp, _vp, _i32, _d, _d, _d, _vp, _vp]),

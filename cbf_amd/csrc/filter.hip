@@ -112,15 +112,124 @@ __device__ __forceinline__ void finish_ego(const KP& P, const Ego& E, int k, dou
     if (cnt) cnt[k] = E.count;
 }
 
-// All-pairs: one lane per ego, candidate tiles of kBlock entities staged in LDS and read by
-// broadcast (every lane reads the same candidate), ascending index order (= reference order).
+// fp32 screen of the cull test (all-pairs path).  A candidate can pass the exact fp64 test
+// s = e0^2 + e1^2 < cull_t (cross_and_rescue.py:141-150) only if S = fl32 distance^2 of the
+// fp32-rounded coordinates is below T32 (bound below); the screen only rejects, every
+// candidate it lets through is re-tested exactly in fp64, so neighbour sets and rows are
+// bit-identical to the unscreened loop.  Bound: with |coords| <= M, u = 2^-24,
+// |E_k - e_k| <= eta = 2uM + u(r + 2uM) (+ fp64 and subnormal slack) for |e_k| < r = sqrt(cull_t),
+// so S <= (cull_t + 2 sqrt2 r eta + 2 eta^2)(1 + 3u); T32 adds slack on every term and rounds up.
+// Coordinates beyond 1e30 (or NaN / inf) switch the screen off for that tile.
+__device__ __forceinline__ float screen_threshold(double cull_t, double M) {
+    if (!(M <= 1e30)) return -1.0f;  // screen off
+    const double u = 0x1p-24;
+    const double r = sqrt(cull_t) * (1.0 + 1e-12);
+    const double eta = 2.0 * u * M + u * (r + 2.0 * u * M) + 1e-14 * r + 1e-35;
+    const double T = (cull_t * (1.0 + 1e-12) + 3.0 * r * eta + 3.0 * eta * eta) * (1.0 + 8.0 * u);
+    float t32 = (float)T;
+    if ((double)t32 < T) t32 = __uint_as_float(__float_as_uint(t32) + 1u);  // next float up (T > 0)
+    return t32;
+}
+
+__device__ __forceinline__ double absmax2(double2 p) { return pmax(fabs(p.x), fabs(p.y)); }
+
+// exact cull test (fp64) + row assembly of staged candidate t (entity base + t)
+__device__ __forceinline__ void ap_exact(const KP& P, Ego& E, const double2* sp, const double2* sv, int base, int t,
+                                         int n_obs, const cbf_diag& D, int k, int& recorded) {
+    const double2 pj = sp[t];
+    double s;
+    if (cull_keep(P, E.r0, E.r1, pj.x, pj.y, base + t < n_obs, s)) {
+        const double2 vj = sv[t];
+        ego_add(P, E, pj.x, pj.y, vj.x, vj.y);
+        if (D.nbr_idx && recorded < D.kmax) D.nbr_idx[(long)k * D.kmax + recorded++] = base + t;
+    }
+}
+
+#ifndef CBF_AP_TILE
+#define CBF_AP_TILE 256   // candidates staged per tile (a multiple of kBlock)
+#endif
+#ifndef CBF_AP_SCREEN
+#define CBF_AP_SCREEN 8   // candidates per screen step
+#endif
+
+// The all-pairs candidate loop of one ego over entities [c0, c1): tiles of CBF_AP_TILE entities
+// staged in LDS (fp64 state plus an fp32 copy of the positions) and read by broadcast (every
+// lane reads the same candidate), ascending index order (= reference order).  CBF_AP_SCREEN
+// candidates per screen step; the exact test and row assembly run only for candidates the
+// screen lets through.  Every lane of the block must call it (it synchronises the block).
+struct ApLds {
+    double2 sp[CBF_AP_TILE];
+    double2 sv[CBF_AP_TILE];
+    float2 sp32[CBF_AP_TILE];
+    double smax[kBlock / 64];
+};
+
+__device__ __forceinline__ void allpairs_scan(const KP& P, Ego& E, bool active, int c0, int c1, int n_obs,
+                                              const double2* __restrict__ pos, const double2* __restrict__ vel,
+                                              const cbf_diag& D, int k, int& recorded, ApLds& L) {
+    constexpr int kScreen = CBF_AP_SCREEN;
+    constexpr int kTile = CBF_AP_TILE;
+    constexpr int kPer = kTile / kBlock;
+    const float ex = (float)E.r0, ey = (float)E.r1;
+    double m_ego = absmax2(make_double2(E.r0, E.r1));
+    if (m_ego != m_ego) m_ego = INFINITY;
+    for (int base = c0; base < c1; base += kTile) {
+        double mj = 0.0;
+#pragma unroll
+        for (int c = 0; c < kPer; ++c) {
+            const int tl = c * kBlock + threadIdx.x;
+            const int j = base + tl;
+            if (j < c1) {
+                const double2 pj = pos[j];
+                L.sp[tl] = pj;
+                L.sv[tl] = vel[j];
+                L.sp32[tl] = make_float2((float)pj.x, (float)pj.y);
+                double a = absmax2(pj);
+                if (a != a) a = INFINITY;  // NaN coordinate: screen off for this tile
+                mj = pmax(mj, a);
+            }
+        }
+        for (int o = 32; o > 0; o >>= 1) mj = pmax(mj, __shfl_xor(mj, o, 64));
+        if ((threadIdx.x & 63) == 0) L.smax[threadIdx.x >> 6] = mj;
+        __syncthreads();
+        const int m = min(kTile, c1 - base);
+        if (active) {
+            double mt = L.smax[0];
+#pragma unroll
+            for (int w = 1; w < kBlock / 64; ++w) mt = pmax(mt, L.smax[w]);
+            const float t32 = screen_threshold(P.cull_t, pmax(mt, m_ego));
+            int t = 0;
+            if (t32 > 0.0f) {
+                for (; t + kScreen <= m; t += kScreen) {
+                    float sq[kScreen];
+#pragma unroll
+                    for (int q = 0; q < kScreen; ++q) {
+                        const float2 c = L.sp32[t + q];
+                        const float d0 = c.x - ex, d1 = c.y - ey;
+                        sq[q] = __builtin_fmaf(d0, d0, d1 * d1);
+                    }
+                    float mn = sq[0];
+#pragma unroll
+                    for (int q = 1; q < kScreen; ++q) mn = fminf(mn, sq[q]);
+                    if (mn < t32) {
+#pragma unroll
+                        for (int q = 0; q < kScreen; ++q)
+                            if (sq[q] < t32) ap_exact(P, E, L.sp, L.sv, base, t + q, n_obs, D, k, recorded);
+                    }
+                }
+            }
+            for (; t < m; ++t) ap_exact(P, E, L.sp, L.sv, base, t, n_obs, D, k, recorded);
+        }
+        __syncthreads();
+    }
+}
+
 __global__ void __launch_bounds__(kBlock) k_filter_allpairs(KP P, int n, int n_obs, const double2* __restrict__ pos,
                                                             const double2* __restrict__ vel, int ego_begin,
                                                             int ego_end, double* __restrict__ u,
                                                             int32_t* __restrict__ status, int32_t* __restrict__ cnt,
                                                             cbf_diag D) {
-    __shared__ double2 sp[kBlock];
-    __shared__ double2 sv[kBlock];
+    __shared__ ApLds L;
     const int e = ego_begin + blockIdx.x * kBlock + threadIdx.x;
     const bool active = e < ego_end;
     Ego E;
@@ -131,33 +240,87 @@ __global__ void __launch_bounds__(kBlock) k_filter_allpairs(KP P, int n, int n_o
     }
     const int k = e - ego_begin;
     int recorded = 0;
-    for (int base = 0; base < n; base += kBlock) {
-        const int j = base + threadIdx.x;
-        if (j < n) {
-            sp[threadIdx.x] = pos[j];
-            sv[threadIdx.x] = vel[j];
-        }
-        __syncthreads();
-        const int m = min(kBlock, n - base);
-        if (active) {
-            for (int t = 0; t < m; ++t) {
-                const double2 pj = sp[t];
-                double s;
-                if (cull_keep(P, E.r0, E.r1, pj.x, pj.y, base + t < n_obs, s)) {
-                    const double2 vj = sv[t];
-                    ego_add(P, E, pj.x, pj.y, vj.x, vj.y);
-                    if (D.nbr_idx && recorded < D.kmax) D.nbr_idx[(long)k * D.kmax + recorded++] = base + t;
-                }
-            }
-        }
-        __syncthreads();
-    }
+    allpairs_scan(P, E, active, 0, n, n_obs, pos, vel, D, k, recorded, L);
     if (!active) return;
     if (D.nbr_idx)
         for (int t = recorded; t < D.kmax; ++t) D.nbr_idx[(long)k * D.kmax + t] = -1;
     Sol S;
     finish_ego(P, E, k, u, status, cnt, S);
     write_diag(P, E, S, k, pos, vel, D);
+}
+
+// Split all-pairs: workgroup (x, y) runs egos [x*kBlock, ...) against candidate chunk y and
+// leaves the chunk's partial QP state; k_allpairs_finish merges the chunks in order.  The
+// per-quadrant minimum ignores NaN rows whatever the order, so merging is exact.
+struct ApPart {
+    double bq0, bq1, bq2, bq3;
+    int present, count;
+};
+
+inline int ap_chunks(long n, long n_ego) {
+    const long ego_waves = (n_ego + 63) / 64;
+    long s = (8192 + ego_waves - 1) / (ego_waves > 0 ? ego_waves : 1);  // ~8 waves per SIMD
+    const long smax = (n + 2047) / 2048;                                 // >= 2048 candidates per chunk
+    if (s > smax) s = smax;
+    return (int)(s < 1 ? 1 : s);
+}
+inline long ap_chunk_len(long n, int s) {
+    const long c = (n + s - 1) / s;
+    return (c + CBF_AP_TILE - 1) / CBF_AP_TILE * CBF_AP_TILE;
+}
+
+__global__ void __launch_bounds__(kBlock) k_allpairs_partial(KP P, int n, int n_obs, const double2* __restrict__ pos,
+                                                             const double2* __restrict__ vel, int ego_begin,
+                                                             int ego_end, int chunk, ApPart* __restrict__ part) {
+    __shared__ ApLds L;
+    const int e = ego_begin + blockIdx.x * kBlock + threadIdx.x;
+    const bool active = e < ego_end;
+    Ego E;
+    {
+        const double2 pe = active ? pos[e] : make_double2(0, 0);
+        const double2 ve = active ? vel[e] : make_double2(0, 0);
+        ego_init(P, E, pe.x, pe.y, ve.x, ve.y, ve.x, ve.y);
+    }
+    const int c0 = blockIdx.y * chunk;
+    const int c1 = min(n, c0 + chunk);
+    const int k = e - ego_begin;
+    int recorded = 0;
+    const cbf_diag D0 = {};
+    allpairs_scan(P, E, active, c0, c1, n_obs, pos, vel, D0, k, recorded, L);
+    if (!active) return;
+    ApPart o;
+    o.bq0 = E.bq0;
+    o.bq1 = E.bq1;
+    o.bq2 = E.bq2;
+    o.bq3 = E.bq3;
+    o.present = (int)E.present;
+    o.count = E.count;
+    part[(long)blockIdx.y * (ego_end - ego_begin) + k] = o;
+}
+
+__global__ void __launch_bounds__(kBlock) k_allpairs_finish(KP P, int nchunk, const double2* __restrict__ pos,
+                                                            const double2* __restrict__ vel, int ego_begin,
+                                                            int ego_end, const ApPart* __restrict__ part,
+                                                            double* __restrict__ u, int32_t* __restrict__ status,
+                                                            int32_t* __restrict__ cnt) {
+    const int e = ego_begin + blockIdx.x * kBlock + threadIdx.x;
+    if (e >= ego_end) return;
+    const int k = e - ego_begin;
+    const long ne = ego_end - ego_begin;
+    const double2 pe = pos[e], ve = vel[e];
+    Ego E;
+    ego_init(P, E, pe.x, pe.y, ve.x, ve.y, ve.x, ve.y);
+    for (int c = 0; c < nchunk; ++c) {
+        const ApPart o = part[c * ne + k];
+        E.bq0 = pmin(E.bq0, o.bq0);
+        E.bq1 = pmin(E.bq1, o.bq1);
+        E.bq2 = pmin(E.bq2, o.bq2);
+        E.bq3 = pmin(E.bq3, o.bq3);
+        E.present |= (unsigned)o.present;
+        E.count += o.count;
+    }
+    Sol S;
+    finish_ego(P, E, k, u, status, cnt, S);
 }
 
 // Cell-list filter over sorted slots: lane = sorted slot (spatially coherent waves).
@@ -268,6 +431,34 @@ extern "C" int cbf_filter_allpairs(const cbf_params* p, int32_t n, int32_t n_obs
     hipLaunchKernelGGL(k_filter_allpairs, dim3(grid_for(ne)), dim3(kBlock), 0, (hipStream_t)stream, make_kp(p), n,
                        n_obs, reinterpret_cast<const double2*>(pos), reinterpret_cast<const double2*>(vel),
                        ego_begin, ego_end, u, status, nbr_count, diag_or_empty(diag));
+    return (int)hipGetLastError();
+}
+
+extern "C" size_t cbf_allpairs_workspace_size(int32_t n, int32_t n_ego) {
+    if (n < 0 || n_ego < 0) return 0;
+    return sizeof(ApPart) * (size_t)ap_chunks(n, n_ego) * (size_t)(n_ego > 0 ? n_ego : 1);
+}
+
+extern "C" int cbf_filter_allpairs_split(const cbf_params* p, int32_t n, int32_t n_obs, const double* pos,
+                                         const double* vel, int32_t ego_begin, int32_t ego_end, double* u,
+                                         int32_t* status, int32_t* nbr_count, void* workspace, size_t workspace_bytes,
+                                         void* stream) {
+    const int rc = check_swarm_args(p, n, n_obs, pos, vel, ego_begin, ego_end, u, status, nullptr);
+    if (rc) return rc;
+    const int ne = ego_end - ego_begin;
+    if (ne == 0) return 0;
+    if (!workspace || workspace_bytes < cbf_allpairs_workspace_size(n, ne)) return CBF_EINVAL;
+    const int s = ap_chunks(n, ne);
+    const long chunk = ap_chunk_len(n, s);
+    const KP kp = make_kp(p);
+    ApPart* part = reinterpret_cast<ApPart*>(workspace);
+    hipStream_t st = (hipStream_t)stream;
+    const double2* p2 = reinterpret_cast<const double2*>(pos);
+    const double2* v2 = reinterpret_cast<const double2*>(vel);
+    hipLaunchKernelGGL(k_allpairs_partial, dim3(grid_for(ne), s), dim3(kBlock), 0, st, kp, n, n_obs, p2, v2,
+                       ego_begin, ego_end, (int)chunk, part);
+    hipLaunchKernelGGL(k_allpairs_finish, dim3(grid_for(ne)), dim3(kBlock), 0, st, kp, s, p2, v2, ego_begin, ego_end,
+                       part, u, status, nbr_count);
     return (int)hipGetLastError();
 }
 

@@ -85,7 +85,14 @@ def filter_swarm(params, pos, vel, n_obs, ego_begin=None, ego_end=None, method="
     if method == "auto":
         method = "allpairs" if n <= 8192 else "cells"
     Dp = None if D is None else _lib.C.byref(D)
-    if method == "allpairs":
+    if method == "allpairs" and D is None:
+        need = lib.cbf_allpairs_workspace_size(n, ne)
+        if workspace is None or workspace.numel() < need:
+            workspace = torch.empty((need,), dtype=torch.uint8, device=dev)
+        check(lib.cbf_filter_allpairs_split(cp, n, n_obs, ptr(pos), ptr(vel), eb, ee, ptr(out["u"]),
+                                            ptr(out["status"]), ptr(out["nbr_count"]), ptr(workspace), need,
+                                            stream_handle()), "cbf_filter_allpairs_split")
+    elif method == "allpairs":
         check(lib.cbf_filter_allpairs(cp, n, n_obs, ptr(pos), ptr(vel), eb, ee, ptr(out["u"]), ptr(out["status"]),
                                       ptr(out["nbr_count"]), Dp, stream_handle()), "cbf_filter_allpairs")
     elif method == "cells":
@@ -208,14 +215,17 @@ class LatticeSwarm:
         self.ws_bytes = lib.cbf_lattice_workspace_size(W, H, _lib.C.byref(self.grid))
         self.ws = torch.zeros((self.ws_bytes,), dtype=torch.uint8, device=self.dev)
         self.solves = torch.zeros((1024,), dtype=torch.int64, device=self.dev)
+        self.ap_ws = torch.empty((lib.cbf_allpairs_workspace_size(n, n) if method == "allpairs" else 1,),
+                                 dtype=torch.uint8, device=self.dev)
         self.graph = None
 
     def _launch(self):
         if self.method == "allpairs":
             consensus_lattice(self.pos, self.W, self.H, self.gain, out=self.vel)
-            check(lib.cbf_filter_allpairs(self.cp, self.n, 0, ptr(self.pos), ptr(self.vel), 0, self.n, ptr(self.u),
-                                          ptr(self.status), ptr(self.nbr_count), None, stream_handle()),
-                  "cbf_filter_allpairs")
+            check(lib.cbf_filter_allpairs_split(self.cp, self.n, 0, ptr(self.pos), ptr(self.vel), 0, self.n,
+                                                ptr(self.u), ptr(self.status), ptr(self.nbr_count),
+                                                ptr(self.ap_ws), self.ap_ws.numel(), stream_handle()),
+                  "cbf_filter_allpairs_split")
             euler(self.pos, self.u, self.T)
             self.solves[0] += (self.nbr_count > 0).sum()
             return

@@ -104,6 +104,15 @@ int cbf_filter_allpairs(const cbf_params* p, int32_t n, int32_t n_obs, const dou
                         int32_t ego_begin, int32_t ego_end, double* u, int32_t* status, int32_t* nbr_count,
                         const cbf_diag* diag, void* stream);
 
+/* cbf_filter_allpairs without diagnostics, for few egos against many entities: the candidate
+ * range is split into chunks run by separate workgroups (so small n_ego still fills the GPU) and
+ * the chunks' partial QP state is merged in order -- results identical to cbf_filter_allpairs.
+ * Workspace: device memory of cbf_allpairs_workspace_size(n, n_ego) bytes, no initialisation. */
+size_t cbf_allpairs_workspace_size(int32_t n, int32_t n_ego);
+int cbf_filter_allpairs_split(const cbf_params* p, int32_t n, int32_t n_obs, const double* pos, const double* vel,
+                              int32_t ego_begin, int32_t ego_end, double* u, int32_t* status, int32_t* nbr_count,
+                              void* workspace, size_t workspace_bytes, void* stream);
+
 /* Uniform cell grid: cell (cx, cy) = clamp(floor((p - origin) * inv_h), 0, n-1).  The cell
  * edge 1/inv_h must be >= the cull radius (checked).  Clamping keeps results exact for
  * entities outside the grid (only speed suffers). */

@@ -353,3 +353,72 @@ def test_gpu_vs_restated_cvxopt_feasible(golden):
             errs.append(float(np.abs(u[t] - uc).max()))
     errs = np.array(errs)
     assert len(errs) > 700 and (errs <= 1e-5).mean() >= 0.98
+
+
+@pytest.mark.parametrize("offset", [0.0, 1e3, 1e6, 1e12, 1e31])
+def test_allpairs_screen_exact_at_any_magnitude(offset):
+    """The all-pairs kernel's fp32 screen only rejects candidates that the exact fp64 test rejects:
+    neighbour sets and controls stay bit-identical to the oracle with coordinates far from the
+    origin (coarse fp32 rounding, wider screen margin) and beyond 1e30 (screen switched off)."""
+    rng = np.random.default_rng(5)
+    p = po.Params(15)
+    fp = swarm.FilterParams()
+    n, n_obs = 600, 60
+    pos, vel = _random_swarm(rng, n, n_obs, 1.0)
+    # pairs straddling the cull radius (s just below / at / above cull_t)
+    for i, d in enumerate([np.nextafter(0.2, 0), 0.2, np.nextafter(0.2, 1), 0.19999999, 0.20000001]):
+        pos[100 + 2 * i + 1] = pos[100 + 2 * i] + [d, 0.0]
+        pos[200 + 2 * i + 1] = pos[200 + 2 * i] + [d * 0.6, d * 0.8]
+    pos = pos + offset
+    ref = coracle.filter_swarm(p, pos, vel, n_obs, kmax=32, diag=True)
+    out = swarm.filter_swarm(fp, _t(pos), _t(vel), n_obs, method="allpairs", kmax=32, diag=True)
+    got = {k: v.cpu().numpy() for k, v in out.items()}
+    assert np.array_equal(got["nbr_count"], ref["cnt"])
+    assert np.array_equal(got["nbr_idx"], ref["nbr_idx"])
+    assert np.array_equal(got["u"], ref["u"])
+    assert np.array_equal(got["status"], ref["status"])
+
+
+def test_allpairs_nonfinite_coordinates():
+    rng = np.random.default_rng(6)
+    p = po.Params(15)
+    fp = swarm.FilterParams()
+    pos, vel = _random_swarm(rng, 300, 30, 0.8)
+    pos[40] = [np.nan, 0.1]
+    pos[41] = [np.inf, 0.0]
+    pos[290] = [0.05, np.nan]
+    ref = coracle.filter_swarm(p, pos, vel, 30, kmax=32, diag=True)
+    out = swarm.filter_swarm(fp, _t(pos), _t(vel), 30, method="allpairs", kmax=32, diag=True)
+    got = {k: v.cpu().numpy() for k, v in out.items()}
+    assert np.array_equal(got["nbr_count"], ref["cnt"])
+    assert np.array_equal(got["nbr_idx"], ref["nbr_idx"])
+    assert np.array_equal(got["status"], ref["status"])
+    assert np.array_equal(got["u"], ref["u"], equal_nan=True)
+
+
+@pytest.mark.parametrize("n,n_obs,spread", [(40, 10, 0.3), (5000, 1500, 4.0), (20000, 0, 6.0)])
+def test_allpairs_split_vs_oracle(n, n_obs, spread):
+    """cbf_filter_allpairs_split (candidate chunks in separate workgroups, merged in order) gives
+    the same controls, statuses and neighbour counts as the oracle's sequential loop."""
+    rng = np.random.default_rng(n)
+    p = po.Params(15)
+    fp = swarm.FilterParams()
+    pos, vel = _random_swarm(rng, n, n_obs, spread)
+    ref = coracle.filter_swarm(p, pos, vel, n_obs)
+    out = swarm.filter_swarm(fp, _t(pos), _t(vel), n_obs, method="allpairs")
+    assert np.array_equal(out["u"].cpu().numpy(), ref["u"])
+    assert np.array_equal(out["status"].cpu().numpy(), ref["status"])
+    assert np.array_equal(out["nbr_count"].cpu().numpy(), ref["cnt"])
+
+
+def test_lattice_allpairs_step_vs_oracle():
+    """cfg3 shape (every pair tested) at 64 x 64: consensus + split all-pairs filter + Euler."""
+    W = H = 64
+    pos = scenarios.lattice(W, H, seed=3)
+    L = swarm.LatticeSwarm(pos, W, H, gain=scenarios.LATTICE_GAIN, method="allpairs")
+    L.step()
+    torch.cuda.synchronize()
+    vel = coracle.consensus_lattice(W, H, 0, H, pos, scenarios.LATTICE_GAIN)
+    ref = coracle.filter_swarm(po.Params(15), pos, vel, 0)
+    assert np.array_equal(L.u.cpu().numpy(), ref["u"])
+    assert np.array_equal(L.pos.cpu().numpy(), coracle.euler(pos, ref["u"], 1 / 30))

@@ -17,6 +17,16 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 OUT = os.path.join(ROOT, "tools", "_ablate")
+SETS = {}
+SETS["allpairs"] = {
+    "ap_base": [],
+    "ap_w5": ["-DCBF_AP_WAVES=5"],
+    "ap_w8": ["-DCBF_AP_WAVES=8"],
+    "ap_t1024": ["-DCBF_AP_TILE=1024"],
+    "ap_t1024_w5": ["-DCBF_AP_TILE=1024", "-DCBF_AP_WAVES=5"],
+    "ap_s16_t1024_w5": ["-DCBF_AP_SCREEN=16", "-DCBF_AP_TILE=1024", "-DCBF_AP_WAVES=5"],
+    "ap_s16_t512_w8": ["-DCBF_AP_SCREEN=16", "-DCBF_AP_TILE=512", "-DCBF_AP_WAVES=8"],
+}
 VARIANTS = {
     "full": [],
     "flush2": ["-DCBF_FLUSH_U=2"],
@@ -29,6 +39,8 @@ VARIANTS = {
 
 
 def _variants():
+    if os.environ.get("ABLATE_SET"):
+        return {k: (None, d) for k, d in SETS[os.environ["ABLATE_SET"]].items()}
     """Compile-time ablations of the working tree plus `rev_<git rev>` builds listed in
     tools/_ablate/revs (one revision per line), so a change can be A/B-timed against an
     earlier commit in the same process."""
@@ -117,9 +129,53 @@ def run(rounds, iters, W, H):
     return res
 
 
+def run_allpairs(rounds, iters, W, H):
+    import numpy as np
+    import torch
+    from cbf_amd import _lib, scenarios
+    torch.cuda.set_device(0)
+    names = list(_variants())
+    libs = {}
+    for name in names:
+        L = C.CDLL(os.path.join(OUT, f"lib_{name}.so"))
+        for fn, (res, args) in _lib.SIGNATURES.items():
+            getattr(L, fn).restype = res
+            getattr(L, fn).argtypes = args
+        libs[name] = L
+    pos = torch.tensor(scenarios.lattice(W, H, seed=0), device="cuda")
+    vel = torch.randn(W * H, 2, dtype=torch.float64, device="cuda") * 0.05
+    n = W * H
+    u = torch.empty(n, 2, dtype=torch.float64, device="cuda")
+    st = torch.empty(n, dtype=torch.int32, device="cuda")
+    cp = _lib.make_params(15)
+    P = _lib.ptr
+    ref = None
+    times = {k: [] for k in names}
+    for r in range(rounds):
+        for name, L in libs.items():
+            for _ in range(iters):
+                a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                a.record()
+                _lib.check(L.cbf_filter_allpairs(cp, n, 0, P(pos), P(vel), 0, n, P(u), P(st), None, None,
+                                                 _lib.stream_handle()), "allpairs")
+                b.record()
+                torch.cuda.synchronize()
+                if r > 0:
+                    times[name].append(a.elapsed_time(b))
+            if ref is None:
+                ref = u.clone()
+            if not torch.equal(u, ref):
+                bad = (u != ref).any(1)
+                print(f"MISMATCH {name}: {int(bad.sum())} egos, max |du| {float((u - ref).abs().max())}",
+                      file=sys.stderr)
+    res = {k: {"median_us": float(np.median(v)) * 1e3, "pair_tests_per_s": n * n / (float(np.median(v)) * 1e-3)}
+           for k, v in times.items()}
+    print(json.dumps(res, indent=1))
+
+
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
-    ap.add_argument("cmd", choices=["build", "run"])
+    ap.add_argument("cmd", choices=["build", "run", "run_allpairs"])
     ap.add_argument("--rounds", type=int, default=6)
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--W", type=int, default=1024)
@@ -128,5 +184,7 @@ if __name__ == "__main__":
     a = ap.parse_args()
     if a.cmd == "build":
         build(a.revs)
+    elif a.cmd == "run_allpairs":
+        run_allpairs(a.rounds, a.iters, a.W, a.H)
     else:
         run(a.rounds, a.iters, a.W, a.H)
