@@ -16,11 +16,13 @@
  *   cull                    cross_and_rescue.py:141-150, meet_at_center.py:124-133
  *   consensus / pursuit     cross_and_rescue.py:108-125, meet_at_center.py:86-103
  *   Euler                   cross_and_rescue.py:173
+ *   Euclidean HOCBF mode    (no reference: restates oracle/pyoracle.py hocbf_row / filter_one_hocbf)
  *
  * Build: gcc -O2 -ffp-contract=off -fno-fast-math -shared -fPIC (see oracle/Makefile).
  */
 #include <math.h>
 #include <stdint.h>
+#include <stdlib.h>
 #include <string.h>
 
 typedef struct {
@@ -105,13 +107,11 @@ typedef struct {
 
 /* Incremental (Seidel) exact min-norm solve over the planes in order; returns -1 when
  * feasible (x set) or the index of the plane at which the prefix became infeasible. */
-static int solve_planes(const planes_t* P, double* x0o, double* x1o) {
-    double tb[8];
-    for (int h = 0; h < P->n; ++h) tb[h] = FEAS_TOL * py_max(1.0, fabs(P->b[h]));
+static int solve_planes_n(int n, const double* A0, const double* A1, const double* B, double* x0o, double* x1o) {
     double x0 = 0.0, x1 = 0.0;
-    for (int h = 0; h < P->n; ++h) {
-        double a0 = P->a0[h], a1 = P->a1[h], b = P->b[h];
-        if ((a0 * x0 + a1 * x1) - b <= tb[h]) continue;
+    for (int h = 0; h < n; ++h) {
+        double a0 = A0[h], a1 = A1[h], b = B[h];
+        if ((a0 * x0 + a1 * x1) - b <= FEAS_TOL * py_max(1.0, fabs(b))) continue;
         double n2 = a0 * a0 + a1 * a1;
         if (!(n2 > 0)) return h;
         double t = b / n2;
@@ -122,7 +122,7 @@ static int solve_planes(const planes_t* P, double* x0o, double* x1o) {
         double rh = 0.0, ah = 0.0, rl = 0.0, al = 0.0;
         int has_hi = 0, has_lo = 0;
         for (int j = 0; j < h; ++j) {
-            double c0 = P->a0[j], c1 = P->a1[j], e = P->b[j];
+            double c0 = A0[j], c1 = A1[j], e = B[j];
             double ad = c0 * d0 + c1 * d1;
             double r = e - (c0 * p0 + c1 * p1);
             if (ad > 0) {
@@ -149,11 +149,15 @@ static int solve_planes(const planes_t* P, double* x0o, double* x1o) {
         x0 = p0 + s * d0;
         x1 = p1 + s * d1;
         for (int j = 0; j <= h; ++j)
-            if (!((P->a0[j] * x0 + P->a1[j] * x1) - P->b[j] <= tb[j])) return h;
+            if (!((A0[j] * x0 + A1[j] * x1) - B[j] <= FEAS_TOL * py_max(1.0, fabs(B[j])))) return h;
     }
     *x0o = x0;
     *x1o = x1;
     return -1;
+}
+
+static int solve_planes(const planes_t* P, double* x0o, double* x1o) {
+    return solve_planes_n(P->n, P->a0, P->a1, P->b, x0o, x1o);
 }
 
 static void box_planes(const double S[8], planes_t* P) {
@@ -425,4 +429,110 @@ void orc_mc_rollout(const orc_params* p, int n_scen, int n_o, int n_a, int steps
         }
         maxviol[s] = mv;
     }
+}
+
+/* ---- Euclidean HOCBF mode (oracle/pyoracle.py: hocbf_row, filter_one_hocbf) ---- */
+static void hocbf_row(const orc_params* p, double a_sum, double a_prod, const double r[4], const double o[4],
+                      const double u0[2], double* a0, double* a1, double* b) {
+    double dx = r[0] - o[0], dy = r[1] - o[1], dvx = r[2] - o[2], dvy = r[3] - o[3];
+    double h = (dx * dx + dy * dy) - p->dmin * p->dmin;
+    double hd = 2.0 * (dx * dvx + dy * dvy);
+    double vv = dvx * dvx + dvy * dvy;
+    double rhs = (2.0 * vv + a_sum * hd) + a_prod * h;
+    *a0 = -2.0 * dx;
+    *a1 = -2.0 * dy;
+    *b = rhs - (*a0 * u0[0] + *a1 * u0[1]);
+}
+
+/* planes: 4 merged box planes then one per neighbour (scratch arrays of m + 4) */
+static int solve_hocbf(const orc_params* p, const double r[4], const double u0[2], int m, double* A0, double* A1,
+                       double* B, double x[2], int* iters_out) {
+    double S[8];
+    box_rhs(p, r, u0, S);
+    planes_t bx;
+    box_planes(S, &bx);
+    for (int i = 0; i < 4; ++i) {
+        A0[i] = bx.a0[i];
+        A1[i] = bx.a1[i];
+        B[i] = bx.b[i];
+    }
+    int iters = 0, status = ST_OPTIMAL;
+    for (;;) {
+        int fail = solve_planes_n(m + 4, A0, A1, B, &x[0], &x[1]);
+        if (fail < 0) break;
+        if (fail < 4) {
+            status = ST_BOX_INFEASIBLE;
+            x[0] = x[1] = 0.0;
+            break;
+        }
+        if (iters >= RELAX_CAP) {
+            status = ST_RELAX_CAP;
+            x[0] = x[1] = 0.0;
+            break;
+        }
+        for (int i = 4; i < m + 4; ++i) B[i] = B[i] + 1.0; /* cbf.py:85-87 */
+        iters++;
+        status = ST_RELAXED;
+    }
+    *iters_out = iters;
+    return status;
+}
+
+int orc_filter_one_hocbf(const orc_params* p, double a_sum, double a_prod, const double r[4], int m, const double* obs,
+                         const double u0[2], double u[2], double x[2], int* iters) {
+    double* A0 = malloc(sizeof(double) * (m + 4));
+    double* A1 = malloc(sizeof(double) * (m + 4));
+    double* B = malloc(sizeof(double) * (m + 4));
+    for (int i = 0; i < m; ++i) hocbf_row(p, a_sum, a_prod, r, obs + 4 * i, u0, &A0[4 + i], &A1[4 + i], &B[4 + i]);
+    int st = solve_hocbf(p, r, u0, m, A0, A1, B, x, iters);
+    clip(p, x, u0, u);
+    free(A0);
+    free(A1);
+    free(B);
+    return st;
+}
+
+/* orc_filter_swarm's loop (cull in index order, Jacobi) with Euclidean HOCBF rows */
+void orc_filter_swarm_hocbf(const orc_params* p, double a_sum, double a_prod, int n, int n_obs, const double* pos,
+                            const double* vel, int ego_begin, int ego_end, double* u, int32_t* status, int32_t* cnt,
+                            double* xdev) {
+    double* A0 = malloc(sizeof(double) * (n + 4));
+    double* A1 = malloc(sizeof(double) * (n + 4));
+    double* B = malloc(sizeof(double) * (n + 4));
+    for (int e = ego_begin; e < ego_end; ++e) {
+        int k = e - ego_begin;
+        double r[4] = {pos[2 * e], pos[2 * e + 1], vel[2 * e], vel[2 * e + 1]};
+        double u0[2] = {vel[2 * e], vel[2 * e + 1]};
+        int m = 0;
+        for (int j = 0; j < n; ++j) {
+            double e0 = pos[2 * j] - r[0], e1 = pos[2 * j + 1] - r[1];
+            double s = (0.0 + e0 * e0) + e1 * e1;
+            if (!(s < p->cull_t && (j < n_obs || s > 0))) continue;
+            double o[4] = {pos[2 * j], pos[2 * j + 1], vel[2 * j], vel[2 * j + 1]};
+            hocbf_row(p, a_sum, a_prod, r, o, u0, &A0[4 + m], &A1[4 + m], &B[4 + m]);
+            m++;
+        }
+        cnt[k] = m;
+        double x[2] = {0.0, 0.0};
+        if (m == 0) {
+            u[2 * k] = u0[0];
+            u[2 * k + 1] = u0[1];
+            status[k] = ST_IDLE;
+        } else {
+            int iters;
+            int st = solve_hocbf(p, r, u0, m, A0, A1, B, x, &iters);
+            double uu[2];
+            clip(p, x, u0, uu);
+            u[2 * k] = uu[0];
+            u[2 * k + 1] = uu[1];
+            status[k] = st | ((iters < (1 << 23) ? iters : (1 << 23) - 1) << 8);
+        }
+        if (xdev) {
+            xdev[2 * k] = x[0];
+            xdev[2 * k + 1] = x[1];
+        }
+    }
+    free(A0);
+    free(A1);
+    free(B);
 }

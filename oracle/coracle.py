@@ -49,6 +49,11 @@ def lib():
         L.orc_euler.argtypes = [C.c_int, dp, dp, C.c_double]
         L.orc_mc_rollout.argtypes = [P, C.c_int, C.c_int, C.c_int, C.c_int, C.c_double, C.c_double, C.c_double,
                                      C.c_double, C.c_double, dp, i64p, dp]
+        L.orc_filter_one_hocbf.argtypes = [P, C.c_double, C.c_double, dp, C.c_int, dp, dp, dp, dp,
+                                           C.POINTER(C.c_int)]
+        L.orc_filter_one_hocbf.restype = C.c_int
+        L.orc_filter_swarm_hocbf.argtypes = [P, C.c_double, C.c_double, C.c_int, C.c_int, dp, dp, C.c_int, C.c_int,
+                                             dp, ip, ip, C.c_void_p]
         _lib = L
     return _lib
 
@@ -137,3 +142,24 @@ def mc_rollout(p, pos, n_o, n_a, steps, T, rot, so, ga):
     counters = np.zeros((n_scen, 4), np.int64); mv = np.zeros(n_scen)
     lib().orc_mc_rollout(C.byref(params(p)), n_scen, n_o, n_a, steps, T, rot[0], rot[1], so, ga, pos, counters, mv)
     return pos, counters, mv
+
+
+def filter_one_hocbf(p, hp, r, obs, u0):
+    """Euclidean HOCBF mode (pyoracle.filter_one_hocbf) in C."""
+    obs = _c(obs).reshape(-1, 4)
+    u = np.zeros(2); x = np.zeros(2); it = C.c_int(0)
+    st = lib().orc_filter_one_hocbf(C.byref(params(p)), hp.a_sum, hp.a_prod, _c(r), obs.shape[0], obs, _c(u0), u, x,
+                                    C.byref(it))
+    return dict(u=u, x=x, status=st, iters=it.value)
+
+
+def filter_swarm_hocbf(p, hp, pos, vel, n_obs, ego_begin=None, ego_end=None):
+    pos = _c(pos).reshape(-1, 2); vel = _c(vel).reshape(-1, 2)
+    n = pos.shape[0]
+    eb = n_obs if ego_begin is None else ego_begin
+    ee = n if ego_end is None else ego_end
+    ne = ee - eb
+    u = np.zeros((ne, 2)); st = np.zeros(ne, np.int32); cnt = np.zeros(ne, np.int32); x = np.zeros((ne, 2))
+    lib().orc_filter_swarm_hocbf(C.byref(params(p)), hp.a_sum, hp.a_prod, n, n_obs, pos, vel, eb, ee, u, st, cnt,
+                                 x.ctypes.data)
+    return dict(u=u, status=st, cnt=cnt, x=x)

@@ -357,3 +357,89 @@ def lattice_neighbors(i, W, H):
 def euler(pos, vel, T):
     """p <- p + T*v (cross_and_rescue.py:173)."""
     return np.asarray(pos) + T * np.asarray(vel)
+
+
+# --------------------------------------------------------------------------------------
+# Euclidean HOCBF barrier mode (BASELINE.json north star (2); SURVEY 8f rank 4).
+# The reference has no such mode, so there is no reference oracle: this restatement
+# defines the arithmetic (Python == C oracle == device, bit for bit) and the QP minimiser
+# is certified by the brute-force KKT check of tests/golden/qp_bruteforce.py.
+#
+# Double integrator per agent: p' = v, v' = u.  For ego i and neighbour j (constant
+# velocity, u_j = 0 -- the decentralised convention of cbf.py, which reads neighbour states
+# only):  h = |p_i - p_j|^2 - Ds^2,  h' = 2 dp.dv,  h'' = 2|dv|^2 + 2 dp.u,
+# psi1 = h' + a1 h,  psi2 = psi1' + a2 psi1 = h'' + (a1 + a2) h' + a1 a2 h >= 0, i.e.
+#     (-2 dp) . u  <=  2|dv|^2 + (a1 + a2) h' + a1 a2 h                    (Ds = dmin)
+# and with x = u - u0 (cbf.py's decision variable):  (-2 dp) . x <= rhs - (-2 dp) . u0.
+# Box rows, +1 relaxation, de-bias and clip are the reference's (cbf.py:62-92) unchanged;
+# every barrier row is its own half-plane (no per-quadrant merge), in neighbour order.
+# --------------------------------------------------------------------------------------
+class HocbfParams:
+    def __init__(self, alpha1=1.0, alpha2=1.0):
+        self.alpha1 = float(alpha1)
+        self.alpha2 = float(alpha2)
+        self.a_sum = self.alpha1 + self.alpha2
+        self.a_prod = self.alpha1 * self.alpha2
+
+
+def hocbf_row(p: Params, hp: HocbfParams, r, o, u0):
+    """(a0, a1, b) of one Euclidean HOCBF row; evaluation order fixed (no fma)."""
+    dx = float(r[0]) - float(o[0])
+    dy = float(r[1]) - float(o[1])
+    dvx = float(r[2]) - float(o[2])
+    dvy = float(r[3]) - float(o[3])
+    h = (dx * dx + dy * dy) - p.dmin * p.dmin
+    hd = 2.0 * (dx * dvx + dy * dvy)
+    vv = dvx * dvx + dvy * dvy
+    rhs = (2.0 * vv + hp.a_sum * hd) + hp.a_prod * h
+    a0 = -2.0 * dx
+    a1 = -2.0 * dy
+    return a0, a1, rhs - (a0 * float(u0[0]) + a1 * float(u0[1]))
+
+
+def filter_one_hocbf(p: Params, hp: HocbfParams, r, obs, u0):
+    """get_safe_control with Euclidean HOCBF rows: box planes first (merged as in the
+    reference mode), then one plane per neighbour in order; +1 relaxation of every barrier
+    row while infeasible (cbf.py:84-87 rule)."""
+    u0 = [float(u0[0]), float(u0[1])]
+    rows = [hocbf_row(p, hp, r, o, u0) for o in obs]
+    box = _box_planes(box_rhs(p, r, u0))
+    fail, x0, x1 = solve_halfplanes(box + rows)
+    status, iters = STATUS_OPTIMAL, 0
+    if fail >= 0:
+        if fail < 4:
+            status, x0, x1 = STATUS_BOX_INFEASIBLE, 0.0, 0.0
+        else:
+            while True:
+                rows = [(a0, a1, b + 1.0) for (a0, a1, b) in rows]
+                iters += 1
+                fail, x0, x1 = solve_halfplanes(box + rows)
+                if fail < 0:
+                    status = STATUS_RELAXED
+                    break
+                if iters >= RELAX_CAP:
+                    status, x0, x1 = STATUS_RELAX_CAP, 0.0, 0.0
+                    break
+    return dict(u=clip(p, x0, x1, u0), x=[x0, x1], status=status, iters=iters, rows=box + rows)
+
+
+def filter_swarm_hocbf(p: Params, hp: HocbfParams, pos, vel, n_obs, ego_begin, ego_end):
+    """filter_swarm (cross_and_rescue.py:135-160 loop) with Euclidean HOCBF rows; the ego
+    state is (pos, vel) with u0 = vel as in the reference mode."""
+    pos = np.asarray(pos, dtype=np.float64)
+    vel = np.asarray(vel, dtype=np.float64)
+    n = ego_end - ego_begin
+    u = np.zeros((n, 2)); status = np.zeros(n, np.int32); cnt = np.zeros(n, np.int32)
+    for e in range(ego_begin, ego_end):
+        nb = cull_one(p, pos, n_obs, e)
+        k = e - ego_begin
+        cnt[k] = len(nb)
+        if not nb:
+            u[k] = vel[e]
+            continue
+        r = [pos[e, 0], pos[e, 1], vel[e, 0], vel[e, 1]]
+        obs = [[pos[j, 0], pos[j, 1], vel[j, 0], vel[j, 1]] for j in nb]
+        res = filter_one_hocbf(p, hp, r, obs, vel[e])
+        u[k] = res["u"]
+        status[k] = res["status"] | (min(res["iters"], (1 << 23) - 1) << 8)
+    return u, status, cnt
