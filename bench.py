@@ -218,13 +218,17 @@ def bench_mc(args, ws, rank, local):
     pos0 = scenarios.mc_scenarios(args.mc_scenarios, n_o, n_a, seed=args.seed)[lo:hi]
     P = torch.tensor(pos0, device="cuda")
     fp = swarm.FilterParams()
-    for _ in range(args.warmup):
-        swarm.mc_rollout(fp, P, n_o, n_a, args.mc_inner, ga=scenarios.MC_GAIN)
+    tot = torch.zeros(4, dtype=torch.int64, device="cuda")
+    mv = torch.zeros(1, dtype=torch.float64, device="cuda")
+    for _ in range(max(1, args.warmup)):  # the same ops as a timed step (loads torch's kernels too)
+        cnt, m = swarm.mc_rollout(fp, P, n_o, n_a, args.mc_inner, ga=scenarios.MC_GAIN)
+        tot += cnt.sum(0)
+        mv = torch.maximum(mv, m.max().reshape(1))
+    tot.zero_()
+    mv.zero_()
     if ws > 1:
         torch.distributed.barrier()
     torch.cuda.synchronize()
-    tot = torch.zeros(4, dtype=torch.int64, device="cuda")
-    mv = torch.zeros(1, dtype=torch.float64, device="cuda")
     t0 = time.perf_counter()
     for _ in range(args.steps):
         cnt, m = swarm.mc_rollout(fp, P, n_o, n_a, args.mc_inner, ga=scenarios.MC_GAIN)

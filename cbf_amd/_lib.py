@@ -16,6 +16,7 @@ LIB_PATH = os.path.join(PKG, "libcbf_amd.so")
 
 CBF_EINVAL = -1
 STATUS_IDLE, STATUS_OPTIMAL, STATUS_RELAXED, STATUS_BOX_INFEASIBLE, STATUS_RELAX_CAP = 0, 1, 2, 3, 4
+STATUS_NBR_OVERFLOW = 5
 
 
 class CbfParams(C.Structure):
@@ -29,6 +30,10 @@ class CbfGrid(C.Structure):
                 ("ny", C.c_int32)]
 
 
+class CbfHocbf(C.Structure):
+    _fields_ = [("alpha1", C.c_double), ("alpha2", C.c_double)]
+
+
 class CbfDiag(C.Structure):
     _fields_ = [("kmax", C.c_int32), ("nbr_idx", C.c_void_p), ("nbr_active", C.c_void_p),
                 ("box_active", C.c_void_p), ("x", C.c_void_p), ("viol", C.c_void_p)]
@@ -37,12 +42,18 @@ class CbfDiag(C.Structure):
 # symbol -> (restype, argtypes); kept in sync with include/cbf_amd.h (tests check every export)
 _vp, _i32, _d, _sz = C.c_void_p, C.c_int32, C.c_double, C.c_size_t
 _P, _G, _D = C.POINTER(CbfParams), C.POINTER(CbfGrid), C.POINTER(CbfDiag)
+_HP = C.POINTER(CbfHocbf)
 SIGNATURES = {
     "cbf_abi_version": (C.c_int, []),
     "cbf_params_init": (C.c_int, [_P, _d, _d, _d, _vp, _vp, _d]),
     "cbf_get_safe_control_batch": (C.c_int, [_P, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "cbf_assemble_rows": (C.c_int, [_P, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "cbf_filter_allpairs": (C.c_int, [_P, _i32, _i32, _vp, _vp, _i32, _i32, _vp, _vp, _vp, _D, _vp]),
+    "cbf_cull_allpairs": (C.c_int, [_P, _i32, _i32, _vp, _i32, _i32, _i32, _vp, _vp, _vp]),
+    "cbf_hocbf_workspace_size": (_sz, [C.c_int64]),
+    "cbf_get_safe_control_batch_hocbf": (C.c_int, [_P, _HP, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _sz, _vp]),
+    "cbf_filter_indexed_hocbf": (C.c_int, [_P, _HP, _i32, _vp, _vp, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _vp,
+                                           _sz, _vp]),
     "cbf_allpairs_workspace_size": (_sz, [_i32, _i32]),
     "cbf_filter_allpairs_split": (C.c_int, [_P, _i32, _i32, _vp, _vp, _i32, _i32, _vp, _vp, _vp, _vp, _sz, _vp]),
     "cbf_cells_workspace_size": (_sz, [_i32, _G]),

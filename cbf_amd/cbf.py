@@ -4,6 +4,11 @@ Same constructor, attributes and ``get_safe_control(robot_state, obs_states, f, 
 signature and return type as the reference; the 2-variable QP is solved exactly on the GPU
 (cbf_get_safe_control_batch) instead of by cvxopt.  ``get_safe_control_batch`` is the batched
 form for many independent egos with explicit neighbour lists.
+
+``barrier="euclidean_hocbf"`` (keyword-only, not in the reference) swaps the reference's
+sign-switched L1 barrier rows (cbf.py:38-59) for Euclidean HOCBF rows of a double integrator,
+h = |p_i - p_j|^2 - dmin^2 with psi1 = h' + alpha1 h, psi2 = psi1' + alpha2 psi1 >= 0
+(include/cbf_amd.h); f and g are then not used (the dynamics are p' = v, v' = u).
 """
 from __future__ import annotations
 
@@ -13,13 +18,21 @@ from . import _lib
 from ._lib import check, lib, ptr, stream_handle
 
 
+BARRIERS = ("reference", "euclidean_hocbf")
+
+
 class ControlBarrierFunction:
-    def __init__(self, max_speed, dmin=0.2, k=1):
-        """cbf.py:6-16."""
+    def __init__(self, max_speed, dmin=0.2, k=1, *, barrier="reference", alpha1=1.0, alpha2=1.0):
+        """cbf.py:6-16 (barrier / alpha1 / alpha2: the HOCBF mode, see the module docstring)."""
         self.dmin = dmin
         self.k = k
         self.max_speed = max_speed
         self.gamma = 0.5
+        if barrier not in BARRIERS:
+            raise ValueError(f"barrier must be one of {BARRIERS}, got {barrier!r}")
+        self.barrier = barrier
+        self.alpha1 = float(alpha1)
+        self.alpha2 = float(alpha2)
 
     def _params(self, f, g):
         f = np.asarray(f, dtype=np.float64)
@@ -69,6 +82,15 @@ class ControlBarrierFunction:
         u = torch.empty((B, 2), dtype=torch.float64, device=dev)
         st = torch.empty((B,), dtype=torch.int32, device=dev)
         x = torch.empty((B, 2), dtype=torch.float64, device=dev) if return_x else None
+        if self.barrier == "euclidean_hocbf":
+            rows = int(off[-1].item())
+            need = lib.cbf_hocbf_workspace_size(rows)
+            ws = torch.empty((need,), dtype=torch.uint8, device=dev)
+            hp = _lib.CbfHocbf(self.alpha1, self.alpha2)
+            check(lib.cbf_get_safe_control_batch_hocbf(p, _lib.C.byref(hp), B, ptr(rs), ptr(u0), ptr(off), ptr(obs),
+                                                       ptr(u), ptr(st), ptr(x), ptr(ws), need, stream_handle()),
+                  "cbf_get_safe_control_batch_hocbf")
+            return u, st, x
         check(lib.cbf_get_safe_control_batch(p, B, ptr(rs), ptr(u0), ptr(off), ptr(obs), ptr(u), ptr(st), ptr(x),
                                              stream_handle()), "cbf_get_safe_control_batch")
         return u, st, x

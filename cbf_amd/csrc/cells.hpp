@@ -13,7 +13,10 @@
 namespace cbf {
 
 constexpr int kScanTile = 2048;  // 256 threads x 8 cells
-constexpr int kHardBlocks = 256; // grid (64-lane blocks) of the hard-QP kernel of the lattice step
+#ifndef CBF_HARD_BLOCKS
+#define CBF_HARD_BLOCKS 256
+#endif
+constexpr int kHardBlocks = CBF_HARD_BLOCKS;  // grid (64-lane blocks) of the hard-QP kernel of the lattice step
 constexpr int kHardHeader = 16;  // int32 words ahead of the hard-QP records (count + padding)
 
 // A QP the filter kernel could not solve at the origin, queued with its assembled state.

@@ -164,14 +164,15 @@ struct ApLds {
     double smax[kBlock / 64];
 };
 
-__device__ __forceinline__ void allpairs_scan(const KP& P, Ego& E, bool active, int c0, int c1, int n_obs,
+template <class Hit>
+__device__ __forceinline__ void allpairs_scan(const KP& P, double r0, double r1, bool active, int c0, int c1,
                                               const double2* __restrict__ pos, const double2* __restrict__ vel,
-                                              const cbf_diag& D, int k, int& recorded, ApLds& L) {
+                                              ApLds& L, Hit& hit) {
     constexpr int kScreen = CBF_AP_SCREEN;
     constexpr int kTile = CBF_AP_TILE;
     constexpr int kPer = kTile / kBlock;
-    const float ex = (float)E.r0, ey = (float)E.r1;
-    double m_ego = absmax2(make_double2(E.r0, E.r1));
+    const float ex = (float)r0, ey = (float)r1;
+    double m_ego = absmax2(make_double2(r0, r1));
     if (m_ego != m_ego) m_ego = INFINITY;
     for (int base = c0; base < c1; base += kTile) {
         double mj = 0.0;
@@ -214,15 +215,46 @@ __device__ __forceinline__ void allpairs_scan(const KP& P, Ego& E, bool active, 
                     if (mn < t32) {
 #pragma unroll
                         for (int q = 0; q < kScreen; ++q)
-                            if (sq[q] < t32) ap_exact(P, E, L.sp, L.sv, base, t + q, n_obs, D, k, recorded);
+                            if (sq[q] < t32) hit(base, t + q);
                     }
                 }
             }
-            for (; t < m; ++t) ap_exact(P, E, L.sp, L.sv, base, t, n_obs, D, k, recorded);
+            for (; t < m; ++t) hit(base, t);
         }
         __syncthreads();
     }
 }
+
+// hit visitors of allpairs_scan (called for candidates the screen lets through)
+struct HitAssemble {  // exact test + row assembly into the ego's QP (+ neighbour list)
+    const KP& P;
+    Ego& E;
+    const ApLds& L;
+    int n_obs;
+    const cbf_diag& D;
+    int k;
+    int recorded;
+    __device__ __forceinline__ void operator()(int base, int t) {
+        ap_exact(P, E, L.sp, L.sv, base, t, n_obs, D, k, recorded);
+    }
+};
+struct HitRecord {  // exact test only: neighbour indices (first kmax, ascending) and count
+    const KP& P;
+    const ApLds& L;
+    double r0, r1;
+    int n_obs;
+    int32_t* idx;
+    int kmax;
+    int count;
+    __device__ __forceinline__ void operator()(int base, int t) {
+        const double2 pj = L.sp[t];
+        double s;
+        if (cull_keep(P, r0, r1, pj.x, pj.y, base + t < n_obs, s)) {
+            if (count < kmax) idx[count] = base + t;
+            ++count;
+        }
+    }
+};
 
 __global__ void __launch_bounds__(kBlock) k_filter_allpairs(KP P, int n, int n_obs, const double2* __restrict__ pos,
                                                             const double2* __restrict__ vel, int ego_begin,
@@ -239,14 +271,32 @@ __global__ void __launch_bounds__(kBlock) k_filter_allpairs(KP P, int n, int n_o
         ego_init(P, E, pe.x, pe.y, ve.x, ve.y, ve.x, ve.y);
     }
     const int k = e - ego_begin;
-    int recorded = 0;
-    allpairs_scan(P, E, active, 0, n, n_obs, pos, vel, D, k, recorded, L);
+    HitAssemble hit{P, E, L, n_obs, D, k, 0};
+    allpairs_scan(P, E.r0, E.r1, active, 0, n, pos, vel, L, hit);
     if (!active) return;
     if (D.nbr_idx)
-        for (int t = recorded; t < D.kmax; ++t) D.nbr_idx[(long)k * D.kmax + t] = -1;
+        for (int t = hit.recorded; t < D.kmax; ++t) D.nbr_idx[(long)k * D.kmax + t] = -1;
     Sol S;
     finish_ego(P, E, k, u, status, cnt, S);
     write_diag(P, E, S, k, pos, vel, D);
+}
+
+// All-pairs cull only (cross_and_rescue.py:141-150): per ego the first kmax neighbour indices in
+// reference order (obstacles, then agents, ascending) and the full count.
+__global__ void __launch_bounds__(kBlock) k_cull_allpairs(KP P, int n, int n_obs, const double2* __restrict__ pos,
+                                                          int ego_begin, int ego_end, int kmax,
+                                                          int32_t* __restrict__ nbr_idx,
+                                                          int32_t* __restrict__ nbr_count) {
+    __shared__ ApLds L;
+    const int e = ego_begin + blockIdx.x * kBlock + threadIdx.x;
+    const bool active = e < ego_end;
+    const double2 pe = active ? pos[e] : make_double2(0, 0);
+    const long k = e - ego_begin;
+    HitRecord hit{P, L, pe.x, pe.y, n_obs, nbr_idx + k * kmax, kmax, 0};
+    allpairs_scan(P, pe.x, pe.y, active, 0, n, pos, pos, L, hit);
+    if (!active) return;
+    for (int t = hit.count; t < kmax; ++t) nbr_idx[k * kmax + t] = -1;
+    nbr_count[k] = hit.count;
 }
 
 // Split all-pairs: workgroup (x, y) runs egos [x*kBlock, ...) against candidate chunk y and
@@ -284,9 +334,9 @@ __global__ void __launch_bounds__(kBlock) k_allpairs_partial(KP P, int n, int n_
     const int c0 = blockIdx.y * chunk;
     const int c1 = min(n, c0 + chunk);
     const int k = e - ego_begin;
-    int recorded = 0;
     const cbf_diag D0 = {};
-    allpairs_scan(P, E, active, c0, c1, n_obs, pos, vel, D0, k, recorded, L);
+    HitAssemble hit{P, E, L, n_obs, D0, k, 0};
+    allpairs_scan(P, E.r0, E.r1, active, c0, c1, pos, vel, L, hit);
     if (!active) return;
     ApPart o;
     o.bq0 = E.bq0;
@@ -431,6 +481,18 @@ extern "C" int cbf_filter_allpairs(const cbf_params* p, int32_t n, int32_t n_obs
     hipLaunchKernelGGL(k_filter_allpairs, dim3(grid_for(ne)), dim3(kBlock), 0, (hipStream_t)stream, make_kp(p), n,
                        n_obs, reinterpret_cast<const double2*>(pos), reinterpret_cast<const double2*>(vel),
                        ego_begin, ego_end, u, status, nbr_count, diag_or_empty(diag));
+    return (int)hipGetLastError();
+}
+
+extern "C" int cbf_cull_allpairs(const cbf_params* p, int32_t n, int32_t n_obs, const double* pos, int32_t ego_begin,
+                                 int32_t ego_end, int32_t kmax, int32_t* nbr_idx, int32_t* nbr_count, void* stream) {
+    if (!p || n < 0 || n_obs < 0 || n_obs > n || ego_begin < n_obs || ego_end > n || ego_begin > ego_end || kmax < 0)
+        return CBF_EINVAL;
+    const int ne = ego_end - ego_begin;
+    if (ne == 0) return 0;
+    if (!pos || !nbr_count || (kmax > 0 && !nbr_idx)) return CBF_EINVAL;
+    hipLaunchKernelGGL(k_cull_allpairs, dim3(grid_for(ne)), dim3(kBlock), 0, (hipStream_t)stream, make_kp(p), n, n_obs,
+                       reinterpret_cast<const double2*>(pos), ego_begin, ego_end, kmax, nbr_idx, nbr_count);
     return (int)hipGetLastError();
 }
 

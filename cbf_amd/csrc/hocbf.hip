@@ -1,0 +1,242 @@
+// hocbf.hip -- Euclidean HOCBF barrier mode on gfx950 (BASELINE.json north star (2); SURVEY 8f
+// rank 4).  The reference's barrier is the sign-switched L1 form of cbf.py:38-59; this mode swaps
+// it for h_ij = |p_i - p_j|^2 - Ds^2 with its relative-degree-2 psi terms (double integrator
+// p' = v, v' = u, neighbours at constant velocity):
+//     (-2 dp) . u  <=  2|dv|^2 + (a1 + a2) h' + a1 a2 h,   h' = 2 dp.dv,
+// keeping everything else of get_safe_control (box rows, +1 relaxation, de-bias, clip).  Every
+// barrier row is its own half-plane, so the exact 2-D solve is the general incremental one over
+// 4 box planes + m rows (rows live in a caller workspace, 32 B each, relaxed in place).  Same
+// arithmetic, order and tolerances as oracle/cbf_oracle.c (hocbf_row / solve_hocbf), so results
+// are bit-identical to the oracle.
+#include "cbf_device.hpp"
+
+using namespace cbf;
+
+namespace {
+
+struct HP {
+    double a_sum, a_prod;  // alpha1 + alpha2, alpha1 * alpha2 (fp64, as the oracle forms them)
+};
+
+__device__ __forceinline__ double4 hocbf_row(const KP& P, const HP& H, double r0, double r1, double r2, double r3,
+                                             double o0, double o1, double o2, double o3, double u0x, double u0y) {
+    const double dx = r0 - o0, dy = r1 - o1, dvx = r2 - o2, dvy = r3 - o3;
+    const double h = (dx * dx + dy * dy) - P.dmin * P.dmin;
+    const double hd = 2.0 * (dx * dvx + dy * dvy);
+    const double vv = dvx * dvx + dvy * dvy;
+    const double rhs = (2.0 * vv + H.a_sum * hd) + H.a_prod * h;
+    const double a0 = -2.0 * dx, a1 = -2.0 * dy;
+    return make_double4(a0, a1, rhs - (a0 * u0x + a1 * u0y), 0.0);
+}
+
+// plane h of [4 merged box planes, rows...] without dynamic indexing of register arrays
+__device__ __forceinline__ void plane(int h, const double (&bb)[4], const double4* rows, double& a0, double& a1,
+                                      double& b) {
+    if (h >= 4) {
+        const double4 r = rows[h - 4];
+        a0 = r.x;
+        a1 = r.y;
+        b = r.z;
+    } else {
+        a0 = h == 0 ? 1.0 : (h == 2 ? -1.0 : 0.0);
+        a1 = h == 1 ? 1.0 : (h == 3 ? -1.0 : 0.0);
+        b = h == 0 ? bb[0] : (h == 1 ? bb[1] : (h == 2 ? bb[2] : bb[3]));
+    }
+}
+
+__device__ __forceinline__ bool feas(double a0, double a1, double b, double x0, double x1) {
+    return (a0 * x0 + a1 * x1) - b <= FEAS_TOL * pmax(1.0, fabs(b));
+}
+
+// oracle/cbf_oracle.c:solve_planes_n over n = 4 + m planes
+__device__ int solve_rows(const double (&bb)[4], int m, const double4* rows, double& xo0, double& xo1) {
+    const int n = 4 + m;
+    double x0 = 0.0, x1 = 0.0;
+    for (int h = 0; h < n; ++h) {
+        double a0, a1, b;
+        plane(h, bb, rows, a0, a1, b);
+        if (feas(a0, a1, b, x0, x1)) continue;
+        const double n2 = a0 * a0 + a1 * a1;
+        if (!(n2 > 0)) return h;
+        const double t = b / n2;
+        const double p0 = t * a0, p1 = t * a1;
+        const double d0 = -a1, d1 = a0;
+        double rh = 0.0, ah = 0.0, rl = 0.0, al = 0.0;
+        bool has_hi = false, has_lo = false;
+        for (int j = 0; j < h; ++j) {
+            double c0, c1, e;
+            plane(j, bb, rows, c0, c1, e);
+            const double ad = c0 * d0 + c1 * d1;
+            const double r = e - (c0 * p0 + c1 * p1);
+            if (ad > 0) {
+                if (!has_hi || r * ah < rh * ad) {
+                    rh = r;
+                    ah = ad;
+                }
+                has_hi = true;
+            } else if (ad < 0) {
+                if (!has_lo || r * al > rl * ad) {
+                    rl = r;
+                    al = ad;
+                }
+                has_lo = true;
+            }
+        }
+        double s = 0.0;
+        bool s_hi = false;
+        if (has_hi && rh < 0) {
+            s = rh / ah;
+            s_hi = true;
+        }
+        if (has_lo && (s_hi ? (rh * al > rl * ah) : (rl < 0))) s = rl / al;
+        x0 = p0 + s * d0;
+        x1 = p1 + s * d1;
+        for (int j = 0; j <= h; ++j) {
+            double c0, c1, e;
+            plane(j, bb, rows, c0, c1, e);
+            if (!feas(c0, c1, e, x0, x1)) return h;
+        }
+    }
+    xo0 = x0;
+    xo1 = x1;
+    return -1;
+}
+
+// oracle/cbf_oracle.c:solve_hocbf -- rows (already assembled) relaxed in place while infeasible
+__device__ Sol solve_hocbf(const KP& P, const Ego& E, int m, double4* rows) {
+    const Box B = box_rhs(P, E);
+    const double bb[4] = {pmin(B.S[0], B.S[4]), pmin(B.S[1], B.S[6]), pmin(B.S[2], B.S[5]), pmin(B.S[3], B.S[7])};
+    Sol S;
+    S.status = CBF_STATUS_OPTIMAL;
+    S.iters = 0;
+    S.x0 = S.x1 = 0.0;
+    S.viol = 0.0;
+    for (;;) {
+        const int fail = solve_rows(bb, m, rows, S.x0, S.x1);
+        if (fail < 0) break;
+        if (fail < 4) {
+            S.status = CBF_STATUS_BOX_INFEASIBLE;
+            S.x0 = S.x1 = 0.0;
+            break;
+        }
+        if (S.iters >= P.relax_cap) {
+            S.status = CBF_STATUS_RELAX_CAP;
+            S.x0 = S.x1 = 0.0;
+            break;
+        }
+        for (int i = 0; i < m; ++i) rows[i].z = rows[i].z + 1.0;  // cbf.py:85-87
+        S.iters++;
+        S.status = CBF_STATUS_RELAXED;
+    }
+    return S;
+}
+
+// get_safe_control with explicit neighbour lists (CSR): rows of ego i at ws[off[i] .. off[i+1])
+__global__ void __launch_bounds__(kBlock) k_hocbf_batch(KP P, HP H, int n, const double* __restrict__ rs,
+                                                        const double* __restrict__ u0, const int32_t* __restrict__ off,
+                                                        const double* __restrict__ obs, double* __restrict__ u,
+                                                        int32_t* __restrict__ status, double* __restrict__ xo,
+                                                        double4* __restrict__ ws) {
+    const int i = blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    const double2 ra = reinterpret_cast<const double2*>(rs)[2 * i];
+    const double2 rb = reinterpret_cast<const double2*>(rs)[2 * i + 1];
+    const double2 uu = reinterpret_cast<const double2*>(u0)[i];
+    Ego E;
+    ego_init(P, E, ra.x, ra.y, rb.x, rb.y, uu.x, uu.y);
+    const int t0 = off[i], m = off[i + 1] - off[i];
+    double4* rows = ws + t0;
+    for (int t = 0; t < m; ++t) {
+        const double2 oa = reinterpret_cast<const double2*>(obs)[2 * (t0 + t)];
+        const double2 ob = reinterpret_cast<const double2*>(obs)[2 * (t0 + t) + 1];
+        rows[t] = hocbf_row(P, H, E.r0, E.r1, E.r2, E.r3, oa.x, oa.y, ob.x, ob.y, E.u0x, E.u0y);
+    }
+    const Sol S = solve_hocbf(P, E, m, rows);
+    double ux, uy;
+    clip_u(P, S, E, ux, uy);
+    reinterpret_cast<double2*>(u)[i] = make_double2(ux, uy);
+    status[i] = pack_status(S);
+    if (xo) reinterpret_cast<double2*>(xo)[i] = make_double2(S.x0, S.x1);
+}
+
+// swarm form: ego e = ego_begin + k with the neighbour indices of cbf_cull_allpairs (reference
+// order); ego state (pos, vel), u0 = vel; rows at ws[k * kmax ..]
+__global__ void __launch_bounds__(kBlock) k_hocbf_indexed(KP P, HP H, const double2* __restrict__ pos,
+                                                          const double2* __restrict__ vel, int ego_begin, int ego_end,
+                                                          int kmax, const int32_t* __restrict__ nbr_idx,
+                                                          const int32_t* __restrict__ nbr_count,
+                                                          double* __restrict__ u, int32_t* __restrict__ status,
+                                                          double* __restrict__ xo, double4* __restrict__ ws) {
+    const int e = ego_begin + blockIdx.x * kBlock + threadIdx.x;
+    if (e >= ego_end) return;
+    const long k = e - ego_begin;
+    const double2 pe = pos[e], ve = vel[e];
+    Ego E;
+    ego_init(P, E, pe.x, pe.y, ve.x, ve.y, ve.x, ve.y);
+    const int m = nbr_count[k];
+    double ux = E.u0x, uy = E.u0y;  // no neighbour: filter not run, u0 unclipped (cross_and_rescue.py:153)
+    int32_t st = CBF_STATUS_IDLE;
+    double x0 = 0.0, x1 = 0.0;
+    if (m > kmax) {
+        st = CBF_STATUS_NBR_OVERFLOW;
+    } else if (m > 0) {
+        double4* rows = ws + k * kmax;
+        for (int t = 0; t < m; ++t) {
+            const int j = nbr_idx[k * kmax + t];
+            const double2 pj = pos[j], vj = vel[j];
+            rows[t] = hocbf_row(P, H, E.r0, E.r1, E.r2, E.r3, pj.x, pj.y, vj.x, vj.y, E.u0x, E.u0y);
+        }
+        const Sol S = solve_hocbf(P, E, m, rows);
+        clip_u(P, S, E, ux, uy);
+        st = pack_status(S);
+        x0 = S.x0;
+        x1 = S.x1;
+    }
+    reinterpret_cast<double2*>(u)[k] = make_double2(ux, uy);
+    status[k] = st;
+    if (xo) reinterpret_cast<double2*>(xo)[k] = make_double2(x0, x1);
+}
+
+inline int nblocks(long n) { return (int)((n + kBlock - 1) / kBlock); }
+
+inline HP make_hp(const cbf_hocbf* h) {
+    HP o;
+    o.a_sum = h->alpha1 + h->alpha2;
+    o.a_prod = h->alpha1 * h->alpha2;
+    return o;
+}
+
+}  // namespace
+
+extern "C" size_t cbf_hocbf_workspace_size(int64_t rows) { return rows > 0 ? 32 * (size_t)rows : 32; }
+
+extern "C" int cbf_get_safe_control_batch_hocbf(const cbf_params* p, const cbf_hocbf* hp, int32_t n_ego,
+                                                const double* robot_state, const double* u0, const int32_t* nbr_off,
+                                                const double* obs_states, double* u, int32_t* status, double* x_out,
+                                                void* workspace, size_t workspace_bytes, void* stream) {
+    if (!p || !hp || n_ego < 0) return CBF_EINVAL;
+    if (n_ego == 0) return 0;
+    if (!robot_state || !u0 || !nbr_off || !u || !status || !workspace) return CBF_EINVAL;
+    // the row count lives on the device (nbr_off[n_ego]): the caller sizes the workspace for it
+    if (workspace_bytes < 32) return CBF_EINVAL;
+    hipLaunchKernelGGL(k_hocbf_batch, dim3(nblocks(n_ego)), dim3(kBlock), 0, (hipStream_t)stream, make_kp(p),
+                       make_hp(hp), n_ego, robot_state, u0, nbr_off, obs_states, u, status, x_out,
+                       reinterpret_cast<double4*>(workspace));
+    return (int)hipGetLastError();
+}
+
+extern "C" int cbf_filter_indexed_hocbf(const cbf_params* p, const cbf_hocbf* hp, int32_t n, const double* pos,
+                                        const double* vel, int32_t ego_begin, int32_t ego_end, int32_t kmax,
+                                        const int32_t* nbr_idx, const int32_t* nbr_count, double* u, int32_t* status,
+                                        double* x_out, void* workspace, size_t workspace_bytes, void* stream) {
+    if (!p || !hp || n < 0 || ego_begin < 0 || ego_end > n || ego_begin > ego_end || kmax < 0) return CBF_EINVAL;
+    const long ne = ego_end - ego_begin;
+    if (ne == 0) return 0;
+    if (!pos || !vel || !nbr_count || !u || !status || (kmax > 0 && (!nbr_idx || !workspace))) return CBF_EINVAL;
+    if (kmax > 0 && workspace_bytes < cbf_hocbf_workspace_size(ne * kmax)) return CBF_EINVAL;
+    hipLaunchKernelGGL(k_hocbf_indexed, dim3(nblocks(ne)), dim3(kBlock), 0, (hipStream_t)stream, make_kp(p),
+                       make_hp(hp), reinterpret_cast<const double2*>(pos), reinterpret_cast<const double2*>(vel),
+                       ego_begin, ego_end, kmax, nbr_idx, nbr_count, u, status, x_out,
+                       reinterpret_cast<double4*>(workspace));
+    return (int)hipGetLastError();
+}

@@ -45,6 +45,45 @@ def grid_for_points(pos_np, cull_radius, margin=1.0, cell_factor=1.02):
     return make_grid(lo[0], lo[1], hi[0], hi[1], cull_radius * cell_factor)
 
 
+def filter_swarm_hocbf(params, pos, vel, n_obs, ego_begin=None, ego_end=None, alpha=(1.0, 1.0), kmax=32,
+                       return_x=False):
+    """The swarm loop (cross_and_rescue.py:135-160 shape) with Euclidean HOCBF rows: all-pairs
+    cull in reference order (cbf_cull_allpairs), then the HOCBF QP per ego
+    (cbf_filter_indexed_hocbf).  kmax grows to the largest neighbour count if needed."""
+    torch = _lib.require_gpu()
+    n = pos.shape[0]
+    eb = n_obs if ego_begin is None else ego_begin
+    ee = n if ego_end is None else ego_end
+    ne = ee - eb
+    if not (0 <= n_obs <= eb <= ee <= n):
+        raise _lib.CbfError(f"filter_swarm_hocbf: need 0 <= n_obs <= ego_begin <= ego_end <= n, got "
+                            f"{n_obs}, {eb}, {ee}, {n}")
+    dev = pos.device
+    pos = pos.contiguous()
+    vel = vel.contiguous()
+    cp = params.c() if isinstance(params, FilterParams) else params
+    cnt = torch.empty((ne,), dtype=torch.int32, device=dev)
+    while True:
+        idx = torch.empty((ne, max(kmax, 1)), dtype=torch.int32, device=dev)
+        check(lib.cbf_cull_allpairs(cp, n, n_obs, ptr(pos), eb, ee, kmax, ptr(idx), ptr(cnt), stream_handle()),
+              "cbf_cull_allpairs")
+        need_k = int(cnt.max().item()) if ne else 0
+        if need_k <= kmax:
+            break
+        kmax = need_k
+    out = {"u": torch.empty((ne, 2), dtype=torch.float64, device=dev),
+           "status": torch.empty((ne,), dtype=torch.int32, device=dev), "nbr_count": cnt, "nbr_idx": idx}
+    if return_x:
+        out["x"] = torch.empty((ne, 2), dtype=torch.float64, device=dev)
+    need = lib.cbf_hocbf_workspace_size(ne * kmax)
+    ws = torch.empty((need,), dtype=torch.uint8, device=dev)
+    hp = _lib.CbfHocbf(float(alpha[0]), float(alpha[1]))
+    check(lib.cbf_filter_indexed_hocbf(cp, _lib.C.byref(hp), n, ptr(pos), ptr(vel), eb, ee, kmax, ptr(idx), ptr(cnt),
+                                       ptr(out["u"]), ptr(out["status"]), ptr(out.get("x")), ptr(ws), need,
+                                       stream_handle()), "cbf_filter_indexed_hocbf")
+    return out
+
+
 def filter_swarm(params, pos, vel, n_obs, ego_begin=None, ego_end=None, method="auto", grid=None, kmax=0,
                  diag=False, workspace=None):
     """cross_and_rescue.py:135-160 for every ego in [ego_begin, ego_end).  Returns a dict of

@@ -12,6 +12,9 @@
  *   Euler integration                      cross_and_rescue.py:173 -> cbf_euler
  *   whole timestep (large swarm)           cross_and_rescue.py:97-175 -> cbf_lattice_step
  *   batched Monte-Carlo rendezvous         meet_at_center.py:76-153 (x n_scen) -> cbf_mc_rollout
+ *   cull alone (neighbour index sets)      cross_and_rescue.py:141-150 -> cbf_cull_allpairs
+ *   Euclidean HOCBF barrier mode           (north star; replaces the rows of cbf.py:38-59)
+ *                                             -> cbf_get_safe_control_batch_hocbf / cbf_filter_indexed_hocbf
  *
  * Conventions
  *  - All arrays are caller-owned DEVICE pointers (hipMalloc / torch CUDA tensors), fp64,
@@ -46,6 +49,7 @@ extern "C" {
 #define CBF_STATUS_RELAXED 2        /* infeasible; CBF rows relaxed by the cbf.py:84-87 rule, then optimal */
 #define CBF_STATUS_BOX_INFEASIBLE 3 /* the 8 box rows alone are infeasible; x = 0 */
 #define CBF_STATUS_RELAX_CAP 4      /* relaxation cap reached; x = 0 */
+#define CBF_STATUS_NBR_OVERFLOW 5   /* indexed HOCBF filter: more neighbours than kmax; u = u0, not filtered */
 
 /* ControlBarrierFunction state (cbf.py:6-16) + the callers' dynamics and cull radius. */
 typedef struct cbf_params {
@@ -112,6 +116,42 @@ size_t cbf_allpairs_workspace_size(int32_t n, int32_t n_ego);
 int cbf_filter_allpairs_split(const cbf_params* p, int32_t n, int32_t n_obs, const double* pos, const double* vel,
                               int32_t ego_begin, int32_t ego_end, double* u, int32_t* status, int32_t* nbr_count,
                               void* workspace, size_t workspace_bytes, void* stream);
+
+/* The cull of cross_and_rescue.py:141-150 alone: per ego e in [ego_begin, ego_end) its neighbour
+ * indices in reference order (obstacles, then agents, ascending), the first kmax in
+ * nbr_idx [n_ego][kmax] (-1 padded), the full count in nbr_count [n_ego]. */
+int cbf_cull_allpairs(const cbf_params* p, int32_t n, int32_t n_obs, const double* pos, int32_t ego_begin,
+                      int32_t ego_end, int32_t kmax, int32_t* nbr_idx, int32_t* nbr_count, void* stream);
+
+/*
+ * Euclidean HOCBF barrier mode (no counterpart in the reference, which uses the sign-switched
+ * L1 barrier of cbf.py:38-59).  Double integrator p' = v, v' = u; neighbours at constant
+ * velocity; h = |p_i - p_j|^2 - dmin^2, psi1 = h' + a1 h, psi2 = psi1' + a2 psi1 >= 0 gives the
+ * row (-2 dp) . u <= 2|dv|^2 + (a1 + a2) h' + a1 a2 h.  Box rows, +1 relaxation, de-bias and
+ * clip are the reference's.  Each barrier row is its own half-plane (neighbour order).
+ * Workspace: 32 bytes per barrier row (cbf_hocbf_workspace_size), rows are relaxed in place.
+ */
+typedef struct cbf_hocbf {
+    double alpha1, alpha2; /* linear class-K gains of psi1 and psi2 */
+} cbf_hocbf;
+
+size_t cbf_hocbf_workspace_size(int64_t rows);
+
+/* get_safe_control with HOCBF rows for a batch with explicit neighbour lists (CSR, as
+ * cbf_get_safe_control_batch); the workspace must hold nbr_off[n_ego] rows. */
+int cbf_get_safe_control_batch_hocbf(const cbf_params* p, const cbf_hocbf* hp, int32_t n_ego,
+                                     const double* robot_state, const double* u0, const int32_t* nbr_off,
+                                     const double* obs_states, double* u, int32_t* status, double* x_out,
+                                     void* workspace, size_t workspace_bytes, void* stream);
+
+/* The swarm loop with HOCBF rows over the neighbour lists of cbf_cull_allpairs: ego e's state is
+ * (pos[e], vel[e]), u0 = vel[e]; no neighbour -> CBF_STATUS_IDLE, u = u0 unclipped; more than
+ * kmax -> CBF_STATUS_NBR_OVERFLOW (rerun with a larger kmax).  Workspace: (ego_end - ego_begin)
+ * * kmax rows.  x_out nullable. */
+int cbf_filter_indexed_hocbf(const cbf_params* p, const cbf_hocbf* hp, int32_t n, const double* pos,
+                             const double* vel, int32_t ego_begin, int32_t ego_end, int32_t kmax,
+                             const int32_t* nbr_idx, const int32_t* nbr_count, double* u, int32_t* status,
+                             double* x_out, void* workspace, size_t workspace_bytes, void* stream);
 
 /* Uniform cell grid: cell (cx, cy) = clamp(floor((p - origin) * inv_h), 0, n-1).  The cell
  * edge 1/inv_h must be >= the cull radius (checked).  Clamping keeps results exact for

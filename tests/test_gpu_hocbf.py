@@ -1,0 +1,94 @@
+"""Euclidean HOCBF barrier mode on the HIP path against the C / Python restatement (bit-exact)
+and the reference-order cull (index sets bit-exact)."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+if not torch.cuda.is_available():
+    pytest.skip("needs a ROCm GPU", allow_module_level=True)
+
+import cbf_amd  # noqa: E402
+from cbf_amd import swarm  # noqa: E402
+from oracle import coracle, pyoracle as po  # noqa: E402
+
+from .test_hocbf_oracle import _cases  # noqa: E402
+
+DEV = torch.device("cuda")
+
+
+def _t(a, dt=torch.float64):
+    return torch.as_tensor(np.ascontiguousarray(a), dtype=dt, device=DEV)
+
+
+def test_batch_vs_oracle():
+    rng = np.random.default_rng(31)
+    groups = {}
+    for p, hp, r, obs, u0 in _cases(rng, 600):
+        groups.setdefault((p.max_speed, p.dmin, hp.alpha1, hp.alpha2), []).append((p, hp, r, obs, u0))
+    n_checked = 0
+    for (ms, dmin, a1, a2), cases in groups.items():
+        c = cbf_amd.ControlBarrierFunction(ms, dmin=dmin, barrier="euclidean_hocbf", alpha1=a1, alpha2=a2)
+        R = np.array([cs[2] for cs in cases])
+        U0 = np.array([cs[4] for cs in cases])
+        u, st, x = c.get_safe_control_batch(_t(R), [_t(cs[3].reshape(-1, 4)) for cs in cases], _t(U0), return_x=True)
+        u, st, x = u.cpu().numpy(), st.cpu().numpy(), x.cpu().numpy()
+        for t, (p, hp, r, obs, u0) in enumerate(cases):
+            ref = coracle.filter_one_hocbf(p, hp, r, obs, u0)
+            assert st[t] & 0xFF == ref["status"] and st[t] >> 8 == ref["iters"], t
+            assert np.array_equal(u[t], ref["u"]) and np.array_equal(x[t], ref["x"]), t
+            n_checked += 1
+    assert n_checked == 600
+
+
+def test_single_call_surface():
+    c = cbf_amd.ControlBarrierFunction(15, barrier="euclidean_hocbf")
+    r = np.array([0.0, 0.0, 0.04, 0.0])
+    u = c.get_safe_control(r, np.array([[0.25, 0.0, 0.0, 0.0]]), np.zeros((4, 4)), np.zeros((4, 2)), [0.0, 0.0])
+    ref = po.filter_one_hocbf(po.Params(15), po.HocbfParams(1.0, 1.0), r, [[0.25, 0.0, 0.0, 0.0]], [0.0, 0.0])
+    assert isinstance(u, np.ndarray) and u.shape == (2,)
+    assert np.array_equal(u, np.array(ref["u"])) and u[0] < 0
+    with pytest.raises(ValueError):
+        cbf_amd.ControlBarrierFunction(15, barrier="nope")
+
+
+@pytest.mark.parametrize("n,n_obs,spread", [(50, 10, 0.4), (2000, 200, 3.0)])
+def test_swarm_vs_oracle(n, n_obs, spread):
+    rng = np.random.default_rng(n)
+    p, hp = po.Params(15), po.HocbfParams(1.0, 2.0)
+    pos = rng.uniform(-spread, spread, (n, 2))
+    vel = rng.normal(0, 0.3, (n, 2))
+    pos[n_obs + 3] = pos[n_obs + 5]               # coincident agents: excluded from each other
+    pos[n_obs + 7] = pos[n_obs + 6] + [0.2, 0.0]  # exactly at the cull radius
+    out = swarm.filter_swarm_hocbf(swarm.FilterParams(), _t(pos), _t(vel), n_obs, alpha=(1.0, 2.0), kmax=4,
+                                   return_x=True)
+    ref = coracle.filter_swarm_hocbf(p, hp, pos, vel, n_obs)
+    assert np.array_equal(out["nbr_count"].cpu().numpy(), ref["cnt"])
+    assert np.array_equal(out["u"].cpu().numpy(), ref["u"])
+    assert np.array_equal(out["status"].cpu().numpy(), ref["status"])
+    assert np.array_equal(out["x"].cpu().numpy(), ref["x"])
+    # neighbour index sets in reference order (cross_and_rescue.py:141-150)
+    idx = out["nbr_idx"].cpu().numpy()
+    for k in range(0, n - n_obs, max(1, (n - n_obs) // 50)):
+        want = po.cull_one(p, pos, n_obs, n_obs + k)
+        assert idx[k, :len(want)].tolist() == want and (idx[k, len(want):] == -1).all()
+
+
+def test_overflow_status_when_kmax_too_small():
+    rng = np.random.default_rng(3)
+    pos = rng.uniform(-0.1, 0.1, (40, 2))
+    vel = np.zeros((40, 2))
+    P = _t(pos)
+    cnt = torch.empty(40, dtype=torch.int32, device=DEV)
+    idx = torch.empty((40, 2), dtype=torch.int32, device=DEV)
+    from cbf_amd._lib import C, CbfHocbf, lib, ptr, stream_handle
+    cp = swarm.FilterParams().c()
+    assert lib.cbf_cull_allpairs(cp, 40, 0, ptr(P), 0, 40, 2, ptr(idx), ptr(cnt), stream_handle()) == 0
+    u = torch.empty((40, 2), dtype=torch.float64, device=DEV)
+    st = torch.empty(40, dtype=torch.int32, device=DEV)
+    ws = torch.empty(lib.cbf_hocbf_workspace_size(80), dtype=torch.uint8, device=DEV)
+    hp = CbfHocbf(1.0, 1.0)
+    assert lib.cbf_filter_indexed_hocbf(cp, C.byref(hp), 40, ptr(P), ptr(_t(vel)), 0, 40, 2, ptr(idx), ptr(cnt),
+                                        ptr(u), ptr(st), None, ptr(ws), ws.numel(), stream_handle()) == 0
+    assert (st.cpu().numpy() == cbf_amd.STATUS_NBR_OVERFLOW).all()
