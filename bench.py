@@ -85,7 +85,7 @@ def bench_lattice(args, ws, rank, local):
         S = ShardedLattice(W, rows, seed=args.seed)
     else:
         pos = scenarios.lattice(W, rows, seed=args.seed)
-        S = swarm.LatticeSwarm(pos, W, rows, gain=scenarios.LATTICE_GAIN)
+        S = swarm.LatticeSwarm(pos, W, rows, gain=scenarios.LATTICE_GAIN, barrier=args.barrier)
     use_graph = not args.eager
     if use_graph:
         S.capture()
@@ -150,7 +150,7 @@ def bench_lattice(args, ws, rank, local):
         "data": "synthetic",
         "config": {"workload": f"cfg4: {W}x{rows * ws} jittered lattice swarm (spacing 0.145), lattice-Laplacian "
                                "consensus + radius-0.2 cell-list cull + CBF QP + clip + Euler, one fused timestep "
-                               "per step",
+                               "per step", "barrier": args.barrier,
                    "agents_total": n_total, "agents_per_gpu": n_local,
                    "parallelism": f"row-stripe shards x{ws}, 1 RCCL all-gather of halo slabs / step" if ws > 1
                    else "single GPU", "graph": use_graph},
@@ -161,7 +161,9 @@ def bench_lattice(args, ws, rank, local):
                                       "box_infeasible": codes[3] / len(status)},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS,
-                     "traffic": traffic, "kernel": "k_lattice_filter", "kernel_ms": k_ms,
+                     "traffic": traffic if args.barrier == "reference" else None,
+                     "kernel": "k_lattice_filter" if args.barrier == "reference" else "k_lattice_filter_hocbf",
+                     "kernel_ms": k_ms,
                      "algorithmic_bytes_per_launch": FILTER_BYTES_PER_AGENT * n_local,
                      "step_algorithmic_GBps": STEP_BYTES_PER_AGENT * n_local * args.steps / elapsed / 1e9 / ws},
     }
@@ -284,6 +286,8 @@ def main():
     ap.add_argument("--eager", action="store_true", help="no hipGraph capture")
     ap.add_argument("--kernel-iters", type=int, default=20)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--barrier", default="reference", choices=["reference", "euclidean_hocbf"],
+                    help="cfg4 single-GPU: the reference's L1 barrier rows or the Euclidean HOCBF mode")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     args = ap.parse_args()
     ws, rank, local = _dist_env()

@@ -9,6 +9,8 @@
 // arithmetic, order and tolerances as oracle/cbf_oracle.c (hocbf_row / solve_hocbf), so results
 // are bit-identical to the oracle.
 #include "cbf_device.hpp"
+#include "cells.hpp"
+#include "lattice.hpp"
 
 using namespace cbf;
 
@@ -29,32 +31,71 @@ __device__ __forceinline__ double4 hocbf_row(const KP& P, const HP& H, double r0
     return make_double4(a0, a1, rhs - (a0 * u0x + a1 * u0y), 0.0);
 }
 
-// plane h of [4 merged box planes, rows...] without dynamic indexing of register arrays
-__device__ __forceinline__ void plane(int h, const double (&bb)[4], const double4* rows, double& a0, double& a1,
-                                      double& b) {
-    if (h >= 4) {
-        const double4 r = rows[h - 4];
-        a0 = r.x;
-        a1 = r.y;
-        b = r.z;
-    } else {
-        a0 = h == 0 ? 1.0 : (h == 2 ? -1.0 : 0.0);
-        a1 = h == 1 ? 1.0 : (h == 3 ? -1.0 : 0.0);
-        b = h == 0 ? bb[0] : (h == 1 ? bb[1] : (h == 2 ? bb[2] : bb[3]));
-    }
+__device__ __forceinline__ void box_plane(int h, const double (&bb)[4], double& a0, double& a1, double& b) {
+    a0 = h == 0 ? 1.0 : (h == 2 ? -1.0 : 0.0);
+    a1 = h == 1 ? 1.0 : (h == 3 ? -1.0 : 0.0);
+    b = h == 0 ? bb[0] : (h == 1 ? bb[1] : (h == 2 ? bb[2] : bb[3]));
 }
+
+// Plane source over rows stored in memory (workspace), relaxed in place.
+struct StoredRows {
+    double4* rows;
+    int m;
+    __device__ __forceinline__ void plane(int h, const double (&bb)[4], double& a0, double& a1, double& b) const {
+        if (h >= 4) {
+            const double4 r = rows[h - 4];
+            a0 = r.x;
+            a1 = r.y;
+            b = r.z;
+        } else {
+            box_plane(h, bb, a0, a1, b);
+        }
+    }
+    __device__ __forceinline__ void relax() {
+        for (int i = 0; i < m; ++i) rows[i].z = rows[i].z + 1.0;  // cbf.py:85-87
+    }
+};
+
+// Plane source recomputing each row from the neighbour's cell-sorted state (lattice step); the
+// neighbours are LDS keys (entity << 32 | slot) in ascending entity order; `t` relaxations are
+// re-applied as t successive +1 additions (the oracle's rounding sequence).
+struct SlotRows {
+    const KP& P;
+    const HP& H;
+    const Ego& E;
+    const unsigned long long* keys;  // keys[i * kBlock + threadIdx.x]
+    const double2* __restrict__ spos;
+    const double2* __restrict__ svel;
+    int m;
+    int t;
+    __device__ __forceinline__ void plane(int h, const double (&bb)[4], double& a0, double& a1, double& b) const {
+        if (h >= 4) {
+            const int slot = (int)(keys[(h - 4) * kBlock + threadIdx.x] & 0xFFFFFFFFull);
+            const double2 o = spos[slot], ov = svel[slot];
+            const double4 r = hocbf_row(P, H, E.r0, E.r1, E.r2, E.r3, o.x, o.y, ov.x, ov.y, E.u0x, E.u0y);
+            a0 = r.x;
+            a1 = r.y;
+            b = r.z;
+            for (int i = 0; i < t; ++i) b = b + 1.0;
+        } else {
+            box_plane(h, bb, a0, a1, b);
+        }
+    }
+    __device__ __forceinline__ void relax() { ++t; }
+};
 
 __device__ __forceinline__ bool feas(double a0, double a1, double b, double x0, double x1) {
     return (a0 * x0 + a1 * x1) - b <= FEAS_TOL * pmax(1.0, fabs(b));
 }
 
 // oracle/cbf_oracle.c:solve_planes_n over n = 4 + m planes
-__device__ int solve_rows(const double (&bb)[4], int m, const double4* rows, double& xo0, double& xo1) {
-    const int n = 4 + m;
+template <class Src>
+__device__ int solve_rows(const double (&bb)[4], const Src& R, double& xo0, double& xo1) {
+    const int n = 4 + R.m;
     double x0 = 0.0, x1 = 0.0;
     for (int h = 0; h < n; ++h) {
         double a0, a1, b;
-        plane(h, bb, rows, a0, a1, b);
+        R.plane(h, bb, a0, a1, b);
         if (feas(a0, a1, b, x0, x1)) continue;
         const double n2 = a0 * a0 + a1 * a1;
         if (!(n2 > 0)) return h;
@@ -65,7 +106,7 @@ __device__ int solve_rows(const double (&bb)[4], int m, const double4* rows, dou
         bool has_hi = false, has_lo = false;
         for (int j = 0; j < h; ++j) {
             double c0, c1, e;
-            plane(j, bb, rows, c0, c1, e);
+            R.plane(j, bb, c0, c1, e);
             const double ad = c0 * d0 + c1 * d1;
             const double r = e - (c0 * p0 + c1 * p1);
             if (ad > 0) {
@@ -93,7 +134,7 @@ __device__ int solve_rows(const double (&bb)[4], int m, const double4* rows, dou
         x1 = p1 + s * d1;
         for (int j = 0; j <= h; ++j) {
             double c0, c1, e;
-            plane(j, bb, rows, c0, c1, e);
+            R.plane(j, bb, c0, c1, e);
             if (!feas(c0, c1, e, x0, x1)) return h;
         }
     }
@@ -102,8 +143,9 @@ __device__ int solve_rows(const double (&bb)[4], int m, const double4* rows, dou
     return -1;
 }
 
-// oracle/cbf_oracle.c:solve_hocbf -- rows (already assembled) relaxed in place while infeasible
-__device__ Sol solve_hocbf(const KP& P, const Ego& E, int m, double4* rows) {
+// oracle/cbf_oracle.c:solve_hocbf -- +1 relaxation of every barrier row while infeasible
+template <class Src>
+__device__ Sol solve_hocbf(const KP& P, const Ego& E, Src& R) {
     const Box B = box_rhs(P, E);
     const double bb[4] = {pmin(B.S[0], B.S[4]), pmin(B.S[1], B.S[6]), pmin(B.S[2], B.S[5]), pmin(B.S[3], B.S[7])};
     Sol S;
@@ -112,7 +154,7 @@ __device__ Sol solve_hocbf(const KP& P, const Ego& E, int m, double4* rows) {
     S.x0 = S.x1 = 0.0;
     S.viol = 0.0;
     for (;;) {
-        const int fail = solve_rows(bb, m, rows, S.x0, S.x1);
+        const int fail = solve_rows(bb, R, S.x0, S.x1);
         if (fail < 0) break;
         if (fail < 4) {
             S.status = CBF_STATUS_BOX_INFEASIBLE;
@@ -124,7 +166,7 @@ __device__ Sol solve_hocbf(const KP& P, const Ego& E, int m, double4* rows) {
             S.x0 = S.x1 = 0.0;
             break;
         }
-        for (int i = 0; i < m; ++i) rows[i].z = rows[i].z + 1.0;  // cbf.py:85-87
+        R.relax();
         S.iters++;
         S.status = CBF_STATUS_RELAXED;
     }
@@ -151,7 +193,8 @@ __global__ void __launch_bounds__(kBlock) k_hocbf_batch(KP P, HP H, int n, const
         const double2 ob = reinterpret_cast<const double2*>(obs)[2 * (t0 + t) + 1];
         rows[t] = hocbf_row(P, H, E.r0, E.r1, E.r2, E.r3, oa.x, oa.y, ob.x, ob.y, E.u0x, E.u0y);
     }
-    const Sol S = solve_hocbf(P, E, m, rows);
+    StoredRows R{rows, m};
+    const Sol S = solve_hocbf(P, E, R);
     double ux, uy;
     clip_u(P, S, E, ux, uy);
     reinterpret_cast<double2*>(u)[i] = make_double2(ux, uy);
@@ -186,7 +229,8 @@ __global__ void __launch_bounds__(kBlock) k_hocbf_indexed(KP P, HP H, const doub
             const double2 pj = pos[j], vj = vel[j];
             rows[t] = hocbf_row(P, H, E.r0, E.r1, E.r2, E.r3, pj.x, pj.y, vj.x, vj.y, E.u0x, E.u0y);
         }
-        const Sol S = solve_hocbf(P, E, m, rows);
+        StoredRows R{rows, m};
+        const Sol S = solve_hocbf(P, E, R);
         clip_u(P, S, E, ux, uy);
         st = pack_status(S);
         x0 = S.x0;
@@ -195,6 +239,88 @@ __global__ void __launch_bounds__(kBlock) k_hocbf_indexed(KP P, HP H, const doub
     reinterpret_cast<double2*>(u)[k] = make_double2(ux, uy);
     status[k] = st;
     if (xo) reinterpret_cast<double2*>(xo)[k] = make_double2(x0, x1);
+}
+
+
+// Lattice step K4 in HOCBF mode: one lane per cell-sorted slot (owned agents); exact cull over
+// the 3x3 cells; hits kept as LDS keys (entity << 32 | slot) in ascending entity order (the
+// oracle's reference-order row sequence, independent of the atomic arrival order inside a cell);
+// rows recomputed from the cell-sorted state during the solve; clip, Euler, outputs as
+// k_lattice_filter.  More than kHocbfCap neighbours: CBF_STATUS_NBR_OVERFLOW, u = u0.
+constexpr int kHocbfCap = 24;
+
+__global__ void __launch_bounds__(kBlock) k_lattice_filter_hocbf(
+    KP P, HP H, CellGrid G, int W, int row_begin, int row_end, int win_row0, long ncell,
+    const double2* __restrict__ spos, const double2* __restrict__ svel, const int32_t* __restrict__ sidx,
+    const int32_t* __restrict__ start, double T, double2* __restrict__ pos_out, double2* __restrict__ u,
+    int32_t* __restrict__ status, int32_t* __restrict__ cnt, int guard_rows, double* __restrict__ ext_part,
+    unsigned long long* __restrict__ solves) {
+    __shared__ unsigned long long keys[kHocbfCap * kBlock];
+    const int slot = blockIdx.x * kBlock + threadIdx.x;
+    const int total = start[ncell];
+    double e0 = INFINITY, e1 = -INFINITY, e2 = -INFINITY, e3 = INFINITY;
+    bool solved = false;
+    if (slot < total) {
+        const int w = sidx[slot];
+        const int r = win_row0 + w / W, c = w % W;
+        if (r >= row_begin && r < row_end) {
+            const double2 pe = spos[slot], ve = svel[slot];
+            Ego E;
+            ego_init(P, E, pe.x, pe.y, ve.x, ve.y, ve.x, ve.y);
+            const int cx = cell_coord(pe.x, G.x0, G.inv_h, G.nx);
+            const int cy = cell_coord(pe.y, G.y0, G.inv_h, G.ny);
+            const int xa = cx > 0 ? cx - 1 : 0;
+            const int xb = cx < G.nx - 1 ? cx + 1 : G.nx - 1;
+            int m = 0;
+            for (int k = 0; k < 3; ++k) {
+                const int yy = cy + k - 1;
+                if (yy < 0 || yy >= G.ny) continue;
+                const int t1 = start[yy * G.nx + xb + 1];
+                for (int t = start[yy * G.nx + xa]; t < t1; ++t) {
+                    const double2 pj = spos[t];
+                    const double q0 = pj.x - E.r0, q1 = pj.y - E.r1;
+                    const double sq = q0 * q0 + q1 * q1;
+                    if (!(sq < P.cull_t && sq > 0)) continue;  // agents only (cross_and_rescue.py:147-150)
+                    const unsigned long long key = ((unsigned long long)(unsigned)sidx[t] << 32) | (unsigned)t;
+                    if (m < kHocbfCap) {  // insertion into the sorted list
+                        int j = m;
+                        while (j > 0 && keys[(j - 1) * kBlock + threadIdx.x] > key) {
+                            keys[j * kBlock + threadIdx.x] = keys[(j - 1) * kBlock + threadIdx.x];
+                            --j;
+                        }
+                        keys[j * kBlock + threadIdx.x] = key;
+                    }
+                    ++m;
+                }
+            }
+            E.count = m;
+            double ux = E.u0x, uy = E.u0y;  // no neighbour: filter not run, u0 unclipped
+            int32_t st = CBF_STATUS_IDLE;
+            if (m > kHocbfCap) {
+                st = CBF_STATUS_NBR_OVERFLOW;
+            } else if (m > 0) {
+                SlotRows R{P, H, E, keys, spos, svel, m, 0};
+                const Sol S = solve_hocbf(P, E, R);
+                clip_u(P, S, E, ux, uy);
+                st = pack_status(S);
+                solved = true;
+            }
+            const long k = (long)(r - row_begin) * W + c;
+            const double2 pn = make_double2(E.r0 + T * ux, E.r1 + T * uy);
+            pos_out[k] = pn;
+            u[k] = make_double2(ux, uy);
+            status[k] = st;
+            if (cnt) cnt[k] = m;
+            ext_accumulate(r, row_begin, row_end, guard_rows, pn.y, e0, e1, e2, e3);
+        }
+    }
+    if (solves) {
+        const unsigned long long mk = __ballot(solved);
+        if ((threadIdx.x & 63) == 0 && mk)
+            atomicAdd(&solves[16 * ((blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6)) & 63)],
+                      (unsigned long long)__popcll(mk));
+    }
+    if (ext_part) block_extents(e0, e1, e2, e3, ext_part + 4l * blockIdx.x);
 }
 
 inline int nblocks(long n) { return (int)((n + kBlock - 1) / kBlock); }
@@ -238,5 +364,28 @@ extern "C" int cbf_filter_indexed_hocbf(const cbf_params* p, const cbf_hocbf* hp
                        make_hp(hp), reinterpret_cast<const double2*>(pos), reinterpret_cast<const double2*>(vel),
                        ego_begin, ego_end, kmax, nbr_idx, nbr_count, u, status, x_out,
                        reinterpret_cast<double4*>(workspace));
+    return (int)hipGetLastError();
+}
+
+extern "C" int cbf_lattice_advance_hocbf(const cbf_params* p, const cbf_hocbf* hp, const cbf_grid* grid, int32_t W,
+                                         int32_t H, int32_t row_begin, int32_t row_end, int32_t win_row0,
+                                         int32_t win_rows, const double* pos, double T, double* pos_out, double* u,
+                                         int32_t* status, int32_t* nbr_count, int32_t guard_rows, double* extents,
+                                         uint64_t* solves, void* workspace, size_t workspace_bytes, void* stream) {
+    if (!hp) return CBF_EINVAL;
+    int rc = check_lattice(p, grid, W, H, row_begin, row_end, win_row0, win_rows, pos, workspace, workspace_bytes);
+    if (rc) return rc;
+    if (!pos_out || !u || !status) return CBF_EINVAL;
+    hipStream_t s = (hipStream_t)stream;
+    const long n = (long)W * win_rows;
+    const CellGrid G = make_grid(grid);
+    CellWs Wk(workspace, n, (long)G.nx * G.ny);
+    double* ext_part = extents ? (double*)((char*)workspace + CellWs::bytes(n, Wk.ncell)) : nullptr;
+    const int nb = nblocks(n);
+    hipLaunchKernelGGL(k_lattice_filter_hocbf, dim3(nb), dim3(kBlock), 0, s, make_kp(p), make_hp(hp), G, W, row_begin,
+                       row_end, win_row0, Wk.ncell, Wk.spos, Wk.svel, Wk.sidx, Wk.start, T,
+                       reinterpret_cast<double2*>(pos_out), reinterpret_cast<double2*>(u), status, nbr_count,
+                       guard_rows, ext_part, reinterpret_cast<unsigned long long*>(solves));
+    if (extents) launch_extents_finalize(nb, ext_part, extents, s);
     return (int)hipGetLastError();
 }

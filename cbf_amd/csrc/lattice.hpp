@@ -1,0 +1,81 @@
+// lattice.hpp -- helpers shared by the lattice-step filters (swarm.hip: reference barrier,
+// hocbf.hip: Euclidean HOCBF mode): halo-guard extents and argument checks.
+#pragma once
+
+#include "cbf_device.hpp"
+#include "cells.hpp"
+
+namespace cbf {
+
+__device__ __forceinline__ double wave_min(double v) {
+    for (int o = 32; o > 0; o >>= 1) v = pmin(v, __shfl_xor(v, o, 64));
+    return v;
+}
+
+__device__ __forceinline__ double wave_max(double v) {
+    for (int o = 32; o > 0; o >>= 1) v = pmax(v, __shfl_xor(v, o, 64));
+    return v;
+}
+
+// Per-block extents of the new owned y (halo guard of the sharded step): {min, max, max over rows
+// < row_end - guard, min over rows >= row_begin + guard}.
+__device__ __forceinline__ void block_extents(double e0, double e1, double e2, double e3, double* out) {
+    __shared__ double red[4][kBlock / 64];
+    const double m0 = wave_min(e0), m1 = wave_max(e1), m2 = wave_max(e2), m3 = wave_min(e3);
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    if (lane == 0) {
+        red[0][wid] = m0;
+        red[1][wid] = m1;
+        red[2][wid] = m2;
+        red[3][wid] = m3;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double a = red[0][0], b = red[1][0], c2 = red[2][0], d = red[3][0];
+        for (int q = 1; q < kBlock / 64; ++q) {
+            a = pmin(a, red[0][q]);
+            b = pmax(b, red[1][q]);
+            c2 = pmax(c2, red[2][q]);
+            d = pmin(d, red[3][q]);
+        }
+        out[0] = a;
+        out[1] = b;
+        out[2] = c2;
+        out[3] = d;
+    }
+}
+
+__device__ __forceinline__ void ext_accumulate(int r, int row_begin, int row_end, int guard_rows, double ny,
+                                               double& e0, double& e1, double& e2, double& e3) {
+    e0 = pmin(e0, ny);
+    e1 = pmax(e1, ny);
+    if (r < row_end - guard_rows) e2 = pmax(e2, ny);
+    if (r >= row_begin + guard_rows) e3 = pmin(e3, ny);
+}
+
+// Reduces nparts per-block extents to out[4] (one-block kernel, defined in swarm.hip).
+void launch_extents_finalize(int nparts, const double* part, double* out, hipStream_t s);
+
+inline size_t lattice_ext_bytes(long win_n) {
+    return align256(32 * (size_t)((win_n + kBlock - 1) / kBlock + kHardBlocks));
+}
+
+inline int check_lattice(const cbf_params* p, const cbf_grid* grid, int32_t W, int32_t H, int32_t row_begin,
+                         int32_t row_end, int32_t win_row0, int32_t win_rows, const double* pos, void* workspace,
+                         size_t workspace_bytes) {
+    if (!p || !grid || W <= 0 || H <= 0) return CBF_EINVAL;
+    if (row_begin < 0 || row_end > H || row_begin >= row_end) return CBF_EINVAL;
+    if (win_row0 < 0 || win_rows <= 0 || win_row0 + win_rows > H) return CBF_EINVAL;
+    // owned rows plus one neighbour row on each side (where it exists) must be in the window
+    if (win_row0 > (row_begin > 0 ? row_begin - 1 : 0)) return CBF_EINVAL;
+    if (win_row0 + win_rows < (row_end < H ? row_end + 1 : H)) return CBF_EINVAL;
+    if ((long)W * win_rows >= (1l << 31)) return CBF_EINVAL;
+    if (!pos || !workspace) return CBF_EINVAL;
+    if (grid->nx <= 0 || grid->ny <= 0 || !(grid->inv_h > 0) || !(1.0 / grid->inv_h >= sqrt(p->cull_t)))
+        return CBF_EINVAL;
+    if ((long)grid->nx * grid->ny > (1l << 30)) return CBF_EINVAL;
+    if (workspace_bytes < cbf_lattice_workspace_size(W, win_rows, grid)) return CBF_EINVAL;
+    return 0;
+}
+
+}  // namespace cbf

@@ -4,6 +4,7 @@
 //   whole timestep of a lattice swarm            SURVEY cfg3/cfg4 (cross_and_rescue.py:97-175 shape)
 #include "cbf_device.hpp"
 #include "cells.hpp"
+#include "lattice.hpp"
 
 using namespace cbf;
 
@@ -164,14 +165,6 @@ __global__ void __launch_bounds__(kBlock) k_lattice_scatter_ordered(long nwin, c
     sidx[d] = b.z;
 }
 
-__device__ __forceinline__ double wave_min(double v) {
-    for (int o = 32; o > 0; o >>= 1) v = pmin(v, __shfl_xor(v, o, 64));
-    return v;
-}
-__device__ __forceinline__ double wave_max(double v) {
-    for (int o = 32; o > 0; o >>= 1) v = pmax(v, __shfl_xor(v, o, 64));
-    return v;
-}
 
 // Lattice step K4: filter + clip + Euler for one owned agent at cell-sorted slot `slot`.
 // QPs that the origin does not solve (after the strip pre-relaxation) are not solved here but
@@ -278,41 +271,7 @@ __device__ __forceinline__ int lattice_ego(const KP& P, const CellGrid& G, int W
     return 1;
 }
 
-// Per-block extents of the new owned y (halo guard of the sharded step): {min, max, max over rows
-// < row_end - guard, min over rows >= row_begin + guard}.
-__device__ __forceinline__ void block_extents(double e0, double e1, double e2, double e3, double* out) {
-    __shared__ double red[4][kBlock / 64];
-    const double m0 = wave_min(e0), m1 = wave_max(e1), m2 = wave_max(e2), m3 = wave_min(e3);
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    if (lane == 0) {
-        red[0][wid] = m0;
-        red[1][wid] = m1;
-        red[2][wid] = m2;
-        red[3][wid] = m3;
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        double a = red[0][0], b = red[1][0], c2 = red[2][0], d = red[3][0];
-        for (int q = 1; q < kBlock / 64; ++q) {
-            a = pmin(a, red[0][q]);
-            b = pmax(b, red[1][q]);
-            c2 = pmax(c2, red[2][q]);
-            d = pmin(d, red[3][q]);
-        }
-        out[0] = a;
-        out[1] = b;
-        out[2] = c2;
-        out[3] = d;
-    }
-}
 
-__device__ __forceinline__ void ext_accumulate(int r, int row_begin, int row_end, int guard_rows, double ny,
-                                               double& e0, double& e1, double& e2, double& e3) {
-    e0 = pmin(e0, ny);
-    e1 = pmax(e1, ny);
-    if (r < row_end - guard_rows) e2 = pmax(e2, ny);
-    if (r >= row_begin + guard_rows) e3 = pmin(e3, ny);
-}
 
 // K4: one lane per cell-sorted slot; easy QPs solved in place, hard ones queued.
 template <bool FZ>
@@ -393,6 +352,7 @@ __global__ void __launch_bounds__(64) k_lattice_filter_hard(KP P, int row_begin,
     }
 }
 
+
 __global__ void __launch_bounds__(kBlock) k_extents_finalize(int nparts, const double* __restrict__ part,
                                                              double* __restrict__ out) {
     double a = INFINITY, b = -INFINITY, c = -INFINITY, d = INFINITY;
@@ -451,6 +411,12 @@ __global__ void k_halo_guard(const double* __restrict__ E, long stride, int ws, 
 
 }  // namespace
 
+namespace cbf {
+void launch_extents_finalize(int nparts, const double* part, double* out, hipStream_t s) {
+    hipLaunchKernelGGL(k_extents_finalize, dim3(1), dim3(kBlock), 0, s, nparts, part, out);
+}
+}  // namespace cbf
+
 extern "C" int cbf_halo_guard(const double* ext_all, int64_t stride, int32_t world_size, int32_t rank, double radius,
                               int32_t* flag, void* stream) {
     if (!ext_all || !flag || world_size < 1 || rank < 0 || rank >= world_size || stride < 4) return CBF_EINVAL;
@@ -493,9 +459,6 @@ extern "C" int cbf_euler(int32_t n, double* pos, const double* vel, double T, vo
     return (int)hipGetLastError();
 }
 
-static size_t lattice_ext_bytes(long win_n) {
-    return align256(32 * (size_t)((win_n + kBlock - 1) / kBlock + kHardBlocks));
-}
 
 extern "C" size_t cbf_lattice_workspace_size(int32_t W, int32_t win_rows, const cbf_grid* grid) {
     if (!grid || W <= 0 || win_rows <= 0 || grid->nx <= 0 || grid->ny <= 0) return 0;
@@ -503,23 +466,6 @@ extern "C" size_t cbf_lattice_workspace_size(int32_t W, int32_t win_rows, const 
     return CellWs::bytes(n, (long)grid->nx * grid->ny) + lattice_ext_bytes(n);
 }
 
-static int check_lattice(const cbf_params* p, const cbf_grid* grid, int32_t W, int32_t H, int32_t row_begin,
-                         int32_t row_end, int32_t win_row0, int32_t win_rows, const double* pos, void* workspace,
-                         size_t workspace_bytes) {
-    if (!p || !grid || W <= 0 || H <= 0) return CBF_EINVAL;
-    if (row_begin < 0 || row_end > H || row_begin >= row_end) return CBF_EINVAL;
-    if (win_row0 < 0 || win_rows <= 0 || win_row0 + win_rows > H) return CBF_EINVAL;
-    // owned rows plus one neighbour row on each side (where it exists) must be in the window
-    if (win_row0 > (row_begin > 0 ? row_begin - 1 : 0)) return CBF_EINVAL;
-    if (win_row0 + win_rows < (row_end < H ? row_end + 1 : H)) return CBF_EINVAL;
-    if ((long)W * win_rows >= (1l << 31)) return CBF_EINVAL;
-    if (!pos || !workspace) return CBF_EINVAL;
-    if (grid->nx <= 0 || grid->ny <= 0 || !(grid->inv_h > 0) || !(1.0 / grid->inv_h >= sqrt(p->cull_t)))
-        return CBF_EINVAL;
-    if ((long)grid->nx * grid->ny > (1l << 30)) return CBF_EINVAL;
-    if (workspace_bytes < cbf_lattice_workspace_size(W, win_rows, grid)) return CBF_EINVAL;
-    return 0;
-}
 
 extern "C" int cbf_lattice_build(const cbf_params* p, const cbf_grid* grid, int32_t W, int32_t H, int32_t row_begin,
                                  int32_t row_end, int32_t win_row0, int32_t win_rows, const double* pos, double gain,
@@ -569,7 +515,7 @@ extern "C" int cbf_lattice_advance(const cbf_params* p, const cbf_grid* grid, in
                        Wk.hardq);
     hipLaunchKernelGGL(k_lattice_filter_hard, dim3(hb), dim3(64), 0, s, kp, row_begin, row_end, T, po, uo, status,
                        nbr_count, guard_rows, ext_part ? ext_part + 4l * nb : nullptr, Wk.hardq);
-    if (extents) hipLaunchKernelGGL(k_extents_finalize, dim3(1), dim3(kBlock), 0, s, nb + hb, ext_part, extents);
+    if (extents) launch_extents_finalize(nb + hb, ext_part, extents, s);
     return (int)hipGetLastError();
 }
 

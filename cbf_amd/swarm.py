@@ -235,12 +235,18 @@ class LatticeSwarm:
     hipGraph.  Single-GPU: the window is the whole lattice."""
 
     def __init__(self, pos, W, H, gain=0.25, params: FilterParams = None, T=1 / 30, grid=None, margin=1.0,
-                 method="cells"):
+                 method="cells", barrier="reference", alpha=(1.0, 1.0)):
         torch = _lib.require_gpu()
         self.dev = torch.device("cuda")
         pos = np.asarray(pos, dtype=np.float64).reshape(W * H, 2)
         self.W, self.H, self.gain, self.T = W, H, float(gain), float(T)
         self.method = method  # "cells" (fused cbf_lattice_step) or "allpairs" (cfg3: every pair tested)
+        if barrier not in ("reference", "euclidean_hocbf"):
+            raise ValueError(f"barrier must be 'reference' or 'euclidean_hocbf', got {barrier!r}")
+        if barrier != "reference" and method != "cells":
+            raise ValueError("the Euclidean HOCBF lattice step uses the cell list (method='cells')")
+        self.barrier = barrier
+        self.hp = _lib.CbfHocbf(float(alpha[0]), float(alpha[1]))
         self.params = params or FilterParams()
         self.cp = self.params.c()
         self.grid = grid or grid_for_points(pos, self.params.safety_distance, margin=margin)
@@ -268,6 +274,10 @@ class LatticeSwarm:
             euler(self.pos, self.u, self.T)
             self.solves[0] += (self.nbr_count > 0).sum()
             return
+        if self.barrier == "euclidean_hocbf":
+            self.build_phase()
+            self.advance_phase()
+            return
         check(lib.cbf_lattice_step(self.cp, _lib.C.byref(self.grid), self.W, self.H, 0, self.H, 0, self.H,
                                    ptr(self.pos), self.gain, self.T, ptr(self.pos), ptr(self.vel), ptr(self.u),
                                    ptr(self.status), ptr(self.nbr_count), 0, None, ptr(self.solves), ptr(self.ws),
@@ -281,6 +291,13 @@ class LatticeSwarm:
 
     def advance_phase(self):
         """filter + clip + Euler only (the dominant kernel, K4)."""
+        if self.barrier == "euclidean_hocbf":
+            check(lib.cbf_lattice_advance_hocbf(self.cp, _lib.C.byref(self.hp), _lib.C.byref(self.grid), self.W,
+                                                self.H, 0, self.H, 0, self.H, ptr(self.pos), self.T, ptr(self.pos),
+                                                ptr(self.u), ptr(self.status), ptr(self.nbr_count), 0, None,
+                                                ptr(self.solves), ptr(self.ws), self.ws_bytes, stream_handle()),
+                  "cbf_lattice_advance_hocbf")
+            return
         check(lib.cbf_lattice_advance(self.cp, _lib.C.byref(self.grid), self.W, self.H, 0, self.H, 0, self.H,
                                       ptr(self.pos), self.T, ptr(self.pos), ptr(self.u), ptr(self.status),
                                       ptr(self.nbr_count), 0, None, ptr(self.solves), ptr(self.ws), self.ws_bytes,

@@ -227,6 +227,16 @@ int cbf_lattice_advance(const cbf_params* p, const cbf_grid* grid, int32_t W, in
                         double* pos_out, double* u, int32_t* status, int32_t* nbr_count, int32_t guard_rows,
                         double* extents, uint64_t* solves, void* workspace, size_t workspace_bytes, void* stream);
 
+/* cbf_lattice_advance with Euclidean HOCBF rows (cbf_hocbf above): after cbf_lattice_build, the
+ * filter of every owned agent over its 3x3-cell neighbours in ascending entity order, the HOCBF
+ * QP, clip and Euler; same outputs, extents and solve counter as cbf_lattice_advance.  More than
+ * 24 neighbours: CBF_STATUS_NBR_OVERFLOW (u = u0). */
+int cbf_lattice_advance_hocbf(const cbf_params* p, const cbf_hocbf* hp, const cbf_grid* grid, int32_t W, int32_t H,
+                              int32_t row_begin, int32_t row_end, int32_t win_row0, int32_t win_rows,
+                              const double* pos, double T, double* pos_out, double* u, int32_t* status,
+                              int32_t* nbr_count, int32_t guard_rows, double* extents, uint64_t* solves,
+                              void* workspace, size_t workspace_bytes, void* stream);
+
 /*
  * Halo guard of the row-sharded lattice step.  ext_all holds world_size records of 4 doubles
  * (record q at ext_all + q * stride) as produced by cbf_lattice_step's `extents` with

@@ -92,3 +92,30 @@ def test_overflow_status_when_kmax_too_small():
     assert lib.cbf_filter_indexed_hocbf(cp, C.byref(hp), 40, ptr(P), ptr(_t(vel)), 0, 40, 2, ptr(idx), ptr(cnt),
                                         ptr(u), ptr(st), None, ptr(ws), ws.numel(), stream_handle()) == 0
     assert (st.cpu().numpy() == cbf_amd.STATUS_NBR_OVERFLOW).all()
+
+
+@pytest.mark.parametrize("alpha", [(1.0, 1.0), (2.0, 0.5)])
+def test_lattice_step_hocbf_vs_oracle(alpha):
+    """The cfg4-shape fused step in HOCBF mode (nominal + cell list + HOCBF filter + clip + Euler),
+    3 steps (the last two replayed from a hipGraph), bit-exact vs the oracle's all-pairs loop."""
+    from cbf_amd import scenarios
+    W = H = 48
+    pos = scenarios.lattice(W, H, seed=7)
+    L = swarm.LatticeSwarm(pos, W, H, gain=scenarios.LATTICE_GAIN, barrier="euclidean_hocbf", alpha=alpha)
+    p, hp = po.Params(15), po.HocbfParams(*alpha)
+    ref_pos = pos.copy()
+    for step in range(3):
+        if step == 1:
+            L.capture()
+            L.pos.copy_(torch.as_tensor(ref_pos, device=DEV))  # capture ran one step: rewind
+        L.step()
+        torch.cuda.synchronize()
+        vel = coracle.consensus_lattice(W, H, 0, H, ref_pos, scenarios.LATTICE_GAIN)
+        ref = coracle.filter_swarm_hocbf(p, hp, ref_pos, vel, 0)
+        ref_pos = coracle.euler(ref_pos, ref["u"], 1 / 30)
+        st = L.status.cpu().numpy()
+        assert not ((st & 0xFF) == cbf_amd.STATUS_NBR_OVERFLOW).any()
+        assert np.array_equal(L.nbr_count.cpu().numpy(), ref["cnt"]), step
+        assert np.array_equal(st, ref["status"]), step
+        assert np.array_equal(L.u.cpu().numpy(), ref["u"]), step
+        assert np.array_equal(L.pos.cpu().numpy(), ref_pos), step

@@ -27,6 +27,18 @@ SETS["allpairs"] = {
     "ap_s16_t1024_w5": ["-DCBF_AP_SCREEN=16", "-DCBF_AP_TILE=1024", "-DCBF_AP_WAVES=5"],
     "ap_s16_t512_w8": ["-DCBF_AP_SCREEN=16", "-DCBF_AP_TILE=512", "-DCBF_AP_WAVES=8"],
 }
+SETS["phases"] = {
+    "full": [],
+    "no_qp": ["-DCBF_ABLATE=1"],
+    "no_qp_no_rows": ["-DCBF_ABLATE=2"],
+    "no_scan": ["-DCBF_ABLATE=3"],
+}
+SETS["hard"] = {
+    "full": [],
+    "hard1024": ["-DCBF_HARD_BLOCKS=1024"],
+    "hard2048": ["-DCBF_HARD_BLOCKS=2048"],
+    "hard4096": ["-DCBF_HARD_BLOCKS=4096"],
+}
 VARIANTS = {
     "full": [],
     "flush2": ["-DCBF_FLUSH_U=2"],
@@ -95,7 +107,7 @@ def run(rounds, iters, W, H):
     pos0 = scenarios.lattice(W, H, seed=0)
     grid = swarm.grid_for_points(pos0, 0.2)
     cp = _lib.make_params(15)
-    ws_bytes = _lib.lib.cbf_lattice_workspace_size(W, H, C.byref(grid))
+    ws_bytes = max(L.cbf_lattice_workspace_size(W, H, C.byref(grid)) for L in libs.values())
     st = {}
     for name in names:
         st[name] = dict(pos=torch.tensor(pos0, device="cuda"), vel=torch.empty((W * H, 2), dtype=torch.float64,
