@@ -260,18 +260,20 @@ __device__ __forceinline__ Box box_rhs(const KP& P, const Ego& E) {
     return B;
 }
 
-// Exact min-norm point of the (<= 8) half-planes a.x <= b whose slot bit is set in mask;
-// slots 0..3 are the merged box rows, 4..7 the CBF quadrants.  Incremental (Seidel) method,
-// identical arithmetic to oracle/cbf_oracle.c:solve_planes.  Returns -1 (feasible) or the slot
-// at which the prefix became infeasible.
-__device__ __forceinline__ int solve8(const double (&a0)[8], const double (&a1)[8], const double (&b)[8],
-                                      unsigned mask, double& xo0, double& xo1) {
-    double tb[8];
+// Exact min-norm point of the (<= N) half-planes a.x <= b whose slot bit is set in mask, in slot
+// order; slots 0..3 are the merged box rows.  Incremental (Seidel) method, identical arithmetic
+// to oracle/cbf_oracle.c:solve_planes_n over the present planes.  All loops are unrolled over
+// the N slots so the planes stay in registers.  Returns -1 (feasible) or the slot at which the
+// prefix became infeasible.
+template <int N>
+__device__ __forceinline__ int solve_planes_reg(const double (&a0)[N], const double (&a1)[N], const double (&b)[N],
+                                                unsigned mask, double& xo0, double& xo1) {
+    double tb[N];
 #pragma unroll
-    for (int h = 0; h < 8; ++h) tb[h] = FEAS_TOL * pmax(1.0, fabs(b[h]));
+    for (int h = 0; h < N; ++h) tb[h] = FEAS_TOL * pmax(1.0, fabs(b[h]));
     double x0 = 0.0, x1 = 0.0;
 #pragma unroll
-    for (int h = 0; h < 8; ++h) {
+    for (int h = 0; h < N; ++h) {
         if (!((mask >> h) & 1u)) continue;
         if ((a0[h] * x0 + a1[h] * x1) - b[h] <= tb[h]) continue;
         const double n2 = a0[h] * a0[h] + a1[h] * a1[h];
@@ -321,6 +323,12 @@ __device__ __forceinline__ int solve8(const double (&a0)[8], const double (&a1)[
     xo0 = x0;
     xo1 = x1;
     return -1;
+}
+
+// slots 0..3: merged box rows, 4..7: the CBF quadrants
+__device__ __forceinline__ int solve8(const double (&a0)[8], const double (&a1)[8], const double (&b)[8],
+                                      unsigned mask, double& xo0, double& xo1) {
+    return solve_planes_reg<8>(a0, a1, b, mask, xo0, xo1);
 }
 
 struct Sol {

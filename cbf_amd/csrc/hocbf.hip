@@ -31,25 +31,16 @@ __device__ __forceinline__ double4 hocbf_row(const KP& P, const HP& H, double r0
     return make_double4(a0, a1, rhs - (a0 * u0x + a1 * u0y), 0.0);
 }
 
-__device__ __forceinline__ void box_plane(int h, const double (&bb)[4], double& a0, double& a1, double& b) {
-    a0 = h == 0 ? 1.0 : (h == 2 ? -1.0 : 0.0);
-    a1 = h == 1 ? 1.0 : (h == 3 ? -1.0 : 0.0);
-    b = h == 0 ? bb[0] : (h == 1 ? bb[1] : (h == 2 ? bb[2] : bb[3]));
-}
 
 // Plane source over rows stored in memory (workspace), relaxed in place.
 struct StoredRows {
     double4* rows;
     int m;
-    __device__ __forceinline__ void plane(int h, const double (&bb)[4], double& a0, double& a1, double& b) const {
-        if (h >= 4) {
-            const double4 r = rows[h - 4];
-            a0 = r.x;
-            a1 = r.y;
-            b = r.z;
-        } else {
-            box_plane(h, bb, a0, a1, b);
-        }
+    __device__ __forceinline__ void row(int i, double& a0, double& a1, double& b) const {
+        const double4 r = rows[i];
+        a0 = r.x;
+        a1 = r.y;
+        b = r.z;
     }
     __device__ __forceinline__ void relax() {
         for (int i = 0; i < m; ++i) rows[i].z = rows[i].z + 1.0;  // cbf.py:85-87
@@ -68,18 +59,14 @@ struct SlotRows {
     const double2* __restrict__ svel;
     int m;
     int t;
-    __device__ __forceinline__ void plane(int h, const double (&bb)[4], double& a0, double& a1, double& b) const {
-        if (h >= 4) {
-            const int slot = (int)(keys[(h - 4) * kBlock + threadIdx.x] & 0xFFFFFFFFull);
-            const double2 o = spos[slot], ov = svel[slot];
-            const double4 r = hocbf_row(P, H, E.r0, E.r1, E.r2, E.r3, o.x, o.y, ov.x, ov.y, E.u0x, E.u0y);
-            a0 = r.x;
-            a1 = r.y;
-            b = r.z;
-            for (int i = 0; i < t; ++i) b = b + 1.0;
-        } else {
-            box_plane(h, bb, a0, a1, b);
-        }
+    __device__ __forceinline__ void row(int i, double& a0, double& a1, double& b) const {
+        const int slot = (int)(keys[i * kBlock + threadIdx.x] & 0xFFFFFFFFull);
+        const double2 o = spos[slot], ov = svel[slot];
+        const double4 r = hocbf_row(P, H, E.r0, E.r1, E.r2, E.r3, o.x, o.y, ov.x, ov.y, E.u0x, E.u0y);
+        a0 = r.x;
+        a1 = r.y;
+        b = r.z;
+        for (int k = 0; k < t; ++k) b = b + 1.0;
     }
     __device__ __forceinline__ void relax() { ++t; }
 };
@@ -88,41 +75,29 @@ __device__ __forceinline__ bool feas(double a0, double a1, double b, double x0, 
     return (a0 * x0 + a1 * x1) - b <= FEAS_TOL * pmax(1.0, fabs(b));
 }
 
-// oracle/cbf_oracle.c:solve_planes_n over n = 4 + m planes
-template <class Src>
-__device__ int solve_rows(const double (&bb)[4], const Src& R, double& xo0, double& xo1) {
-    const int n = 4 + R.m;
-    double x0 = 0.0, x1 = 0.0;
-    for (int h = 0; h < n; ++h) {
-        double a0, a1, b;
-        R.plane(h, bb, a0, a1, b);
-        if (feas(a0, a1, b, x0, x1)) continue;
-        const double n2 = a0 * a0 + a1 * a1;
-        if (!(n2 > 0)) return h;
-        const double t = b / n2;
-        const double p0 = t * a0, p1 = t * a1;
-        const double d0 = -a1, d1 = a0;
-        double rh = 0.0, ah = 0.0, rl = 0.0, al = 0.0;
-        bool has_hi = false, has_lo = false;
-        for (int j = 0; j < h; ++j) {
-            double c0, c1, e;
-            R.plane(j, bb, c0, c1, e);
-            const double ad = c0 * d0 + c1 * d1;
-            const double r = e - (c0 * p0 + c1 * p1);
-            if (ad > 0) {
-                if (!has_hi || r * ah < rh * ad) {
-                    rh = r;
-                    ah = ad;
-                }
-                has_hi = true;
-            } else if (ad < 0) {
-                if (!has_lo || r * al > rl * ad) {
-                    rl = r;
-                    al = ad;
-                }
-                has_lo = true;
+// 1-D interval of the incremental solve: bounds r/ad compared by cross-multiplication, only the
+// binding one divided out (oracle/cbf_oracle.c:solve_planes_n, inner loop).
+struct Interval {
+    double rh = 0.0, ah = 0.0, rl = 0.0, al = 0.0;
+    bool has_hi = false, has_lo = false;
+    __device__ __forceinline__ void add(double c0, double c1, double e, double d0, double d1, double p0, double p1) {
+        const double ad = c0 * d0 + c1 * d1;
+        const double r = e - (c0 * p0 + c1 * p1);
+        if (ad > 0) {
+            if (!has_hi || r * ah < rh * ad) {
+                rh = r;
+                ah = ad;
             }
+            has_hi = true;
+        } else if (ad < 0) {
+            if (!has_lo || r * al > rl * ad) {
+                rl = r;
+                al = ad;
+            }
+            has_lo = true;
         }
+    }
+    __device__ __forceinline__ double clamp0() const {
         double s = 0.0;
         bool s_hi = false;
         if (has_hi && rh < 0) {
@@ -130,12 +105,65 @@ __device__ int solve_rows(const double (&bb)[4], const Src& R, double& xo0, doub
             s_hi = true;
         }
         if (has_lo && (s_hi ? (rh * al > rl * ah) : (rl < 0))) s = rl / al;
+        return s;
+    }
+};
+
+// oracle/cbf_oracle.c:solve_planes_n over the 4 merged box planes (static, in registers) then the
+// m barrier rows of R (dynamic), in that order; same arithmetic.  The box planes are never
+// selected by a runtime index (that would be lowered to scratch).
+template <class Src>
+__device__ __forceinline__ int solve_rows(const double (&bb)[4], const Src& R, double& xo0, double& xo1) {
+    const double ba0[4] = {1.0, 0.0, -1.0, 0.0}, ba1[4] = {0.0, 1.0, 0.0, -1.0};
+    double x0 = 0.0, x1 = 0.0;
+    // box planes h = 0..3
+#pragma unroll
+    for (int h = 0; h < 4; ++h) {
+        if (feas(ba0[h], ba1[h], bb[h], x0, x1)) continue;
+        const double n2 = ba0[h] * ba0[h] + ba1[h] * ba1[h];
+        const double t = bb[h] / n2;
+        const double p0 = t * ba0[h], p1 = t * ba1[h];
+        const double d0 = -ba1[h], d1 = ba0[h];
+        Interval I;
+#pragma unroll
+        for (int j = 0; j < h; ++j) I.add(ba0[j], ba1[j], bb[j], d0, d1, p0, p1);
+        const double s = I.clamp0();
         x0 = p0 + s * d0;
         x1 = p1 + s * d1;
-        for (int j = 0; j <= h; ++j) {
+        bool ok = true;
+#pragma unroll
+        for (int j = 0; j <= h; ++j) ok = ok && feas(ba0[j], ba1[j], bb[j], x0, x1);
+        if (!ok) return h;
+    }
+    // barrier rows h = 4 + i
+    for (int i = 0; i < R.m; ++i) {
+        double a0, a1, b;
+        R.row(i, a0, a1, b);
+        if (feas(a0, a1, b, x0, x1)) continue;
+        const double n2 = a0 * a0 + a1 * a1;
+        if (!(n2 > 0)) return 4 + i;
+        const double t = b / n2;
+        const double p0 = t * a0, p1 = t * a1;
+        const double d0 = -a1, d1 = a0;
+        Interval I;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) I.add(ba0[j], ba1[j], bb[j], d0, d1, p0, p1);
+        for (int j = 0; j < i; ++j) {
             double c0, c1, e;
-            R.plane(j, bb, c0, c1, e);
-            if (!feas(c0, c1, e, x0, x1)) return h;
+            R.row(j, c0, c1, e);
+            I.add(c0, c1, e, d0, d1, p0, p1);
+        }
+        const double s = I.clamp0();
+        x0 = p0 + s * d0;
+        x1 = p1 + s * d1;
+        bool ok = true;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) ok = ok && feas(ba0[j], ba1[j], bb[j], x0, x1);
+        if (!ok) return 4 + i;
+        for (int j = 0; j <= i; ++j) {
+            double c0, c1, e;
+            R.row(j, c0, c1, e);
+            if (!feas(c0, c1, e, x0, x1)) return 4 + i;
         }
     }
     xo0 = x0;
@@ -145,7 +173,7 @@ __device__ int solve_rows(const double (&bb)[4], const Src& R, double& xo0, doub
 
 // oracle/cbf_oracle.c:solve_hocbf -- +1 relaxation of every barrier row while infeasible
 template <class Src>
-__device__ Sol solve_hocbf(const KP& P, const Ego& E, Src& R) {
+__device__ __forceinline__ Sol solve_hocbf(const KP& P, const Ego& E, Src& R) {
     const Box B = box_rhs(P, E);
     const double bb[4] = {pmin(B.S[0], B.S[4]), pmin(B.S[1], B.S[6]), pmin(B.S[2], B.S[5]), pmin(B.S[3], B.S[7])};
     Sol S;
@@ -172,6 +200,25 @@ __device__ Sol solve_hocbf(const KP& P, const Ego& E, Src& R) {
     }
     return S;
 }
+
+// Plane source over rows staged per lane in LDS (the lattice kernel's key area, reused once the
+// keys are in registers): row i's a0, a1, b at lds[(3i + c) * kBlock + lane]; relaxed in place.
+constexpr int kLdsRows = 8;
+struct LdsRows {
+    double* lds;
+    int m;
+    __device__ __forceinline__ void row(int i, double& a0, double& a1, double& b) const {
+        a0 = lds[(3 * i) * kBlock + threadIdx.x];
+        a1 = lds[(3 * i + 1) * kBlock + threadIdx.x];
+        b = lds[(3 * i + 2) * kBlock + threadIdx.x];
+    }
+    __device__ __forceinline__ void relax() {
+        for (int i = 0; i < m; ++i) {
+            double& v = lds[(3 * i + 2) * kBlock + threadIdx.x];
+            v = v + 1.0;  // cbf.py:85-87
+        }
+    }
+};
 
 // get_safe_control with explicit neighbour lists (CSR): rows of ego i at ws[off[i] .. off[i+1])
 __global__ void __launch_bounds__(kBlock) k_hocbf_batch(KP P, HP H, int n, const double* __restrict__ rs,
@@ -299,8 +346,30 @@ __global__ void __launch_bounds__(kBlock) k_lattice_filter_hocbf(
             if (m > kHocbfCap) {
                 st = CBF_STATUS_NBR_OVERFLOW;
             } else if (m > 0) {
-                SlotRows R{P, H, E, keys, spos, svel, m, 0};
-                const Sol S = solve_hocbf(P, E, R);
+                Sol S;
+                if (m <= kLdsRows) {  // rows computed once into the key area (keys read out first)
+                    unsigned long long kr[kLdsRows];
+#pragma unroll
+                    for (int i = 0; i < kLdsRows; ++i) kr[i] = i < m ? keys[i * kBlock + threadIdx.x] : 0ull;
+                    double* rl = reinterpret_cast<double*>(keys);
+#pragma unroll
+                    for (int i = 0; i < kLdsRows; ++i) {
+                        if (i < m) {
+                            const int sl = (int)(kr[i] & 0xFFFFFFFFull);
+                            const double2 o = spos[sl], ov = svel[sl];
+                            const double4 rw =
+                                hocbf_row(P, H, E.r0, E.r1, E.r2, E.r3, o.x, o.y, ov.x, ov.y, E.u0x, E.u0y);
+                            rl[(3 * i) * kBlock + threadIdx.x] = rw.x;
+                            rl[(3 * i + 1) * kBlock + threadIdx.x] = rw.y;
+                            rl[(3 * i + 2) * kBlock + threadIdx.x] = rw.z;
+                        }
+                    }
+                    LdsRows R{rl, m};
+                    S = solve_hocbf(P, E, R);
+                } else {
+                    SlotRows R{P, H, E, keys, spos, svel, m, 0};
+                    S = solve_hocbf(P, E, R);
+                }
                 clip_u(P, S, E, ux, uy);
                 st = pack_status(S);
                 solved = true;
