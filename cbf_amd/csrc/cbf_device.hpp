@@ -28,6 +28,21 @@
 #ifndef CBF_SCAN_U
 #define CBF_SCAN_U 6
 #endif
+// Lattice filter variants (tools/ablate.py): CBF_PUSH_BF = branch-free hit push (one LDS store per
+// candidate into the hit row or a dummy row); CBF_BQ_LDS = per-quadrant minima kept in LDS
+// (one read-compare-write per hit instead of four register compare-selects).
+#ifndef CBF_PUSH_BF
+#define CBF_PUSH_BF 0
+#endif
+#ifndef CBF_BQ_LDS
+#define CBF_BQ_LDS 1
+#endif
+// CBF_SCAN32 = the lattice filter's candidate scan reads fp32 positions (8 B instead of 16 B per
+// candidate through the vector memory pipe) and screens with screen_threshold(); every candidate
+// the screen lets through is re-tested exactly in fp64 in the flush.
+#ifndef CBF_SCAN32
+#define CBF_SCAN32 0
+#endif
 
 namespace cbf {
 
@@ -66,6 +81,25 @@ inline KP make_kp(const cbf_params* p) {
 
 __device__ __forceinline__ double pmin(double a, double b) { return (b < a) ? b : a; }  // Python min(a, b)
 __device__ __forceinline__ double pmax(double a, double b) { return (b > a) ? b : a; }  // Python max(a, b)
+
+// fp32 screen of the cull test.  A candidate can pass the exact fp64 test s = e0^2 + e1^2 < cull_t
+// (cross_and_rescue.py:141-150) only if S = the fp32 distance^2 of the fp32-rounded coordinates
+// is below the returned T32; the screen only rejects, every candidate it lets through is
+// re-tested exactly.  Bound: with |coords| <= M, u = 2^-24, |E_k - e_k| <= eta = 2uM + u(r + 2uM)
+// (+ fp64 and subnormal slack) for |e_k| < r = sqrt(cull_t), so S <= (cull_t + 2 sqrt2 r eta +
+// 2 eta^2)(1 + 3u); T32 adds slack on every term and rounds up.  M beyond 1e30 (or NaN) switches
+// the screen off (returns -1).  For a true neighbour both coordinates lie within r of the ego's,
+// so M = max(|ego coords|) + r suffices.
+__device__ __forceinline__ float screen_threshold(double cull_t, double M) {
+    if (!(M <= 1e30)) return -1.0f;
+    const double u = 0x1p-24;
+    const double r = sqrt(cull_t) * (1.0 + 1e-12);
+    const double eta = 2.0 * u * M + u * (r + 2.0 * u * M) + 1e-14 * r + 1e-35;
+    const double T = (cull_t * (1.0 + 1e-12) + 3.0 * r * eta + 3.0 * eta * eta) * (1.0 + 8.0 * u);
+    float t32 = (float)T;
+    if ((double)t32 < T) t32 = __uint_as_float(__float_as_uint(t32) + 1u);  // next float up (T > 0)
+    return t32;
+}
 
 // One ego's accumulated QP: its state, g@u0, and the per-sign-quadrant minimum barrier rhs.
 struct Ego {
@@ -144,8 +178,50 @@ struct HitList {
         if (n < kHitCap) lds[n * kBlock + threadIdx.x] = t;
         ++n;
     }
+    // branch-free form: lds has kHitCap + 1 rows, row kHitCap takes the non-hits
+    __device__ __forceinline__ void push_if(int* lds, int t, bool hit) {
+        const int row = (hit && n < kHitCap) ? n : kHitCap;
+        lds[row * kBlock + threadIdx.x] = t;
+        n += hit ? 1 : 0;
+    }
     __device__ __forceinline__ bool overflowed() const { return n > kHitCap; }
-    template <bool FZ = false>
+    // flush with the per-quadrant minima in LDS (bq[q * kBlock + lane], preset to +inf by the
+    // caller and read back into E after); same rows, same order, same minimum
+    template <bool FZ = false, bool EXACT = false>
+    __device__ __forceinline__ void flush_bq(const int* lds, double* bq, const KP& P, Ego& E,
+                                             const double2* __restrict__ pos, const double2* __restrict__ vel) {
+        for (int i = 0; i < n; i += CBF_FLUSH_U) {
+            double2 pj[CBF_FLUSH_U], vj[CBF_FLUSH_U];
+#pragma unroll
+            for (int q = 0; q < CBF_FLUSH_U; ++q) {
+                if (i + q < n) {
+                    const int t = lds[(i + q) * kBlock + threadIdx.x];
+                    pj[q] = pos[t];
+                    vj[q] = vel[t];
+                }
+            }
+#pragma unroll
+            for (int q = 0; q < CBF_FLUSH_U; ++q) {
+                bool keep = i + q < n;
+                if (EXACT && keep) {  // screened candidate: the exact agent cull test
+                    const double e0 = pj[q].x - E.r0, e1 = pj[q].y - E.r1;
+                    const double s = e0 * e0 + e1 * e1;
+                    keep = s < P.cull_t && s > 0;
+                }
+                if (keep) {
+                    int qd;
+                    const double b = row_b<FZ>(P, E, pj[q].x, pj[q].y, vj[q].x, vj[q].y, qd);
+                    double* slot = bq + qd * kBlock + threadIdx.x;
+                    const double cur = *slot;
+                    *slot = (b < cur) ? b : cur;
+                    E.present |= 1u << qd;
+                    E.count++;
+                }
+            }
+        }
+        n = 0;
+    }
+    template <bool FZ = false, bool EXACT = false>
     __device__ __forceinline__ void flush(const int* lds, const KP& P, Ego& E, const double2* __restrict__ pos,
                                           const double2* __restrict__ vel) {
         // CBF_FLUSH_U hits' loads in flight per lane (same assembly order as one at a time)
@@ -160,8 +236,15 @@ struct HitList {
                 }
             }
 #pragma unroll
-            for (int q = 0; q < CBF_FLUSH_U; ++q)
-                if (i + q < n) ego_add<FZ>(P, E, pj[q].x, pj[q].y, vj[q].x, vj[q].y);
+            for (int q = 0; q < CBF_FLUSH_U; ++q) {
+                bool keep = i + q < n;
+                if (EXACT && keep) {  // screened candidate: the exact agent cull test
+                    const double e0 = pj[q].x - E.r0, e1 = pj[q].y - E.r1;
+                    const double s = e0 * e0 + e1 * e1;
+                    keep = s < P.cull_t && s > 0;
+                }
+                if (keep) ego_add<FZ>(P, E, pj[q].x, pj[q].y, vj[q].x, vj[q].y);
+            }
         }
         n = 0;
     }
@@ -212,7 +295,43 @@ __device__ __forceinline__ void scan_rows_joint(const int (&t0)[3], const int (&
             if (v + q < L) {
                 const double e0 = p[q].x - E.r0, e1 = p[q].y - E.r1;
                 const double s = e0 * e0 + e1 * e1;
+#if CBF_PUSH_BF
+                H.push_if(lds, tt[q], s < P.cull_t && s > 0);
+#else
                 if (s < P.cull_t && s > 0) H.push(lds, tt[q]);
+#endif
+            }
+        }
+    }
+}
+#endif
+
+#if CBF_SCAN_U > 0
+// scan_rows_joint over fp32 positions with the screen threshold t32 (pushes candidates that
+// may be neighbours, including the ego itself; the flush decides exactly).
+__device__ __forceinline__ void scan_rows_joint32(const int (&t0)[3], const int (&t1)[3], float t32, float ex,
+                                                  float ey, HitList& H, int* lds, const float2* __restrict__ spos32) {
+    const int l0 = t1[0] - t0[0], l01 = l0 + (t1[1] - t0[1]);
+    const int L = l01 + (t1[2] - t0[2]);
+    for (int v = 0; v < L; v += CBF_SCAN_U) {
+        float2 p[CBF_SCAN_U];
+        int tt[CBF_SCAN_U];
+#pragma unroll
+        for (int q = 0; q < CBF_SCAN_U; ++q) {
+            const int vv = v + q;
+            tt[q] = vv < l0 ? t0[0] + vv : (vv < l01 ? t0[1] + (vv - l0) : t0[2] + (vv - l01));
+            if (vv < L) p[q] = spos32[tt[q]];
+        }
+#pragma unroll
+        for (int q = 0; q < CBF_SCAN_U; ++q) {
+            if (v + q < L) {
+                const float d0 = p[q].x - ex, d1 = p[q].y - ey;
+                const float sq = __builtin_fmaf(d0, d0, d1 * d1);
+#if CBF_PUSH_BF
+                H.push_if(lds, tt[q], sq < t32);
+#else
+                if (sq < t32) H.push(lds, tt[q]);
+#endif
             }
         }
     }

@@ -53,6 +53,7 @@ struct CellWs {
     double2* svel;    // [n] cell-sorted velocities / nominal controls
     int32_t* sidx;    // [n] entity index of each sorted slot
     double2* wvel;    // [n] scratch velocities (lattice step: nominal of window agents)
+    float2* spos32;   // [n] fp32 copy of spos (lattice step: the filter's distance screen)
     int32_t* hardq;   // lattice step: [0] = count, records (HardRec) from word kHardHeader
     long ncell;
     int ntiles;
@@ -60,7 +61,7 @@ struct CellWs {
     static int tiles(long ncell) { return (int)((ncell + kScanTile - 1) / kScanTile); }
     static size_t bytes(long n, long ncell) {
         return align256(4 * ncell) + align256(4 * (ncell + 1)) + align256(8 * (size_t)tiles(ncell)) + 256 +
-               align256(16 * n) + 2 * align256(16 * n) + align256(4 * n) + align256(16 * n) +
+               align256(16 * n) + 2 * align256(16 * n) + align256(4 * n) + align256(16 * n) + align256(8 * n) +
                align256(4 * kHardHeader + sizeof(HardRec) * (size_t)n);
     }
     CellWs(void* base, long n, long nc) : ncell(nc), ntiles(tiles(nc)) {
@@ -83,6 +84,8 @@ struct CellWs {
         p += align256(4 * n);
         wvel = (double2*)p;
         p += align256(16 * n);
+        spos32 = (float2*)p;
+        p += align256(8 * n);
         hardq = (int32_t*)p;
     }
 };

@@ -112,25 +112,6 @@ __device__ __forceinline__ void finish_ego(const KP& P, const Ego& E, int k, dou
     if (cnt) cnt[k] = E.count;
 }
 
-// fp32 screen of the cull test (all-pairs path).  A candidate can pass the exact fp64 test
-// s = e0^2 + e1^2 < cull_t (cross_and_rescue.py:141-150) only if S = fl32 distance^2 of the
-// fp32-rounded coordinates is below T32 (bound below); the screen only rejects, every
-// candidate it lets through is re-tested exactly in fp64, so neighbour sets and rows are
-// bit-identical to the unscreened loop.  Bound: with |coords| <= M, u = 2^-24,
-// |E_k - e_k| <= eta = 2uM + u(r + 2uM) (+ fp64 and subnormal slack) for |e_k| < r = sqrt(cull_t),
-// so S <= (cull_t + 2 sqrt2 r eta + 2 eta^2)(1 + 3u); T32 adds slack on every term and rounds up.
-// Coordinates beyond 1e30 (or NaN / inf) switch the screen off for that tile.
-__device__ __forceinline__ float screen_threshold(double cull_t, double M) {
-    if (!(M <= 1e30)) return -1.0f;  // screen off
-    const double u = 0x1p-24;
-    const double r = sqrt(cull_t) * (1.0 + 1e-12);
-    const double eta = 2.0 * u * M + u * (r + 2.0 * u * M) + 1e-14 * r + 1e-35;
-    const double T = (cull_t * (1.0 + 1e-12) + 3.0 * r * eta + 3.0 * eta * eta) * (1.0 + 8.0 * u);
-    float t32 = (float)T;
-    if ((double)t32 < T) t32 = __uint_as_float(__float_as_uint(t32) + 1u);  // next float up (T > 0)
-    return t32;
-}
-
 __device__ __forceinline__ double absmax2(double2 p) { return pmax(fabs(p.x), fabs(p.y)); }
 
 // exact cull test (fp64) + row assembly of staged candidate t (entity base + t)

@@ -146,6 +146,7 @@ __global__ void __launch_bounds__(kBlock) k_lattice_scatter_ordered(long nwin, c
                                                                     double2* __restrict__ spos,
                                                                     double2* __restrict__ svel,
                                                                     int32_t* __restrict__ sidx,
+                                                                    float2* __restrict__ spos32,
                                                                     int32_t* __restrict__ order_state, long n,
                                                                     long ncell, int win_row0, int H) {
     const long t = (long)blockIdx.x * kBlock + threadIdx.x;
@@ -160,9 +161,13 @@ __global__ void __launch_bounds__(kBlock) k_lattice_scatter_ordered(long nwin, c
     const int4 b = bcs[t];
     if (b.x < 0) return;
     const int d = start[b.x] + b.y;
-    spos[d] = pos[b.z];
+    const double2 p = pos[b.z];
+    spos[d] = p;
     svel[d] = wvel[b.z];
     sidx[d] = b.z;
+#if CBF_SCAN32
+    spos32[d] = make_float2((float)p.x, (float)p.y);
+#endif
 }
 
 
@@ -178,7 +183,7 @@ __device__ __forceinline__ int lattice_ego(const KP& P, const CellGrid& G, int W
                                            const int32_t* __restrict__ start, double T, double2* __restrict__ pos_out,
                                            double2* __restrict__ u, int32_t* __restrict__ status,
                                            int32_t* __restrict__ cnt, int32_t* __restrict__ hardq, int* hit_lds,
-                                           double* ny, int* row, int* nbrs) {
+                                           const float2* __restrict__ spos32, double* ny, int* row, int* nbrs) {
     const int w = sidx[slot];
     const int r = win_row0 + w / W;
     const int c = w % W;
@@ -204,15 +209,36 @@ __device__ __forceinline__ int lattice_ego(const KP& P, const CellGrid& G, int W
     }
 #if CBF_ABLATE < 3
     HitList Hl;
-#if CBF_SCAN_U > 0
+#if CBF_SCAN32
+    // screen bound from the ego's own magnitude: a true neighbour lies within r of it
+    const float t32 = screen_threshold(P.cull_t, pmax(fabs(E.r0), fabs(E.r1)) + sqrt(P.cull_t));
+    constexpr bool kExact = true;
+    if (t32 > 0.0f)
+        scan_rows_joint32(rt0, rt1, t32, (float)E.r0, (float)E.r1, Hl, hit_lds, spos32);
+    else
+        Hl.n = kHitCap + 1;  // screen off (non-finite or huge coordinates): the exact direct scan
+#elif CBF_SCAN_U > 0
+    constexpr bool kExact = false;
     scan_rows_joint(rt0, rt1, P, E, Hl, hit_lds, spos);
 #else
+    constexpr bool kExact = false;
 #pragma unroll
     for (int k = 0; k < 3; ++k) scan_range(rt0[k], rt1[k], P, E, Hl, hit_lds, spos);
 #endif
 #if CBF_ABLATE < 2
     if (!Hl.overflowed()) {
-        Hl.template flush<FZ>(hit_lds, P, E, spos, svel);
+#if CBF_BQ_LDS
+        double* bq = reinterpret_cast<double*>(hit_lds + (kHitCap + 1) * kBlock);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) bq[q * kBlock + threadIdx.x] = INFINITY;
+        Hl.template flush_bq<FZ, kExact>(hit_lds, bq, P, E, spos, svel);
+        E.bq0 = bq[threadIdx.x];
+        E.bq1 = bq[kBlock + threadIdx.x];
+        E.bq2 = bq[2 * kBlock + threadIdx.x];
+        E.bq3 = bq[3 * kBlock + threadIdx.x];
+#else
+        Hl.template flush<FZ, kExact>(hit_lds, P, E, spos, svel);
+#endif
     } else {
 #pragma unroll
         for (int k = 0; k < 3; ++k) scan_range_direct<FZ>(rt0[k], rt1[k], P, E, spos, svel);
@@ -284,8 +310,10 @@ __global__ void __launch_bounds__(kBlock) k_lattice_filter(KP P, CellGrid G, int
                                                            int32_t* __restrict__ status, int32_t* __restrict__ cnt,
                                                            int guard_rows, double* __restrict__ ext_part,
                                                            unsigned long long* __restrict__ solves,
-                                                           int32_t* __restrict__ hardq) {
-    __shared__ int hit_lds[kHitCap * kBlock];
+                                                           int32_t* __restrict__ hardq,
+                                                           const float2* __restrict__ spos32) {
+    // hit rows + a dummy row (branch-free push) + 4 x fp64 per-quadrant minima (CBF_BQ_LDS)
+    __shared__ int hit_lds[(kHitCap + 1) * kBlock + (CBF_BQ_LDS ? 8 * kBlock : 0)];
     const int slot = blockIdx.x * kBlock + threadIdx.x;
     const int total = start[ncell];
     double e0 = INFINITY, e1 = -INFINITY, e2 = -INFINITY, e3 = INFINITY;
@@ -294,7 +322,7 @@ __global__ void __launch_bounds__(kBlock) k_lattice_filter(KP P, CellGrid G, int
         double ny;
         int r, nb = 0;
         const int res = lattice_ego<FZ>(P, G, W, row_begin, row_end, win_row0, slot, spos, svel, sidx, start,
-                                               T, pos_out, u, status, cnt, hardq, hit_lds, &ny, &r, &nb);
+                                               T, pos_out, u, status, cnt, hardq, hit_lds, spos32, &ny, &r, &nb);
         solved = res != 0 && nb > 0;
         if (res == 1) ext_accumulate(r, row_begin, row_end, guard_rows, ny, e0, e1, e2, e3);
     }
@@ -487,7 +515,7 @@ extern "C" int cbf_lattice_build(const cbf_params* p, const cbf_grid* grid, int3
                        Wk.start, Wk.ncell, bcs, Wk.hardq);
     launch_scan(Wk, s);
     hipLaunchKernelGGL(k_lattice_scatter_ordered, dim3(nblk(n)), dim3(kBlock), 0, s, n, bcs, Wk.start, p2, wv, Wk.spos,
-                       Wk.svel, Wk.sidx, Wk.hardq + 2, n, Wk.ncell, win_row0, H);
+                       Wk.svel, Wk.sidx, Wk.spos32, Wk.hardq + 2, n, Wk.ncell, win_row0, H);
     return (int)hipGetLastError();
 }
 
@@ -512,7 +540,7 @@ extern "C" int cbf_lattice_advance(const cbf_params* p, const cbf_grid* grid, in
     hipLaunchKernelGGL(p->f_is_zero ? k_lattice_filter<true> : k_lattice_filter<false>, dim3(nb), dim3(kBlock), 0, s,
                        kp, G, W, row_begin, row_end, win_row0, Wk.ncell, Wk.spos, Wk.svel, Wk.sidx, Wk.start, T, po, uo,
                        status, nbr_count, guard_rows, ext_part, reinterpret_cast<unsigned long long*>(solves),
-                       Wk.hardq);
+                       Wk.hardq, Wk.spos32);
     hipLaunchKernelGGL(k_lattice_filter_hard, dim3(hb), dim3(64), 0, s, kp, row_begin, row_end, T, po, uo, status,
                        nbr_count, guard_rows, ext_part ? ext_part + 4l * nb : nullptr, Wk.hardq);
     if (extents) launch_extents_finalize(nb + hb, ext_part, extents, s);

@@ -33,6 +33,22 @@ SETS["phases"] = {
     "no_qp_no_rows": ["-DCBF_ABLATE=2"],
     "no_scan": ["-DCBF_ABLATE=3"],
 }
+SETS["flush"] = {
+    "full": [],
+    "pushbf": ["-DCBF_PUSH_BF=1"],
+    "bqlds": ["-DCBF_BQ_LDS=1"],
+    "both": ["-DCBF_PUSH_BF=1", "-DCBF_BQ_LDS=1"],
+    "both_f2": ["-DCBF_PUSH_BF=1", "-DCBF_BQ_LDS=1", "-DCBF_FLUSH_U=2"],
+    "both_s8": ["-DCBF_PUSH_BF=1", "-DCBF_BQ_LDS=1", "-DCBF_SCAN_U=8"],
+}
+SETS["scan32"] = {
+    "full": [],
+    "s32": ["-DCBF_SCAN32=1"],
+    "s32_bq": ["-DCBF_SCAN32=1", "-DCBF_BQ_LDS=1"],
+    "s32_bq_s8": ["-DCBF_SCAN32=1", "-DCBF_BQ_LDS=1", "-DCBF_SCAN_U=8"],
+    "s32_bq_bf": ["-DCBF_SCAN32=1", "-DCBF_BQ_LDS=1", "-DCBF_PUSH_BF=1"],
+    "bq": ["-DCBF_BQ_LDS=1"],
+}
 SETS["hard"] = {
     "full": [],
     "hard1024": ["-DCBF_HARD_BLOCKS=1024"],
