@@ -303,7 +303,8 @@ __global__ void __launch_bounds__(kBlock) k_lattice_filter_hocbf(
     int32_t* __restrict__ status, int32_t* __restrict__ cnt, int guard_rows, double* __restrict__ ext_part,
     unsigned long long* __restrict__ solves) {
     __shared__ unsigned long long keys[kHocbfCap * kBlock];
-    const int slot = blockIdx.x * kBlock + threadIdx.x;
+    const int bx = xcd_block();
+    const int slot = bx * kBlock + threadIdx.x;
     const int total = start[ncell];
     double e0 = INFINITY, e1 = -INFINITY, e2 = -INFINITY, e3 = INFINITY;
     bool solved = false;
@@ -386,10 +387,10 @@ __global__ void __launch_bounds__(kBlock) k_lattice_filter_hocbf(
     if (solves) {
         const unsigned long long mk = __ballot(solved);
         if ((threadIdx.x & 63) == 0 && mk)
-            atomicAdd(&solves[16 * ((blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6)) & 63)],
+            atomicAdd(&solves[16 * ((bx * (kBlock / 64) + (threadIdx.x >> 6)) & 63)],
                       (unsigned long long)__popcll(mk));
     }
-    if (ext_part) block_extents(e0, e1, e2, e3, ext_part + 4l * blockIdx.x);
+    if (ext_part) block_extents(e0, e1, e2, e3, ext_part + 4l * bx);
 }
 
 inline int nblocks(long n) { return (int)((n + kBlock - 1) / kBlock); }

@@ -7,6 +7,24 @@
 
 namespace cbf {
 
+// CBF_XCD_REMAP: blocks are dealt round-robin over the 8 XCDs (b and b+8 share one L2), so
+// consecutive blocks -- which read the same cell rows of the sorted arrays -- would pull the same
+// lines into every XCD's L2.  The remap is a bijection of [0, nb) that hands each XCD one
+// contiguous range of logical blocks.  Speed only: placement is never assumed for correctness.
+#ifndef CBF_XCD_REMAP
+#define CBF_XCD_REMAP 1
+#endif
+
+__device__ __forceinline__ int xcd_block() {
+#if CBF_XCD_REMAP
+    const int b = blockIdx.x, nb = gridDim.x;
+    const int q = nb >> 3, rem = nb & 7, x = b & 7, j = b >> 3;
+    return (x < rem ? x * (q + 1) : rem * (q + 1) + (x - rem) * q) + j;
+#else
+    return blockIdx.x;
+#endif
+}
+
 __device__ __forceinline__ double wave_min(double v) {
     for (int o = 32; o > 0; o >>= 1) v = pmin(v, __shfl_xor(v, o, 64));
     return v;

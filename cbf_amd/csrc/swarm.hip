@@ -92,7 +92,7 @@ __global__ void __launch_bounds__(kBlock) k_lattice_nominal_bin_ordered(
     double gain, double2* __restrict__ wvel, double2* __restrict__ vel_out, int32_t* __restrict__ count,
     const int32_t* __restrict__ order, const int32_t* __restrict__ start, long ncell, int4* __restrict__ bcs,
     int32_t* __restrict__ hardq) {
-    const long t = (long)blockIdx.x * kBlock + threadIdx.x;
+    const long t = (long)xcd_block() * kBlock + threadIdx.x;
     const long nwin = (long)win_rows * W;
     // hardq[2..4]: the previous build left a cell order for this window size and grid (else
     // identity); the order only permutes the work, so a stale one costs speed, never results
@@ -149,7 +149,7 @@ __global__ void __launch_bounds__(kBlock) k_lattice_scatter_ordered(long nwin, c
                                                                     float2* __restrict__ spos32,
                                                                     int32_t* __restrict__ order_state, long n,
                                                                     long ncell, int win_row0, int H) {
-    const long t = (long)blockIdx.x * kBlock + threadIdx.x;
+    const long t = (long)xcd_block() * kBlock + threadIdx.x;
     if (t == 0) {  // the cell order now exists for this window and grid: the next build walks it
         order_state[0] = 1;
         order_state[1] = (int)n;
@@ -314,7 +314,8 @@ __global__ void __launch_bounds__(kBlock) k_lattice_filter(KP P, CellGrid G, int
                                                            const float2* __restrict__ spos32) {
     // hit rows + a dummy row (branch-free push) + 4 x fp64 per-quadrant minima (CBF_BQ_LDS)
     __shared__ int hit_lds[(kHitCap + 1) * kBlock + (CBF_BQ_LDS ? 8 * kBlock : 0)];
-    const int slot = blockIdx.x * kBlock + threadIdx.x;
+    const int bx = xcd_block();
+    const int slot = bx * kBlock + threadIdx.x;
     const int total = start[ncell];
     double e0 = INFINITY, e1 = -INFINITY, e2 = -INFINITY, e3 = INFINITY;
     bool solved = false;
@@ -329,10 +330,10 @@ __global__ void __launch_bounds__(kBlock) k_lattice_filter(KP P, CellGrid G, int
     if (solves) {  // wave-aggregated, spread over 64 counters on separate 128-B lines
         const unsigned long long m = __ballot(solved);
         if ((threadIdx.x & 63) == 0 && m)
-            atomicAdd(&solves[16 * ((blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6)) & 63)],
+            atomicAdd(&solves[16 * ((bx * (kBlock / 64) + (threadIdx.x >> 6)) & 63)],
                       (unsigned long long)__popcll(m));
     }
-    if (ext_part) block_extents(e0, e1, e2, e3, ext_part + 4l * blockIdx.x);
+    if (ext_part) block_extents(e0, e1, e2, e3, ext_part + 4l * bx);
 }
 
 // K5: the queued hard QPs (state assembled by K4), 64-lane blocks spread over the CUs.

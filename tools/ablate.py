@@ -55,6 +55,10 @@ SETS["hard"] = {
     "hard2048": ["-DCBF_HARD_BLOCKS=2048"],
     "hard4096": ["-DCBF_HARD_BLOCKS=4096"],
 }
+SETS["xcd"] = {
+    "full": [],
+    "noxcd": ["-DCBF_XCD_REMAP=0"],
+}
 VARIANTS = {
     "full": [],
     "flush2": ["-DCBF_FLUSH_U=2"],
@@ -153,6 +157,13 @@ def run(rounds, iters, W, H):
                     times[name]["advance"].append(e1.elapsed_time(e2))
     res = {n: {k: {"median_us": float(np.median(v)) * 1e3, "min_us": float(np.min(v)) * 1e3}
                for k, v in t.items()} for n, t in times.items()}
+    # every variant ran the same number of steps from the same state: results must be bit-identical
+    ref = names[0]
+    for n in names[1:]:
+        same = all(torch.equal(st[n][f], st[ref][f]) for f in ("pos", "vel", "u", "status", "cnt"))
+        res[n]["bit_identical_to_" + ref] = bool(same)
+        if not same:
+            print(f"MISMATCH {n} vs {ref}", file=sys.stderr)
     print(json.dumps(res, indent=1))
     return res
 
