@@ -39,10 +39,25 @@ class CbfDiag(C.Structure):
                 ("box_active", C.c_void_p), ("x", C.c_void_p), ("viol", C.c_void_p)]
 
 
+class CbfCertParams(C.Structure):
+    _fields_ = [("barrier_gain", C.c_double), ("safety_radius", C.c_double), ("magnitude_limit", C.c_double),
+                ("boundary_points", C.c_double * 4), ("viol_tol", C.c_double), ("max_iter", C.c_int32)]
+
+
+class CbfUnicycleParams(C.Structure):
+    _fields_ = [("projection_distance", C.c_double), ("angular_velocity_limit", C.c_double),
+                ("time_step", C.c_double), ("wheel_radius", C.c_double), ("base_length", C.c_double),
+                ("max_linear_velocity", C.c_double), ("max_angular_velocity", C.c_double),
+                ("max_wheel_velocity", C.c_double), ("wheel_threshold", C.c_int32)]
+
+
+CERT_OPTIMAL, CERT_INFEASIBLE, CERT_MAXITER = 1, 2, 3
+
 # symbol -> (restype, argtypes); kept in sync with include/cbf_amd.h (tests check every export)
 _vp, _i32, _d, _sz = C.c_void_p, C.c_int32, C.c_double, C.c_size_t
 _P, _G, _D = C.POINTER(CbfParams), C.POINTER(CbfGrid), C.POINTER(CbfDiag)
 _HP = C.POINTER(CbfHocbf)
+_CP, _UP = C.POINTER(CbfCertParams), C.POINTER(CbfUnicycleParams)
 SIGNATURES = {
     "cbf_abi_version": (C.c_int, []),
     "cbf_params_init": (C.c_int, [_P, _d, _d, _d, _vp, _vp, _d]),
@@ -71,6 +86,12 @@ SIGNATURES = {
                                             _vp, _i32, _vp, _vp, _vp, _sz, _vp]),
     "cbf_mc_rollout": (C.c_int, [_P, _i32, _i32, _i32, _i32, _d, _d, _d, _d, _d, _vp, _vp, _vp, _vp]),
     "cbf_halo_guard": (C.c_int, [_vp, C.c_int64, _i32, _i32, _d, _vp, _vp]),
+    "cbf_cert_params_init": (C.c_int, [_CP, _d, _d, _d, _vp]),
+    "cbf_si_barrier_cert_lds_bytes": (_sz, [_i32]),
+    "cbf_si_barrier_cert": (C.c_int, [_CP, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "cbf_unicycle_params_init": (C.c_int, [_UP]),
+    "cbf_uni_to_si": (C.c_int, [_UP, _i32, _vp, _vp, _vp]),
+    "cbf_unicycle_advance": (C.c_int, [_UP, _i32, _vp, _vp, _vp, _i32, _vp]),
 }
 
 if not os.path.exists(LIB_PATH):

@@ -259,6 +259,65 @@ int cbf_halo_guard(const double* ext_all, int64_t stride, int32_t world_size, in
 int cbf_mc_rollout(const cbf_params* p, int32_t n_scen, int32_t n_o, int32_t n_a, int32_t steps, double T, double rc,
                    double rs, double so, double ga, double* pos, int64_t* counters, double* maxviol, void* stream);
 
+/*
+ * robotarium-lite: the rps calls the reference scripts wrap around the
+ * filter.  rps is third-party and absent (install.sh:1 clones it unpinned): these restate its
+ * published algorithms; parity against rps itself is unpinned.
+ *
+ * Single-integrator barrier certificate with boundary -- replaces
+ *   si_barrier_cert = create_single_integrator_barrier_certificate_with_boundary(safety_radius=0.12)
+ *   si_velocities = si_barrier_cert(si_velocities, x_si[:, :4])      cross_and_rescue.py:72,163
+ * (meet_at_center.py:58,109 creates it; its application is commented out there).  The coupled
+ * QP  min |v - y|^2  s.t.  -2 e_ij.(v_i - v_j) <= gain h_ij^3 for every pair i < j and four
+ * boundary rows per agent, y = dxi thresholded to magnitude_limit, is solved EXACTLY
+ * (Goldfarb-Idnani dual active set; rps calls cvxopt.solvers.qp).  batch independent
+ * scenarios of n_agents (1..32) each: dxi, x, out are [batch][n_agents][2] (agent-major: the
+ * (2, N) rps arrays transposed).  status[batch] = CBF_CERT_*; iters / n_active may be NULL.
+ * An infeasible QP (or the iteration cap) returns the thresholded input.
+ */
+#define CBF_CERT_OPTIMAL 1
+#define CBF_CERT_INFEASIBLE 2
+#define CBF_CERT_MAXITER 3
+typedef struct cbf_cert_params {
+    double barrier_gain;       /* 100 */
+    double safety_radius;      /* 0.17 (cross_and_rescue.py:72 passes 0.12) */
+    double magnitude_limit;    /* 0.2 */
+    double boundary_points[4]; /* (-1.6, 1.6, -1.0, 1.0): x_min, x_max, y_min, y_max */
+    double viol_tol;           /* a row counts as violated below -viol_tol * max(1, |b|) (1e-12) */
+    int32_t max_iter;          /* 0 = 10 (m + 2 n_agents) + 10 */
+} cbf_cert_params;
+int cbf_cert_params_init(cbf_cert_params* c, double barrier_gain, double safety_radius, double magnitude_limit,
+                         const double* boundary_points4);
+size_t cbf_si_barrier_cert_lds_bytes(int32_t n_agents);
+int cbf_si_barrier_cert(const cbf_cert_params* c, int32_t batch, int32_t n_agents, const double* dxi, const double* x,
+                        double* out, int32_t* status, int32_t* iters, int32_t* n_active, void* stream);
+
+/*
+ * Unicycle side of the robotarium: poses are [n][3] = (x, y, theta) (the (3, N) rps array
+ * transposed), single-integrator vectors [n][2].
+ *   cbf_uni_to_si        uni_to_si_states (create_si_to_uni_mapping)  cross_and_rescue.py:75,101
+ *   cbf_unicycle_advance mode 0: si_to_uni_dyn (:167) -> Robotarium.set_velocities (:170) ->
+ *                        step (:175): motor (wheel-speed) threshold, Euler on (x, y, theta),
+ *                        atan2 wrap; poses updated in place; dxu [n][2] = si_to_uni_dyn output
+ *                        (may be NULL).  mode 1: si_to_uni_dyn alone (poses untouched, dxu
+ *                        required).  mode 2: `dxi` holds unicycle (v, w): set_velocities + step.
+ */
+typedef struct cbf_unicycle_params {
+    double projection_distance;    /* 0.05 */
+    double angular_velocity_limit; /* pi (si_to_uni_dyn clamp) */
+    double time_step;              /* 0.033 */
+    double wheel_radius;           /* 0.016 */
+    double base_length;            /* 0.105 */
+    double max_linear_velocity;    /* 0.2 */
+    double max_angular_velocity;   /* 2 (r / 0.11) (0.2 / r) */
+    double max_wheel_velocity;     /* 0.2 / r */
+    int32_t wheel_threshold;       /* 1: step() thresholds the wheel speeds */
+} cbf_unicycle_params;
+int cbf_unicycle_params_init(cbf_unicycle_params* u);
+int cbf_uni_to_si(const cbf_unicycle_params* u, int32_t n, const double* poses, double* si, void* stream);
+int cbf_unicycle_advance(const cbf_unicycle_params* u, int32_t n, double* poses, const double* dxi, double* dxu,
+                         int32_t mode, void* stream);
+
 /* ABI version of the loaded library (== CBF_ABI_VERSION). */
 int cbf_abi_version(void);
 
