@@ -261,6 +261,81 @@ def bench_mc(args, ws, rank, local):
                          "traffic": None, "note": "state lives in LDS for the whole rollout; no HBM traffic per step"}}
 
 
+def cert_scenarios(B, N, seed=0):
+    """Certificate workload: B independent scenarios of N agents on a jittered ring of radius
+    min(0.05 N, 0.8) (inside the arena, neighbours >= 0.15 apart), each agent commanded toward
+    the centre (pair rows bind, as in a rendezvous)."""
+    rng = np.random.default_rng(seed)
+    th = np.arange(N) * (2 * np.pi / N)
+    rad = min(0.05 * N, 0.8)
+    x = np.stack([rad * np.cos(th), rad * np.sin(th)], axis=1)[None] + rng.normal(0, 0.02, (B, N, 2))
+    dxi = -x * rng.uniform(0.5, 2.0, (B, 1, 1))
+    return np.ascontiguousarray(dxi), np.ascontiguousarray(x)
+
+
+def cpu_baseline_cert(dxi, x, budget_s):
+    """rps's CPU path for the certificate: the QP of barrier_certificates.py solved by the
+    restated cvxopt coneqp with the options rps sets (reltol = feastol = 1e-2, maxiters 50;
+    upstream, unverified) on a bounded sample, one core."""
+    from oracle import cvxqp, rps_lite as R
+    t0 = time.perf_counter()
+    done = 0
+    while time.perf_counter() - t0 < budget_s and done < dxi.shape[0]:
+        y, A, b = R.si_barrier_qp(dxi[done].T, x[done].T, safety_radius=0.12)
+        n = y.shape[0]
+        cvxqp.coneqp(2 * np.eye(n), -2 * y, A, b, maxiters=50, reltol=1e-2, feastol=1e-2)
+        done += 1
+    dt = time.perf_counter() - t0
+    return {"value": done / dt, "unit": "certificate QPs/s", "cores": 1, "kind": "port",
+            "sample": f"{done} scenarios of the same workload: rps's QP assembly + cvxopt coneqp restated in numpy "
+                      f"(rps options), {dt:.1f} s on one core; rps and cvxopt are absent from the image"}
+
+
+def bench_cert(args, ws, rank, local):
+    """the coupled single-integrator barrier certificate (cross_and_rescue.py:163),
+    batched over independent scenarios (scenario-sharded across ranks, weak scaling)."""
+    import torch
+    from cbf_amd import rps
+    B, N = args.cert_scenarios, args.cert_agents
+    dxi, x = cert_scenarios(B, N, seed=args.seed + rank)
+    D, X = torch.tensor(dxi, device="cuda"), torch.tensor(x, device="cuda")
+    cert = rps.SiBarrierCert(safety_radius=0.12)
+    for _ in range(max(1, args.warmup)):
+        r = cert.batch(D, X, iters=True)
+    if ws > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    e0.record()
+    for _ in range(args.steps):
+        r = cert.batch(D, X, iters=True)
+    e1.record()
+    torch.cuda.synchronize()
+    if ws > 1:
+        torch.distributed.barrier()
+    elapsed, _ = _reduce(time.perf_counter() - t0, 0, ws)
+    st = r["status"].cpu().numpy()
+    na = r["n_active"].cpu().numpy()
+    it = r["iters"].cpu().numpy()
+    total = B * ws * args.steps
+    return {"metric": "certificate QPs/s (coupled si_barrier_cert, SURVEY 8f row 3)", "value": total / elapsed,
+            "unit": "certificate QPs/s", "n_gpus": ws, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "f64", "data": "synthetic",
+            "config": {"workload": f"{B} scenarios x {N} agents per GPU, rendezvous-shaped, exact Goldfarb-Idnani "
+                                   f"solve of {N * (N - 1) // 2 + 4 * N} rows x {2 * N} variables per scenario",
+                       "parallelism": f"scenario shards x{ws}" if ws > 1 else "single GPU"},
+            "agent_velocities_per_s": total * N / elapsed,
+            "kernel_ms": e0.elapsed_time(e1) / args.steps,
+            "optimal_fraction": float((st == 1).mean()), "mean_active_rows": float(na.mean()),
+            "mean_iterations": float(it.mean()),
+            "roofline": {"bound": "latency (LDS + dependent Givens chains)", "achieved": None, "peak": None,
+                         "unit": None, "frac": None, "traffic": None,
+                         "note": "one wavefront per scenario; the factors live in LDS, HBM traffic is 48 B/agent"},
+            "_cert_sample": (dxi[:512], x[:512])}
+
+
 def _reduce(elapsed, solves, ws):
     if ws == 1:
         return elapsed, solves
@@ -274,7 +349,9 @@ def _reduce(elapsed, solves, ws):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--config", default="cfg4", choices=["cfg4", "cfg3", "cfg5"])
+    ap.add_argument("--config", default="cfg4", choices=["cfg4", "cfg3", "cfg5", "cert"])
+    ap.add_argument("--cert-scenarios", type=int, default=100000)
+    ap.add_argument("--cert-agents", type=int, default=16)
     ap.add_argument("--mc-scenarios", type=int, default=100000)
     ap.add_argument("--mc-inner", type=int, default=10, help="cfg5: timesteps per bench step")
     ap.add_argument("--gpus", type=int, default=1)
@@ -304,11 +381,16 @@ def main():
         res = bench_allpairs(args, ws, rank, local)
     elif args.config == "cfg5":
         res = bench_mc(args, ws, rank, local)
+    elif args.config == "cert":
+        res = bench_cert(args, ws, rank, local)
     else:
         res = bench_lattice(args, ws, rank, local)
     if rank == 0:
+        sample = res.pop("_cert_sample", None)
         if ws == 1 and not args.no_cpu_baseline and args.config == "cfg4":
             res["cpu_baseline"] = cpu_baseline_lattice(args.width, args.rows, args.seed, args.cpu_budget)
+        elif ws == 1 and not args.no_cpu_baseline and args.config == "cert":
+            res["cpu_baseline"] = cpu_baseline_cert(*sample, budget_s=min(args.cpu_budget, 8.0))
         else:
             res["cpu_baseline"] = None
         print(json.dumps(res), flush=True)
