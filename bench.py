@@ -33,13 +33,15 @@ def _dist_env():
     return ws, rank, local
 
 
-def load_pmc_traffic(kernel="k_lattice_filter"):
-    """HBM bytes per launch of the dominant kernel from the committed PMC summary, if any."""
+def load_pmc_traffic(kernels=("k_lattice_filter", "k_lattice_filter_hard")):
+    """HBM bytes per launch of the advance phase (sum over its kernels) from the committed PMC
+    summary (profiles/pmc_summary.json, written by tools/summarize_profile.py), if present."""
     path = os.path.join(ROOT, "profiles", "pmc_summary.json")
     try:
         with open(path) as f:
             d = json.load(f)
-        return d.get(kernel, {}).get("hbm_bytes_per_launch")
+        vals = [d.get(k, {}).get("hbm_bytes_per_launch") for k in kernels]
+        return None if any(v is None for v in vals) else float(sum(vals))
     except (OSError, ValueError):
         return None
 
@@ -80,13 +82,15 @@ def bench_lattice(args, ws, rank, local):
     from cbf_amd import scenarios, swarm
     W = args.width
     rows = args.rows
-    if ws > 1:
+    if ws > 1 or args.shard:
         from cbf_amd.shard import ShardedLattice
         S = ShardedLattice(W, rows, seed=args.seed)
     else:
         pos = scenarios.lattice(W, rows, seed=args.seed)
         S = swarm.LatticeSwarm(pos, W, rows, gain=scenarios.LATTICE_GAIN, barrier=args.barrier)
-    use_graph = not args.eager
+    # the sharded step stays eager: two graph replays around the collective measured slower
+    # (121 vs 106 us per step at one rank) than eager launches
+    use_graph = not args.eager and not (ws > 1 or args.shard)
     if use_graph:
         S.capture()
     for _ in range(args.warmup):
@@ -109,7 +113,7 @@ def bench_lattice(args, ws, rank, local):
     t1 = time.perf_counter()
     elapsed = t1 - t0
     solves = S.solves_total()
-    n_local = S.n_owned if ws > 1 else S.n
+    n_local = S.n_owned if (ws > 1 or args.shard) else S.n
     if ws > 1:
         t = torch.tensor([elapsed, float(solves), float(n_local)], dtype=torch.float64, device="cuda")
         mx = t.clone()
@@ -152,8 +156,8 @@ def bench_lattice(args, ws, rank, local):
                                "consensus + radius-0.2 cell-list cull + CBF QP + clip + Euler, one fused timestep "
                                "per step", "barrier": args.barrier,
                    "agents_total": n_total, "agents_per_gpu": n_local,
-                   "parallelism": f"row-stripe shards x{ws}, 1 RCCL all-gather of halo slabs / step" if ws > 1
-                   else "single GPU", "graph": use_graph},
+                   "parallelism": f"row-stripe shards x{ws}, 1 RCCL all-gather of halo slabs / step"
+                   if (ws > 1 or args.shard) else "single GPU", "graph": use_graph},
         "timesteps_per_s": args.steps / elapsed,
         "solves_per_step": solves / args.steps,
         "status_fraction_last_step": {"idle": codes[0] / len(status), "optimal": codes[1] / len(status),
@@ -162,7 +166,8 @@ def bench_lattice(args, ws, rank, local):
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS,
                      "traffic": traffic if args.barrier == "reference" else None,
-                     "kernel": "k_lattice_filter" if args.barrier == "reference" else "k_lattice_filter_hocbf",
+                     "kernel": "advance phase: k_lattice_filter + k_lattice_filter_hard" if args.barrier == "reference"
+                     else "k_lattice_filter_hocbf",
                      "kernel_ms": k_ms,
                      "algorithmic_bytes_per_launch": FILTER_BYTES_PER_AGENT * n_local,
                      "step_algorithmic_GBps": STEP_BYTES_PER_AGENT * n_local * args.steps / elapsed / 1e9 / ws},
@@ -366,13 +371,18 @@ def main():
     ap.add_argument("--barrier", default="reference", choices=["reference", "euclidean_hocbf"],
                     help="cfg4 single-GPU: the reference's L1 barrier rows or the Euclidean HOCBF mode")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
+    ap.add_argument("--shard", action="store_true",
+                    help="cfg4: run the sharded step (halo pack + collective + unpack) even on one rank")
     args = ap.parse_args()
     ws, rank, local = _dist_env()
     import torch
-    if ws > 1:
+    if ws > 1 or args.shard:
         torch.cuda.set_device(local)
         os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
-        torch.distributed.init_process_group("nccl", device_id=torch.device("cuda", local))
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29533")
+        torch.distributed.init_process_group("nccl", device_id=torch.device("cuda", local), rank=rank,
+                                             world_size=ws)
     else:
         torch.cuda.set_device(0)
     if args.config == "cfg3":
@@ -394,7 +404,7 @@ def main():
         else:
             res["cpu_baseline"] = None
         print(json.dumps(res), flush=True)
-    if ws > 1:
+    if torch.distributed.is_initialized():
         torch.distributed.destroy_process_group()
 
 

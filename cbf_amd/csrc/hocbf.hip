@@ -390,7 +390,7 @@ __global__ void __launch_bounds__(kBlock) k_lattice_filter_hocbf(
             atomicAdd(&solves[16 * ((bx * (kBlock / 64) + (threadIdx.x >> 6)) & 63)],
                       (unsigned long long)__popcll(mk));
     }
-    if (ext_part) block_extents(e0, e1, e2, e3, ext_part + 4l * bx);
+    if (ext_part) wave_extents(e0, e1, e2, e3, ext_part, (long)bx * (kBlock / 64) + (threadIdx.x >> 6));
 }
 
 inline int nblocks(long n) { return (int)((n + kBlock - 1) / kBlock); }
@@ -456,6 +456,6 @@ extern "C" int cbf_lattice_advance_hocbf(const cbf_params* p, const cbf_hocbf* h
                        row_end, win_row0, Wk.ncell, Wk.spos, Wk.svel, Wk.sidx, Wk.start, T,
                        reinterpret_cast<double2*>(pos_out), reinterpret_cast<double2*>(u), status, nbr_count,
                        guard_rows, ext_part, reinterpret_cast<unsigned long long*>(solves));
-    if (extents) launch_extents_finalize(nb, ext_part, extents, s);
+    if (extents) launch_extents_finalize((int)lattice_ext_waves(n), ext_part, extents, s);
     return (int)hipGetLastError();
 }

@@ -35,31 +35,18 @@ __device__ __forceinline__ double wave_max(double v) {
     return v;
 }
 
-// Per-block extents of the new owned y (halo guard of the sharded step): {min, max, max over rows
-// < row_end - guard, min over rows >= row_begin + guard}.
-__device__ __forceinline__ void block_extents(double e0, double e1, double e2, double e3, double* out) {
-    __shared__ double red[4][kBlock / 64];
+// Per-wave extents of the new owned y (halo guard of the sharded step): {min, max, max over rows
+// < row_end - guard, min over rows >= row_begin + guard}; lane 0 writes part[4 * wave].  Per wave,
+// not per block: a block-wide barrier at the end would hold every wave of a block until its
+// slowest finished.
+__device__ __forceinline__ void wave_extents(double e0, double e1, double e2, double e3, double* part, long wave) {
     const double m0 = wave_min(e0), m1 = wave_max(e1), m2 = wave_max(e2), m3 = wave_min(e3);
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    if (lane == 0) {
-        red[0][wid] = m0;
-        red[1][wid] = m1;
-        red[2][wid] = m2;
-        red[3][wid] = m3;
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        double a = red[0][0], b = red[1][0], c2 = red[2][0], d = red[3][0];
-        for (int q = 1; q < kBlock / 64; ++q) {
-            a = pmin(a, red[0][q]);
-            b = pmax(b, red[1][q]);
-            c2 = pmax(c2, red[2][q]);
-            d = pmin(d, red[3][q]);
-        }
-        out[0] = a;
-        out[1] = b;
-        out[2] = c2;
-        out[3] = d;
+    if ((threadIdx.x & 63) == 0) {
+        double* o = part + 4 * wave;
+        o[0] = m0;
+        o[1] = m1;
+        o[2] = m2;
+        o[3] = m3;
     }
 }
 
@@ -71,12 +58,12 @@ __device__ __forceinline__ void ext_accumulate(int r, int row_begin, int row_end
     if (r >= row_begin + guard_rows) e3 = pmin(e3, ny);
 }
 
-// Reduces nparts per-block extents to out[4] (one-block kernel, defined in swarm.hip).
+// Reduces nparts per-wave extents to out[4] (one-block kernel, defined in swarm.hip).
 void launch_extents_finalize(int nparts, const double* part, double* out, hipStream_t s);
 
-inline size_t lattice_ext_bytes(long win_n) {
-    return align256(32 * (size_t)((win_n + kBlock - 1) / kBlock + kHardBlocks));
-}
+// partial extents: one record per wave of the filter grid, then one per hard-QP block
+inline long lattice_ext_waves(long win_n) { return (win_n + kBlock - 1) / kBlock * (kBlock / 64); }
+inline size_t lattice_ext_bytes(long win_n) { return align256(32 * (size_t)(lattice_ext_waves(win_n) + kHardBlocks)); }
 
 inline int check_lattice(const cbf_params* p, const cbf_grid* grid, int32_t W, int32_t H, int32_t row_begin,
                          int32_t row_end, int32_t win_row0, int32_t win_rows, const double* pos, void* workspace,

@@ -12,6 +12,8 @@ namespace {
 
 inline int nblk(long n) { return (int)((n + kBlock - 1) / kBlock); }
 
+constexpr int kExtSlotWords = 16;  // one 128-B line per extents slot (4 keys used)
+
 __global__ void __launch_bounds__(kBlock) k_consensus_csr(int n_dst, int self_offset, int n_group,
                                                           const double2* __restrict__ src,
                                                           const double2* __restrict__ anchors,
@@ -91,7 +93,7 @@ __global__ void __launch_bounds__(kBlock) k_lattice_nominal_bin_ordered(
     CellGrid G, int W, int H, int row_begin, int row_end, int win_row0, int win_rows, const double2* __restrict__ pos,
     double gain, double2* __restrict__ wvel, double2* __restrict__ vel_out, int32_t* __restrict__ count,
     const int32_t* __restrict__ order, const int32_t* __restrict__ start, long ncell, int4* __restrict__ bcs,
-    int32_t* __restrict__ hardq) {
+    int32_t* __restrict__ hardq, unsigned long long* __restrict__ ext_keys, int guard_rows) {
     const long t = (long)xcd_block() * kBlock + threadIdx.x;
     const long nwin = (long)win_rows * W;
     // hardq[2..4]: the previous build left a cell order for this window size and grid (else
@@ -114,8 +116,47 @@ __global__ void __launch_bounds__(kBlock) k_lattice_nominal_bin_ordered(
             }
         }
     }
-    // runs of equal cells inside the wave: one atomic per run
     const int lane = threadIdx.x & 63;
+    if (ext_keys) {
+        // y-extents of the owned INPUT positions (halo guard of the sharded step, checked one
+        // exchange later): reduced per block, then one atomic per value into one of 64 slots on
+        // separate 128-B lines (cross-XCD atomics on a shared line serialise at the memory side)
+        __shared__ double red[4][kBlock / 64];
+        double e0 = INFINITY, e1 = -INFINITY, e2 = -INFINITY, e3 = INFINITY;
+        int any = 0;
+        if (cell >= 0) {
+            const int r = win_row0 + (int)(w / W);
+            if (r >= row_begin && r < row_end) {
+                ext_accumulate(r, row_begin, row_end, guard_rows, p.y, e0, e1, e2, e3);
+                any = 1;
+            }
+        }
+        e0 = wave_min(e0);
+        e1 = wave_max(e1);
+        e2 = wave_max(e2);
+        e3 = wave_min(e3);
+        const int wid = threadIdx.x >> 6;
+        if (lane == 0) {
+            red[0][wid] = e0;
+            red[1][wid] = e1;
+            red[2][wid] = e2;
+            red[3][wid] = e3;
+        }
+        if (__syncthreads_or(any) && threadIdx.x == 0) {
+            for (int q = 1; q < kBlock / 64; ++q) {
+                e0 = pmin(e0, red[0][q]);
+                e1 = pmax(e1, red[1][q]);
+                e2 = pmax(e2, red[2][q]);
+                e3 = pmin(e3, red[3][q]);
+            }
+            unsigned long long* k = ext_keys + kExtSlotWords * (blockIdx.x & 63);
+            atomicMin(&k[0], dkey(e0));
+            atomicMax(&k[1], dkey(e1));
+            atomicMax(&k[2], dkey(e2));
+            atomicMin(&k[3], dkey(e3));
+        }
+    }
+    // runs of equal cells inside the wave: one atomic per run
     int cprev = __shfl_up(cell, 1, 64);
     const bool leader = lane == 0 || cell != cprev;
     const unsigned long long lm = __ballot(leader);
@@ -333,7 +374,7 @@ __global__ void __launch_bounds__(kBlock) k_lattice_filter(KP P, CellGrid G, int
             atomicAdd(&solves[16 * ((bx * (kBlock / 64) + (threadIdx.x >> 6)) & 63)],
                       (unsigned long long)__popcll(m));
     }
-    if (ext_part) block_extents(e0, e1, e2, e3, ext_part + 4l * bx);
+    if (ext_part) wave_extents(e0, e1, e2, e3, ext_part, (long)bx * (kBlock / 64) + (threadIdx.x >> 6));
 }
 
 // K5: the queued hard QPs (state assembled by K4), 64-lane blocks spread over the CUs.
@@ -382,20 +423,32 @@ __global__ void __launch_bounds__(64) k_lattice_filter_hard(KP P, int row_begin,
 }
 
 
-__global__ void __launch_bounds__(kBlock) k_extents_finalize(int nparts, const double* __restrict__ part,
-                                                             double* __restrict__ out) {
+constexpr int kFinBlock = 1024;
+__global__ void __launch_bounds__(kFinBlock) k_extents_finalize(int nparts, const double* __restrict__ part,
+                                                                double* __restrict__ out) {
     double a = INFINITY, b = -INFINITY, c = -INFINITY, d = INFINITY;
-    for (int i = threadIdx.x; i < nparts; i += kBlock) {
-        a = pmin(a, part[4 * i]);
-        b = pmax(b, part[4 * i + 1]);
-        c = pmax(c, part[4 * i + 2]);
-        d = pmin(d, part[4 * i + 3]);
+    // 8 records in flight per thread (the reduction is latency-bound on one block)
+    for (int i0 = threadIdx.x; i0 < nparts; i0 += 8 * kFinBlock) {
+        double4 r[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const int i = i0 + k * kFinBlock;
+            r[k] = i < nparts ? reinterpret_cast<const double4*>(part)[i]
+                              : make_double4(INFINITY, -INFINITY, -INFINITY, INFINITY);
+        }
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            a = pmin(a, r[k].x);
+            b = pmax(b, r[k].y);
+            c = pmax(c, r[k].z);
+            d = pmin(d, r[k].w);
+        }
     }
     a = wave_min(a);
     b = wave_max(b);
     c = wave_max(c);
     d = wave_min(d);
-    __shared__ double red[4][kBlock / 64];
+    __shared__ double red[4][kFinBlock / 64];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     if (lane == 0) {
         red[0][wid] = a;
@@ -405,7 +458,7 @@ __global__ void __launch_bounds__(kBlock) k_extents_finalize(int nparts, const d
     }
     __syncthreads();
     if (threadIdx.x == 0) {
-        for (int q = 1; q < kBlock / 64; ++q) {
+        for (int q = 1; q < kFinBlock / 64; ++q) {
             red[0][0] = pmin(red[0][0], red[0][q]);
             red[1][0] = pmax(red[1][0], red[1][q]);
             red[2][0] = pmax(red[2][0], red[2][q]);
@@ -442,7 +495,7 @@ __global__ void k_halo_guard(const double* __restrict__ E, long stride, int ws, 
 
 namespace cbf {
 void launch_extents_finalize(int nparts, const double* part, double* out, hipStream_t s) {
-    hipLaunchKernelGGL(k_extents_finalize, dim3(1), dim3(kBlock), 0, s, nparts, part, out);
+    hipLaunchKernelGGL(k_extents_finalize, dim3(1), dim3(kFinBlock), 0, s, nparts, part, out);
 }
 }  // namespace cbf
 
@@ -496,9 +549,10 @@ extern "C" size_t cbf_lattice_workspace_size(int32_t W, int32_t win_rows, const 
 }
 
 
-extern "C" int cbf_lattice_build(const cbf_params* p, const cbf_grid* grid, int32_t W, int32_t H, int32_t row_begin,
-                                 int32_t row_end, int32_t win_row0, int32_t win_rows, const double* pos, double gain,
-                                 double* vel_out, void* workspace, size_t workspace_bytes, void* stream) {
+static int lattice_build(const cbf_params* p, const cbf_grid* grid, int32_t W, int32_t H, int32_t row_begin,
+                         int32_t row_end, int32_t win_row0, int32_t win_rows, const double* pos, double gain,
+                         double* vel_out, void* workspace, size_t workspace_bytes, unsigned long long* ext_keys,
+                         int32_t guard_rows, void* stream) {
     int rc = check_lattice(p, grid, W, H, row_begin, row_end, win_row0, win_rows, pos, workspace, workspace_bytes);
     if (rc) return rc;
     if (!vel_out) return CBF_EINVAL;
@@ -513,11 +567,18 @@ extern "C" int cbf_lattice_build(const cbf_params* p, const cbf_grid* grid, int3
     int4* bcs = reinterpret_cast<int4*>(Wk.cs);
     hipLaunchKernelGGL(k_lattice_nominal_bin_ordered, dim3(nblk(n)), dim3(kBlock), 0, s, G, W, H, row_begin, row_end,
                        win_row0, win_rows, p2, gain, wv, reinterpret_cast<double2*>(vel_out), Wk.count, Wk.sidx,
-                       Wk.start, Wk.ncell, bcs, Wk.hardq);
+                       Wk.start, Wk.ncell, bcs, Wk.hardq, ext_keys, guard_rows);
     launch_scan(Wk, s);
     hipLaunchKernelGGL(k_lattice_scatter_ordered, dim3(nblk(n)), dim3(kBlock), 0, s, n, bcs, Wk.start, p2, wv, Wk.spos,
                        Wk.svel, Wk.sidx, Wk.spos32, Wk.hardq + 2, n, Wk.ncell, win_row0, H);
     return (int)hipGetLastError();
+}
+
+extern "C" int cbf_lattice_build(const cbf_params* p, const cbf_grid* grid, int32_t W, int32_t H, int32_t row_begin,
+                                 int32_t row_end, int32_t win_row0, int32_t win_rows, const double* pos, double gain,
+                                 double* vel_out, void* workspace, size_t workspace_bytes, void* stream) {
+    return lattice_build(p, grid, W, H, row_begin, row_end, win_row0, win_rows, pos, gain, vel_out, workspace,
+                         workspace_bytes, nullptr, 0, stream);
 }
 
 extern "C" int cbf_lattice_advance(const cbf_params* p, const cbf_grid* grid, int32_t W, int32_t H,
@@ -543,8 +604,8 @@ extern "C" int cbf_lattice_advance(const cbf_params* p, const cbf_grid* grid, in
                        status, nbr_count, guard_rows, ext_part, reinterpret_cast<unsigned long long*>(solves),
                        Wk.hardq, Wk.spos32);
     hipLaunchKernelGGL(k_lattice_filter_hard, dim3(hb), dim3(64), 0, s, kp, row_begin, row_end, T, po, uo, status,
-                       nbr_count, guard_rows, ext_part ? ext_part + 4l * nb : nullptr, Wk.hardq);
-    if (extents) launch_extents_finalize(nb + hb, ext_part, extents, s);
+                       nbr_count, guard_rows, ext_part ? ext_part + 4l * lattice_ext_waves(n) : nullptr, Wk.hardq);
+    if (extents) launch_extents_finalize((int)lattice_ext_waves(n) + hb, ext_part, extents, s);
     return (int)hipGetLastError();
 }
 
@@ -558,4 +619,139 @@ extern "C" int cbf_lattice_step(const cbf_params* p, const cbf_grid* grid, int32
     if (rc) return rc;
     return cbf_lattice_advance(p, grid, W, H, row_begin, row_end, win_row0, win_rows, pos, T, pos_out, u, status,
                                nbr_count, guard_rows, extents, solves, workspace, workspace_bytes, stream);
+}
+
+extern "C" int cbf_lattice_step_sharded(const cbf_params* p, const cbf_grid* grid, int32_t W, int32_t H,
+                                        int32_t row_begin, int32_t row_end, int32_t win_row0, int32_t win_rows,
+                                        const double* pos, double gain, double T, double* pos_out, double* vel_out,
+                                        double* u, int32_t* status, int32_t* nbr_count, int32_t guard_rows,
+                                        uint64_t* ext_keys, uint64_t* solves, void* workspace, size_t workspace_bytes,
+                                        void* stream) {
+    if (!ext_keys || guard_rows < 0) return CBF_EINVAL;
+    int rc = lattice_build(p, grid, W, H, row_begin, row_end, win_row0, win_rows, pos, gain, vel_out, workspace,
+                           workspace_bytes, reinterpret_cast<unsigned long long*>(ext_keys), guard_rows, stream);
+    if (rc) return rc;
+    return cbf_lattice_advance(p, grid, W, H, row_begin, row_end, win_row0, win_rows, pos, T, pos_out, u, status,
+                               nbr_count, guard_rows, nullptr, solves, workspace, workspace_bytes, stream);
+}
+
+// ---- halo exchange of the row-sharded step -----------------------------------------
+namespace {
+
+__device__ __forceinline__ double dkey_inv(unsigned long long k) {
+    const unsigned long long u = (k >> 63) ? (k & 0x7FFFFFFFFFFFFFFFull) : ~k;
+    return __longlong_as_double((long long)u);
+}
+
+// send = [first halo rows | last halo rows | 4 extents]; block 0's first wave reduces the 64
+// extent-key slots into the 4 extents and resets them for the next accumulation.
+__global__ void __launch_bounds__(kBlock) k_halo_pack(int W, int halo, long n_own, const double2* __restrict__ own,
+                                                      unsigned long long* __restrict__ keys, double* __restrict__ send) {
+    const long t = (long)blockIdx.x * kBlock + threadIdx.x;
+    const long rs = (long)halo * W;
+    double2* s2 = reinterpret_cast<double2*>(send);
+    if (t < rs) s2[t] = own[t];
+    else if (t < 2 * rs) s2[t] = own[n_own - 2 * rs + t];
+    if (blockIdx.x == 0 && threadIdx.x < 64) {
+        const int l = threadIdx.x;
+        unsigned long long* kl = keys + kExtSlotWords * l;
+        unsigned long long k0 = kl[0], k1 = kl[1], k2 = kl[2], k3 = kl[3];
+        for (int o = 32; o > 0; o >>= 1) {
+            const unsigned long long a = __shfl_xor(k0, o, 64), b = __shfl_xor(k1, o, 64);
+            const unsigned long long c = __shfl_xor(k2, o, 64), d = __shfl_xor(k3, o, 64);
+            k0 = a < k0 ? a : k0;
+            k1 = b > k1 ? b : k1;
+            k2 = c > k2 ? c : k2;
+            k3 = d < k3 ? d : k3;
+        }
+        kl[0] = dkey(INFINITY);
+        kl[1] = dkey(-INFINITY);
+        kl[2] = dkey(-INFINITY);
+        kl[3] = dkey(INFINITY);
+        if (l == 0) {
+            double* e = send + 4 * rs;
+            e[0] = dkey_inv(k0);
+            e[1] = dkey_inv(k1);
+            e[2] = dkey_inv(k2);
+            e[3] = dkey_inv(k3);
+        }
+    }
+}
+
+__global__ void k_ext_reset(unsigned long long* __restrict__ keys) {
+    unsigned long long* kl = keys + kExtSlotWords * threadIdx.x;
+    kl[0] = dkey(INFINITY);
+    kl[1] = dkey(-INFINITY);
+    kl[2] = dkey(-INFINITY);
+    kl[3] = dkey(INFINITY);
+}
+
+__device__ __forceinline__ bool halo_guard_ok(const double* E, long stride, int ws, int rank, double radius) {
+    const double rm = radius * (1.0 + 1e-9) + 1e-12;
+    const double* me = E + (long)rank * stride;
+    const double ymin = me[0], ymax = me[1];
+    bool ok = true;
+    for (int q = 0; q < ws; ++q) {
+        const double* o = E + (long)q * stride;
+        if (q < rank) {  // rows below: rank-1's rows outside our halo, everything of lower ranks
+            const double lim = (q == rank - 1) ? o[2] : o[1];
+            if (!(ymin - lim > rm)) ok = false;
+        } else if (q > rank) {
+            const double lim = (q == rank + 1) ? o[3] : o[0];
+            if (!(lim - ymax > rm)) ok = false;
+        }
+    }
+    return ok;
+}
+
+// Window halo rows from the gathered slabs (rank-1's last rows below, rank+1's first rows above);
+// block 0 lane 0 runs the guard on the gathered extents.
+__global__ void __launch_bounds__(kBlock) k_halo_unpack(int W, int halo, int rows_lo, int rows_hi, long hi_off,
+                                                        const double* __restrict__ recv, long stride, int ws, int rank,
+                                                        double radius, double2* __restrict__ wpos,
+                                                        int32_t* __restrict__ flag) {
+    const long t = (long)blockIdx.x * kBlock + threadIdx.x;
+    const long nlo = (long)rows_lo * W, nhi = (long)rows_hi * W, rs = (long)halo * W;
+    if (t < nlo) {
+        const double2* src = reinterpret_cast<const double2*>(recv + (long)(rank - 1) * stride) + rs + (rs - nlo);
+        wpos[t] = src[t];
+    } else if (t < nlo + nhi) {
+        const double2* src = reinterpret_cast<const double2*>(recv + (long)(rank + 1) * stride);
+        wpos[hi_off + (t - nlo)] = src[t - nlo];
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0 && !halo_guard_ok(recv + 4 * rs, stride, ws, rank, radius)) flag[0] |= 1;
+}
+
+}  // namespace
+
+extern "C" size_t cbf_halo_ext_bytes(void) { return 64 * kExtSlotWords * sizeof(unsigned long long); }
+
+extern "C" int cbf_halo_ext_reset(uint64_t* ext_keys, void* stream) {
+    if (!ext_keys) return CBF_EINVAL;
+    hipLaunchKernelGGL(k_ext_reset, dim3(1), dim3(64), 0, (hipStream_t)stream,
+                       reinterpret_cast<unsigned long long*>(ext_keys));
+    return (int)hipGetLastError();
+}
+
+extern "C" int cbf_halo_pack(int32_t W, int32_t halo, int64_t n_own, const double* own, uint64_t* ext_keys,
+                             double* send, void* stream) {
+    if (W <= 0 || halo <= 0 || n_own < 2l * halo * W || !own || !ext_keys || !send) return CBF_EINVAL;
+    const long n = 2l * halo * W;
+    hipLaunchKernelGGL(k_halo_pack, dim3(nblk(n)), dim3(kBlock), 0, (hipStream_t)stream, W, halo, (long)n_own,
+                       reinterpret_cast<const double2*>(own), reinterpret_cast<unsigned long long*>(ext_keys), send);
+    return (int)hipGetLastError();
+}
+
+extern "C" int cbf_halo_unpack(int32_t W, int32_t halo, int32_t rows_lo, int32_t rows_hi, int64_t hi_row_offset,
+                               const double* recv, int64_t stride, int32_t world_size, int32_t rank, double radius,
+                               double* wpos, int32_t* flag, void* stream) {
+    if (W <= 0 || halo <= 0 || rows_lo < 0 || rows_hi < 0 || rows_lo > halo || rows_hi > halo || !recv || !wpos ||
+        !flag || world_size < 1 || rank < 0 || rank >= world_size || stride < 4l * halo * W + 4 ||
+        (rows_lo > 0 && rank == 0) || (rows_hi > 0 && rank == world_size - 1) || hi_row_offset < 0)
+        return CBF_EINVAL;
+    const long n = (long)(rows_lo + rows_hi) * W;
+    hipLaunchKernelGGL(k_halo_unpack, dim3(nblk(n > 0 ? n : 1)), dim3(kBlock), 0, (hipStream_t)stream, W, halo,
+                       rows_lo, rows_hi, (long)hi_row_offset * W, recv, (long)stride, world_size, rank, radius,
+                       reinterpret_cast<double2*>(wpos), flag);
+    return (int)hipGetLastError();
 }

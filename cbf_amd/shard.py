@@ -1,18 +1,22 @@
 """Row-stripe sharding of the lattice swarm across GPUs (SURVEY 8e, cfg4 at 1/2/4/8 GPUs).
 
 Rank r owns lattice rows [r R, (r+1) R) of a W x (R * world) lattice (weak scaling: R rows per
-GPU).  Each timestep:
-  1. pack   the rank's first and last `halo` owned rows (+ the 4 extents of its owned
-            positions written by the previous step's kernel) into one send slab;
-  2. ONE    all_gather_into_tensor of the slabs (RCCL over xGMI) -- 2 * halo * W * 16 B per rank;
-  3. unpack rank r-1's last rows and rank r+1's first rows into the halo rows of the window;
-  4. guard  (device, one lane) that every agent outside the candidate rows is out of cull range;
-  5. step   cbf_lattice_step on the window: nominal control, cell list, filter, clip, Euler for
-            the owned rows, writing the owned rows in place and the new extents into the slab.
+GPU).  Each timestep is four device operations around ONE collective:
+  1. pack    (cbf_halo_pack)   the rank's first and last `halo` owned rows + 4 y-extents of the
+             owned positions that the previous step's build accumulated, into one send slab;
+  2. gather  ONE all_gather_into_tensor of the slabs (RCCL over xGMI) -- 2 * halo * W * 16 B per rank;
+  3. unpack  (cbf_halo_unpack) rank r-1's last rows and rank r+1's first rows into the halo rows of
+             the window, and the halo guard on the gathered extents;
+  4. step    (cbf_lattice_step_sharded) nominal control, cell list, filter, clip, Euler for the
+             owned rows, writing them in place; its build accumulates the extents of its inputs.
 The halo holds `halo` rows per side; the outermost halo row only feeds the consensus of the
-next row, so candidates reach halo-1 rows beyond the stripe (guard_rows = halo - 1).
-Results are bit-identical to the single-GPU step of the whole lattice whenever the guard holds
-(checked by tests and by check_guard()).
+next row, so candidates reach halo-1 rows beyond the stripe (guard_rows = halo - 1).  The guard
+proves that every agent outside a rank's candidate rows is farther than the cull radius (in y)
+from every agent it owns; it runs on the extents of step t's inputs at step t+1's exchange, and
+check_guard() does one last exchange for the final step.  Results are bit-identical to the
+single-GPU step of the whole lattice whenever the guard holds (checked by tests and by
+check_guard()).  With capture(), steps 1 and 3-4 replay as two hipGraphs around the eager
+collective.
 
 The backend object does the device work (HipBackend here; the CPU gloo tests plug in the
 oracle as a backend to check the exchange logic).
@@ -68,16 +72,30 @@ class HipBackend:
         self.ws_bytes = _lib.lib.cbf_lattice_workspace_size(W, win_rows, _lib.C.byref(grid))
         self.ws = torch.zeros((self.ws_bytes,), dtype=torch.uint8, device=self.dev)
         self.flag = torch.zeros((1,), dtype=torch.int32, device=self.dev)
+        self.ext_keys = torch.empty((_lib.lib.cbf_halo_ext_bytes() // 8,), dtype=torch.int64, device=self.dev)
+        _lib.check(_lib.lib.cbf_halo_ext_reset(_lib.ptr(self.ext_keys), _lib.stream_handle()), "cbf_halo_ext_reset")
 
     def tensor(self, a):
         return self.torch.as_tensor(np.ascontiguousarray(a), device=self.dev)
 
-    def lattice_step(self, S, ext_out):
+    def pack(self, S):
         L, P = self._lib, self._lib.ptr
-        L.check(L.lib.cbf_lattice_step(self.cp, L.C.byref(self.grid), self.W, self.H, S.rb, S.re, S.w0, S.win_rows,
-                                       P(S.wpos), self.gain, self.T, P(S.own), P(S.vel), P(S.u), P(S.status),
-                                       P(S.nbr_count), S.halo - 1, P(ext_out), P(S.solves), P(self.ws),
-                                       self.ws_bytes, L.stream_handle()), "cbf_lattice_step")
+        L.check(L.lib.cbf_halo_pack(self.W, S.halo, S.n_owned, P(S.own), P(self.ext_keys), P(S.send),
+                                    L.stream_handle()), "cbf_halo_pack")
+
+    def unpack_guard(self, S):
+        L, P = self._lib, self._lib.ptr
+        L.check(L.lib.cbf_halo_unpack(self.W, S.halo, S.rb - S.w0, S.w1 - S.re, S.re - S.w0, P(S.recv), S.stride,
+                                      S.ws, S.rank, self.radius, P(S.wpos), P(self.flag), L.stream_handle()),
+                "cbf_halo_unpack")
+
+    def lattice_step(self, S):
+        L, P = self._lib, self._lib.ptr
+        L.check(L.lib.cbf_lattice_step_sharded(self.cp, L.C.byref(self.grid), self.W, self.H, S.rb, S.re, S.w0,
+                                               S.win_rows, P(S.wpos), self.gain, self.T, P(S.own), P(S.vel), P(S.u),
+                                               P(S.status), P(S.nbr_count), S.halo - 1, P(self.ext_keys),
+                                               P(S.solves), P(self.ws), self.ws_bytes, L.stream_handle()),
+                "cbf_lattice_step_sharded")
 
     def lattice_build(self, S):
         L, P = self._lib, self._lib.ptr
@@ -85,17 +103,12 @@ class HipBackend:
                                         P(S.wpos), self.gain, P(S.vel), P(self.ws), self.ws_bytes,
                                         L.stream_handle()), "cbf_lattice_build")
 
-    def lattice_advance(self, S, ext_out):
+    def lattice_advance(self, S):
         L, P = self._lib, self._lib.ptr
         L.check(L.lib.cbf_lattice_advance(self.cp, L.C.byref(self.grid), self.W, self.H, S.rb, S.re, S.w0,
                                           S.win_rows, P(S.wpos), self.T, P(S.own), P(S.u), P(S.status),
-                                          P(S.nbr_count), S.halo - 1, P(ext_out), P(S.solves), P(self.ws),
+                                          P(S.nbr_count), S.halo - 1, None, P(S.solves), P(self.ws),
                                           self.ws_bytes, L.stream_handle()), "cbf_lattice_advance")
-
-    def guard(self, recv_ext, stride, ws, rank):
-        L = self._lib
-        L.check(L.lib.cbf_halo_guard(L.ptr(recv_ext), stride, ws, rank, self.radius, L.ptr(self.flag),
-                                     L.stream_handle()), "cbf_halo_guard")
 
     def guard_failed(self) -> bool:
         return bool(self.flag.item())
@@ -143,22 +156,13 @@ class ShardedLattice:
         # send slab: [first halo rows | last halo rows | 4 extents (+4 pad)] doubles
         self.slab = 2 * halo * W * 2
         self.stride = self.slab + 8
-        send = np.zeros(self.stride)
-        own_np = pos_global[self.rb * W:self.re * W]
-        send[self.slab:self.slab + 4] = stripe_extents(own_np, W, halo - 1)
-        self.send = t(send)
+        self.send = t(np.zeros(self.stride))
         self.recv = t(np.zeros(self.stride * self.ws))
-        self.send_ext = self.send[self.slab:self.slab + 4]
         self.use_list_gather = dist.get_backend(group) == "gloo"
         self.graph = None
 
     # ---- one timestep -------------------------------------------------------------------------
-    def exchange(self):
-        W, h = self.W, self.halo
-        rs = h * W * 2
-        own = self.own.view(-1)
-        self.send[:rs].copy_(own[:rs])
-        self.send[rs:2 * rs].copy_(own[own.numel() - rs:])
+    def _gather(self):
         if self.use_list_gather:   # gloo (CPU tests, or a 1-GPU rehearsal of several ranks via host staging)
             if self.send.is_cuda:
                 rc = self.recv.cpu()
@@ -170,29 +174,46 @@ class ShardedLattice:
                                      group=self.group)
         else:                      # RCCL: one all-gather into the contiguous receive slab
             self.dist.all_gather_into_tensor(self.recv, self.send, group=self.group)
-        wv = self.wpos.view(-1)
-        if self.rank > 0:
-            lo = (self.rank - 1) * self.stride
-            wv[:(self.rb - self.w0) * W * 2].copy_(self.recv[lo + rs:lo + 2 * rs])
-        if self.rank < self.ws - 1:
-            hi = (self.rank + 1) * self.stride
-            a = (self.re - self.w0) * W * 2
-            wv[a:a + (self.w1 - self.re) * W * 2].copy_(self.recv[hi:hi + (self.w1 - self.re) * W * 2])
-        self.be.guard(self.recv[self.slab:], self.stride, self.ws, self.rank)
+
+    def exchange(self):
+        self.be.pack(self)
+        self._gather()
+        self.be.unpack_guard(self)
+
+    def _post(self):
+        self.be.unpack_guard(self)
+        self.be.lattice_step(self)
 
     def step(self):
+        if self.graph is not None:   # two captured graphs around the (eager) collective
+            self.graph[0].replay()
+            self._gather()
+            self.graph[1].replay()
+            return
         self.exchange()
-        self.be.lattice_step(self, self.send_ext)
+        self.be.lattice_step(self)
 
     def build_phase(self):
         self.be.lattice_build(self)
 
     def advance_phase(self):
-        self.be.lattice_advance(self, self.send_ext)
+        self.be.lattice_advance(self)
 
     def capture(self):
-        """Collectives stay eager (no RCCL inside captured graphs); nothing to capture."""
-        return None
+        """Capture the device work of a step into two hipGraphs -- the halo pack, and unpack +
+        guard + the fused lattice step -- so one step is two graph launches around the eager
+        collective (RCCL stays outside the graphs)."""
+        torch = self.torch
+        if not self.own.is_cuda:
+            return None
+        torch.cuda.synchronize()
+        g0, g1 = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g0):
+            self.be.pack(self)
+        with torch.cuda.graph(g1):
+            self._post()
+        self.graph = (g0, g1)
+        return self.graph
 
     def reset_solves(self):
         self.solves.zero_()
@@ -201,6 +222,8 @@ class ShardedLattice:
         return int(self.solves.view(64, 16)[:, 0].sum().item())
 
     def check_guard(self):
+        """Certify the last step (one more exchange of extents) and raise if any step's guard failed."""
+        self.exchange()
         if self.be.guard_failed():
             raise RuntimeError(f"rank {self.rank}: halo guard failed -- an agent moved within the cull radius of "
                                f"a stripe from outside the {self.halo}-row halo; raise halo")

@@ -248,6 +248,34 @@ int cbf_halo_guard(const double* ext_all, int64_t stride, int32_t world_size, in
                    int32_t* flag, void* stream);
 
 /*
+ * Row-sharded step, fused form (what cbf_amd/shard.py runs).  One timestep is
+ *   cbf_halo_pack -> all-gather of the send slabs (RCCL) -> cbf_halo_unpack -> cbf_lattice_step_sharded.
+ * cbf_lattice_step_sharded = cbf_lattice_step whose BUILD phase also accumulates the y-extents of
+ * the owned INPUT positions (the 4 values of `extents` above, guard_rows as given) into
+ * ext_keys (device, cbf_halo_ext_bytes(): 64 slots x 4 monotone uint64 keys; set to identity
+ * once with cbf_halo_ext_reset); the advance phase computes no extents.
+ * cbf_halo_pack writes send = [first halo owned rows | last halo owned rows | 4 extents reduced
+ * from ext_keys] (own = the n_own owned positions) and resets ext_keys.  cbf_halo_unpack copies
+ * rank-1's last rows_lo rows into window rows [0, rows_lo) and rank+1's first rows_hi rows into
+ * window rows [hi_row_offset, +rows_hi) from the gathered recv (world_size slabs of `stride`
+ * doubles), and runs the halo guard on the gathered extents -- the extents of the PREVIOUS
+ * step's inputs, so a step is certified one exchange later (a final pack + gather + unpack
+ * certifies the last one).
+ */
+size_t cbf_halo_ext_bytes(void);
+int cbf_halo_ext_reset(uint64_t* ext_keys, void* stream);
+int cbf_halo_pack(int32_t W, int32_t halo, int64_t n_own, const double* own, uint64_t* ext_keys, double* send,
+                  void* stream);
+int cbf_halo_unpack(int32_t W, int32_t halo, int32_t rows_lo, int32_t rows_hi, int64_t hi_row_offset,
+                    const double* recv, int64_t stride, int32_t world_size, int32_t rank, double radius, double* wpos,
+                    int32_t* flag, void* stream);
+int cbf_lattice_step_sharded(const cbf_params* p, const cbf_grid* grid, int32_t W, int32_t H, int32_t row_begin,
+                             int32_t row_end, int32_t win_row0, int32_t win_rows, const double* pos, double gain,
+                             double T, double* pos_out, double* vel_out, double* u, int32_t* status,
+                             int32_t* nbr_count, int32_t guard_rows, uint64_t* ext_keys, uint64_t* solves,
+                             void* workspace, size_t workspace_bytes, void* stream);
+
+/*
  * Batched Monte-Carlo rendezvous (SURVEY cfg5): n_scen independent scenarios, each with
  * n_o pursuit obstacles (ring i -> i+1, rotation (rc, rs), scale so) then n_a free agents
  * (complete-graph consensus, gain ga; only they are filtered), `steps` Euler steps of T.

@@ -17,16 +17,45 @@ from oracle import coracle, pyoracle as po
 
 
 class OracleBackend:
+    """Device work restated on the CPU (oracle): the same pack / unpack+guard / step contract as
+    HipBackend, including the guard running one exchange after the step it certifies."""
+
     def __init__(self, W, H, gain, T, radius):
         self.W, self.H, self.gain, self.T, self.radius = W, H, gain, T, radius
         self.p = po.Params(15)
         self.flag = 0
+        self.pending = np.array([np.inf, -np.inf, -np.inf, np.inf])   # extents of the last step's inputs
 
     def tensor(self, a):
         return torch.as_tensor(np.ascontiguousarray(a)).clone()
 
-    def lattice_step(self, S, ext_out):
+    def pack(self, S):
+        rs = S.halo * S.W * 2
+        own = S.own.reshape(-1)
+        S.send[:rs].copy_(own[:rs])
+        S.send[rs:2 * rs].copy_(own[own.numel() - rs:])
+        S.send[S.slab:S.slab + 4].copy_(torch.as_tensor(self.pending))
+        self.pending = np.array([np.inf, -np.inf, -np.inf, np.inf])
+
+    def unpack_guard(self, S):
+        W, rs = S.W, S.halo * S.W * 2
+        wv = S.wpos.view(-1)
+        if S.rank > 0:
+            lo = (S.rank - 1) * S.stride
+            n = (S.rb - S.w0) * W * 2
+            wv[:n].copy_(S.recv[lo + 2 * rs - n:lo + 2 * rs])
+        if S.rank < S.ws - 1:
+            hi = (S.rank + 1) * S.stride
+            a = (S.re - S.w0) * W * 2
+            n = (S.w1 - S.re) * W * 2
+            wv[a:a + n].copy_(S.recv[hi:hi + n])
+        ext = np.stack([S.recv[q * S.stride + S.slab:q * S.stride + S.slab + 4].numpy() for q in range(S.ws)])
+        if not guard_ok(ext, S.rank, self.radius):
+            self.flag = 1
+
+    def lattice_step(self, S):
         W, H = self.W, self.H
+        self.pending = stripe_extents(S.own.numpy(), W, S.halo - 1)       # extents of this step's inputs
         full = np.zeros((W * H, 2))
         full[S.w0 * W:S.w1 * W] = S.wpos.numpy()
         lo = S.w0 if S.w0 == 0 else S.w0 + 1
@@ -39,13 +68,7 @@ class OracleBackend:
         S.own.copy_(torch.as_tensor(new))
         S.vel.copy_(torch.as_tensor(vel[eb:ee])); S.u.copy_(torch.as_tensor(out["u"]))
         S.status.copy_(torch.as_tensor(out["status"])); S.nbr_count.copy_(torch.as_tensor(out["cnt"]))
-        ext_out.copy_(torch.as_tensor(stripe_extents(new, W, S.halo - 1)))
         S.solves[0] += int((out["cnt"] > 0).sum())
-
-    def guard(self, recv_ext, stride, ws, rank):
-        ext = np.stack([recv_ext[q * stride:q * stride + 4].numpy() for q in range(ws)])
-        if not guard_ok(ext, rank, self.radius):
-            self.flag = 1
 
     def guard_failed(self):
         return bool(self.flag)
@@ -117,3 +140,35 @@ def test_guard_logic():
     bad[2, 0] = ext[0, 1] + 0.05           # rank 2 reaches down to rank 0
     assert not guard_ok(bad, 0, 0.2)
     assert a * (halo - 2) > 0.2            # default halo leaves slack for the jittered lattice
+
+
+def _worker_small_halo(rank, ws, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=ws)
+    W, R = 12, 6
+    be = OracleBackend(W, R * ws, scenarios.LATTICE_GAIN, scenarios.T, 0.2)
+    S = ShardedLattice(W, R, seed=3, halo=2, backend=be)
+    S.step()
+    try:
+        S.check_guard()
+        q.put((rank, "ok"))
+    except RuntimeError:
+        q.put((rank, "raised"))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_too_small_halo_is_caught_after_the_step():
+    """halo 2 lets rows two apart (0.29 - jitter < 0.2) reach past the candidate rows: the
+    guard, run at the exchange after the step, must flag it and check_guard() must raise."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_small_halo, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=300) for _ in range(2)])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert any(r[1] == "raised" for r in res)

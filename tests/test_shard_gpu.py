@@ -24,12 +24,14 @@ def _free_port():
     return p
 
 
-def _worker(rank, ws, port, W, R, steps, q):
+def _worker(rank, ws, port, W, R, steps, q, graph=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     torch.cuda.set_device(0)
     dist.init_process_group("gloo", rank=rank, world_size=ws)
     from cbf_amd.shard import ShardedLattice
     S = ShardedLattice(W, R, seed=7)
+    if graph:
+        S.capture()
     S.reset_solves()
     for _ in range(steps):
         S.step()
@@ -40,14 +42,14 @@ def _worker(rank, ws, port, W, R, steps, q):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("ws", [2, 3])
-def test_sharded_equals_single_gpu(ws):
+@pytest.mark.parametrize("ws,graph", [(2, False), (3, False), (2, True)])
+def test_sharded_equals_single_gpu(ws, graph):
     from cbf_amd import scenarios, swarm
     W, R, steps = 96, 40, 6
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, ws, port, W, R, steps, q)) for r in range(ws)]
+    procs = [ctx.Process(target=_worker, args=(r, ws, port, W, R, steps, q, graph)) for r in range(ws)]
     for p in procs:
         p.start()
     res = sorted([q.get(timeout=300) for _ in range(ws)], key=lambda t: t[0])

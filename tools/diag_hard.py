@@ -13,7 +13,7 @@ L = swarm.LatticeSwarm(scenarios.lattice(W, H, seed=0), W, H, gain=scenarios.LAT
 n = W * H
 nc = L.grid.nx * L.grid.ny
 ntiles = (nc + 2047) // 2048
-off = a256(4 * nc) + a256(4 * (nc + 1)) + a256(8 * ntiles) + 256 + a256(16 * n) + 2 * a256(16 * n) + a256(4 * n) + a256(16 * n)
+off = a256(4 * nc) + a256(4 * (nc + 1)) + a256(8 * ntiles) + 256 + a256(16 * n) + 2 * a256(16 * n) + a256(4 * n) + a256(16 * n) + a256(8 * n)
 for step in range(240):
     L.step()
     if step % 20 == 0 or step == 239:
