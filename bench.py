@@ -84,12 +84,12 @@ def bench_lattice(args, ws, rank, local):
     rows = args.rows
     if ws > 1 or args.shard:
         from cbf_amd.shard import ShardedLattice
-        S = ShardedLattice(W, rows, seed=args.seed)
+        S = ShardedLattice(W, rows, seed=args.seed, substeps=args.substeps)
     else:
         pos = scenarios.lattice(W, rows, seed=args.seed)
         S = swarm.LatticeSwarm(pos, W, rows, gain=scenarios.LATTICE_GAIN, barrier=args.barrier)
-    # the sharded step stays eager: two graph replays around the collective measured slower
-    # (121 vs 106 us per step at one rank) than eager launches
+    # the sharded path stays eager: per-sub-step graph replays measured slower than eager
+    # launches (110 vs 104 us per step at one rank, 4 sub-steps per exchange)
     use_graph = not args.eager and not (ws > 1 or args.shard)
     if use_graph:
         S.capture()
@@ -156,8 +156,9 @@ def bench_lattice(args, ws, rank, local):
                                "consensus + radius-0.2 cell-list cull + CBF QP + clip + Euler, one fused timestep "
                                "per step", "barrier": args.barrier,
                    "agents_total": n_total, "agents_per_gpu": n_local,
-                   "parallelism": f"row-stripe shards x{ws}, 1 RCCL all-gather of halo slabs / step"
-                   if (ws > 1 or args.shard) else "single GPU", "graph": use_graph},
+                   "parallelism": f"row-stripe shards x{ws}, 1 RCCL all-gather of ghost-row slabs per "
+                                  f"{args.substeps} steps" if (ws > 1 or args.shard) else "single GPU",
+                   "graph": use_graph},
         "timesteps_per_s": args.steps / elapsed,
         "solves_per_step": solves / args.steps,
         "status_fraction_last_step": {"idle": codes[0] / len(status), "optimal": codes[1] / len(status),
@@ -371,6 +372,8 @@ def main():
     ap.add_argument("--barrier", default="reference", choices=["reference", "euclidean_hocbf"],
                     help="cfg4 single-GPU: the reference's L1 barrier rows or the Euclidean HOCBF mode")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
+    ap.add_argument("--substeps", type=int, default=4,
+                    help="sharded cfg4: timesteps per halo exchange (ghost rows = 4 x substeps)")
     ap.add_argument("--shard", action="store_true",
                     help="cfg4: run the sharded step (halo pack + collective + unpack) even on one rank")
     args = ap.parse_args()

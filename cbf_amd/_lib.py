@@ -86,13 +86,13 @@ SIGNATURES = {
                                             _vp, _i32, _vp, _vp, _vp, _sz, _vp]),
     "cbf_mc_rollout": (C.c_int, [_P, _i32, _i32, _i32, _i32, _d, _d, _d, _d, _d, _vp, _vp, _vp, _vp]),
     "cbf_halo_guard": (C.c_int, [_vp, C.c_int64, _i32, _i32, _d, _vp, _vp]),
-    "cbf_halo_ext_bytes": (_sz, []),
-    "cbf_halo_ext_reset": (C.c_int, [_vp, _vp]),
-    "cbf_halo_pack": (C.c_int, [_i32, _i32, C.c_int64, _vp, _vp, _vp, _vp]),
-    "cbf_halo_unpack": (C.c_int, [_i32, _i32, _i32, _i32, C.c_int64, _vp, C.c_int64, _i32, _i32, _d, _vp, _vp,
+    "cbf_halo_ext_bytes": (_sz, [_i32]),
+    "cbf_halo_ext_reset": (C.c_int, [_vp, _i32, _vp]),
+    "cbf_halo_pack": (C.c_int, [_i32, _i32, C.c_int64, _vp, _vp, _i32, _vp, _vp]),
+    "cbf_halo_unpack": (C.c_int, [_i32, _i32, _i32, _i32, C.c_int64, _vp, C.c_int64, _i32, _i32, _d, _i32, _vp, _vp,
                                   _vp]),
-    "cbf_lattice_step_sharded": (C.c_int, [_P, _G, _i32, _i32, _i32, _i32, _i32, _i32, _vp, _d, _d, _vp, _vp, _vp,
-                                           _vp, _vp, _i32, _vp, _vp, _vp, _sz, _vp]),
+    "cbf_lattice_step_sharded": (C.c_int, [_P, _G, _i32, _i32, _i32, _i32, _i32, _i32, _i32, _i32, _vp, _d, _d, _vp,
+                                           _vp, _vp, _vp, _vp, _i32, _vp, _vp, _vp, _sz, _vp]),
     "cbf_cert_params_init": (C.c_int, [_CP, _d, _d, _d, _vp]),
     "cbf_si_barrier_cert_lds_bytes": (_sz, [_i32]),
     "cbf_si_barrier_cert": (C.c_int, [_CP, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),

@@ -12,7 +12,20 @@ namespace {
 
 inline int nblk(long n) { return (int)((n + kBlock - 1) / kBlock); }
 
-constexpr int kExtSlotWords = 16;  // one 128-B line per extents slot (4 keys used)
+constexpr int kExtSlotWords = 16;  // one 128-B line per extents slot (6 keys used)
+#ifndef CBF_EXT_SLOTS
+#define CBF_EXT_SLOTS 64
+#endif
+#ifndef CBF_EXT_WAVE
+#define CBF_EXT_WAVE 0
+#endif
+constexpr int kExtSlots = CBF_EXT_SLOTS;  // slots per sub-step set (tools/ablate.py times the choices)
+constexpr int kExtVals = 6;        // {ego min, ego max, owned max below guard, owned min above guard, owned min, max}
+__host__ __device__ constexpr bool ext_is_min(int q) { return q == 0 || q == 3 || q == 4; }
+
+struct ExtSpec {
+    int own_begin, own_end, guard;
+};
 
 __global__ void __launch_bounds__(kBlock) k_consensus_csr(int n_dst, int self_offset, int n_group,
                                                           const double2* __restrict__ src,
@@ -93,7 +106,7 @@ __global__ void __launch_bounds__(kBlock) k_lattice_nominal_bin_ordered(
     CellGrid G, int W, int H, int row_begin, int row_end, int win_row0, int win_rows, const double2* __restrict__ pos,
     double gain, double2* __restrict__ wvel, double2* __restrict__ vel_out, int32_t* __restrict__ count,
     const int32_t* __restrict__ order, const int32_t* __restrict__ start, long ncell, int4* __restrict__ bcs,
-    int32_t* __restrict__ hardq, unsigned long long* __restrict__ ext_keys, int guard_rows) {
+    int32_t* __restrict__ hardq, unsigned long long* __restrict__ ext_keys, ExtSpec X) {
     const long t = (long)xcd_block() * kBlock + threadIdx.x;
     const long nwin = (long)win_rows * W;
     // hardq[2..4]: the previous build left a cell order for this window size and grid (else
@@ -118,43 +131,77 @@ __global__ void __launch_bounds__(kBlock) k_lattice_nominal_bin_ordered(
     }
     const int lane = threadIdx.x & 63;
     if (ext_keys) {
-        // y-extents of the owned INPUT positions (halo guard of the sharded step, checked one
-        // exchange later): reduced per block, then one atomic per value into one of 64 slots on
-        // separate 128-B lines (cross-XCD atomics on a shared line serialise at the memory side)
-        __shared__ double red[4][kBlock / 64];
-        double e0 = INFINITY, e1 = -INFINITY, e2 = -INFINITY, e3 = INFINITY;
+        // y-extents of the INPUT positions for the halo guard of the sharded step (checked at the
+        // next exchange): {min, max} over the computed rows [row_begin, row_end), and over the
+        // owned rows {max y of rows < own_end - guard, min y of rows >= own_begin + guard, min,
+        // max}.  Reduced per block, then one atomic per value into one of 64 slots on separate
+        // 128-B lines (cross-XCD atomics on a shared line serialise at the memory side).
+        __shared__ double red[6][kBlock / 64];
+        double e[6] = {INFINITY, -INFINITY, -INFINITY, INFINITY, INFINITY, -INFINITY};
         int any = 0;
         if (cell >= 0) {
             const int r = win_row0 + (int)(w / W);
             if (r >= row_begin && r < row_end) {
-                ext_accumulate(r, row_begin, row_end, guard_rows, p.y, e0, e1, e2, e3);
+                e[0] = p.y;
+                e[1] = p.y;
+                any = 1;
+            }
+            if (r >= X.own_begin && r < X.own_end) {
+                if (r < X.own_end - X.guard) e[2] = p.y;
+                if (r >= X.own_begin + X.guard) e[3] = p.y;
+                e[4] = p.y;
+                e[5] = p.y;
                 any = 1;
             }
         }
-        e0 = wave_min(e0);
-        e1 = wave_max(e1);
-        e2 = wave_max(e2);
-        e3 = wave_min(e3);
-        const int wid = threadIdx.x >> 6;
-        if (lane == 0) {
-            red[0][wid] = e0;
-            red[1][wid] = e1;
-            red[2][wid] = e2;
-            red[3][wid] = e3;
+        // the common wave has one membership pattern for all its agents: two reductions (min and
+        // max of y) instead of six
+        const unsigned code = any ? ((e[0] != INFINITY ? 1u : 0u) | (e[2] != -INFINITY ? 2u : 0u) |
+                                     (e[3] != INFINITY ? 4u : 0u) | (e[4] != INFINITY ? 8u : 0u))
+                                  : 0u;
+        const unsigned long long act = __ballot(any);
+        const unsigned c0 = (unsigned)__shfl((int)code, act ? __ffsll((long long)act) - 1 : 0, 64);
+        if (__ballot(any && code != c0) == 0) {
+            const double mn = wave_min(any ? p.y : INFINITY), mx = wave_max(any ? p.y : -INFINITY);
+            const bool has = act != 0;
+            e[0] = (has && (c0 & 1u)) ? mn : INFINITY;
+            e[1] = (has && (c0 & 1u)) ? mx : -INFINITY;
+            e[2] = (has && (c0 & 2u)) ? mx : -INFINITY;
+            e[3] = (has && (c0 & 4u)) ? mn : INFINITY;
+            e[4] = (has && (c0 & 8u)) ? mn : INFINITY;
+            e[5] = (has && (c0 & 8u)) ? mx : -INFINITY;
+        } else {
+#pragma unroll
+            for (int q = 0; q < 6; ++q) e[q] = ext_is_min(q) ? wave_min(e[q]) : wave_max(e[q]);
         }
-        if (__syncthreads_or(any) && threadIdx.x == 0) {
-            for (int q = 1; q < kBlock / 64; ++q) {
-                e0 = pmin(e0, red[0][q]);
-                e1 = pmax(e1, red[1][q]);
-                e2 = pmax(e2, red[2][q]);
-                e3 = pmin(e3, red[3][q]);
+#if CBF_EXT_WAVE
+        // per wave: lane 0 of every wave with an agent in range does the atomics (no block barrier)
+        if (__ballot(any) && lane == 0) {
+            unsigned long long* k = ext_keys + kExtSlotWords * ((t >> 6) & (kExtSlots - 1));
+#pragma unroll
+            for (int q = 0; q < 6; ++q) {
+                if (ext_is_min(q)) atomicMin(&k[q], dkey(e[q]));
+                else atomicMax(&k[q], dkey(e[q]));
             }
-            unsigned long long* k = ext_keys + kExtSlotWords * (blockIdx.x & 63);
-            atomicMin(&k[0], dkey(e0));
-            atomicMax(&k[1], dkey(e1));
-            atomicMax(&k[2], dkey(e2));
-            atomicMin(&k[3], dkey(e3));
         }
+#else
+        const int wid = threadIdx.x >> 6;
+        if (lane == 0)
+#pragma unroll
+            for (int q = 0; q < 6; ++q) red[q][wid] = e[q];
+        if (__syncthreads_or(any) && threadIdx.x == 0) {
+            for (int v = 1; v < kBlock / 64; ++v)
+#pragma unroll
+                for (int q = 0; q < 6; ++q)
+                    e[q] = ext_is_min(q) ? pmin(e[q], red[q][v]) : pmax(e[q], red[q][v]);
+            unsigned long long* k = ext_keys + kExtSlotWords * (blockIdx.x & (kExtSlots - 1));
+#pragma unroll
+            for (int q = 0; q < 6; ++q) {
+                if (ext_is_min(q)) atomicMin(&k[q], dkey(e[q]));
+                else atomicMax(&k[q], dkey(e[q]));
+            }
+        }
+#endif
     }
     // runs of equal cells inside the wave: one atomic per run
     int cprev = __shfl_up(cell, 1, 64);
@@ -352,7 +399,8 @@ __global__ void __launch_bounds__(kBlock) k_lattice_filter(KP P, CellGrid G, int
                                                            int guard_rows, double* __restrict__ ext_part,
                                                            unsigned long long* __restrict__ solves,
                                                            int32_t* __restrict__ hardq,
-                                                           const float2* __restrict__ spos32) {
+                                                           const float2* __restrict__ spos32, int cnt_begin,
+                                                           int cnt_end) {
     // hit rows + a dummy row (branch-free push) + 4 x fp64 per-quadrant minima (CBF_BQ_LDS)
     __shared__ int hit_lds[(kHitCap + 1) * kBlock + (CBF_BQ_LDS ? 8 * kBlock : 0)];
     const int bx = xcd_block();
@@ -365,7 +413,7 @@ __global__ void __launch_bounds__(kBlock) k_lattice_filter(KP P, CellGrid G, int
         int r, nb = 0;
         const int res = lattice_ego<FZ>(P, G, W, row_begin, row_end, win_row0, slot, spos, svel, sidx, start,
                                                T, pos_out, u, status, cnt, hardq, hit_lds, spos32, &ny, &r, &nb);
-        solved = res != 0 && nb > 0;
+        solved = res != 0 && nb > 0 && r >= cnt_begin && r < cnt_end;
         if (res == 1) ext_accumulate(r, row_begin, row_end, guard_rows, ny, e0, e1, e2, e3);
     }
     if (solves) {  // wave-aggregated, spread over 64 counters on separate 128-B lines
@@ -552,7 +600,7 @@ extern "C" size_t cbf_lattice_workspace_size(int32_t W, int32_t win_rows, const 
 static int lattice_build(const cbf_params* p, const cbf_grid* grid, int32_t W, int32_t H, int32_t row_begin,
                          int32_t row_end, int32_t win_row0, int32_t win_rows, const double* pos, double gain,
                          double* vel_out, void* workspace, size_t workspace_bytes, unsigned long long* ext_keys,
-                         int32_t guard_rows, void* stream) {
+                         ExtSpec X, void* stream) {
     int rc = check_lattice(p, grid, W, H, row_begin, row_end, win_row0, win_rows, pos, workspace, workspace_bytes);
     if (rc) return rc;
     if (!vel_out) return CBF_EINVAL;
@@ -567,7 +615,7 @@ static int lattice_build(const cbf_params* p, const cbf_grid* grid, int32_t W, i
     int4* bcs = reinterpret_cast<int4*>(Wk.cs);
     hipLaunchKernelGGL(k_lattice_nominal_bin_ordered, dim3(nblk(n)), dim3(kBlock), 0, s, G, W, H, row_begin, row_end,
                        win_row0, win_rows, p2, gain, wv, reinterpret_cast<double2*>(vel_out), Wk.count, Wk.sidx,
-                       Wk.start, Wk.ncell, bcs, Wk.hardq, ext_keys, guard_rows);
+                       Wk.start, Wk.ncell, bcs, Wk.hardq, ext_keys, X);
     launch_scan(Wk, s);
     hipLaunchKernelGGL(k_lattice_scatter_ordered, dim3(nblk(n)), dim3(kBlock), 0, s, n, bcs, Wk.start, p2, wv, Wk.spos,
                        Wk.svel, Wk.sidx, Wk.spos32, Wk.hardq + 2, n, Wk.ncell, win_row0, H);
@@ -578,14 +626,14 @@ extern "C" int cbf_lattice_build(const cbf_params* p, const cbf_grid* grid, int3
                                  int32_t row_end, int32_t win_row0, int32_t win_rows, const double* pos, double gain,
                                  double* vel_out, void* workspace, size_t workspace_bytes, void* stream) {
     return lattice_build(p, grid, W, H, row_begin, row_end, win_row0, win_rows, pos, gain, vel_out, workspace,
-                         workspace_bytes, nullptr, 0, stream);
+                         workspace_bytes, nullptr, ExtSpec{0, 0, 0}, stream);
 }
 
-extern "C" int cbf_lattice_advance(const cbf_params* p, const cbf_grid* grid, int32_t W, int32_t H,
-                                   int32_t row_begin, int32_t row_end, int32_t win_row0, int32_t win_rows,
-                                   const double* pos, double T, double* pos_out, double* u, int32_t* status,
-                                   int32_t* nbr_count, int32_t guard_rows, double* extents, uint64_t* solves,
-                                   void* workspace, size_t workspace_bytes, void* stream) {
+static int lattice_advance(const cbf_params* p, const cbf_grid* grid, int32_t W, int32_t H, int32_t row_begin,
+                           int32_t row_end, int32_t win_row0, int32_t win_rows, const double* pos, double T,
+                           double* pos_out, double* u, int32_t* status, int32_t* nbr_count, int32_t guard_rows,
+                           double* extents, uint64_t* solves, void* workspace, size_t workspace_bytes,
+                           int32_t cnt_begin, int32_t cnt_end, void* stream) {
     int rc = check_lattice(p, grid, W, H, row_begin, row_end, win_row0, win_rows, pos, workspace, workspace_bytes);
     if (rc) return rc;
     if (!pos_out || !u || !status) return CBF_EINVAL;
@@ -602,11 +650,20 @@ extern "C" int cbf_lattice_advance(const cbf_params* p, const cbf_grid* grid, in
     hipLaunchKernelGGL(p->f_is_zero ? k_lattice_filter<true> : k_lattice_filter<false>, dim3(nb), dim3(kBlock), 0, s,
                        kp, G, W, row_begin, row_end, win_row0, Wk.ncell, Wk.spos, Wk.svel, Wk.sidx, Wk.start, T, po, uo,
                        status, nbr_count, guard_rows, ext_part, reinterpret_cast<unsigned long long*>(solves),
-                       Wk.hardq, Wk.spos32);
+                       Wk.hardq, Wk.spos32, cnt_begin, cnt_end);
     hipLaunchKernelGGL(k_lattice_filter_hard, dim3(hb), dim3(64), 0, s, kp, row_begin, row_end, T, po, uo, status,
                        nbr_count, guard_rows, ext_part ? ext_part + 4l * lattice_ext_waves(n) : nullptr, Wk.hardq);
     if (extents) launch_extents_finalize((int)lattice_ext_waves(n) + hb, ext_part, extents, s);
     return (int)hipGetLastError();
+}
+
+extern "C" int cbf_lattice_advance(const cbf_params* p, const cbf_grid* grid, int32_t W, int32_t H,
+                                   int32_t row_begin, int32_t row_end, int32_t win_row0, int32_t win_rows,
+                                   const double* pos, double T, double* pos_out, double* u, int32_t* status,
+                                   int32_t* nbr_count, int32_t guard_rows, double* extents, uint64_t* solves,
+                                   void* workspace, size_t workspace_bytes, void* stream) {
+    return lattice_advance(p, grid, W, H, row_begin, row_end, win_row0, win_rows, pos, T, pos_out, u, status, nbr_count,
+                           guard_rows, extents, solves, workspace, workspace_bytes, row_begin, row_end, stream);
 }
 
 extern "C" int cbf_lattice_step(const cbf_params* p, const cbf_grid* grid, int32_t W, int32_t H, int32_t row_begin,
@@ -622,17 +679,19 @@ extern "C" int cbf_lattice_step(const cbf_params* p, const cbf_grid* grid, int32
 }
 
 extern "C" int cbf_lattice_step_sharded(const cbf_params* p, const cbf_grid* grid, int32_t W, int32_t H,
-                                        int32_t row_begin, int32_t row_end, int32_t win_row0, int32_t win_rows,
-                                        const double* pos, double gain, double T, double* pos_out, double* vel_out,
-                                        double* u, int32_t* status, int32_t* nbr_count, int32_t guard_rows,
-                                        uint64_t* ext_keys, uint64_t* solves, void* workspace, size_t workspace_bytes,
-                                        void* stream) {
-    if (!ext_keys || guard_rows < 0) return CBF_EINVAL;
+                                        int32_t row_begin, int32_t row_end, int32_t own_begin, int32_t own_end,
+                                        int32_t win_row0, int32_t win_rows, const double* pos, double gain, double T,
+                                        double* pos_out, double* vel_out, double* u, int32_t* status,
+                                        int32_t* nbr_count, int32_t guard_rows, uint64_t* ext_keys, uint64_t* solves,
+                                        void* workspace, size_t workspace_bytes, void* stream) {
+    if (!ext_keys || guard_rows < 0 || own_begin < row_begin || own_end > row_end || own_begin >= own_end)
+        return CBF_EINVAL;
     int rc = lattice_build(p, grid, W, H, row_begin, row_end, win_row0, win_rows, pos, gain, vel_out, workspace,
-                           workspace_bytes, reinterpret_cast<unsigned long long*>(ext_keys), guard_rows, stream);
+                           workspace_bytes, reinterpret_cast<unsigned long long*>(ext_keys),
+                           ExtSpec{own_begin, own_end, guard_rows}, stream);
     if (rc) return rc;
-    return cbf_lattice_advance(p, grid, W, H, row_begin, row_end, win_row0, win_rows, pos, T, pos_out, u, status,
-                               nbr_count, guard_rows, nullptr, solves, workspace, workspace_bytes, stream);
+    return lattice_advance(p, grid, W, H, row_begin, row_end, win_row0, win_rows, pos, T, pos_out, u, status, nbr_count,
+                           guard_rows, nullptr, solves, workspace, workspace_bytes, own_begin, own_end, stream);
 }
 
 // ---- halo exchange of the row-sharded step -----------------------------------------
@@ -643,61 +702,72 @@ __device__ __forceinline__ double dkey_inv(unsigned long long k) {
     return __longlong_as_double((long long)u);
 }
 
-// send = [first halo rows | last halo rows | 4 extents]; block 0's first wave reduces the 64
-// extent-key slots into the 4 extents and resets them for the next accumulation.
+// send = [first halo rows | last halo rows | nsub records of 8 doubles (6 extents used)]; wave q
+// of block 0 (q < nsub) reduces the 64 extent-key slots of sub-step q into its record and resets
+// them for the next accumulation.
 __global__ void __launch_bounds__(kBlock) k_halo_pack(int W, int halo, long n_own, const double2* __restrict__ own,
-                                                      unsigned long long* __restrict__ keys, double* __restrict__ send) {
+                                                      unsigned long long* __restrict__ keys, int nsub,
+                                                      double* __restrict__ send) {
     const long t = (long)blockIdx.x * kBlock + threadIdx.x;
     const long rs = (long)halo * W;
     double2* s2 = reinterpret_cast<double2*>(send);
     if (t < rs) s2[t] = own[t];
     else if (t < 2 * rs) s2[t] = own[n_own - 2 * rs + t];
-    if (blockIdx.x == 0 && threadIdx.x < 64) {
-        const int l = threadIdx.x;
-        unsigned long long* kl = keys + kExtSlotWords * l;
-        unsigned long long k0 = kl[0], k1 = kl[1], k2 = kl[2], k3 = kl[3];
-        for (int o = 32; o > 0; o >>= 1) {
-            const unsigned long long a = __shfl_xor(k0, o, 64), b = __shfl_xor(k1, o, 64);
-            const unsigned long long c = __shfl_xor(k2, o, 64), d = __shfl_xor(k3, o, 64);
-            k0 = a < k0 ? a : k0;
-            k1 = b > k1 ? b : k1;
-            k2 = c > k2 ? c : k2;
-            k3 = d < k3 ? d : k3;
-        }
-        kl[0] = dkey(INFINITY);
-        kl[1] = dkey(-INFINITY);
-        kl[2] = dkey(-INFINITY);
-        kl[3] = dkey(INFINITY);
-        if (l == 0) {
-            double* e = send + 4 * rs;
-            e[0] = dkey_inv(k0);
-            e[1] = dkey_inv(k1);
-            e[2] = dkey_inv(k2);
-            e[3] = dkey_inv(k3);
+    if (blockIdx.x == 0) {
+        const int l = threadIdx.x & 63;
+        for (int q = threadIdx.x >> 6; q < nsub; q += kBlock / 64) {
+            unsigned long long k[kExtVals];
+#pragma unroll
+            for (int v = 0; v < kExtVals; ++v) k[v] = dkey(ext_is_min(v) ? INFINITY : -INFINITY);
+            for (int j = l; j < kExtSlots; j += 64) {
+                unsigned long long* kl = keys + (long)kExtSlotWords * (kExtSlots * q + j);
+#pragma unroll
+                for (int v = 0; v < kExtVals; ++v) {
+                    const unsigned long long x = kl[v];
+                    k[v] = ext_is_min(v) ? (x < k[v] ? x : k[v]) : (x > k[v] ? x : k[v]);
+                    kl[v] = dkey(ext_is_min(v) ? INFINITY : -INFINITY);
+                }
+            }
+            for (int o = 32; o > 0; o >>= 1)
+#pragma unroll
+                for (int v = 0; v < kExtVals; ++v) {
+                    const unsigned long long x = __shfl_xor(k[v], o, 64);
+                    k[v] = ext_is_min(v) ? (x < k[v] ? x : k[v]) : (x > k[v] ? x : k[v]);
+                }
+            if (l == 0) {
+                double* e = send + 4 * rs + 8 * q;
+#pragma unroll
+                for (int v = 0; v < kExtVals; ++v) e[v] = dkey_inv(k[v]);
+            }
         }
     }
 }
 
-__global__ void k_ext_reset(unsigned long long* __restrict__ keys) {
-    unsigned long long* kl = keys + kExtSlotWords * threadIdx.x;
-    kl[0] = dkey(INFINITY);
-    kl[1] = dkey(-INFINITY);
-    kl[2] = dkey(-INFINITY);
-    kl[3] = dkey(INFINITY);
+__global__ void k_ext_reset(unsigned long long* __restrict__ keys, int nsub) {
+    for (int i = threadIdx.x; i < kExtSlots * nsub; i += blockDim.x) {
+        unsigned long long* kl = keys + (long)kExtSlotWords * i;
+#pragma unroll
+        for (int v = 0; v < kExtVals; ++v) kl[v] = dkey(ext_is_min(v) ? INFINITY : -INFINITY);
+    }
 }
 
+// Guard of one sub-step: every agent outside rank's candidate rows is farther than the cull
+// radius (in y) from every agent rank computed.  Record layout (per rank q, per sub-step): {min y,
+// max y of q's computed rows, max y of q's owned rows below its top `guard` rows, min y above its
+// bottom `guard` rows, min y, max y of q's owned rows}.
 __device__ __forceinline__ bool halo_guard_ok(const double* E, long stride, int ws, int rank, double radius) {
     const double rm = radius * (1.0 + 1e-9) + 1e-12;
     const double* me = E + (long)rank * stride;
     const double ymin = me[0], ymax = me[1];
+    if (!(ymin <= ymax)) return true;  // no computed agents recorded (identity record)
     bool ok = true;
     for (int q = 0; q < ws; ++q) {
         const double* o = E + (long)q * stride;
-        if (q < rank) {  // rows below: rank-1's rows outside our halo, everything of lower ranks
-            const double lim = (q == rank - 1) ? o[2] : o[1];
+        if (q < rank) {  // rows below: rank-1's rows outside our candidate band, all of lower ranks
+            const double lim = (q == rank - 1) ? o[2] : o[5];
             if (!(ymin - lim > rm)) ok = false;
         } else if (q > rank) {
-            const double lim = (q == rank + 1) ? o[3] : o[0];
+            const double lim = (q == rank + 1) ? o[3] : o[4];
             if (!(lim - ymax > rm)) ok = false;
         }
     }
@@ -708,7 +778,7 @@ __device__ __forceinline__ bool halo_guard_ok(const double* E, long stride, int 
 // block 0 lane 0 runs the guard on the gathered extents.
 __global__ void __launch_bounds__(kBlock) k_halo_unpack(int W, int halo, int rows_lo, int rows_hi, long hi_off,
                                                         const double* __restrict__ recv, long stride, int ws, int rank,
-                                                        double radius, double2* __restrict__ wpos,
+                                                        double radius, int nsub, double2* __restrict__ wpos,
                                                         int32_t* __restrict__ flag) {
     const long t = (long)blockIdx.x * kBlock + threadIdx.x;
     const long nlo = (long)rows_lo * W, nhi = (long)rows_hi * W, rs = (long)halo * W;
@@ -719,39 +789,44 @@ __global__ void __launch_bounds__(kBlock) k_halo_unpack(int W, int halo, int row
         const double2* src = reinterpret_cast<const double2*>(recv + (long)(rank + 1) * stride);
         wpos[hi_off + (t - nlo)] = src[t - nlo];
     }
-    if (blockIdx.x == 0 && threadIdx.x == 0 && !halo_guard_ok(recv + 4 * rs, stride, ws, rank, radius)) flag[0] |= 1;
+    if (blockIdx.x == 0 && threadIdx.x < nsub && !halo_guard_ok(recv + 4 * rs + 8 * threadIdx.x, stride, ws, rank, radius))
+        atomicOr(flag, 1);
 }
 
 }  // namespace
 
-extern "C" size_t cbf_halo_ext_bytes(void) { return 64 * kExtSlotWords * sizeof(unsigned long long); }
+extern "C" size_t cbf_halo_ext_bytes(int32_t nsub) {
+    return nsub < 1 ? 0 : (size_t)nsub * kExtSlots * kExtSlotWords * sizeof(unsigned long long);
+}
 
-extern "C" int cbf_halo_ext_reset(uint64_t* ext_keys, void* stream) {
-    if (!ext_keys) return CBF_EINVAL;
-    hipLaunchKernelGGL(k_ext_reset, dim3(1), dim3(64), 0, (hipStream_t)stream,
-                       reinterpret_cast<unsigned long long*>(ext_keys));
+extern "C" int cbf_halo_ext_reset(uint64_t* ext_keys, int32_t nsub, void* stream) {
+    if (!ext_keys || nsub < 1) return CBF_EINVAL;
+    hipLaunchKernelGGL(k_ext_reset, dim3(1), dim3(kBlock), 0, (hipStream_t)stream,
+                       reinterpret_cast<unsigned long long*>(ext_keys), nsub);
     return (int)hipGetLastError();
 }
 
 extern "C" int cbf_halo_pack(int32_t W, int32_t halo, int64_t n_own, const double* own, uint64_t* ext_keys,
-                             double* send, void* stream) {
-    if (W <= 0 || halo <= 0 || n_own < 2l * halo * W || !own || !ext_keys || !send) return CBF_EINVAL;
+                             int32_t nsub, double* send, void* stream) {
+    if (W <= 0 || halo <= 0 || n_own < 2l * halo * W || !own || !ext_keys || !send || nsub < 1) return CBF_EINVAL;
     const long n = 2l * halo * W;
     hipLaunchKernelGGL(k_halo_pack, dim3(nblk(n)), dim3(kBlock), 0, (hipStream_t)stream, W, halo, (long)n_own,
-                       reinterpret_cast<const double2*>(own), reinterpret_cast<unsigned long long*>(ext_keys), send);
+                       reinterpret_cast<const double2*>(own), reinterpret_cast<unsigned long long*>(ext_keys), nsub,
+                       send);
     return (int)hipGetLastError();
 }
 
 extern "C" int cbf_halo_unpack(int32_t W, int32_t halo, int32_t rows_lo, int32_t rows_hi, int64_t hi_row_offset,
                                const double* recv, int64_t stride, int32_t world_size, int32_t rank, double radius,
-                               double* wpos, int32_t* flag, void* stream) {
+                               int32_t nsub, double* wpos, int32_t* flag, void* stream) {
     if (W <= 0 || halo <= 0 || rows_lo < 0 || rows_hi < 0 || rows_lo > halo || rows_hi > halo || !recv || !wpos ||
-        !flag || world_size < 1 || rank < 0 || rank >= world_size || stride < 4l * halo * W + 4 ||
-        (rows_lo > 0 && rank == 0) || (rows_hi > 0 && rank == world_size - 1) || hi_row_offset < 0)
+        !flag || world_size < 1 || rank < 0 || rank >= world_size || nsub < 1 || nsub > 64 ||
+        stride < 4l * halo * W + 8l * nsub || (rows_lo > 0 && rank == 0) || (rows_hi > 0 && rank == world_size - 1) ||
+        hi_row_offset < 0)
         return CBF_EINVAL;
     const long n = (long)(rows_lo + rows_hi) * W;
     hipLaunchKernelGGL(k_halo_unpack, dim3(nblk(n > 0 ? n : 1)), dim3(kBlock), 0, (hipStream_t)stream, W, halo,
-                       rows_lo, rows_hi, (long)hi_row_offset * W, recv, (long)stride, world_size, rank, radius,
+                       rows_lo, rows_hi, (long)hi_row_offset * W, recv, (long)stride, world_size, rank, radius, nsub,
                        reinterpret_cast<double2*>(wpos), flag);
     return (int)hipGetLastError();
 }

@@ -1,22 +1,24 @@
 """Row-stripe sharding of the lattice swarm across GPUs (SURVEY 8e, cfg4 at 1/2/4/8 GPUs).
 
 Rank r owns lattice rows [r R, (r+1) R) of a W x (R * world) lattice (weak scaling: R rows per
-GPU).  Each timestep is four device operations around ONE collective:
-  1. pack    (cbf_halo_pack)   the rank's first and last `halo` owned rows + 4 y-extents of the
-             owned positions that the previous step's build accumulated, into one send slab;
-  2. gather  ONE all_gather_into_tensor of the slabs (RCCL over xGMI) -- 2 * halo * W * 16 B per rank;
-  3. unpack  (cbf_halo_unpack) rank r-1's last rows and rank r+1's first rows into the halo rows of
-             the window, and the halo guard on the gathered extents;
-  4. step    (cbf_lattice_step_sharded) nominal control, cell list, filter, clip, Euler for the
-             owned rows, writing them in place; its build accumulates the extents of its inputs.
-The halo holds `halo` rows per side; the outermost halo row only feeds the consensus of the
-next row, so candidates reach halo-1 rows beyond the stripe (guard_rows = halo - 1).  The guard
-proves that every agent outside a rank's candidate rows is farther than the cull radius (in y)
-from every agent it owns; it runs on the extents of step t's inputs at step t+1's exchange, and
-check_guard() does one last exchange for the final step.  Results are bit-identical to the
-single-GPU step of the whole lattice whenever the guard holds (checked by tests and by
-check_guard()).  With capture(), steps 1 and 3-4 replay as two hipGraphs around the eager
-collective.
+GPU).  One timestep depends on lattice rows up to `halo` = 4 away (cull candidates up to 3 rows
+away, plus the row that forms their nominal control), so a rank that holds G = halo * k ghost rows
+on each side can advance k timesteps ("sub-steps") between exchanges, recomputing the ghost rows
+that are still exact.  Each exchange (every k sub-steps) is ONE collective:
+  1. pack    (cbf_halo_pack)   the first and last G owned rows + the guard records of the last k
+             sub-steps into one send slab;
+  2. gather  ONE all_gather_into_tensor of the slabs (RCCL over xGMI) -- 2 G W 16 B per rank;
+  3. unpack  (cbf_halo_unpack) rank r-1's last rows and rank r+1's first rows into the ghost rows
+             of the window, and the halo guard of the k recorded sub-steps;
+then sub-step s (cbf_lattice_step_sharded) computes rows [rb - D_s, re + D_s), D_s = G - halo (s+1)
+(the owned rows at the last sub-step), over the window of those rows +- halo, with its own
+workspace (so each sub-step keeps its cell order from cycle to cycle).
+The guard proves that every agent outside a sub-step's candidate rows was farther than the cull
+radius (in y) from every agent it computed; the records of a cycle are checked at the next
+exchange, and check_guard() does one more exchange for the last ones.  Results are bit-identical
+to the single-GPU step of the whole lattice whenever the guard holds (checked by tests and by
+check_guard()).  The extra work is the ghost rows: about 2 G / R of the binned rows and G / R of
+the computed rows per rank (k = 4, R = 1024: 3 % and 1.6 %), for a k-fold cut in collectives.
 
 The backend object does the device work (HipBackend here; the CPU gloo tests plug in the
 oracle as a backend to check the exchange logic).
@@ -32,35 +34,50 @@ from . import scenarios
 RADIUS_GUARD_EPS = (1e-9, 1e-12)
 
 
-def guard_ok(ext_all: np.ndarray, rank: int, radius: float) -> bool:
-    """Host restatement of the device guard (cbf_halo_guard)."""
+def guard_ok(recs: np.ndarray, rank: int, radius: float) -> bool:
+    """Host restatement of the device guard of one sub-step (k_halo_unpack): recs[q] = {min y, max
+    y of q's computed rows, max y of q's owned rows below its top `guard` rows, min y above its
+    bottom `guard` rows, min y, max y of q's owned rows}."""
     rm = radius * (1.0 + RADIUS_GUARD_EPS[0]) + RADIUS_GUARD_EPS[1]
-    ymin, ymax = ext_all[rank, 0], ext_all[rank, 1]
-    for q in range(ext_all.shape[0]):
+    ymin, ymax = recs[rank, 0], recs[rank, 1]
+    if not ymin <= ymax:
+        return True
+    for q in range(recs.shape[0]):
         if q < rank:
-            lim = ext_all[q, 2] if q == rank - 1 else ext_all[q, 1]
+            lim = recs[q, 2] if q == rank - 1 else recs[q, 5]
             if not (ymin - lim > rm):
                 return False
         elif q > rank:
-            lim = ext_all[q, 3] if q == rank + 1 else ext_all[q, 0]
+            lim = recs[q, 3] if q == rank + 1 else recs[q, 4]
             if not (lim - ymax > rm):
                 return False
     return True
 
 
-def stripe_extents(pos_rows: np.ndarray, W: int, guard_rows: int) -> np.ndarray:
-    """{min y, max y, max y of rows < R - guard_rows, min y of rows >= guard_rows} of an owned stripe."""
-    y = pos_rows[:, 1].reshape(-1, W)
-    R = y.shape[0]
-    e2 = y[:R - guard_rows].max() if R > guard_rows else -math.inf
-    e3 = y[guard_rows:].min() if R > guard_rows else math.inf
-    return np.array([y.min(), y.max(), e2, e3], dtype=np.float64)
+def sub_extents(win_pos: np.ndarray, W: int, w0: int, a: int, b: int, rb: int, re: int, guard: int) -> np.ndarray:
+    """The guard record of a sub-step from its input window positions (rows [w0, ...)): {min, max}
+    y over computed rows [a, b), {max y of owned rows < re - guard, min y of owned rows >= rb +
+    guard, min y, max y} over owned rows [rb, re)."""
+    y = win_pos[:, 1].reshape(-1, W)
+    comp = y[a - w0:b - w0]
+    own = y[rb - w0:re - w0]
+    R = own.shape[0]
+    e2 = own[:R - guard].max() if R > guard else -math.inf
+    e3 = own[guard:].min() if R > guard else math.inf
+    return np.array([comp.min(), comp.max(), e2, e3, own.min(), own.max()], dtype=np.float64)
+
+
+class Sub:
+    """Geometry of sub-step s: computed rows [a, b), window [w0, w1), guard rows."""
+
+    def __init__(self, a, b, w0, w1, guard):
+        self.a, self.b, self.w0, self.w1, self.guard = a, b, w0, w1, guard
 
 
 class HipBackend:
     """Device work of one rank through libcbf_amd.so."""
 
-    def __init__(self, W, H, gain, T, params, grid, win_rows):
+    def __init__(self, W, H, gain, T, params, grid, win_rows, nsub=1):
         import torch
         from . import _lib, swarm
         self.torch, self._lib, self.swarm = torch, _lib, swarm
@@ -69,46 +86,53 @@ class HipBackend:
         self.cp = params.c()
         self.radius = params.safety_distance
         self.grid = grid
+        self.nsub = nsub
         self.ws_bytes = _lib.lib.cbf_lattice_workspace_size(W, win_rows, _lib.C.byref(grid))
-        self.ws = torch.zeros((self.ws_bytes,), dtype=torch.uint8, device=self.dev)
+        # one workspace per sub-step: each keeps the cell order of its own window across cycles
+        self.wss = [torch.zeros((self.ws_bytes,), dtype=torch.uint8, device=self.dev) for _ in range(nsub)]
         self.flag = torch.zeros((1,), dtype=torch.int32, device=self.dev)
-        self.ext_keys = torch.empty((_lib.lib.cbf_halo_ext_bytes() // 8,), dtype=torch.int64, device=self.dev)
-        _lib.check(_lib.lib.cbf_halo_ext_reset(_lib.ptr(self.ext_keys), _lib.stream_handle()), "cbf_halo_ext_reset")
+        self.set_words = _lib.lib.cbf_halo_ext_bytes(1) // 8
+        self.ext_keys = torch.empty((nsub * self.set_words,), dtype=torch.int64, device=self.dev)
+        _lib.check(_lib.lib.cbf_halo_ext_reset(_lib.ptr(self.ext_keys), nsub, _lib.stream_handle()),
+                   "cbf_halo_ext_reset")
 
     def tensor(self, a):
         return self.torch.as_tensor(np.ascontiguousarray(a), device=self.dev)
 
     def pack(self, S):
         L, P = self._lib, self._lib.ptr
-        L.check(L.lib.cbf_halo_pack(self.W, S.halo, S.n_owned, P(S.own), P(self.ext_keys), P(S.send),
+        L.check(L.lib.cbf_halo_pack(self.W, S.G, S.n_owned, P(S.own), P(self.ext_keys), self.nsub, P(S.send),
                                     L.stream_handle()), "cbf_halo_pack")
 
     def unpack_guard(self, S):
         L, P = self._lib, self._lib.ptr
-        L.check(L.lib.cbf_halo_unpack(self.W, S.halo, S.rb - S.w0, S.w1 - S.re, S.re - S.w0, P(S.recv), S.stride,
-                                      S.ws, S.rank, self.radius, P(S.wpos), P(self.flag), L.stream_handle()),
-                "cbf_halo_unpack")
+        L.check(L.lib.cbf_halo_unpack(self.W, S.G, S.rb - S.w0, S.w1 - S.re, S.re - S.w0, P(S.recv), S.stride,
+                                      S.ws, S.rank, self.radius, self.nsub, P(S.wpos), P(self.flag),
+                                      L.stream_handle()), "cbf_halo_unpack")
 
-    def lattice_step(self, S):
-        L, P = self._lib, self._lib.ptr
-        L.check(L.lib.cbf_lattice_step_sharded(self.cp, L.C.byref(self.grid), self.W, self.H, S.rb, S.re, S.w0,
-                                               S.win_rows, P(S.wpos), self.gain, self.T, P(S.own), P(S.vel), P(S.u),
-                                               P(S.status), P(S.nbr_count), S.halo - 1, P(self.ext_keys),
-                                               P(S.solves), P(self.ws), self.ws_bytes, L.stream_handle()),
-                "cbf_lattice_step_sharded")
+    def lattice_step(self, S, s, sub):
+        L, P, W = self._lib, self._lib.ptr, self.W
+        o = (sub.a - S.w0) * W
+        L.check(L.lib.cbf_lattice_step_sharded(
+            self.cp, L.C.byref(self.grid), W, self.H, sub.a, sub.b, S.rb, S.re, sub.w0, sub.w1 - sub.w0,
+            P(S.wpos[(sub.w0 - S.w0) * W:]), self.gain, self.T, P(S.wpos[o:]), P(S.wvel[o:]), P(S.wu[o:]),
+            P(S.wstatus[o:]), P(S.wcnt[o:]), sub.guard, P(self.ext_keys[s * self.set_words:]), P(S.solves),
+            P(self.wss[s]), self.ws_bytes, L.stream_handle()), "cbf_lattice_step_sharded")
 
     def lattice_build(self, S):
         L, P = self._lib, self._lib.ptr
-        L.check(L.lib.cbf_lattice_build(self.cp, L.C.byref(self.grid), self.W, self.H, S.rb, S.re, S.w0, S.win_rows,
-                                        P(S.wpos), self.gain, P(S.vel), P(self.ws), self.ws_bytes,
-                                        L.stream_handle()), "cbf_lattice_build")
+        sub = S.subs[-1]
+        L.check(L.lib.cbf_lattice_build(self.cp, L.C.byref(self.grid), self.W, self.H, S.rb, S.re, sub.w0,
+                                        sub.w1 - sub.w0, P(S.wpos[(sub.w0 - S.w0) * self.W:]), self.gain, P(S.vel),
+                                        P(self.wss[-1]), self.ws_bytes, L.stream_handle()), "cbf_lattice_build")
 
     def lattice_advance(self, S):
         L, P = self._lib, self._lib.ptr
-        L.check(L.lib.cbf_lattice_advance(self.cp, L.C.byref(self.grid), self.W, self.H, S.rb, S.re, S.w0,
-                                          S.win_rows, P(S.wpos), self.T, P(S.own), P(S.u), P(S.status),
-                                          P(S.nbr_count), S.halo - 1, None, P(S.solves), P(self.ws),
-                                          self.ws_bytes, L.stream_handle()), "cbf_lattice_advance")
+        sub = S.subs[-1]
+        L.check(L.lib.cbf_lattice_advance(self.cp, L.C.byref(self.grid), self.W, self.H, S.rb, S.re, sub.w0,
+                                          sub.w1 - sub.w0, P(S.wpos[(sub.w0 - S.w0) * self.W:]), self.T, P(S.own),
+                                          P(S.u), P(S.status), P(S.nbr_count), sub.guard, None, P(S.solves),
+                                          P(self.wss[-1]), self.ws_bytes, L.stream_handle()), "cbf_lattice_advance")
 
     def guard_failed(self) -> bool:
         return bool(self.flag.item())
@@ -117,22 +141,28 @@ class HipBackend:
 class ShardedLattice:
     """One rank's stripe of a W x (rows_per_rank * world) lattice swarm (see module docstring)."""
 
-    def __init__(self, W, rows_per_rank, seed=0, halo=4, gain=scenarios.LATTICE_GAIN, T=scenarios.T, params=None,
-                 backend=None, group=None, pos_global=None):
+    def __init__(self, W, rows_per_rank, seed=0, halo=4, substeps=4, gain=scenarios.LATTICE_GAIN, T=scenarios.T,
+                 params=None, backend=None, group=None, pos_global=None):
         import torch
         import torch.distributed as dist
         from .swarm import FilterParams, make_grid
         self.torch, self.dist, self.group = torch, dist, group
         self.ws = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
-        self.W, self.R, self.halo = W, rows_per_rank, halo
-        if not (2 <= halo <= rows_per_rank):
-            raise ValueError("need 2 <= halo <= rows_per_rank")
+        self.W, self.R, self.halo, self.k = W, rows_per_rank, halo, substeps
+        self.G = halo * substeps
+        if not (2 <= halo and 1 <= substeps and self.G <= rows_per_rank):
+            raise ValueError("need halo >= 2, substeps >= 1 and halo * substeps <= rows_per_rank")
         self.H = rows_per_rank * self.ws
         self.rb, self.re = self.rank * rows_per_rank, (self.rank + 1) * rows_per_rank
-        self.w0 = max(0, self.rb - halo)
-        self.w1 = min(self.H, self.re + halo)
+        self.w0 = max(0, self.rb - self.G)
+        self.w1 = min(self.H, self.re + self.G)
         self.win_rows = self.w1 - self.w0
+        self.subs = []
+        for s in range(substeps):
+            d = self.G - halo * (s + 1)
+            a, b = max(0, self.rb - d), min(self.H, self.re + d)
+            self.subs.append(Sub(a, b, max(0, a - halo), min(self.H, b + halo), d + halo - 1))
         self.params = params or FilterParams()
         if pos_global is None:
             pos_global = scenarios.lattice(W, self.H, seed=seed)
@@ -141,25 +171,32 @@ class ShardedLattice:
         grid = make_grid(-1.0 - a, self.w0 * a - 1.0 - a, W * a + 1.0, self.w1 * a + 1.0,
                          self.params.safety_distance * 1.02)
         if backend is None:
-            backend = HipBackend(W, self.H, gain, T, self.params, grid, self.win_rows)
+            backend = HipBackend(W, self.H, gain, T, self.params, grid, self.win_rows, substeps)
         self.be = backend
         t = backend.tensor
         self.wpos = t(win)
         self.n_owned = rows_per_rank * W
         o0 = (self.rb - self.w0) * W
         self.own = self.wpos[o0:o0 + self.n_owned]
-        self.vel = t(np.zeros((self.n_owned, 2)))
-        self.u = t(np.zeros((self.n_owned, 2)))
-        self.status = t(np.zeros(self.n_owned, np.int32))
-        self.nbr_count = t(np.zeros(self.n_owned, np.int32))
+        # per-window-row outputs (sub-steps write their computed rows); the owned rows are views
+        nw = self.win_rows * W
+        self.wvel = t(np.zeros((nw, 2)))
+        self.wu = t(np.zeros((nw, 2)))
+        self.wstatus = t(np.zeros(nw, np.int32))
+        self.wcnt = t(np.zeros(nw, np.int32))
+        self.vel = self.wvel[o0:o0 + self.n_owned]
+        self.u = self.wu[o0:o0 + self.n_owned]
+        self.status = self.wstatus[o0:o0 + self.n_owned]
+        self.nbr_count = self.wcnt[o0:o0 + self.n_owned]
         self.solves = t(np.zeros(1024, np.int64))
-        # send slab: [first halo rows | last halo rows | 4 extents (+4 pad)] doubles
-        self.slab = 2 * halo * W * 2
-        self.stride = self.slab + 8
+        # send slab: [first G rows | last G rows | k guard records of 8 doubles] doubles
+        self.slab = 2 * self.G * W * 2
+        self.stride = self.slab + 8 * substeps
         self.send = t(np.zeros(self.stride))
         self.recv = t(np.zeros(self.stride * self.ws))
         self.use_list_gather = dist.get_backend(group) == "gloo"
         self.graph = None
+        self.sub = 0   # next sub-step of the current exchange cycle
 
     # ---- one timestep -------------------------------------------------------------------------
     def _gather(self):
@@ -180,18 +217,14 @@ class ShardedLattice:
         self._gather()
         self.be.unpack_guard(self)
 
-    def _post(self):
-        self.be.unpack_guard(self)
-        self.be.lattice_step(self)
-
     def step(self):
-        if self.graph is not None:   # two captured graphs around the (eager) collective
-            self.graph[0].replay()
-            self._gather()
-            self.graph[1].replay()
-            return
-        self.exchange()
-        self.be.lattice_step(self)
+        if self.sub == 0:
+            self.exchange()
+        if self.graph is not None:
+            self.graph[self.sub].replay()
+        else:
+            self.be.lattice_step(self, self.sub, self.subs[self.sub])
+        self.sub = (self.sub + 1) % self.k
 
     def build_phase(self):
         self.be.lattice_build(self)
@@ -200,20 +233,20 @@ class ShardedLattice:
         self.be.lattice_advance(self)
 
     def capture(self):
-        """Capture the device work of a step into two hipGraphs -- the halo pack, and unpack +
-        guard + the fused lattice step -- so one step is two graph launches around the eager
-        collective (RCCL stays outside the graphs)."""
+        """Capture each sub-step's device work (cbf_lattice_step_sharded) into its own hipGraph;
+        the exchange (pack, collective, unpack) stays eager at the start of a cycle."""
         torch = self.torch
         if not self.own.is_cuda:
             return None
         torch.cuda.synchronize()
-        g0, g1 = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g0):
-            self.be.pack(self)
-        with torch.cuda.graph(g1):
-            self._post()
-        self.graph = (g0, g1)
-        return self.graph
+        graphs = []
+        for s in range(self.k):
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                self.be.lattice_step(self, s, self.subs[s])
+            graphs.append(g)
+        self.graph = graphs
+        return graphs
 
     def reset_solves(self):
         self.solves.zero_()
@@ -222,7 +255,8 @@ class ShardedLattice:
         return int(self.solves.view(64, 16)[:, 0].sum().item())
 
     def check_guard(self):
-        """Certify the last step (one more exchange of extents) and raise if any step's guard failed."""
+        """Certify the sub-steps since the last exchange (one more exchange, which also refreshes
+        the ghost rows) and raise if any sub-step's guard failed."""
         self.exchange()
         if self.be.guard_failed():
             raise RuntimeError(f"rank {self.rank}: halo guard failed -- an agent moved within the cull radius of "

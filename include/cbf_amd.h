@@ -248,32 +248,40 @@ int cbf_halo_guard(const double* ext_all, int64_t stride, int32_t world_size, in
                    int32_t* flag, void* stream);
 
 /*
- * Row-sharded step, fused form (what cbf_amd/shard.py runs).  One timestep is
- *   cbf_halo_pack -> all-gather of the send slabs (RCCL) -> cbf_halo_unpack -> cbf_lattice_step_sharded.
- * cbf_lattice_step_sharded = cbf_lattice_step whose BUILD phase also accumulates the y-extents of
- * the owned INPUT positions (the 4 values of `extents` above, guard_rows as given) into
- * ext_keys (device, cbf_halo_ext_bytes(): 64 slots x 4 monotone uint64 keys; set to identity
- * once with cbf_halo_ext_reset); the advance phase computes no extents.
- * cbf_halo_pack writes send = [first halo owned rows | last halo owned rows | 4 extents reduced
- * from ext_keys] (own = the n_own owned positions) and resets ext_keys.  cbf_halo_unpack copies
- * rank-1's last rows_lo rows into window rows [0, rows_lo) and rank+1's first rows_hi rows into
- * window rows [hi_row_offset, +rows_hi) from the gathered recv (world_size slabs of `stride`
- * doubles), and runs the halo guard on the gathered extents -- the extents of the PREVIOUS
- * step's inputs, so a step is certified one exchange later (a final pack + gather + unpack
- * certifies the last one).
+ * Row-sharded step with ghost rows (what cbf_amd/shard.py runs).  A rank exchanges
+ * every `nsub` sub-steps; each exchange is
+ *   cbf_halo_pack -> all-gather of the send slabs (RCCL) -> cbf_halo_unpack,
+ * and sub-step s then runs cbf_lattice_step_sharded on rows [row_begin, row_end) = the owned rows
+ * widened by the ghost rows still exact at s, over the window of those rows +- the per-step halo.
+ * cbf_lattice_step_sharded = cbf_lattice_step with solves counted over the owned rows
+ * [own_begin, own_end) only, whose BUILD also accumulates y-extents of its INPUT positions into
+ * ext_keys (sub-step s's set: ext_keys + s * cbf_halo_ext_bytes(1) / 8): {min, max over computed
+ * rows, max over owned rows < own_end - guard_rows, min over owned rows >= own_begin +
+ * guard_rows, min, max over owned rows}; guard_rows = the rows of a neighbour inside this
+ * rank's candidate band at s.  The advance phase computes no extents.
+ * cbf_halo_ext_bytes(nsub): size of nsub sets (512 slots x 16 uint64 keys each), set to identity
+ * once with cbf_halo_ext_reset.  cbf_halo_pack writes send = [first `halo` owned rows | last
+ * `halo` owned rows | nsub records of 8 doubles] (own = the n_own owned positions; halo = the
+ * ghost depth) and resets the sets.  cbf_halo_unpack copies rank-1's last rows_lo rows into
+ * window rows [0, rows_lo) and rank+1's first rows_hi rows into window rows [hi_row_offset,
+ * +rows_hi) from the gathered recv (world_size slabs of `stride` doubles), and runs the halo guard
+ * of every recorded sub-step: *flag |= 1 unless every agent outside a sub-step's candidate rows
+ * was farther than the cull radius (in y) from every agent it computed.  The records describe the
+ * sub-steps since the previous exchange, so a step is certified one exchange later (a final pack
+ * + gather + unpack certifies the last ones).
  */
-size_t cbf_halo_ext_bytes(void);
-int cbf_halo_ext_reset(uint64_t* ext_keys, void* stream);
-int cbf_halo_pack(int32_t W, int32_t halo, int64_t n_own, const double* own, uint64_t* ext_keys, double* send,
-                  void* stream);
+size_t cbf_halo_ext_bytes(int32_t nsub);
+int cbf_halo_ext_reset(uint64_t* ext_keys, int32_t nsub, void* stream);
+int cbf_halo_pack(int32_t W, int32_t halo, int64_t n_own, const double* own, uint64_t* ext_keys, int32_t nsub,
+                  double* send, void* stream);
 int cbf_halo_unpack(int32_t W, int32_t halo, int32_t rows_lo, int32_t rows_hi, int64_t hi_row_offset,
-                    const double* recv, int64_t stride, int32_t world_size, int32_t rank, double radius, double* wpos,
-                    int32_t* flag, void* stream);
+                    const double* recv, int64_t stride, int32_t world_size, int32_t rank, double radius, int32_t nsub,
+                    double* wpos, int32_t* flag, void* stream);
 int cbf_lattice_step_sharded(const cbf_params* p, const cbf_grid* grid, int32_t W, int32_t H, int32_t row_begin,
-                             int32_t row_end, int32_t win_row0, int32_t win_rows, const double* pos, double gain,
-                             double T, double* pos_out, double* vel_out, double* u, int32_t* status,
-                             int32_t* nbr_count, int32_t guard_rows, uint64_t* ext_keys, uint64_t* solves,
-                             void* workspace, size_t workspace_bytes, void* stream);
+                             int32_t row_end, int32_t own_begin, int32_t own_end, int32_t win_row0, int32_t win_rows,
+                             const double* pos, double gain, double T, double* pos_out, double* vel_out, double* u,
+                             int32_t* status, int32_t* nbr_count, int32_t guard_rows, uint64_t* ext_keys,
+                             uint64_t* solves, void* workspace, size_t workspace_bytes, void* stream);
 
 /*
  * Batched Monte-Carlo rendezvous (SURVEY cfg5): n_scen independent scenarios, each with

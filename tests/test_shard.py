@@ -12,33 +12,37 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 from cbf_amd import scenarios
-from cbf_amd.shard import ShardedLattice, guard_ok, stripe_extents
+from cbf_amd.shard import ShardedLattice, guard_ok, sub_extents
 from oracle import coracle, pyoracle as po
 
 
-class OracleBackend:
-    """Device work restated on the CPU (oracle): the same pack / unpack+guard / step contract as
-    HipBackend, including the guard running one exchange after the step it certifies."""
+IDENT = np.array([np.inf, -np.inf, -np.inf, np.inf, np.inf, -np.inf])
 
-    def __init__(self, W, H, gain, T, radius):
-        self.W, self.H, self.gain, self.T, self.radius = W, H, gain, T, radius
+
+class OracleBackend:
+    """Device work restated on the CPU (oracle): the same pack / unpack+guard / sub-step contract
+    as HipBackend, including the guard running at the exchange after the sub-steps it certifies."""
+
+    def __init__(self, W, H, gain, T, radius, nsub):
+        self.W, self.H, self.gain, self.T, self.radius, self.nsub = W, H, gain, T, radius, nsub
         self.p = po.Params(15)
         self.flag = 0
-        self.pending = np.array([np.inf, -np.inf, -np.inf, np.inf])   # extents of the last step's inputs
+        self.recs = np.tile(IDENT, (nsub, 1))
 
     def tensor(self, a):
         return torch.as_tensor(np.ascontiguousarray(a)).clone()
 
     def pack(self, S):
-        rs = S.halo * S.W * 2
+        rs = S.G * S.W * 2
         own = S.own.reshape(-1)
         S.send[:rs].copy_(own[:rs])
         S.send[rs:2 * rs].copy_(own[own.numel() - rs:])
-        S.send[S.slab:S.slab + 4].copy_(torch.as_tensor(self.pending))
-        self.pending = np.array([np.inf, -np.inf, -np.inf, np.inf])
+        for s in range(self.nsub):
+            S.send[S.slab + 8 * s:S.slab + 8 * s + 6].copy_(torch.as_tensor(self.recs[s]))
+        self.recs = np.tile(IDENT, (self.nsub, 1))
 
     def unpack_guard(self, S):
-        W, rs = S.W, S.halo * S.W * 2
+        W, rs = S.W, S.G * S.W * 2
         wv = S.wpos.view(-1)
         if S.rank > 0:
             lo = (S.rank - 1) * S.stride
@@ -49,26 +53,32 @@ class OracleBackend:
             a = (S.re - S.w0) * W * 2
             n = (S.w1 - S.re) * W * 2
             wv[a:a + n].copy_(S.recv[hi:hi + n])
-        ext = np.stack([S.recv[q * S.stride + S.slab:q * S.stride + S.slab + 4].numpy() for q in range(S.ws)])
-        if not guard_ok(ext, S.rank, self.radius):
-            self.flag = 1
+        for s in range(self.nsub):
+            recs = np.stack([S.recv[q * S.stride + S.slab + 8 * s:q * S.stride + S.slab + 8 * s + 6].numpy()
+                             for q in range(S.ws)])
+            if not guard_ok(recs, S.rank, self.radius):
+                self.flag = 1
 
-    def lattice_step(self, S):
+    def lattice_step(self, S, s, sub):
         W, H = self.W, self.H
-        self.pending = stripe_extents(S.own.numpy(), W, S.halo - 1)       # extents of this step's inputs
+        win = S.wpos.numpy()[(sub.w0 - S.w0) * W:(sub.w1 - S.w0) * W]
+        self.recs[s] = sub_extents(win, W, sub.w0, sub.a, sub.b, S.rb, S.re, sub.guard)
         full = np.zeros((W * H, 2))
-        full[S.w0 * W:S.w1 * W] = S.wpos.numpy()
-        lo = S.w0 if S.w0 == 0 else S.w0 + 1
-        hi = S.w1 if S.w1 == H else S.w1 - 1
+        full[sub.w0 * W:sub.w1 * W] = win
+        lo = sub.w0 if sub.w0 == 0 else sub.w0 + 1        # rows whose nominal control exists
+        hi = sub.w1 if sub.w1 == H else sub.w1 - 1
         vel = coracle.consensus_lattice(W, H, lo, hi, full, self.gain)
         cand = full[lo * W:hi * W]
-        eb, ee = (S.rb - lo) * W, (S.re - lo) * W
+        eb, ee = (sub.a - lo) * W, (sub.b - lo) * W
         out = coracle.filter_swarm(self.p, cand, vel, 0, eb, ee)
         new = coracle.euler(cand[eb:ee], out["u"], self.T)
-        S.own.copy_(torch.as_tensor(new))
-        S.vel.copy_(torch.as_tensor(vel[eb:ee])); S.u.copy_(torch.as_tensor(out["u"]))
-        S.status.copy_(torch.as_tensor(out["status"])); S.nbr_count.copy_(torch.as_tensor(out["cnt"]))
-        S.solves[0] += int((out["cnt"] > 0).sum())
+        o = (sub.a - S.w0) * W
+        n = (sub.b - sub.a) * W
+        S.wpos[o:o + n].copy_(torch.as_tensor(new))
+        S.wvel[o:o + n].copy_(torch.as_tensor(vel[eb:ee])); S.wu[o:o + n].copy_(torch.as_tensor(out["u"]))
+        S.wstatus[o:o + n].copy_(torch.as_tensor(out["status"])); S.wcnt[o:o + n].copy_(torch.as_tensor(out["cnt"]))
+        oe, of = (S.rb - sub.a) * W, (S.re - sub.a) * W
+        S.solves[0] += int((out["cnt"][oe:of] > 0).sum())
 
     def guard_failed(self):
         return bool(self.flag)
@@ -82,12 +92,12 @@ def _free_port():
     return port
 
 
-def _worker(rank, ws, port, W, R, steps, halo, q):
+def _worker(rank, ws, port, W, R, steps, halo, q, k=1):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=ws)
     H = R * ws
-    be = OracleBackend(W, H, scenarios.LATTICE_GAIN, scenarios.T, 0.2)
-    S = ShardedLattice(W, R, seed=2, halo=halo, backend=be)
+    be = OracleBackend(W, H, scenarios.LATTICE_GAIN, scenarios.T, 0.2, k)
+    S = ShardedLattice(W, R, seed=2, halo=halo, substeps=k, backend=be)
     for _ in range(steps):
         S.step()
     S.check_guard()
@@ -96,13 +106,13 @@ def _worker(rank, ws, port, W, R, steps, halo, q):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("ws", [2, 3])
-def test_sharded_rollout_equals_single_lattice(ws):
-    W, R, steps, halo = 20, 8, 4, 4
+@pytest.mark.parametrize("ws,k", [(2, 1), (3, 1), (2, 2), (3, 3)])
+def test_sharded_rollout_equals_single_lattice(ws, k):
+    W, R, steps, halo = 20, 12, 5, 4
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, ws, port, W, R, steps, halo, q)) for r in range(ws)]
+    procs = [ctx.Process(target=_worker, args=(r, ws, port, W, R, steps, halo, q, k)) for r in range(ws)]
     for p in procs:
         p.start()
     res = sorted([q.get(timeout=300) for _ in range(ws)], key=lambda t: t[0])
@@ -129,26 +139,29 @@ def test_guard_logic():
     W, halo = 10, 4
     a = scenarios.LATTICE_SPACING
     pos = scenarios.lattice(W, 30, seed=0)
-    ext = np.stack([stripe_extents(pos[r * 10 * W:(r + 1) * 10 * W], W, halo - 1) for r in range(3)])
+    recs = np.stack([sub_extents(pos, W, 0, 10 * r, 10 * r + 10, 10 * r, 10 * r + 10, halo - 1) for r in range(3)])
     for r in range(3):
-        assert guard_ok(ext, r, 0.2)
-    bad = ext.copy()
-    bad[0, 2] = ext[1, 0] - 0.1            # rank 0's non-halo rows reach into rank 1's range
+        assert guard_ok(recs, r, 0.2)
+    bad = recs.copy()
+    bad[0, 2] = recs[1, 0] - 0.1            # rank 0's rows outside the band reach into rank 1's range
     assert not guard_ok(bad, 1, 0.2)
     assert guard_ok(bad, 2, 0.2)
-    bad = ext.copy()
-    bad[2, 0] = ext[0, 1] + 0.05           # rank 2 reaches down to rank 0
+    bad = recs.copy()
+    bad[2, 4] = recs[0, 1] + 0.05           # rank 2 reaches down to rank 0
     assert not guard_ok(bad, 0, 0.2)
+    ident = np.array([np.inf, -np.inf, -np.inf, np.inf, np.inf, -np.inf])
+    assert guard_ok(np.stack([ident, recs[1], ident]), 1, 0.2)    # unrecorded sub-steps pass
     assert a * (halo - 2) > 0.2            # default halo leaves slack for the jittered lattice
 
 
-def _worker_small_halo(rank, ws, port, q):
+def _worker_small_halo(rank, ws, port, q, k):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=ws)
     W, R = 12, 6
-    be = OracleBackend(W, R * ws, scenarios.LATTICE_GAIN, scenarios.T, 0.2)
-    S = ShardedLattice(W, R, seed=3, halo=2, backend=be)
-    S.step()
+    be = OracleBackend(W, R * ws, scenarios.LATTICE_GAIN, scenarios.T, 0.2, k)
+    S = ShardedLattice(W, R, seed=3, halo=2, substeps=k, backend=be)
+    for _ in range(k):
+        S.step()
     try:
         S.check_guard()
         q.put((rank, "ok"))
@@ -158,13 +171,14 @@ def _worker_small_halo(rank, ws, port, q):
     dist.destroy_process_group()
 
 
-def test_too_small_halo_is_caught_after_the_step():
+@pytest.mark.parametrize("k", [1, 2])
+def test_too_small_halo_is_caught_after_the_step(k):
     """halo 2 lets rows two apart (0.29 - jitter < 0.2) reach past the candidate rows: the
     guard, run at the exchange after the step, must flag it and check_guard() must raise."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker_small_halo, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker_small_halo, args=(r, 2, port, q, k)) for r in range(2)]
     for p in procs:
         p.start()
     res = sorted([q.get(timeout=300) for _ in range(2)])

@@ -1,5 +1,6 @@
 """Sharded lattice step on the HIP path: 2 and 3 ranks rehearsed on one GPU (gloo, host-staged
-exchange), compared bit-for-bit with the single-GPU step of the whole lattice."""
+exchange), with 1 and 4 sub-steps per exchange (6 steps: the last cycle is partial), compared
+bit-for-bit with the single-GPU step of the whole lattice."""
 import os
 import socket
 
@@ -24,12 +25,12 @@ def _free_port():
     return p
 
 
-def _worker(rank, ws, port, W, R, steps, q, graph=False):
+def _worker(rank, ws, port, W, R, steps, q, k=4, graph=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     torch.cuda.set_device(0)
     dist.init_process_group("gloo", rank=rank, world_size=ws)
     from cbf_amd.shard import ShardedLattice
-    S = ShardedLattice(W, R, seed=7)
+    S = ShardedLattice(W, R, seed=7, substeps=k)
     if graph:
         S.capture()
     S.reset_solves()
@@ -42,14 +43,14 @@ def _worker(rank, ws, port, W, R, steps, q, graph=False):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("ws,graph", [(2, False), (3, False), (2, True)])
-def test_sharded_equals_single_gpu(ws, graph):
+@pytest.mark.parametrize("ws,k,graph", [(2, 1, False), (3, 4, False), (2, 4, True)])
+def test_sharded_equals_single_gpu(ws, k, graph):
     from cbf_amd import scenarios, swarm
     W, R, steps = 96, 40, 6
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, ws, port, W, R, steps, q, graph)) for r in range(ws)]
+    procs = [ctx.Process(target=_worker, args=(r, ws, port, W, R, steps, q, k, graph)) for r in range(ws)]
     for p in procs:
         p.start()
     res = sorted([q.get(timeout=300) for _ in range(ws)], key=lambda t: t[0])

@@ -59,6 +59,12 @@ SETS["xcd"] = {
     "full": [],
     "noxcd": ["-DCBF_XCD_REMAP=0"],
 }
+SETS["ext"] = {
+    "block64": [],
+    "wave64": ["-DCBF_EXT_WAVE=1"],
+    "wave512": ["-DCBF_EXT_WAVE=1", "-DCBF_EXT_SLOTS=512"],
+    "block16": ["-DCBF_EXT_SLOTS=16"],
+}
 VARIANTS = {
     "full": [],
     "flush2": ["-DCBF_FLUSH_U=2"],
@@ -168,6 +174,69 @@ def run(rounds, iters, W, H):
     return res
 
 
+def run_shard(rounds, iters, W, H, k=4):
+    """The sharded step at one rank (cbf_halo_pack every k sub-steps + cbf_lattice_step_sharded),
+    per variant, against the plain cbf_lattice_step; results checked bit-for-bit."""
+    import numpy as np
+    import torch
+    from cbf_amd import _lib, scenarios, swarm
+    torch.cuda.set_device(0)
+    libs = {}
+    names = list(_variants())
+    for name in names:
+        L = C.CDLL(os.path.join(OUT, f"lib_{name}.so"))
+        for fn, (res, args) in _lib.SIGNATURES.items():
+            getattr(L, fn).restype = res
+            getattr(L, fn).argtypes = args
+        libs[name] = L
+    pos0 = scenarios.lattice(W, H, seed=0)
+    grid = swarm.grid_for_points(pos0, 0.2)
+    cp = _lib.make_params(15)
+    P = _lib.ptr
+    st = {}
+    for name, L in libs.items():
+        wsb = L.cbf_lattice_workspace_size(W, H, C.byref(grid))
+        kb = L.cbf_halo_ext_bytes(k)
+        d = dict(pos=torch.tensor(pos0, device="cuda"), vel=torch.empty((W * H, 2), dtype=torch.float64, device="cuda"),
+                 u=torch.empty((W * H, 2), dtype=torch.float64, device="cuda"),
+                 status=torch.empty(W * H, dtype=torch.int32, device="cuda"),
+                 cnt=torch.empty(W * H, dtype=torch.int32, device="cuda"),
+                 ws=torch.zeros(wsb, dtype=torch.uint8, device="cuda"), wsb=wsb,
+                 keys=torch.empty(kb // 8, dtype=torch.int64, device="cuda"),
+                 send=torch.zeros(2 * 16 * W * 2 + 8 * k, dtype=torch.float64, device="cuda"),
+                 solves=torch.zeros(1024, dtype=torch.int64, device="cuda"))
+        _lib.check(L.cbf_halo_ext_reset(P(d["keys"]), k, _lib.stream_handle()), "reset")
+        st[name] = d
+    times = {n: [] for n in names}
+    for r in range(rounds):
+        for name, L in libs.items():
+            d = st[name]
+            sw = L.cbf_halo_ext_bytes(1) // 8
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for it in range(iters):
+                s = it % k
+                if s == 0:
+                    _lib.check(L.cbf_halo_pack(W, 16, W * H, P(d["pos"]), P(d["keys"]), k, P(d["send"]),
+                                               _lib.stream_handle()), "pack")
+                _lib.check(L.cbf_lattice_step_sharded(cp, C.byref(grid), W, H, 0, H, 0, H, 0, H, P(d["pos"]), 0.25,
+                                                      1 / 30, P(d["pos"]), P(d["vel"]), P(d["u"]), P(d["status"]),
+                                                      P(d["cnt"]), 3, P(d["keys"][s * sw:]), P(d["solves"]),
+                                                      P(d["ws"]), d["wsb"], _lib.stream_handle()), "step")
+            e1.record()
+            torch.cuda.synchronize()
+            if r > 0:
+                times[name].append(e0.elapsed_time(e1) / iters)
+    res = {n: {"us_per_step": float(np.median(v)) * 1e3} for n, v in times.items()}
+    ref = names[0]
+    for n in names[1:]:
+        for f in ("pos", "u", "status", "send"):
+            res[n][f"{f}_identical"] = bool(torch.equal(st[n][f], st[ref][f]))
+        res[n]["send_ext"] = st[n]["send"][-8 * k:].view(k, 8)[:, :6].tolist()
+    res[ref]["send_ext"] = st[ref]["send"][-8 * k:].view(k, 8)[:, :6].tolist()
+    print(json.dumps(res, indent=1))
+
+
 def run_allpairs(rounds, iters, W, H):
     import numpy as np
     import torch
@@ -214,7 +283,7 @@ def run_allpairs(rounds, iters, W, H):
 
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
-    ap.add_argument("cmd", choices=["build", "run", "run_allpairs"])
+    ap.add_argument("cmd", choices=["build", "run", "run_allpairs", "run_shard"])
     ap.add_argument("--rounds", type=int, default=6)
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--W", type=int, default=1024)
@@ -225,5 +294,7 @@ if __name__ == "__main__":
         build(a.revs)
     elif a.cmd == "run_allpairs":
         run_allpairs(a.rounds, a.iters, a.W, a.H)
+    elif a.cmd == "run_shard":
+        run_shard(a.rounds, a.iters, a.W, a.H)
     else:
         run(a.rounds, a.iters, a.W, a.H)
