@@ -259,6 +259,62 @@ __global__ void __launch_bounds__(kBlock) k_lattice_scatter_ordered(long nwin, c
 }
 
 
+// Tail of the lattice filter for one owned ego whose QP rows are accumulated in E: solve at the
+// origin or queue to the hard kernel, clip, Euler, outputs.  Returns 1 (done, *ny = new y) or 2.
+template <bool FZ>
+__device__ __forceinline__ int ego_finish(const KP& P, Ego& E, int W, int row_begin, int r, int c, double T,
+                                          double2* __restrict__ pos_out, double2* __restrict__ u,
+                                          int32_t* __restrict__ status, int32_t* __restrict__ cnt,
+                                          int32_t* __restrict__ hardq, double* ny) {
+    const double2 pe = make_double2(E.r0, E.r1);
+    const long k = (long)(r - row_begin) * W + c;
+    double ux, uy;
+    int32_t st;
+    if (E.count == 0) {
+        ux = E.u0x;
+        uy = E.u0y;
+        st = CBF_STATUS_IDLE;
+    } else {
+        Sol S;
+#if CBF_ABLATE >= 1
+        S.x0 = S.x1 = 0.0;
+        S.status = CBF_STATUS_OPTIMAL;
+        S.iters = 0;
+        S.viol = E.bq0 + E.bq1 + E.bq2 + E.bq3;
+        asm volatile("" ::"v"(S.viol));
+#else
+        if (!solve_easy(P, E, S)) {
+            HardRec* q = reinterpret_cast<HardRec*>(hardq + kHardHeader);
+            HardRec& h = q[atomicAdd(&hardq[0], 1)];
+            h.r0 = E.r0;
+            h.r1 = E.r1;
+            h.r2 = E.r2;
+            h.r3 = E.r3;
+            h.u0x = E.u0x;
+            h.u0y = E.u0y;
+            h.bq0 = E.bq0;
+            h.bq1 = E.bq1;
+            h.bq2 = E.bq2;
+            h.bq3 = E.bq3;
+            h.present = (int)E.present;
+            h.count = E.count;
+            h.k = (int)k;
+            h.row = r;
+            return 2;
+        }
+#endif
+        clip_u(P, S, E, ux, uy);
+        st = pack_status(S);
+    }
+    const double2 pn = make_double2(pe.x + T * ux, pe.y + T * uy);
+    pos_out[k] = pn;
+    u[k] = make_double2(ux, uy);
+    status[k] = st;
+    if (cnt) cnt[k] = E.count;
+    *ny = pn.y;
+    return 1;
+}
+
 // Lattice step K4: filter + clip + Euler for one owned agent at cell-sorted slot `slot`.
 // QPs that the origin does not solve (after the strip pre-relaxation) are not solved here but
 // appended, with their assembled state, to the hard queue: one such lane would otherwise make
@@ -337,55 +393,8 @@ __device__ __forceinline__ int lattice_ego(const KP& P, const CellGrid& G, int W
 #endif
 #endif
     *nbrs = E.count;
-    const long k = (long)(r - row_begin) * W + c;
-    double ux, uy;
-    int32_t st;
-    if (E.count == 0) {
-        ux = E.u0x;
-        uy = E.u0y;
-        st = CBF_STATUS_IDLE;
-    } else {
-        Sol S;
-#if CBF_ABLATE >= 1
-        S.x0 = S.x1 = 0.0;
-        S.status = CBF_STATUS_OPTIMAL;
-        S.iters = 0;
-        S.viol = E.bq0 + E.bq1 + E.bq2 + E.bq3;
-        asm volatile("" ::"v"(S.viol));
-#else
-        if (!solve_easy(P, E, S)) {
-            HardRec* q = reinterpret_cast<HardRec*>(hardq + kHardHeader);
-            HardRec& h = q[atomicAdd(&hardq[0], 1)];
-            h.r0 = E.r0;
-            h.r1 = E.r1;
-            h.r2 = E.r2;
-            h.r3 = E.r3;
-            h.u0x = E.u0x;
-            h.u0y = E.u0y;
-            h.bq0 = E.bq0;
-            h.bq1 = E.bq1;
-            h.bq2 = E.bq2;
-            h.bq3 = E.bq3;
-            h.present = (int)E.present;
-            h.count = E.count;
-            h.k = (int)k;
-            h.row = r;
-            return 2;
-        }
-#endif
-        clip_u(P, S, E, ux, uy);
-        st = pack_status(S);
-    }
-    const double2 pn = make_double2(pe.x + T * ux, pe.y + T * uy);
-    pos_out[k] = pn;
-    u[k] = make_double2(ux, uy);
-    status[k] = st;
-    if (cnt) cnt[k] = E.count;
-    *ny = pn.y;
-    return 1;
+    return ego_finish<FZ>(P, E, W, row_begin, r, c, T, pos_out, u, status, cnt, hardq, ny);
 }
-
-
 
 // K4: one lane per cell-sorted slot; easy QPs solved in place, hard ones queued.
 template <bool FZ>
@@ -423,6 +432,156 @@ __global__ void __launch_bounds__(kBlock) k_lattice_filter(KP P, CellGrid G, int
                       (unsigned long long)__popcll(m));
     }
     if (ext_part) wave_extents(e0, e1, e2, e3, ext_part, (long)bx * (kBlock / 64) + (threadIdx.x >> 6));
+}
+
+// K4, LDS-staged form (CBF_LDS_STAGE): the egos of a wave are consecutive cell-sorted slots, so
+// the union of their three cell-row candidate ranges is three short contiguous slot segments
+// (~210 agents at the cfg4 density).  The wave loads that union once, coalesced, into its own
+// LDS region (positions and nominal controls), then every lane culls and assembles its own ~17
+// candidates from LDS: no per-lane gathers, no hit list, no flush.  A wave whose union exceeds
+// kStageCap (a sparse or wrapped region) takes the direct path from global memory.  Same rows,
+// same per-quadrant minima as k_lattice_filter (the minimum is order-independent).
+#ifndef CBF_LDS_STAGE
+#define CBF_LDS_STAGE 0
+#endif
+constexpr int kStageCap = 256;
+
+template <bool FZ>
+__global__ void __launch_bounds__(kBlock) k_lattice_filter_lds(KP P, CellGrid G, int W, int row_begin, int row_end,
+                                                               int win_row0, long ncell,
+                                                               const double2* __restrict__ spos,
+                                                               const double2* __restrict__ svel,
+                                                               const int32_t* __restrict__ sidx,
+                                                               const int32_t* __restrict__ start, double T,
+                                                               double2* __restrict__ pos_out, double2* __restrict__ u,
+                                                               int32_t* __restrict__ status, int32_t* __restrict__ cnt,
+                                                               unsigned long long* __restrict__ solves,
+                                                               int32_t* __restrict__ hardq, int cnt_begin,
+                                                               int cnt_end) {
+    __shared__ double2 st_pos[kBlock / 64][kStageCap];
+    __shared__ double2 st_vel[kBlock / 64][kStageCap];
+    const int bx = xcd_block();
+    const int slot = bx * kBlock + threadIdx.x;
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int total = start[ncell];
+    bool act = false;
+    int r = 0, c = 0;
+    Ego E;
+    int rt0[3] = {0, 0, 0}, rt1[3] = {0, 0, 0};
+    if (slot < total) {
+        const int w = sidx[slot];
+        r = win_row0 + w / W;
+        c = w % W;
+        if (r >= row_begin && r < row_end) {
+            act = true;
+            const double2 pe = spos[slot], ve = svel[slot];
+            ego_init(P, E, pe.x, pe.y, ve.x, ve.y, ve.x, ve.y);
+            const int cx = cell_coord(pe.x, G.x0, G.inv_h, G.nx);
+            const int cy = cell_coord(pe.y, G.y0, G.inv_h, G.ny);
+            const int xa = cx > 0 ? cx - 1 : 0;
+            const int xb = cx < G.nx - 1 ? cx + 1 : G.nx - 1;
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+                const int yy = cy + k - 1;
+                if (yy >= 0 && yy < G.ny) {
+                    rt0[k] = start[yy * G.nx + xa];
+                    rt1[k] = start[yy * G.nx + xb + 1];
+                }
+            }
+        }
+    }
+    // wave union of the three row ranges
+    int lo[3], len[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const bool ne = act && rt1[k] > rt0[k];
+        int a = ne ? rt0[k] : 0x7FFFFFFF, b = ne ? rt1[k] : -1;
+        for (int o = 32; o > 0; o >>= 1) {
+            const int a2 = __shfl_xor(a, o, 64), b2 = __shfl_xor(b, o, 64);
+            a = a2 < a ? a2 : a;
+            b = b2 > b ? b2 : b;
+        }
+        lo[k] = a;
+        len[k] = b > a ? b - a : 0;
+    }
+    const int off1 = len[0], off2 = len[0] + len[1], L = off2 + len[2];
+    if (L <= kStageCap) {
+#pragma unroll
+        for (int j = 0; j < kStageCap / 64; ++j) {
+            const int i = lane + 64 * j;
+            if (i < L) {
+                const int g = i >= off2 ? lo[2] + (i - off2) : (i >= off1 ? lo[1] + (i - off1) : lo[0] + i);
+                st_pos[wid][i] = spos[g];
+                st_vel[wid][i] = svel[g];
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        if (act) {
+#if CBF_LDS_STAGE == 2
+            // pass 1: cull test only, hits as a bit mask per row range; pass 2: assembly per hit
+            // (the wave iterates max-hits times instead of max-candidates times)
+            unsigned m[3] = {0u, 0u, 0u};
+            bool wide = false;
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+                const int base = (k == 0 ? 0 : (k == 1 ? off1 : off2)) - lo[k];
+                wide = wide || rt1[k] - rt0[k] > 32;
+                const int te = rt1[k] - rt0[k] > 32 ? rt0[k] + 32 : rt1[k];
+                for (int t = rt0[k]; t < te; ++t) {
+                    const double2 pj = st_pos[wid][base + t];
+                    const double e0 = pj.x - E.r0, e1 = pj.y - E.r1;
+                    const double s = e0 * e0 + e1 * e1;
+                    if (s < P.cull_t && s > 0) m[k] |= 1u << (t - rt0[k]);
+                }
+            }
+            if (!wide) {
+#pragma unroll
+                for (int k = 0; k < 3; ++k) {
+                    const int base = (k == 0 ? 0 : (k == 1 ? off1 : off2)) - lo[k] + rt0[k];
+                    while (m[k]) {
+                        const int b = __ffs((int)m[k]) - 1;
+                        m[k] &= m[k] - 1u;
+                        const double2 pj = st_pos[wid][base + b];
+                        const double2 vj = st_vel[wid][base + b];
+                        ego_add<FZ>(P, E, pj.x, pj.y, vj.x, vj.y);
+                    }
+                }
+            } else {
+#pragma unroll
+                for (int k = 0; k < 3; ++k) scan_range_direct<FZ>(rt0[k], rt1[k], P, E, spos, svel);
+            }
+#else
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+                const int base = (k == 0 ? 0 : (k == 1 ? off1 : off2)) - lo[k];
+                for (int t = rt0[k]; t < rt1[k]; ++t) {
+                    const double2 pj = st_pos[wid][base + t];
+                    const double e0 = pj.x - E.r0, e1 = pj.y - E.r1;
+                    const double s = e0 * e0 + e1 * e1;
+                    if (!(s < P.cull_t && s > 0)) continue;
+                    const double2 vj = st_vel[wid][base + t];
+                    ego_add<FZ>(P, E, pj.x, pj.y, vj.x, vj.y);
+                }
+            }
+#endif
+        }
+    } else if (act) {
+#pragma unroll
+        for (int k = 0; k < 3; ++k) scan_range_direct<FZ>(rt0[k], rt1[k], P, E, spos, svel);
+    }
+    bool solved = false;
+    if (act) {
+        double ny;
+        const int res = ego_finish<FZ>(P, E, W, row_begin, r, c, T, pos_out, u, status, cnt, hardq, &ny);
+        solved = res != 0 && E.count > 0 && r >= cnt_begin && r < cnt_end;
+    }
+    if (solves) {
+        const unsigned long long m = __ballot(solved);
+        if (lane == 0 && m)
+            atomicAdd(&solves[16 * ((bx * (kBlock / 64) + wid) & 63)], (unsigned long long)__popcll(m));
+    }
 }
 
 // K5: the queued hard QPs (state assembled by K4), 64-lane blocks spread over the CUs.
@@ -647,10 +806,17 @@ static int lattice_advance(const cbf_params* p, const cbf_grid* grid, int32_t W,
     const KP kp = make_kp(p);
     double2* po = reinterpret_cast<double2*>(pos_out);
     double2* uo = reinterpret_cast<double2*>(u);
-    hipLaunchKernelGGL(p->f_is_zero ? k_lattice_filter<true> : k_lattice_filter<false>, dim3(nb), dim3(kBlock), 0, s,
-                       kp, G, W, row_begin, row_end, win_row0, Wk.ncell, Wk.spos, Wk.svel, Wk.sidx, Wk.start, T, po, uo,
-                       status, nbr_count, guard_rows, ext_part, reinterpret_cast<unsigned long long*>(solves),
-                       Wk.hardq, Wk.spos32, cnt_begin, cnt_end);
+    if (CBF_LDS_STAGE && !ext_part) {
+        hipLaunchKernelGGL(p->f_is_zero ? k_lattice_filter_lds<true> : k_lattice_filter_lds<false>, dim3(nb),
+                           dim3(kBlock), 0, s, kp, G, W, row_begin, row_end, win_row0, Wk.ncell, Wk.spos, Wk.svel,
+                           Wk.sidx, Wk.start, T, po, uo, status, nbr_count,
+                           reinterpret_cast<unsigned long long*>(solves), Wk.hardq, cnt_begin, cnt_end);
+    } else {
+        hipLaunchKernelGGL(p->f_is_zero ? k_lattice_filter<true> : k_lattice_filter<false>, dim3(nb), dim3(kBlock), 0,
+                           s, kp, G, W, row_begin, row_end, win_row0, Wk.ncell, Wk.spos, Wk.svel, Wk.sidx, Wk.start, T,
+                           po, uo, status, nbr_count, guard_rows, ext_part,
+                           reinterpret_cast<unsigned long long*>(solves), Wk.hardq, Wk.spos32, cnt_begin, cnt_end);
+    }
     hipLaunchKernelGGL(k_lattice_filter_hard, dim3(hb), dim3(64), 0, s, kp, row_begin, row_end, T, po, uo, status,
                        nbr_count, guard_rows, ext_part ? ext_part + 4l * lattice_ext_waves(n) : nullptr, Wk.hardq);
     if (extents) launch_extents_finalize((int)lattice_ext_waves(n) + hb, ext_part, extents, s);

@@ -59,6 +59,11 @@ SETS["xcd"] = {
     "full": [],
     "noxcd": ["-DCBF_XCD_REMAP=0"],
 }
+SETS["stage"] = {
+    "full": [],
+    "stage": ["-DCBF_LDS_STAGE=1"],
+    "stage2": ["-DCBF_LDS_STAGE=2"],
+}
 SETS["ext"] = {
     "block64": [],
     "wave64": ["-DCBF_EXT_WAVE=1"],
