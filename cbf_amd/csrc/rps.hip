@@ -86,7 +86,8 @@ __global__ void __launch_bounds__(64) k_si_barrier_cert(CertArgs C, int N, const
     double* xp = brow + m;       // [n] agent positions (x-major per agent)
     double* xv = xp + n;         // [n] current iterate
     double* dv = xv + n;         // [n] d = J' n+
-    int2* rij = reinterpret_cast<int2*>(dv + n);  // [m]
+    double* rid = dv + n;        // [n] 1 / R[j][j]
+    int2* rij = reinterpret_cast<int2*>(rid + n);  // [m]
     int* isact = reinterpret_cast<int*>(rij + m);  // [m]
 
     // inputs; magnitude threshold of rps (norms > magnitude_limit -> scaled onto the limit)
@@ -188,13 +189,26 @@ __global__ void __launch_bounds__(64) k_si_barrier_cert(CertArgs C, int N, const
             }
             __syncthreads();
             // z = J[:, q:] d[q:] (lane = row)
+            // (four partial sums: the LDS loads of consecutive columns overlap)
             double zl = 0.0;
-            if (lane < n)
-                for (int c = q; c < n; ++c) zl += J[lane * ld + c] * dv[c];
-            // r = R^-1 d[:q], column-oriented back substitution (lane j ends with r_j)
+            if (lane < n) {
+                double z0 = 0.0, z1 = 0.0, z2 = 0.0, z3 = 0.0;
+                const double* Jr = J + lane * ld;
+                int c = q;
+                for (; c + 4 <= n; c += 4) {
+                    z0 += Jr[c] * dv[c];
+                    z1 += Jr[c + 1] * dv[c + 1];
+                    z2 += Jr[c + 2] * dv[c + 2];
+                    z3 += Jr[c + 3] * dv[c + 3];
+                }
+                for (; c < n; ++c) z0 += Jr[c] * dv[c];
+                zl = (z0 + z1) + (z2 + z3);
+            }
+            // r = R^-1 d[:q], column-oriented back substitution (lane j ends with r_j); rid holds
+            // the reciprocals of R's diagonal
             double rl = lane < q ? dl : 0.0;
             for (int j = q - 1; j >= 0; --j) {
-                const double rj = __shfl(rl, j, 64) / R[j * ld + j];
+                const double rj = __shfl(rl, j, 64) * rid[j];
                 if (lane == j) rl = rj;
                 else if (lane < j) rl -= R[lane * ld + j] * rj;
             }
@@ -223,26 +237,32 @@ __global__ void __launch_bounds__(64) k_si_barrier_cert(CertArgs C, int N, const
             if (lane < q) ul -= t * rl;
             up += t;
             if (full) {
-                // add p: rotate d[q:] onto e_q bottom-up, the same rotations on J's columns
-                double carry = __shfl(dl, n - 1, 64);
-                for (int j = n - 1; j > q; --j) {
-                    const double a = __shfl(dl, j - 1, 64);
-                    if (carry != 0.0) {
-                        const double h = hypot(a, carry);
-                        const double cs = a / h, sn = carry / h;
-                        if (lane < n) {
-                            const double Ja = J[lane * ld + j - 1], Jb = J[lane * ld + j];
-                            J[lane * ld + j - 1] = cs * Ja + sn * Jb;
-                            J[lane * ld + j] = -sn * Ja + cs * Jb;
-                        }
-                        carry = h;
-                    } else {
-                        carry = a;
+                // add p: one Householder reflection H = I - v v' / (sg vq) maps d[q:] onto
+                // -sg e_q (v = d[q:] + sg e_q, sg = |d[q:]| with the sign of d_q); J[:, q:] <- J[:, q:] H,
+                // lane-parallel over J's rows
+                const double dq = __shfl(dl, q, 64);
+                const double sg = copysign(sqrt(zn), dq);
+                const double vq = dq + sg;
+                const double beta = 1.0 / (sg * vq);
+                if (lane < n) {
+                    double* Jr = J + lane * ld;
+                    double a0 = Jr[q] * vq, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+                    int c = q + 1;
+                    for (; c + 3 <= n; c += 3) {
+                        a1 += Jr[c] * dv[c];
+                        a2 += Jr[c + 1] * dv[c + 1];
+                        a3 += Jr[c + 2] * dv[c + 2];
                     }
+                    for (; c < n; ++c) a1 += Jr[c] * dv[c];
+                    const double f = beta * ((a0 + a1) + (a2 + a3));
+                    Jr[q] -= f * vq;
+                    for (c = q + 1; c < n; ++c) Jr[c] -= f * dv[c];
                 }
+                const double carry = -sg;
                 if (lane < q) R[lane * ld + q] = dl;
                 if (lane == q) {
                     R[q * ld + q] = carry;
+                    rid[q] = 1.0 / carry;
                     ul = up;
                     actl = p;
                     isact[p] = 1;
@@ -258,6 +278,8 @@ __global__ void __launch_bounds__(64) k_si_barrier_cert(CertArgs C, int N, const
                 R[lane * ld + q - 1] = 0.0;
             }
             __syncthreads();
+            if (lane >= kk && lane < q - 1) rid[lane] = 1.0 / R[lane * ld + lane];  // shifted diagonal
+            __syncthreads();
             for (int j = kk; j < q - 1; ++j) {
                 const double a = R[j * ld + j], b = R[(j + 1) * ld + j];
                 const double h = hypot(a, b);
@@ -266,8 +288,10 @@ __global__ void __launch_bounds__(64) k_si_barrier_cert(CertArgs C, int N, const
                     const double cs = a / h, sn = b / h;
                     if (lane >= j && lane < q - 1) {
                         const double Ra = R[j * ld + lane], Rb = R[(j + 1) * ld + lane];
-                        R[j * ld + lane] = cs * Ra + sn * Rb;
+                        const double Rn = cs * Ra + sn * Rb;
+                        R[j * ld + lane] = Rn;
                         R[(j + 1) * ld + lane] = lane == j ? 0.0 : -sn * Ra + cs * Rb;
+                        if (lane == j) rid[j] = 1.0 / Rn;
                     }
                     if (lane < n) {
                         const double Ja = J[lane * ld + j], Jb = J[lane * ld + j + 1];
@@ -383,7 +407,7 @@ extern "C" int cbf_cert_params_init(cbf_cert_params* c, double barrier_gain, dou
 extern "C" size_t cbf_si_barrier_cert_lds_bytes(int32_t n_agents) {
     if (n_agents < 1 || n_agents > kCertMaxAgents) return 0;
     const size_t n = 2 * (size_t)n_agents, m = (size_t)n_agents * (n_agents - 1) / 2 + 4 * (size_t)n_agents;
-    return 8 * (2 * n * (n + 1) + m + 3 * n) + 8 * m + 4 * m;
+    return 8 * (2 * n * (n + 1) + m + 4 * n) + 8 * m + 4 * m;
 }
 
 extern "C" int cbf_si_barrier_cert(const cbf_cert_params* c, int32_t batch, int32_t n_agents, const double* dxi,
