@@ -132,6 +132,10 @@ __device__ __forceinline__ void ap_exact(const KP& P, Ego& E, const double2* sp,
 #ifndef CBF_AP_SCREEN
 #define CBF_AP_SCREEN 8   // candidates per screen step
 #endif
+#ifndef CBF_AP_PACKED
+#define CBF_AP_PACKED 0   // packed-fp32 screen (tools/ablate.py times it)
+#endif
+typedef float pf2 __attribute__((ext_vector_type(2)));
 
 // The all-pairs candidate loop of one ego over entities [c0, c1): tiles of CBF_AP_TILE entities
 // staged in LDS (fp64 state plus an fp32 copy of the positions) and read by broadcast (every
@@ -141,7 +145,12 @@ __device__ __forceinline__ void ap_exact(const KP& P, Ego& E, const double2* sp,
 struct ApLds {
     double2 sp[CBF_AP_TILE];
     double2 sv[CBF_AP_TILE];
+#if CBF_AP_PACKED
+    float xs32[CBF_AP_TILE];  // fp32 copies, SoA: 4 consecutive candidates per 16-B LDS read
+    float ys32[CBF_AP_TILE];
+#else
     float2 sp32[CBF_AP_TILE];
+#endif
     double smax[kBlock / 64];
 };
 
@@ -165,7 +174,12 @@ __device__ __forceinline__ void allpairs_scan(const KP& P, double r0, double r1,
                 const double2 pj = pos[j];
                 L.sp[tl] = pj;
                 L.sv[tl] = vel[j];
+#if CBF_AP_PACKED
+                L.xs32[tl] = (float)pj.x;
+                L.ys32[tl] = (float)pj.y;
+#else
                 L.sp32[tl] = make_float2((float)pj.x, (float)pj.y);
+#endif
                 double a = absmax2(pj);
                 if (a != a) a = INFINITY;  // NaN coordinate: screen off for this tile
                 mj = pmax(mj, a);
@@ -184,6 +198,27 @@ __device__ __forceinline__ void allpairs_scan(const KP& P, double r0, double r1,
             if (t32 > 0.0f) {
                 for (; t + kScreen <= m; t += kScreen) {
                     float sq[kScreen];
+#if CBF_AP_PACKED
+                    // two candidates per packed fp32 op (v_pk_add / v_pk_mul / v_pk_fma): same
+                    // arithmetic per candidate as the scalar form, fma(d0, d0, d1 * d1)
+                    const pf2 e2x = {ex, ex}, e2y = {ey, ey};
+                    pf2 mn2 = {INFINITY, INFINITY};
+#pragma unroll
+                    for (int q = 0; q < kScreen; q += 4) {
+                        const float4 X = *reinterpret_cast<const float4*>(&L.xs32[t + q]);
+                        const float4 Y = *reinterpret_cast<const float4*>(&L.ys32[t + q]);
+                        const pf2 dxa = pf2{X.x, X.y} - e2x, dxb = pf2{X.z, X.w} - e2x;
+                        const pf2 dya = pf2{Y.x, Y.y} - e2y, dyb = pf2{Y.z, Y.w} - e2y;
+                        const pf2 sa = __builtin_elementwise_fma(dxa, dxa, dya * dya);
+                        const pf2 sb = __builtin_elementwise_fma(dxb, dxb, dyb * dyb);
+                        sq[q] = sa.x;
+                        sq[q + 1] = sa.y;
+                        sq[q + 2] = sb.x;
+                        sq[q + 3] = sb.y;
+                        mn2 = __builtin_elementwise_min(mn2, __builtin_elementwise_min(sa, sb));
+                    }
+                    const float mn = fminf(mn2.x, mn2.y);
+#else
 #pragma unroll
                     for (int q = 0; q < kScreen; ++q) {
                         const float2 c = L.sp32[t + q];
@@ -193,6 +228,7 @@ __device__ __forceinline__ void allpairs_scan(const KP& P, double r0, double r1,
                     float mn = sq[0];
 #pragma unroll
                     for (int q = 1; q < kScreen; ++q) mn = fminf(mn, sq[q]);
+#endif
                     if (mn < t32) {
 #pragma unroll
                         for (int q = 0; q < kScreen; ++q)

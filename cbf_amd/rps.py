@@ -211,6 +211,62 @@ class CrossAndRescue:
         return self.last
 
 
+class MeetAtCenter:
+    """meet_at_center.py:24-153 as shipped, device-resident: N unicycle robots (default 10), the
+    first N/2 in cyclic pursuit on the projection points (ring, rotation -pi/(N/2)), the rest in
+    complete-graph consensus (x gain; the script has gain 1); the CBF filter of every free robot
+    against all obstacle robots and the other free robots (raw poses, Jacobi); si_to_uni_dyn ->
+    set_velocities -> unicycle step for every robot.  The certificate is commented out in the
+    script (:109) and is not applied."""
+
+    def __init__(self, N=10, params: FilterParams = None, gain=1.0, wheel_threshold=True):
+        torch = _lib.require_gpu()
+        dev = torch.device("cuda")
+        if N < 4 or N % 2:
+            raise ValueError("N must be even and >= 4")
+        self.N, self.half, self.dev = N, N // 2, dev
+        self.params = params or FilterParams()
+        self.cp = self.params.c()
+        self.u = unicycle_params(wheel_threshold=wheel_threshold)
+        self.poses = torch.tensor(np.ascontiguousarray(_meet_at_center_initial(N).T), device=dev)   # (N, 3)
+        h = self.half
+        th = -np.pi / h
+        self.rot = (float(np.cos(th)), float(np.sin(th)))
+        self.ring = csr_from_rows([[(i + 1) % h] for i in range(h)], dev)                            # L1, :65-71
+        self.full = csr_from_rows([[j for j in range(h) if j != i] for i in range(h)], dev)          # completeGL, :74
+        self.gain = float(gain)
+        self.vel = torch.zeros((N, 2), dtype=torch.float64, device=dev)
+        self.last = None
+
+    def step(self):
+        h = self.half
+        x_si = uni_to_si(self.u, self.poses)                                                        # :80
+        consensus_csr(x_si[:h], *self.ring, 0, None, self.rot, 1.0, out=self.vel[:h])               # :86-96
+        consensus_csr(x_si[h:], *self.full, 0, None, None, self.gain, out=self.vel[h:])             # :99-103
+        nominal = self.vel.clone()
+        f = filter_swarm(self.cp, self.poses[:, :2].contiguous(), self.vel, h, method="allpairs")  # :114-143
+        self.vel[h:] = f["u"]
+        dxu = unicycle_advance(self.u, self.poses, self.vel)                                        # :148-153
+        self.last = {"nominal": nominal, "filtered": self.vel.clone(), "status": f["status"],
+                     "nbr_count": f["nbr_count"], "x_si": x_si}
+        return self.last
+
+
+def _meet_at_center_initial(N):
+    """meet_at_center.py:37-48: (3, N) poses (N/2 on radius 0.7, N/2 on radius 1.05)."""
+    half = N // 2
+    ic = np.zeros((N, 3))
+    diameter = 0.7
+    for i in range(half):
+        th = i * (2 * np.pi / half)
+        ic[i] = np.array([0, 0, 0]) + [diameter * np.cos(th), diameter * np.sin(th), th + (2 / 3 * np.pi)]
+    for i in range(half, N):
+        th = i * (2 * np.pi / half) + np.pi / 5
+        ic[i] = np.array([0, 0, 0]) + [1.5 * diameter * np.cos(th), 1.5 * diameter * np.sin(th),
+                                       th + (2 / 3 * np.pi)]
+    return ic.T.copy()
+
+
 def _cross_and_rescue_initial():
     """cross_and_rescue.py:36-57: robot poses (4, 3) and obstacle positions (6, 2)."""
     N_robots, N_obs, diameter = 4, 6, 0.6

@@ -346,3 +346,52 @@ def cross_and_rescue_step(poses, obs_pos, params, T=1 / 30, safety_radius=0.12):
     rec = dict(nominal=nominal, filtered=filtered, status=status, cnt=cnt, cert=si_velocities, dxu=dxu,
                cert_status=info["status"])
     return poses_next, obs_next, rec
+
+
+# ------------------------------------------------------------------------------------------
+# meet_at_center.py as shipped: N unicycle robots (half pursuit obstacles), no certificate
+# ------------------------------------------------------------------------------------------
+def meet_at_center_initial(N=10):
+    """meet_at_center.py:37-48 (written for N = 10: 5 obstacles on radius 0.7, 5 agents on 1.05)."""
+    half = N // 2
+    ic = np.zeros((N, 3))
+    diameter = 0.7
+    for i in range(half):
+        th = i * (2 * np.pi / half)
+        ic[i] = np.array([0, 0, 0]) + [diameter * np.cos(th), diameter * np.sin(th), th + (2 / 3 * np.pi)]
+    for i in range(half, N):
+        th = i * (2 * np.pi / half) + np.pi / 5
+        ic[i] = np.array([0, 0, 0]) + [1.5 * diameter * np.cos(th), 1.5 * diameter * np.sin(th),
+                                       th + (2 / 3 * np.pi)]
+    return ic.T.copy()
+
+
+def meet_at_center_step(poses, params, gain=1.0):
+    """One iteration of meet_at_center.py:76-153 with rps-lite: cyclic pursuit of the first N/2
+    robots on the projection points (L1 ring, rotation -pi/(N/2)), complete-graph consensus of
+    the rest (x gain; the script has gain 1), the CBF filter of every free robot against all
+    obstacle robots and the other free robots (raw poses, Jacobi), si_to_uni_dyn ->
+    set_velocities -> unicycle step for every robot (the certificate is commented out, :109)."""
+    from . import pyoracle as po
+    N = poses.shape[1]
+    half = N // 2
+    x = poses
+    x_si = uni_to_si_states(x)                                                   # :80
+    si_velocities = np.zeros((2, N))
+    theta = -np.pi / half
+    rotation = np.array([[np.cos(theta), np.sin(theta)], [-np.sin(theta), np.cos(theta)]])
+    for i in range(half):                                                        # :86-96
+        j = [(i + 1) % half]
+        si_velocities[:, i] = np.sum(x_si[:, j] - x_si[:, i, None], 1) @ rotation
+    for i in range(half, N):                                                     # :99-103
+        j = [q for q in range(half, N) if q != i]
+        v = np.sum(x_si[:, j] - x_si[:, i, None], 1)
+        si_velocities[:, i] = v if gain == 1.0 else v * gain
+    nominal = si_velocities.copy()
+    states = np.concatenate((x[:2, :], si_velocities), axis=0).transpose()      # :114
+    u, status, cnt, _ = po.filter_swarm(params, states[:, :2], states[:, 2:], half, half, N)  # :117-143
+    si_velocities[:, half:] = u.T
+    dxu = si_to_uni_dyn(si_velocities, x)                                        # :148
+    dxu = set_velocities(dxu)                                                    # :151
+    poses_next = unicycle_step(x, dxu)                                           # :153
+    return poses_next, dict(nominal=nominal, filtered=si_velocities.copy(), status=status, cnt=cnt, dxu=dxu)

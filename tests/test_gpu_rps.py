@@ -136,3 +136,25 @@ def test_cross_and_rescue_shipped_free_run():
     got = sim.poses.cpu().numpy().T
     assert np.abs(got[:2] - poses[:2]).max() <= 1e-6
     assert np.all(np.abs(got[0]) <= 1.6) and np.all(np.abs(got[1]) <= 1.0)
+
+
+def test_meet_at_center_shipped_teacher_forced():
+    """meet_at_center.py as shipped (10 unicycle robots, no certificate), per-step outputs from the
+    oracle's state of that step: filter decisions identical, values to rounding, 300 steps."""
+    p = po.Params(15)
+    sim = rps.MeetAtCenter()
+    poses = R.meet_at_center_initial(10)
+    filtered = 0
+    for k in range(300):
+        sim.poses.copy_(_t(poses.T))
+        g = sim.step()
+        poses_n, rec = R.meet_at_center_step(poses, p)
+        assert np.array_equal(g["nbr_count"].cpu().numpy(), rec["cnt"]), k
+        assert np.array_equal(g["status"].cpu().numpy() & 0xFF, rec["status"] & 0xFF), k
+        e = max(np.abs(g["nominal"].cpu().numpy().T - rec["nominal"]).max(),
+                np.abs(g["filtered"].cpu().numpy().T - rec["filtered"]).max(),
+                np.abs(sim.poses.cpu().numpy().T[:2] - poses_n[:2]).max())
+        assert e <= 1e-9, (k, e)
+        filtered += int((rec["cnt"] > 0).sum())
+        poses = poses_n
+    assert filtered > 0          # the filter did run during the rollout

@@ -125,3 +125,15 @@ def test_cross_and_rescue_shipped_rollout_is_safe_and_bounded():
         assert np.all(np.abs(poses[0]) <= 1.6) and np.all(np.abs(poses[1]) <= 1.0)
     # the robots moved toward the goal at (1.5, 0)
     assert poses[0].mean() > -1.15
+
+
+def test_meet_at_center_shipped_rollout_runs():
+    from oracle import pyoracle as po
+    p = po.Params(15)
+    poses = R.meet_at_center_initial(10)
+    ran = 0
+    for _ in range(200):
+        poses, rec = R.meet_at_center_step(poses, p)
+        ran += int((rec["cnt"] > 0).sum())
+        assert np.all(np.isfinite(poses)) and np.all(np.abs(poses[2]) <= np.pi)
+    assert ran > 0

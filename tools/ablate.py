@@ -20,12 +20,11 @@ OUT = os.path.join(ROOT, "tools", "_ablate")
 SETS = {}
 SETS["allpairs"] = {
     "ap_base": [],
-    "ap_w5": ["-DCBF_AP_WAVES=5"],
-    "ap_w8": ["-DCBF_AP_WAVES=8"],
-    "ap_t1024": ["-DCBF_AP_TILE=1024"],
-    "ap_t1024_w5": ["-DCBF_AP_TILE=1024", "-DCBF_AP_WAVES=5"],
-    "ap_s16_t1024_w5": ["-DCBF_AP_SCREEN=16", "-DCBF_AP_TILE=1024", "-DCBF_AP_WAVES=5"],
-    "ap_s16_t512_w8": ["-DCBF_AP_SCREEN=16", "-DCBF_AP_TILE=512", "-DCBF_AP_WAVES=8"],
+    "ap_packed": ["-DCBF_AP_PACKED=1"],
+    "ap_packed_s16": ["-DCBF_AP_PACKED=1", "-DCBF_AP_SCREEN=16"],
+    "ap_packed_s16_t1024": ["-DCBF_AP_PACKED=1", "-DCBF_AP_SCREEN=16", "-DCBF_AP_TILE=1024"],
+    "ap_packed_s32_t1024": ["-DCBF_AP_PACKED=1", "-DCBF_AP_SCREEN=32", "-DCBF_AP_TILE=1024"],
+    "ap_s16_t1024": ["-DCBF_AP_SCREEN=16", "-DCBF_AP_TILE=1024"],
 }
 SETS["phases"] = {
     "full": [],
@@ -262,6 +261,8 @@ def run_allpairs(rounds, iters, W, H):
     st = torch.empty(n, dtype=torch.int32, device="cuda")
     cp = _lib.make_params(15)
     P = _lib.ptr
+    ws = {name: torch.empty(L.cbf_allpairs_workspace_size(n, n), dtype=torch.uint8, device="cuda")
+          for name, L in libs.items()}
     ref = None
     times = {k: [] for k in names}
     for r in range(rounds):
@@ -269,8 +270,9 @@ def run_allpairs(rounds, iters, W, H):
             for _ in range(iters):
                 a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 a.record()
-                _lib.check(L.cbf_filter_allpairs(cp, n, 0, P(pos), P(vel), 0, n, P(u), P(st), None, None,
-                                                 _lib.stream_handle()), "allpairs")
+                _lib.check(L.cbf_filter_allpairs_split(cp, n, 0, P(pos), P(vel), 0, n, P(u), P(st), None,
+                                                       P(ws[name]), ws[name].numel(), _lib.stream_handle()),
+                           "allpairs_split")
                 b.record()
                 torch.cuda.synchronize()
                 if r > 0:
