@@ -8,6 +8,14 @@
 
 using namespace cbf;
 
+// tools/ablate.py switches: fp32 cull screen, solve_easy fast path
+#ifndef CBF_MC_SCREEN
+#define CBF_MC_SCREEN 0
+#endif
+#ifndef CBF_MC_EASY
+#define CBF_MC_EASY 0
+#endif
+
 namespace {
 
 template <bool FZ>
@@ -26,8 +34,14 @@ __global__ void __launch_bounds__(kBlock) k_mc_rollout(KP P, int n_scen, int n_o
     const bool valid = ls < S && scen < n_scen;
     double2* sp = lds + (valid ? ls : 0) * stride;
     double2* sv = lds + S * stride + (valid ? ls : 0) * stride;
+    // fp32 copies of the positions for the cull screen, after the counter-reduction area
+    float2* sp32 = reinterpret_cast<float2*>(lds + 2 * S * stride + kBlock * 3) + (valid ? ls : 0) * stride;
     if (valid)
-        for (int i = k; i < n; i += tps) sp[i] = pos[(long)scen * n + i];
+        for (int i = k; i < n; i += tps) {
+            const double2 p = pos[(long)scen * n + i];
+            sp[i] = p;
+            sp32[i] = make_float2((float)p.x, (float)p.y);
+        }
     __syncthreads();
     long long c_calls = 0, c_relax = 0, c_box = 0, c_cap = 0;
     double mv = 0.0;
@@ -57,8 +71,26 @@ __global__ void __launch_bounds__(kBlock) k_mc_rollout(KP P, int n_scen, int n_o
             const double2 pe = sp[n_o + k], ve = sv[n_o + k];
             Ego E;
             ego_init(P, E, pe.x, pe.y, ve.x, ve.y, ve.x, ve.y);
-            // cull pass with hits compacted into a per-lane LDS list, then assembly over hits only
+            // cull pass: an fp32 screen (conservative: screen_threshold) over the fp32 copies,
+            // candidates it lets through compacted into a per-lane LDS list, then the exact fp64
+            // cull test + assembly over those only
             int nh = 0;
+#if CBF_MC_SCREEN
+            const float t32 = screen_threshold(P.cull_t, pmax(fabs(E.r0), fabs(E.r1)) + sqrt(P.cull_t));
+            if (t32 > 0.0f) {
+                const float ex = (float)E.r0, ey = (float)E.r1;
+                for (int j = 0; j < n; ++j) {
+                    const float2 c = sp32[j];
+                    const float d0 = c.x - ex, d1 = c.y - ey;
+                    if (__builtin_fmaf(d0, d0, d1 * d1) < t32) {
+                        if (nh < kHitCap) hit_lds[nh * kBlock + threadIdx.x] = j;
+                        ++nh;
+                    }
+                }
+            } else {
+                nh = kHitCap + 1;  // screen off (non-finite or huge coordinates): the direct path
+            }
+#else
             for (int j = 0; j < n; ++j) {
                 const double2 pj = sp[j];
                 double s;
@@ -67,10 +99,16 @@ __global__ void __launch_bounds__(kBlock) k_mc_rollout(KP P, int n_scen, int n_o
                     ++nh;
                 }
             }
+#endif
             if (nh <= kHitCap) {
                 for (int i = 0; i < nh; ++i) {
                     const int j = hit_lds[i * kBlock + threadIdx.x];
-                    const double2 pj = sp[j], vj = sv[j];
+                    const double2 pj = sp[j];
+#if CBF_MC_SCREEN
+                    double s;
+                    if (!cull_keep(P, E.r0, E.r1, pj.x, pj.y, j < n_o, s)) continue;
+#endif
+                    const double2 vj = sv[j];
                     ego_add<FZ>(P, E, pj.x, pj.y, vj.x, vj.y);
                 }
             } else {
@@ -87,7 +125,12 @@ __global__ void __launch_bounds__(kBlock) k_mc_rollout(KP P, int n_scen, int n_o
                 ux = E.u0x;
                 uy = E.u0y;
             } else {
+#if CBF_MC_EASY
+                Sol Sl;
+                if (!solve_easy(P, E, Sl)) Sl = solve_ego(P, E);  // bit-identical on the easy path
+#else
                 const Sol Sl = solve_ego(P, E);
+#endif
                 clip_u(P, Sl, E, ux, uy);
                 c_calls++;
                 if (Sl.status == CBF_STATUS_RELAXED) c_relax++;
@@ -100,11 +143,15 @@ __global__ void __launch_bounds__(kBlock) k_mc_rollout(KP P, int n_scen, int n_o
         if (valid) {
             if (k < n_o) {
                 const double2 p = sp[k], v = sv[k];
-                sp[k] = make_double2(p.x + T * v.x, p.y + T * v.y);
+                const double2 q = make_double2(p.x + T * v.x, p.y + T * v.y);
+                sp[k] = q;
+                sp32[k] = make_float2((float)q.x, (float)q.y);
             }
             if (k < n_a) {
                 const double2 p = sp[n_o + k];
-                sp[n_o + k] = make_double2(p.x + T * ux, p.y + T * uy);
+                const double2 q = make_double2(p.x + T * ux, p.y + T * uy);
+                sp[n_o + k] = q;
+                sp32[n_o + k] = make_float2((float)q.x, (float)q.y);
             }
         }
         __syncthreads();
@@ -150,7 +197,8 @@ extern "C" int cbf_mc_rollout(const cbf_params* p, int32_t n_scen, int32_t n_o, 
     const int tps = n_o > n_a ? n_o : n_a;
     const int S = kBlock / tps;
     const int stride = n_o + n_a + 1;
-    const size_t lds = sizeof(double2) * 2 * S * stride + (sizeof(long long) * 4 + sizeof(double)) * kBlock;
+    // [positions | velocities | counter reduction (3 double2 per thread) | fp32 positions]
+    const size_t lds = sizeof(double2) * (2 * S * stride + 3 * kBlock) + sizeof(float2) * S * stride;
     const int blocks = (n_scen + S - 1) / S;
     hipLaunchKernelGGL(p->f_is_zero ? k_mc_rollout<true> : k_mc_rollout<false>, dim3(blocks), dim3(kBlock), lds, (hipStream_t)stream, make_kp(p), n_scen, n_o,
                        n_a, steps, T, rc, rs, so, ga, reinterpret_cast<double2*>(pos),

@@ -63,6 +63,12 @@ SETS["stage"] = {
     "stage": ["-DCBF_LDS_STAGE=1"],
     "stage2": ["-DCBF_LDS_STAGE=2"],
 }
+SETS["mc"] = {
+    "mc_base": [],
+    "mc_screen": ["-DCBF_MC_SCREEN=1"],
+    "mc_easy": ["-DCBF_MC_EASY=1"],
+    "mc_both": ["-DCBF_MC_SCREEN=1", "-DCBF_MC_EASY=1"],
+}
 SETS["ext"] = {
     "block64": [],
     "wave64": ["-DCBF_EXT_WAVE=1"],
@@ -241,6 +247,47 @@ def run_shard(rounds, iters, W, H, k=4):
     print(json.dumps(res, indent=1))
 
 
+def run_mc(rounds, iters, n_scen=100000, steps=10):
+    """cbf_mc_rollout (cfg5 shape) per variant; final positions and counters checked bit-for-bit."""
+    import numpy as np
+    import torch
+    from cbf_amd import _lib, scenarios
+    torch.cuda.set_device(0)
+    names = list(_variants())
+    libs = {}
+    for name in names:
+        L = C.CDLL(os.path.join(OUT, f"lib_{name}.so"))
+        for fn, (res, args) in _lib.SIGNATURES.items():
+            getattr(L, fn).restype = res
+            getattr(L, fn).argtypes = args
+        libs[name] = L
+    pos0 = torch.tensor(scenarios.mc_scenarios(n_scen, 16, 16, seed=0), device="cuda")
+    cp = _lib.make_params(15)
+    P = _lib.ptr
+    th = -np.pi / 16
+    st = {n: dict(pos=pos0.clone(), cnt=torch.zeros((n_scen, 4), dtype=torch.int64, device="cuda"),
+                  mv=torch.zeros(n_scen, dtype=torch.float64, device="cuda")) for n in names}
+    times = {n: [] for n in names}
+    for r in range(rounds):
+        for name, L in libs.items():
+            d = st[name]
+            for _ in range(iters):
+                a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                a.record()
+                _lib.check(L.cbf_mc_rollout(cp, n_scen, 16, 16, steps, 1 / 30, float(np.cos(th)), float(np.sin(th)),
+                                            1.0, scenarios.MC_GAIN, P(d["pos"]), P(d["cnt"]), P(d["mv"]),
+                                            _lib.stream_handle()), "mc")
+                b.record()
+                torch.cuda.synchronize()
+                if r > 0:
+                    times[name].append(a.elapsed_time(b))
+    res = {n: {"ms_per_call": float(np.median(v))} for n, v in times.items()}
+    ref = names[0]
+    for n in names[1:]:
+        res[n]["bit_identical"] = bool(all(torch.equal(st[n][f], st[ref][f]) for f in ("pos", "cnt", "mv")))
+    print(json.dumps(res, indent=1))
+
+
 def run_allpairs(rounds, iters, W, H):
     import numpy as np
     import torch
@@ -290,7 +337,7 @@ def run_allpairs(rounds, iters, W, H):
 
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
-    ap.add_argument("cmd", choices=["build", "run", "run_allpairs", "run_shard"])
+    ap.add_argument("cmd", choices=["build", "run", "run_allpairs", "run_shard", "run_mc"])
     ap.add_argument("--rounds", type=int, default=6)
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--W", type=int, default=1024)
@@ -303,5 +350,7 @@ if __name__ == "__main__":
         run_allpairs(a.rounds, a.iters, a.W, a.H)
     elif a.cmd == "run_shard":
         run_shard(a.rounds, a.iters, a.W, a.H)
+    elif a.cmd == "run_mc":
+        run_mc(a.rounds, a.iters)
     else:
         run(a.rounds, a.iters, a.W, a.H)
