@@ -74,8 +74,27 @@ def test_argument_validation_without_launch():
                               1 << 24, null) == _lib.CBF_EINVAL
     # mc: too many entities per scenario
     assert L.cbf_mc_rollout(cp, 4, 200, 100, 1, 0.1, 1.0, 0.0, 1.0, 1.0, 1, 1, 1, null) == _lib.CBF_EINVAL
+    # sharded halo exchange: bad geometry is refused before any launch
+    assert L.cbf_halo_ext_bytes(0) == 0 and L.cbf_halo_ext_bytes(4) == 4 * L.cbf_halo_ext_bytes(1)
+    assert L.cbf_halo_pack(8, 4, 16, 1, 1, 1, 1, null) == _lib.CBF_EINVAL          # fewer owned rows than 2 halos
+    assert L.cbf_halo_pack(8, 2, 64, 1, 1, 0, 1, null) == _lib.CBF_EINVAL          # no sub-step records
+    assert L.cbf_halo_unpack(8, 2, 2, 0, 0, 1, 4 * 2 * 8 + 8, 2, 0, 0.2, 1, 1, 1, null) == _lib.CBF_EINVAL  # rank 0 below
+    assert L.cbf_halo_unpack(8, 2, 0, 2, 2, 1, 4 * 2 * 8, 2, 0, 0.2, 1, 1, 1, null) == _lib.CBF_EINVAL      # stride short
+    assert L.cbf_lattice_step_sharded(cp, C.byref(g), 8, 8, 0, 8, 2, 9, 0, 8, 1, 0.25, 0.1, 1, 1, 1, 1, null, 3, 1,
+                                      null, 1, 1 << 24, null) == _lib.CBF_EINVAL   # owned rows outside the computed rows
+    # certificate / unicycle
+    cc = _lib.CbfCertParams()
+    assert L.cbf_cert_params_init(C.byref(cc), 100.0, 0.12, 0.2, null) == 0 and list(cc.boundary_points) == [-1.6, 1.6,
+                                                                                                               -1.0, 1.0]
+    assert L.cbf_si_barrier_cert(C.byref(cc), 4, 33, 1, 1, 1, 1, null, null, null) == _lib.CBF_EINVAL   # > 32 agents
+    assert L.cbf_si_barrier_cert_lds_bytes(16) > 0 and L.cbf_si_barrier_cert_lds_bytes(33) == 0
+    uu = _lib.CbfUnicycleParams()
+    assert L.cbf_unicycle_params_init(C.byref(uu)) == 0 and uu.max_wheel_velocity == 12.5
+    assert L.cbf_unicycle_advance(C.byref(uu), 4, 1, 1, null, 1, null) == _lib.CBF_EINVAL   # mode 1 needs dxu
+    assert L.cbf_unicycle_advance(C.byref(uu), 4, 1, 1, 1, 3, null) == _lib.CBF_EINVAL      # no mode 3
     # zero-size calls are no-ops
     assert L.cbf_euler(0, null, null, 0.1, null) == 0
+    assert L.cbf_si_barrier_cert(C.byref(cc), 0, 4, null, null, null, null, null, null, null) == 0
     assert L.cbf_get_safe_control_batch(cp, 0, null, null, null, null, null, null, null, null) == 0
 
 
