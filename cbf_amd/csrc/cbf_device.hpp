@@ -306,6 +306,98 @@ __device__ __forceinline__ void scan_rows_joint(const int (&t0)[3], const int (&
 }
 #endif
 
+#ifndef CBF_HIT_MASK
+#define CBF_HIT_MASK 0
+#endif
+#if CBF_SCAN_U > 0
+// Hits of the joint 3-row candidate sequence as a 96-bit mask in registers (bit v = candidate v
+// of the sequence) instead of an LDS index list; returns false when the sequence is longer than
+// 96 (the caller takes the direct path).
+struct HitMask {
+    unsigned m0 = 0u, m1 = 0u, m2 = 0u;
+    int l0 = 0, l01 = 0, L = 0;
+    __device__ __forceinline__ void set(int v) {
+        const unsigned b = 1u << (v & 31);
+        if (v < 32) m0 |= b;
+        else if (v < 64) m1 |= b;
+        else m2 |= b;
+    }
+    // next set bit (ascending), -1 when none
+    __device__ __forceinline__ int pop() {
+        if (m0) {
+            const int b = __ffs((int)m0) - 1;
+            m0 &= m0 - 1u;
+            return b;
+        }
+        if (m1) {
+            const int b = __ffs((int)m1) - 1;
+            m1 &= m1 - 1u;
+            return 32 + b;
+        }
+        if (m2) {
+            const int b = __ffs((int)m2) - 1;
+            m2 &= m2 - 1u;
+            return 64 + b;
+        }
+        return -1;
+    }
+};
+
+__device__ __forceinline__ bool scan_rows_joint_mask(const int (&t0)[3], const int (&t1)[3], const KP& P,
+                                                     const Ego& E, HitMask& H, const double2* __restrict__ spos) {
+    H.l0 = t1[0] - t0[0];
+    H.l01 = H.l0 + (t1[1] - t0[1]);
+    H.L = H.l01 + (t1[2] - t0[2]);
+    if (H.L > 96) return false;
+    const int l0 = H.l0, l01 = H.l01, L = H.L;
+    for (int v = 0; v < L; v += CBF_SCAN_U) {
+        double2 p[CBF_SCAN_U];
+#pragma unroll
+        for (int q = 0; q < CBF_SCAN_U; ++q) {
+            const int vv = v + q;
+            const int tt = vv < l0 ? t0[0] + vv : (vv < l01 ? t0[1] + (vv - l0) : t0[2] + (vv - l01));
+            if (vv < L) p[q] = spos[tt];
+        }
+#pragma unroll
+        for (int q = 0; q < CBF_SCAN_U; ++q) {
+            if (v + q < L) {
+                const double e0 = p[q].x - E.r0, e1 = p[q].y - E.r1;
+                const double s = e0 * e0 + e1 * e1;
+                if (s < P.cull_t && s > 0) H.set(v + q);
+            }
+        }
+    }
+    return true;
+}
+
+// Row assembly over the masked hits, CBF_FLUSH_U hits' loads in flight per lane.
+template <bool FZ>
+__device__ __forceinline__ void flush_mask(HitMask& H, const int (&t0)[3], const KP& P, Ego& E,
+                                           const double2* __restrict__ spos, const double2* __restrict__ svel) {
+    for (;;) {
+        int tt[CBF_FLUSH_U];
+        bool any = false;
+#pragma unroll
+        for (int q = 0; q < CBF_FLUSH_U; ++q) {
+            const int v = H.pop();
+            tt[q] = v < 0 ? -1 : (v < H.l0 ? t0[0] + v : (v < H.l01 ? t0[1] + (v - H.l0) : t0[2] + (v - H.l01)));
+            any = any || v >= 0;
+        }
+        if (!any) break;
+        double2 pj[CBF_FLUSH_U], vj[CBF_FLUSH_U];
+#pragma unroll
+        for (int q = 0; q < CBF_FLUSH_U; ++q)
+            if (tt[q] >= 0) {
+                pj[q] = spos[tt[q]];
+                vj[q] = svel[tt[q]];
+            }
+#pragma unroll
+        for (int q = 0; q < CBF_FLUSH_U; ++q)
+            if (tt[q] >= 0) ego_add<FZ>(P, E, pj[q].x, pj[q].y, vj[q].x, vj[q].y);
+    }
+}
+#endif
+
 #if CBF_SCAN_U > 0
 // scan_rows_joint over fp32 positions with the screen threshold t32 (pushes candidates that
 // may be neighbours, including the ego itself; the flush decides exactly).

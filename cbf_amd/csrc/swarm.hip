@@ -351,7 +351,19 @@ __device__ __forceinline__ int lattice_ego(const KP& P, const CellGrid& G, int W
         rt0[k] = in ? start[yy * G.nx + xa] : 0;
         rt1[k] = in ? start[yy * G.nx + xb + 1] : 0;
     }
-#if CBF_ABLATE < 3
+#if CBF_HIT_MASK && CBF_SCAN_U > 0 && CBF_ABLATE == 0
+    {
+        HitMask Hm;
+        if (scan_rows_joint_mask(rt0, rt1, P, E, Hm, spos)) {
+            flush_mask<FZ>(Hm, rt0, P, E, spos, svel);
+        } else {
+#pragma unroll
+            for (int k = 0; k < 3; ++k) scan_range_direct<FZ>(rt0[k], rt1[k], P, E, spos, svel);
+        }
+        (void)hit_lds;
+        (void)spos32;
+    }
+#elif CBF_ABLATE < 3
     HitList Hl;
 #if CBF_SCAN32
     // screen bound from the ego's own magnitude: a true neighbour lies within r of it
@@ -411,7 +423,7 @@ __global__ void __launch_bounds__(kBlock) k_lattice_filter(KP P, CellGrid G, int
                                                            const float2* __restrict__ spos32, int cnt_begin,
                                                            int cnt_end) {
     // hit rows + a dummy row (branch-free push) + 4 x fp64 per-quadrant minima (CBF_BQ_LDS)
-    __shared__ int hit_lds[(kHitCap + 1) * kBlock + (CBF_BQ_LDS ? 8 * kBlock : 0)];
+    __shared__ int hit_lds[CBF_HIT_MASK ? 1 : (kHitCap + 1) * kBlock + (CBF_BQ_LDS ? 8 * kBlock : 0)];
     const int bx = xcd_block();
     const int slot = bx * kBlock + threadIdx.x;
     const int total = start[ncell];

@@ -63,6 +63,12 @@ SETS["stage"] = {
     "stage": ["-DCBF_LDS_STAGE=1"],
     "stage2": ["-DCBF_LDS_STAGE=2"],
 }
+SETS["mask"] = {
+    "full": [],
+    "mask": ["-DCBF_HIT_MASK=1"],
+    "mask_f2": ["-DCBF_HIT_MASK=1", "-DCBF_FLUSH_U=2"],
+    "mask_s8": ["-DCBF_HIT_MASK=1", "-DCBF_SCAN_U=8"],
+}
 SETS["mc"] = {
     "mc_base": [],
     "mc_screen": ["-DCBF_MC_SCREEN=1"],
