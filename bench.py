@@ -114,6 +114,26 @@ def cpu_baseline_parallel(W, H, seed, budget_s, procs):
                       f"{dt:.1f} s"}
 
 
+def full_size_check(S, args):
+    """After the timed run (untimed): one more fused step of the full swarm against the separate
+    cell-list filter (cbf_filter_cells with diagnostics) on the same input state -- controls
+    bit-identical, and the largest row violation over the solved QPs (north star: <= 1e-7)."""
+    import torch
+    from cbf_amd import scenarios, swarm
+    pos0 = S.pos.clone()
+    S.step()
+    torch.cuda.synchronize()
+    vel = swarm.consensus_lattice(pos0, S.W, S.H, scenarios.LATTICE_GAIN)
+    out = swarm.filter_swarm(S.params, pos0, vel, 0, method="cells", grid=S.grid, diag=True)
+    st = out["status"]
+    solved = ((st & 0xFF) == 1) | ((st & 0xFF) == 2)
+    viol = float(out["viol"][solved].max().item()) if bool(solved.any()) else 0.0
+    return {"agents": int(pos0.shape[0]), "u_bit_identical_to_cell_filter": bool(torch.equal(out["u"], S.u)),
+            "status_identical": bool(torch.equal(st, S.status)), "max_row_violation": viol,
+            "relaxed_fraction": float(((st & 0xFF) == 2).float().mean().item()),
+            "max_relaxations": int((st >> 8).max().item())}
+
+
 def bench_lattice(args, ws, rank, local):
     import torch
     from cbf_amd import scenarios, swarm
@@ -174,6 +194,7 @@ def bench_lattice(args, ws, rank, local):
     k_ms = float(np.mean([a.elapsed_time(b) for a, b in kt]))
     status = S.status.cpu().numpy()
     codes = np.bincount(status & 0xFF, minlength=5)
+    check = full_size_check(S, args) if (ws == 1 and not args.shard and args.barrier == "reference") else None
     achieved = FILTER_BYTES_PER_AGENT * n_local / (k_ms * 1e-3) / 1e9
     traffic = load_pmc_traffic()
     res = {
@@ -198,6 +219,7 @@ def bench_lattice(args, ws, rank, local):
                    "graph": use_graph},
         "timesteps_per_s": args.steps / elapsed,
         "solves_per_step": solves / args.steps,
+        "full_size_check": check,
         "status_fraction_last_step": {"idle": codes[0] / len(status), "optimal": codes[1] / len(status),
                                       "relaxed": codes[2] / len(status),
                                       "box_infeasible": codes[3] / len(status)},
