@@ -33,10 +33,12 @@ __device__ __forceinline__ double cube1(double h) {
     return fma(p, h, e * h);
 }
 
-__device__ __forceinline__ void wave_argmin(double& v, int& i) {
-    for (int o = 32; o > 0; o >>= 1) {
-        const double ov = __shfl_xor(v, o, 64);
-        const int oi = __shfl_xor(i, o, 64);
+// Reductions over the G lanes of one scenario's group (G divides the wave).
+template <int G>
+__device__ __forceinline__ void group_argmin(double& v, int& i) {
+    for (int o = G / 2; o > 0; o >>= 1) {
+        const double ov = __shfl_xor(v, o, G);
+        const int oi = __shfl_xor(i, o, G);
         if (ov < v || (ov == v && oi < i)) {
             v = ov;
             i = oi;
@@ -44,9 +46,18 @@ __device__ __forceinline__ void wave_argmin(double& v, int& i) {
     }
 }
 
-__device__ __forceinline__ double wave_sum(double v) {
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+template <int G>
+__device__ __forceinline__ double group_sum(double v) {
+    for (int o = G / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, G);
     return v;
+}
+
+// LDS ordering between the lanes of the (single-wave) workgroup; groups of one wave run
+// independent loops, so no workgroup barrier is used inside them.
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
 // Pair index c (lexicographic i < j) -> (i, j).
@@ -72,14 +83,21 @@ __device__ __forceinline__ double row_dot(int2 ij, const double* xp, const doubl
     return s;
 }
 
-__global__ void __launch_bounds__(64) k_si_barrier_cert(CertArgs C, int N, const double2* __restrict__ dxi,
+// One scenario per group of G lanes (G >= 2N; 64 / G scenarios per wave), lane l of the group
+// owns QP variable l; each group has its own LDS region of `sdw` doubles.
+template <int G>
+__global__ void __launch_bounds__(64) k_si_barrier_cert(CertArgs C, int N, int batch, long sdw,
+                                                        const double2* __restrict__ dxi,
                                                         const double2* __restrict__ xs, double2* __restrict__ out,
                                                         int32_t* __restrict__ status, int32_t* __restrict__ iters,
                                                         int32_t* __restrict__ n_active) {
-    extern __shared__ double lds[];
+    extern __shared__ double lds_all[];
     const int n = 2 * N, m = N * (N - 1) / 2 + 4 * N, ld = n + 1;
-    const int lane = threadIdx.x;
-    const long sc = blockIdx.x;
+    const int lane = threadIdx.x & (G - 1), grp = threadIdx.x / G;
+    const long sc_raw = (long)blockIdx.x * (64 / G) + grp;
+    const bool valid = sc_raw < batch;
+    const long sc = valid ? sc_raw : batch - 1;  // idle groups shadow the last scenario, write nothing
+    double* lds = lds_all + grp * sdw;
     double* J = lds;             // [n][ld]
     double* R = J + n * ld;      // [n][ld], column j = active constraint j
     double* brow = R + n * ld;   // [m]
@@ -107,15 +125,15 @@ __global__ void __launch_bounds__(64) k_si_barrier_cert(CertArgs C, int N, const
             yl = c;
         }
     }
-    for (int r = lane; r < n; r += 64) {
+    for (int r = lane; r < n; r += G) {
         for (int c = 0; c < n; ++c) {
             J[r * ld + c] = (r == c) ? 1.0 / sqrt(2.0) : 0.0;
             R[r * ld + c] = 0.0;
         }
     }
-    __syncthreads();
+    wave_sync();
     const int npair = N * (N - 1) / 2;
-    for (int c = lane; c < m; c += 64) {
+    for (int c = lane; c < m; c += G) {
         int2 ij;
         double b;
         if (c < npair) {
@@ -143,14 +161,14 @@ __global__ void __launch_bounds__(64) k_si_barrier_cert(CertArgs C, int N, const
     int actl = -1;    // lane j < q: its row
     int q = 0, st = CBF_CERT_MAXITER, it = 0;
     if (lane < n) xv[lane] = xl;
-    __syncthreads();
+    wave_sync();
 
     while (true) {
         if (++it > C.max_iter) break;
         // most violated inactive row (first index on ties)
         double best = INFINITY;
         int bi = m;
-        for (int c = lane; c < m; c += 64) {
+        for (int c = lane; c < m; c += G) {
             if (isact[c]) continue;
             const double s = brow[c] - row_dot(rij[c], xp, xv);
             if (s < best) {
@@ -158,7 +176,7 @@ __global__ void __launch_bounds__(64) k_si_barrier_cert(CertArgs C, int N, const
                 bi = c;
             }
         }
-        wave_argmin(best, bi);
+        group_argmin<G>(best, bi);
         if (bi >= m || !(best < -C.tol * pmax(1.0, fabs(brow[bi])))) {
             st = CBF_CERT_OPTIMAL;
             break;
@@ -187,7 +205,7 @@ __global__ void __launch_bounds__(64) k_si_barrier_cert(CertArgs C, int N, const
                 if (k1 >= 0) dl = ((dl + n1 * J[k1 * ld + lane]) + n2 * J[k2 * ld + lane]) + n3 * J[k3 * ld + lane];
                 dv[lane] = dl;
             }
-            __syncthreads();
+            wave_sync();
             // z = J[:, q:] d[q:] (lane = row)
             // (four partial sums: the LDS loads of consecutive columns overlap)
             double zl = 0.0;
@@ -208,20 +226,20 @@ __global__ void __launch_bounds__(64) k_si_barrier_cert(CertArgs C, int N, const
             // the reciprocals of R's diagonal
             double rl = lane < q ? dl : 0.0;
             for (int j = q - 1; j >= 0; --j) {
-                const double rj = __shfl(rl, j, 64) * rid[j];
+                const double rj = __shfl(rl, j, G) * rid[j];
                 if (lane == j) rl = rj;
                 else if (lane < j) rl -= R[lane * ld + j] * rj;
             }
             // partial (dual) step: the first active constraint whose multiplier reaches 0
             double t1 = INFINITY;
-            int kk = 64;
+            int kk = G;
             if (lane < q && rl > 0.0) {
                 t1 = ul / rl;
                 kk = lane;
             }
-            wave_argmin(t1, kk);
-            const double zn = wave_sum((lane >= q && lane < n) ? dl * dl : 0.0);
-            const double dd = wave_sum(lane < n ? dl * dl : 0.0);
+            group_argmin<G>(t1, kk);
+            const double zn = group_sum<G>((lane >= q && lane < n) ? dl * dl : 0.0);
+            const double dd = group_sum<G>(lane < n ? dl * dl : 0.0);
             double t2 = INFINITY;
             if (zn > 1e-28 * dd) t2 = -(brow[p] - row_dot(pij, xp, xv)) / zn;
             if (t1 == INFINITY && t2 == INFINITY) {
@@ -240,7 +258,7 @@ __global__ void __launch_bounds__(64) k_si_barrier_cert(CertArgs C, int N, const
                 // add p: one Householder reflection H = I - v v' / (sg vq) maps d[q:] onto
                 // -sg e_q (v = d[q:] + sg e_q, sg = |d[q:]| with the sign of d_q); J[:, q:] <- J[:, q:] H,
                 // lane-parallel over J's rows
-                const double dq = __shfl(dl, q, 64);
+                const double dq = __shfl(dl, q, G);
                 const double sg = copysign(sqrt(zn), dq);
                 const double vq = dq + sg;
                 const double beta = 1.0 / (sg * vq);
@@ -268,7 +286,7 @@ __global__ void __launch_bounds__(64) k_si_barrier_cert(CertArgs C, int N, const
                     isact[p] = 1;
                 }
                 ++q;
-                __syncthreads();
+                wave_sync();
                 break;
             }
             // drop active constraint kk: delete R's column kk, restore the triangle with Givens on
@@ -277,13 +295,13 @@ __global__ void __launch_bounds__(64) k_si_barrier_cert(CertArgs C, int N, const
                 for (int j = kk; j < q - 1; ++j) R[lane * ld + j] = R[lane * ld + j + 1];
                 R[lane * ld + q - 1] = 0.0;
             }
-            __syncthreads();
+            wave_sync();
             if (lane >= kk && lane < q - 1) rid[lane] = 1.0 / R[lane * ld + lane];  // shifted diagonal
-            __syncthreads();
+            wave_sync();
             for (int j = kk; j < q - 1; ++j) {
                 const double a = R[j * ld + j], b = R[(j + 1) * ld + j];
                 const double h = hypot(a, b);
-                __syncthreads();
+                wave_sync();
                 if (h != 0.0) {
                     const double cs = a / h, sn = b / h;
                     if (lane >= j && lane < q - 1) {
@@ -299,11 +317,11 @@ __global__ void __launch_bounds__(64) k_si_barrier_cert(CertArgs C, int N, const
                         J[lane * ld + j + 1] = -sn * Ja + cs * Jb;
                     }
                 }
-                __syncthreads();
+                wave_sync();
             }
-            const int gone = __shfl(actl, kk, 64);
-            const double un = __shfl_down(ul, 1, 64);
-            const int an = __shfl_down(actl, 1, 64);
+            const int gone = __shfl(actl, kk, G);
+            const double un = __shfl_down(ul, 1, G);
+            const int an = __shfl_down(actl, 1, G);
             if (lane >= kk && lane < q - 1) {
                 ul = un;
                 actl = an;
@@ -314,7 +332,7 @@ __global__ void __launch_bounds__(64) k_si_barrier_cert(CertArgs C, int N, const
             }
             if (lane == 0) isact[gone] = 0;
             --q;
-            __syncthreads();
+            wave_sync();
         }
         if (infeasible) {
             st = CBF_CERT_INFEASIBLE;
@@ -322,9 +340,9 @@ __global__ void __launch_bounds__(64) k_si_barrier_cert(CertArgs C, int N, const
         }
     }
     const double val = st == CBF_CERT_OPTIMAL ? xl : yl;
-    const double ox = __shfl(val, (2 * lane) & 63, 64), oy = __shfl(val, (2 * lane + 1) & 63, 64);
-    if (lane < N) out[sc * N + lane] = make_double2(ox, oy);
-    if (lane == 0) {
+    const double ox = __shfl(val, (2 * lane) & (G - 1), G), oy = __shfl(val, (2 * lane + 1) & (G - 1), G);
+    if (valid && lane < N) out[sc * N + lane] = make_double2(ox, oy);
+    if (valid && lane == 0) {
         status[sc] = st;
         if (iters) iters[sc] = it;
         if (n_active) n_active[sc] = q;
@@ -428,9 +446,16 @@ extern "C" int cbf_si_barrier_cert(const cbf_cert_params* c, int32_t batch, int3
     A.tol = c->viol_tol;
     const int m = n_agents * (n_agents - 1) / 2 + 4 * n_agents;
     A.max_iter = c->max_iter > 0 ? c->max_iter : 10 * (m + 2 * n_agents) + 10;
-    const size_t lds = cbf_si_barrier_cert_lds_bytes(n_agents);
-    hipLaunchKernelGGL(k_si_barrier_cert, dim3(batch), dim3(64), lds, (hipStream_t)stream, A, n_agents,
-                       reinterpret_cast<const double2*>(dxi), reinterpret_cast<const double2*>(x),
+    // per-scenario LDS region, rounded to 16 B.  Small scenarios share a wave: groups of G = 8 / 16
+    // lanes (G >= 2N) for N <= 8; beyond that one scenario per wave (2 per wave measured slower
+    // at N = 16: the doubled LDS per workgroup costs more resident waves than it saves lanes)
+    const size_t per = (cbf_si_barrier_cert_lds_bytes(n_agents) + 15) / 16 * 16;
+    const int G = 2 * n_agents <= 8 ? 8 : (2 * n_agents <= 16 ? 16 : 64);
+    const int spw = 64 / G;
+    const int blocks = (batch + spw - 1) / spw;
+    auto kern = G == 8 ? k_si_barrier_cert<8> : (G == 16 ? k_si_barrier_cert<16> : k_si_barrier_cert<64>);
+    hipLaunchKernelGGL(kern, dim3(blocks), dim3(64), per * spw, (hipStream_t)stream, A, n_agents, batch,
+                       (long)(per / 8), reinterpret_cast<const double2*>(dxi), reinterpret_cast<const double2*>(x),
                        reinterpret_cast<double2*>(out), status, iters, n_active);
     return (int)hipGetLastError();
 }
