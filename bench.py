@@ -433,6 +433,8 @@ def main():
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     ap.add_argument("--cpu-procs", type=int, default=min(16, os.cpu_count() or 1),
                     help="host processes for the parallel C-port baseline (1 = skip)")
+    ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
+                    help="torch.distributed backend for N > 1 (nccl = RCCL; gloo = host-staged rehearsal)")
     ap.add_argument("--substeps", type=int, default=4,
                     help="sharded cfg4: timesteps per halo exchange (ghost rows = 4 x substeps)")
     ap.add_argument("--shard", action="store_true",
@@ -441,12 +443,17 @@ def main():
     ws, rank, local = _dist_env()
     import torch
     if ws > 1 or args.shard:
-        torch.cuda.set_device(local)
+        # (gloo: a rehearsal of several ranks on fewer GPUs, exchanges staged through the host)
+        dev = local % torch.cuda.device_count() if args.backend == "gloo" else local
+        torch.cuda.set_device(dev)
         os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29533")
-        torch.distributed.init_process_group("nccl", device_id=torch.device("cuda", local), rank=rank,
-                                             world_size=ws)
+        if args.backend == "gloo":
+            torch.distributed.init_process_group("gloo", rank=rank, world_size=ws)
+        else:
+            torch.distributed.init_process_group("nccl", device_id=torch.device("cuda", local), rank=rank,
+                                                 world_size=ws)
     else:
         torch.cuda.set_device(0)
     if args.config == "cfg3":
