@@ -295,6 +295,10 @@ __global__ void __launch_bounds__(kBlock) k_hocbf_indexed(KP P, HP H, const doub
 // rows recomputed from the cell-sorted state during the solve; clip, Euler, outputs as
 // k_lattice_filter.  More than kHocbfCap neighbours: CBF_STATUS_NBR_OVERFLOW, u = u0.
 constexpr int kHocbfCap = 24;
+#ifndef CBF_HSCAN_U
+#define CBF_HSCAN_U 6
+#endif
+constexpr int kHScan = CBF_HSCAN_U;  // candidates in flight per lane in the HOCBF scan
 
 __global__ void __launch_bounds__(kBlock) k_lattice_filter_hocbf(
     KP P, HP H, CellGrid G, int W, int row_begin, int row_end, int win_row0, long ncell,
@@ -320,16 +324,36 @@ __global__ void __launch_bounds__(kBlock) k_lattice_filter_hocbf(
             const int xa = cx > 0 ? cx - 1 : 0;
             const int xb = cx < G.nx - 1 ? cx + 1 : G.nx - 1;
             int m = 0;
+            // the three cell-row ranges as one sequence, kHScan candidates (position + entity index)
+            // in flight per lane; hits go into the ascending-entity key list
+            int t0[3], t1[3];
+#pragma unroll
             for (int k = 0; k < 3; ++k) {
                 const int yy = cy + k - 1;
-                if (yy < 0 || yy >= G.ny) continue;
-                const int t1 = start[yy * G.nx + xb + 1];
-                for (int t = start[yy * G.nx + xa]; t < t1; ++t) {
-                    const double2 pj = spos[t];
-                    const double q0 = pj.x - E.r0, q1 = pj.y - E.r1;
+                const bool in = yy >= 0 && yy < G.ny;
+                t0[k] = in ? start[yy * G.nx + xa] : 0;
+                t1[k] = in ? start[yy * G.nx + xb + 1] : 0;
+            }
+            const int l0 = t1[0] - t0[0], l01 = l0 + (t1[1] - t0[1]), L = l01 + (t1[2] - t0[2]);
+            for (int v = 0; v < L; v += kHScan) {
+                double2 pq[kHScan];
+                int tq[kHScan], iq[kHScan];
+#pragma unroll
+                for (int q = 0; q < kHScan; ++q) {
+                    const int vv = v + q;
+                    tq[q] = vv < l0 ? t0[0] + vv : (vv < l01 ? t0[1] + (vv - l0) : t0[2] + (vv - l01));
+                    if (vv < L) {
+                        pq[q] = spos[tq[q]];
+                        iq[q] = sidx[tq[q]];
+                    }
+                }
+#pragma unroll
+                for (int q = 0; q < kHScan; ++q) {
+                    if (v + q >= L) continue;
+                    const double q0 = pq[q].x - E.r0, q1 = pq[q].y - E.r1;
                     const double sq = q0 * q0 + q1 * q1;
                     if (!(sq < P.cull_t && sq > 0)) continue;  // agents only (cross_and_rescue.py:147-150)
-                    const unsigned long long key = ((unsigned long long)(unsigned)sidx[t] << 32) | (unsigned)t;
+                    const unsigned long long key = ((unsigned long long)(unsigned)iq[q] << 32) | (unsigned)tq[q];
                     if (m < kHocbfCap) {  // insertion into the sorted list
                         int j = m;
                         while (j > 0 && keys[(j - 1) * kBlock + threadIdx.x] > key) {

@@ -1,7 +1,7 @@
-# GPU box: parity tests then the cfg4 bench in HOCBF mode
+# GPU box: HOCBF parity tests then the cfg4 bench in HOCBF mode
 set -o pipefail
 mkdir -p gpurun_out
-timeout -k 10 500 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1 || { echo TESTS_FAILED; tail -40 gpurun_out/gpu_tests.log; exit 1; }
-tail -2 gpurun_out/gpu_tests.log
+timeout -k 10 300 python -u -m pytest tests/test_gpu_hocbf.py -x -q --timeout 200 --timeout-method thread > gpurun_out/hocbf_tests.log 2>&1 || { echo TESTS_FAILED; tail -40 gpurun_out/hocbf_tests.log; exit 1; }
+tail -2 gpurun_out/hocbf_tests.log
 timeout -k 10 300 python bench.py --barrier euclidean_hocbf --no-cpu-baseline --steps 100 > gpurun_out/bench_cfg4_hocbf.json 2> gpurun_out/bench_hocbf.err || { tail gpurun_out/bench_hocbf.err; exit 3; }
 cat gpurun_out/bench_cfg4_hocbf.json
