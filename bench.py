@@ -227,7 +227,7 @@ def bench_lattice(args, ws, rank, local):
                      "frac": achieved / HBM_PEAK_GBS,
                      "traffic": traffic if args.barrier == "reference" else None,
                      "kernel": "advance phase: k_lattice_filter + k_lattice_filter_hard" if args.barrier == "reference"
-                     else "k_lattice_filter_hocbf",
+                     else "advance phase: k_lattice_filter_hocbf + k_lattice_filter_hocbf_wide",
                      "kernel_ms": k_ms,
                      "algorithmic_bytes_per_launch": FILTER_BYTES_PER_AGENT * n_local,
                      "step_algorithmic_GBps": STEP_BYTES_PER_AGENT * n_local * args.steps / elapsed / 1e9 / ws},

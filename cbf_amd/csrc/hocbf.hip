@@ -54,13 +54,14 @@ struct SlotRows {
     const KP& P;
     const HP& H;
     const Ego& E;
-    const unsigned long long* keys;  // keys[i * kBlock + threadIdx.x]
+    const unsigned long long* keys;  // keys[i * ks + lane]
+    int ks, lane;
     const double2* __restrict__ spos;
     const double2* __restrict__ svel;
     int m;
     int t;
     __device__ __forceinline__ void row(int i, double& a0, double& a1, double& b) const {
-        const int slot = (int)(keys[i * kBlock + threadIdx.x] & 0xFFFFFFFFull);
+        const int slot = (int)(keys[i * ks + lane] & 0xFFFFFFFFull);
         const double2 o = spos[slot], ov = svel[slot];
         const double4 r = hocbf_row(P, H, E.r0, E.r1, E.r2, E.r3, o.x, o.y, ov.x, ov.y, E.u0x, E.u0y);
         a0 = r.x;
@@ -202,19 +203,20 @@ __device__ __forceinline__ Sol solve_hocbf(const KP& P, const Ego& E, Src& R) {
 }
 
 // Plane source over rows staged per lane in LDS (the lattice kernel's key area, reused once the
-// keys are in registers): row i's a0, a1, b at lds[(3i + c) * kBlock + lane]; relaxed in place.
+// keys are in registers): row i's a0, a1, b at lds[(3i + c) * ks + lane]; relaxed in place.
 constexpr int kLdsRows = 8;
 struct LdsRows {
     double* lds;
+    int ks, lane;
     int m;
     __device__ __forceinline__ void row(int i, double& a0, double& a1, double& b) const {
-        a0 = lds[(3 * i) * kBlock + threadIdx.x];
-        a1 = lds[(3 * i + 1) * kBlock + threadIdx.x];
-        b = lds[(3 * i + 2) * kBlock + threadIdx.x];
+        a0 = lds[(3 * i) * ks + lane];
+        a1 = lds[(3 * i + 1) * ks + lane];
+        b = lds[(3 * i + 2) * ks + lane];
     }
     __device__ __forceinline__ void relax() {
         for (int i = 0; i < m; ++i) {
-            double& v = lds[(3 * i + 2) * kBlock + threadIdx.x];
+            double& v = lds[(3 * i + 2) * ks + lane];
             v = v + 1.0;  // cbf.py:85-87
         }
     }
@@ -300,12 +302,117 @@ constexpr int kHocbfCap = 24;
 #endif
 constexpr int kHScan = CBF_HSCAN_U;  // candidates in flight per lane in the HOCBF scan
 
+// Neighbour scan of one ego (slot) over its 3x3 cells; hits go into the ascending-entity key
+// list keys[i * ks + lane] (first kHocbfCap of them).  Returns the hit count m.
+__device__ __forceinline__ int hocbf_scan(const KP& P, const CellGrid& G, const Ego& E, const double2* __restrict__ spos,
+                                          const int32_t* __restrict__ sidx, const int32_t* __restrict__ start,
+                                          unsigned long long* keys, int ks, int lane) {
+    const int cx = cell_coord(E.r0, G.x0, G.inv_h, G.nx);
+    const int cy = cell_coord(E.r1, G.y0, G.inv_h, G.ny);
+    const int xa = cx > 0 ? cx - 1 : 0;
+    const int xb = cx < G.nx - 1 ? cx + 1 : G.nx - 1;
+    int m = 0;
+    // the three cell-row ranges as one sequence, kHScan candidates (position + entity index)
+    // in flight per lane
+    int t0[3], t1[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const int yy = cy + k - 1;
+        const bool in = yy >= 0 && yy < G.ny;
+        t0[k] = in ? start[yy * G.nx + xa] : 0;
+        t1[k] = in ? start[yy * G.nx + xb + 1] : 0;
+    }
+    const int l0 = t1[0] - t0[0], l01 = l0 + (t1[1] - t0[1]), L = l01 + (t1[2] - t0[2]);
+    for (int v = 0; v < L; v += kHScan) {
+        double2 pq[kHScan];
+        int tq[kHScan], iq[kHScan];
+#pragma unroll
+        for (int q = 0; q < kHScan; ++q) {
+            const int vv = v + q;
+            tq[q] = vv < l0 ? t0[0] + vv : (vv < l01 ? t0[1] + (vv - l0) : t0[2] + (vv - l01));
+            if (vv < L) {
+                pq[q] = spos[tq[q]];
+                iq[q] = sidx[tq[q]];
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < kHScan; ++q) {
+            if (v + q >= L) continue;
+            const double q0 = pq[q].x - E.r0, q1 = pq[q].y - E.r1;
+            const double sq = q0 * q0 + q1 * q1;
+            if (!(sq < P.cull_t && sq > 0)) continue;  // agents only (cross_and_rescue.py:147-150)
+            const unsigned long long key = ((unsigned long long)(unsigned)iq[q] << 32) | (unsigned)tq[q];
+            if (m < kHocbfCap) {  // insertion into the sorted list
+                int j = m;
+                while (j > 0 && keys[(j - 1) * ks + lane] > key) {
+                    keys[j * ks + lane] = keys[(j - 1) * ks + lane];
+                    --j;
+                }
+                keys[j * ks + lane] = key;
+            }
+            ++m;
+        }
+    }
+    return m;
+}
+
+// Rows of the m <= cap sorted keys computed once into lds[(3i + c) * ks + lane] (the keys are
+// read out first when the row area aliases the key area), then the relaxation loop.
+template <int CAP>
+__device__ __forceinline__ Sol hocbf_solve_lds(const KP& P, const HP& H, const Ego& E, const double2* __restrict__ spos,
+                                               const double2* __restrict__ svel, const unsigned long long* keys,
+                                               double* rl, int ks, int lane, int m) {
+    unsigned long long kr[CAP];
+#pragma unroll
+    for (int i = 0; i < CAP; ++i) kr[i] = i < m ? keys[i * ks + lane] : 0ull;
+#pragma unroll
+    for (int i = 0; i < CAP; ++i) {
+        if (i < m) {
+            const int sl = (int)(kr[i] & 0xFFFFFFFFull);
+            const double2 o = spos[sl], ov = svel[sl];
+            const double4 rw = hocbf_row(P, H, E.r0, E.r1, E.r2, E.r3, o.x, o.y, ov.x, ov.y, E.u0x, E.u0y);
+            rl[(3 * i) * ks + lane] = rw.x;
+            rl[(3 * i + 1) * ks + lane] = rw.y;
+            rl[(3 * i + 2) * ks + lane] = rw.z;
+        }
+    }
+    LdsRows R{rl, ks, lane, m};
+    return solve_hocbf(P, E, R);
+}
+
+// Outputs of an owned ego (clip, Euler, status, count) and its guard extents.
+__device__ __forceinline__ void hocbf_finish(const KP& P, const Sol* S, const Ego& E, int m, int W, int row_begin,
+                                             int row_end, int r, int c, double T, double2* __restrict__ pos_out,
+                                             double2* __restrict__ u, int32_t* __restrict__ status,
+                                             int32_t* __restrict__ cnt, int guard_rows, double& e0, double& e1,
+                                             double& e2, double& e3) {
+    double ux = E.u0x, uy = E.u0y;  // no neighbour: filter not run, u0 unclipped
+    int32_t st = m > kHocbfCap ? CBF_STATUS_NBR_OVERFLOW : CBF_STATUS_IDLE;
+    if (S) {
+        clip_u(P, *S, E, ux, uy);
+        st = pack_status(*S);
+    }
+    const long k = (long)(r - row_begin) * W + c;
+    const double2 pn = make_double2(E.r0 + T * ux, E.r1 + T * uy);
+    pos_out[k] = pn;
+    u[k] = make_double2(ux, uy);
+    status[k] = st;
+    if (cnt) cnt[k] = m;
+    ext_accumulate(r, row_begin, row_end, guard_rows, pn.y, e0, e1, e2, e3);
+}
+
+// Lattice step K4 in HOCBF mode: one lane per cell-sorted slot (owned agents); exact cull over
+// the 3x3 cells; hits kept as LDS keys (entity << 32 | slot) in ascending entity order (the
+// oracle's reference-order row sequence, independent of the atomic arrival order inside a cell);
+// rows computed into LDS, solve, clip, Euler, outputs as k_lattice_filter.  Egos with more than
+// kLdsRows neighbours are queued (their slot, hardq) for k_lattice_filter_hocbf_wide, so the
+// long tail does not hold whole waves; more than kHocbfCap: CBF_STATUS_NBR_OVERFLOW, u = u0.
 __global__ void __launch_bounds__(kBlock) k_lattice_filter_hocbf(
     KP P, HP H, CellGrid G, int W, int row_begin, int row_end, int win_row0, long ncell,
     const double2* __restrict__ spos, const double2* __restrict__ svel, const int32_t* __restrict__ sidx,
     const int32_t* __restrict__ start, double T, double2* __restrict__ pos_out, double2* __restrict__ u,
     int32_t* __restrict__ status, int32_t* __restrict__ cnt, int guard_rows, double* __restrict__ ext_part,
-    unsigned long long* __restrict__ solves) {
+    unsigned long long* __restrict__ solves, int32_t* __restrict__ hardq) {
     __shared__ unsigned long long keys[kHocbfCap * kBlock];
     const int bx = xcd_block();
     const int slot = bx * kBlock + threadIdx.x;
@@ -319,93 +426,20 @@ __global__ void __launch_bounds__(kBlock) k_lattice_filter_hocbf(
             const double2 pe = spos[slot], ve = svel[slot];
             Ego E;
             ego_init(P, E, pe.x, pe.y, ve.x, ve.y, ve.x, ve.y);
-            const int cx = cell_coord(pe.x, G.x0, G.inv_h, G.nx);
-            const int cy = cell_coord(pe.y, G.y0, G.inv_h, G.ny);
-            const int xa = cx > 0 ? cx - 1 : 0;
-            const int xb = cx < G.nx - 1 ? cx + 1 : G.nx - 1;
-            int m = 0;
-            // the three cell-row ranges as one sequence, kHScan candidates (position + entity index)
-            // in flight per lane; hits go into the ascending-entity key list
-            int t0[3], t1[3];
-#pragma unroll
-            for (int k = 0; k < 3; ++k) {
-                const int yy = cy + k - 1;
-                const bool in = yy >= 0 && yy < G.ny;
-                t0[k] = in ? start[yy * G.nx + xa] : 0;
-                t1[k] = in ? start[yy * G.nx + xb + 1] : 0;
-            }
-            const int l0 = t1[0] - t0[0], l01 = l0 + (t1[1] - t0[1]), L = l01 + (t1[2] - t0[2]);
-            for (int v = 0; v < L; v += kHScan) {
-                double2 pq[kHScan];
-                int tq[kHScan], iq[kHScan];
-#pragma unroll
-                for (int q = 0; q < kHScan; ++q) {
-                    const int vv = v + q;
-                    tq[q] = vv < l0 ? t0[0] + vv : (vv < l01 ? t0[1] + (vv - l0) : t0[2] + (vv - l01));
-                    if (vv < L) {
-                        pq[q] = spos[tq[q]];
-                        iq[q] = sidx[tq[q]];
-                    }
-                }
-#pragma unroll
-                for (int q = 0; q < kHScan; ++q) {
-                    if (v + q >= L) continue;
-                    const double q0 = pq[q].x - E.r0, q1 = pq[q].y - E.r1;
-                    const double sq = q0 * q0 + q1 * q1;
-                    if (!(sq < P.cull_t && sq > 0)) continue;  // agents only (cross_and_rescue.py:147-150)
-                    const unsigned long long key = ((unsigned long long)(unsigned)iq[q] << 32) | (unsigned)tq[q];
-                    if (m < kHocbfCap) {  // insertion into the sorted list
-                        int j = m;
-                        while (j > 0 && keys[(j - 1) * kBlock + threadIdx.x] > key) {
-                            keys[j * kBlock + threadIdx.x] = keys[(j - 1) * kBlock + threadIdx.x];
-                            --j;
-                        }
-                        keys[j * kBlock + threadIdx.x] = key;
-                    }
-                    ++m;
-                }
-            }
+            const int m = hocbf_scan(P, G, E, spos, sidx, start, keys, kBlock, threadIdx.x);
             E.count = m;
-            double ux = E.u0x, uy = E.u0y;  // no neighbour: filter not run, u0 unclipped
-            int32_t st = CBF_STATUS_IDLE;
-            if (m > kHocbfCap) {
-                st = CBF_STATUS_NBR_OVERFLOW;
-            } else if (m > 0) {
-                Sol S;
-                if (m <= kLdsRows) {  // rows computed once into the key area (keys read out first)
-                    unsigned long long kr[kLdsRows];
-#pragma unroll
-                    for (int i = 0; i < kLdsRows; ++i) kr[i] = i < m ? keys[i * kBlock + threadIdx.x] : 0ull;
-                    double* rl = reinterpret_cast<double*>(keys);
-#pragma unroll
-                    for (int i = 0; i < kLdsRows; ++i) {
-                        if (i < m) {
-                            const int sl = (int)(kr[i] & 0xFFFFFFFFull);
-                            const double2 o = spos[sl], ov = svel[sl];
-                            const double4 rw =
-                                hocbf_row(P, H, E.r0, E.r1, E.r2, E.r3, o.x, o.y, ov.x, ov.y, E.u0x, E.u0y);
-                            rl[(3 * i) * kBlock + threadIdx.x] = rw.x;
-                            rl[(3 * i + 1) * kBlock + threadIdx.x] = rw.y;
-                            rl[(3 * i + 2) * kBlock + threadIdx.x] = rw.z;
-                        }
-                    }
-                    LdsRows R{rl, m};
-                    S = solve_hocbf(P, E, R);
-                } else {
-                    SlotRows R{P, H, E, keys, spos, svel, m, 0};
-                    S = solve_hocbf(P, E, R);
-                }
-                clip_u(P, S, E, ux, uy);
-                st = pack_status(S);
+            if (m > kLdsRows && m <= kHocbfCap) {
+                hardq[kHardHeader + atomicAdd(&hardq[0], 1)] = slot;
+            } else if (m > 0 && m <= kLdsRows) {
+                const Sol S = hocbf_solve_lds<kLdsRows>(P, H, E, spos, svel, keys, reinterpret_cast<double*>(keys),
+                                                        kBlock, threadIdx.x, m);
                 solved = true;
+                hocbf_finish(P, &S, E, m, W, row_begin, row_end, r, c, T, pos_out, u, status, cnt, guard_rows, e0,
+                             e1, e2, e3);
+            } else {
+                hocbf_finish(P, nullptr, E, m, W, row_begin, row_end, r, c, T, pos_out, u, status, cnt, guard_rows,
+                             e0, e1, e2, e3);
             }
-            const long k = (long)(r - row_begin) * W + c;
-            const double2 pn = make_double2(E.r0 + T * ux, E.r1 + T * uy);
-            pos_out[k] = pn;
-            u[k] = make_double2(ux, uy);
-            status[k] = st;
-            if (cnt) cnt[k] = m;
-            ext_accumulate(r, row_begin, row_end, guard_rows, pn.y, e0, e1, e2, e3);
         }
     }
     if (solves) {
@@ -415,6 +449,42 @@ __global__ void __launch_bounds__(kBlock) k_lattice_filter_hocbf(
                       (unsigned long long)__popcll(mk));
     }
     if (ext_part) wave_extents(e0, e1, e2, e3, ext_part, (long)bx * (kBlock / 64) + (threadIdx.x >> 6));
+}
+
+// The queued egos (kLdsRows < m <= kHocbfCap), 64-lane blocks spread over the CUs: rescan, all
+// rows in this block's LDS, same solve.  The last block to finish empties the queue.
+__global__ void __launch_bounds__(64) k_lattice_filter_hocbf_wide(
+    KP P, HP H, CellGrid G, int W, int row_begin, int row_end, int win_row0, const double2* __restrict__ spos,
+    const double2* __restrict__ svel, const int32_t* __restrict__ sidx, const int32_t* __restrict__ start, double T,
+    double2* __restrict__ pos_out, double2* __restrict__ u, int32_t* __restrict__ status, int32_t* __restrict__ cnt,
+    int guard_rows, double* __restrict__ ext_part, unsigned long long* __restrict__ solves,
+    int32_t* __restrict__ hardq) {
+    __shared__ unsigned long long keys[kHocbfCap * 64];
+    __shared__ double rows[3 * kHocbfCap * 64];
+    const int nq = hardq[0];
+    double e0 = INFINITY, e1 = -INFINITY, e2 = -INFINITY, e3 = INFINITY;
+    int ns = 0;
+    for (int i = blockIdx.x * 64 + threadIdx.x; i < nq; i += gridDim.x * 64) {
+        const int slot = hardq[kHardHeader + i];
+        const int w = sidx[slot];
+        const int r = win_row0 + w / W, c = w % W;
+        const double2 pe = spos[slot], ve = svel[slot];
+        Ego E;
+        ego_init(P, E, pe.x, pe.y, ve.x, ve.y, ve.x, ve.y);
+        const int m = hocbf_scan(P, G, E, spos, sidx, start, keys, 64, threadIdx.x);
+        E.count = m;
+        const Sol S = hocbf_solve_lds<kHocbfCap>(P, H, E, spos, svel, keys, rows, 64, threadIdx.x, m);
+        ++ns;
+        hocbf_finish(P, &S, E, m, W, row_begin, row_end, r, c, T, pos_out, u, status, cnt, guard_rows, e0, e1, e2,
+                     e3);
+    }
+    if (solves) {
+        int t = (int)ns;
+        for (int o = 32; o > 0; o >>= 1) t += __shfl_xor(t, o, 64);
+        if (threadIdx.x == 0 && t) atomicAdd(&solves[16 * (blockIdx.x & 63)], (unsigned long long)t);
+    }
+    if (ext_part) wave_extents(e0, e1, e2, e3, ext_part, blockIdx.x);
+    hard_queue_done(hardq);
 }
 
 inline int nblocks(long n) { return (int)((n + kBlock - 1) / kBlock); }
@@ -479,7 +549,13 @@ extern "C" int cbf_lattice_advance_hocbf(const cbf_params* p, const cbf_hocbf* h
     hipLaunchKernelGGL(k_lattice_filter_hocbf, dim3(nb), dim3(kBlock), 0, s, make_kp(p), make_hp(hp), G, W, row_begin,
                        row_end, win_row0, Wk.ncell, Wk.spos, Wk.svel, Wk.sidx, Wk.start, T,
                        reinterpret_cast<double2*>(pos_out), reinterpret_cast<double2*>(u), status, nbr_count,
-                       guard_rows, ext_part, reinterpret_cast<unsigned long long*>(solves));
-    if (extents) launch_extents_finalize((int)lattice_ext_waves(n), ext_part, extents, s);
+                       guard_rows, ext_part, reinterpret_cast<unsigned long long*>(solves), Wk.hardq);
+    const int hb = nb < kHardBlocks ? nb : kHardBlocks;
+    hipLaunchKernelGGL(k_lattice_filter_hocbf_wide, dim3(hb), dim3(64), 0, s, make_kp(p), make_hp(hp), G, W,
+                       row_begin, row_end, win_row0, Wk.spos, Wk.svel, Wk.sidx, Wk.start, T,
+                       reinterpret_cast<double2*>(pos_out), reinterpret_cast<double2*>(u), status, nbr_count,
+                       guard_rows, ext_part ? ext_part + 4l * lattice_ext_waves(n) : nullptr,
+                       reinterpret_cast<unsigned long long*>(solves), Wk.hardq);
+    if (extents) launch_extents_finalize((int)lattice_ext_waves(n) + hb, ext_part, extents, s);
     return (int)hipGetLastError();
 }

@@ -58,6 +58,18 @@ __device__ __forceinline__ void ext_accumulate(int r, int row_begin, int row_end
     if (r >= row_begin + guard_rows) e3 = pmin(e3, ny);
 }
 
+// End of a 64-lane queue kernel (every block has read hardq[0]): the last block to finish
+// empties the queue, so an advance run again without a build starts from an empty queue.
+__device__ __forceinline__ void hard_queue_done(int32_t* hardq) {
+    if (threadIdx.x == 0) {
+        __threadfence();
+        if (atomicAdd(&hardq[1], 1) == (int)gridDim.x - 1) {
+            hardq[0] = 0;
+            hardq[1] = 0;
+        }
+    }
+}
+
 // Reduces nparts per-wave extents to out[4] (one-block kernel, defined in swarm.hip).
 void launch_extents_finalize(int nparts, const double* part, double* out, hipStream_t s);
 

@@ -115,7 +115,10 @@ __global__ void __launch_bounds__(kBlock) k_lattice_nominal_bin_ordered(
                          hardq[6] == H;
     int n_order = ordered ? start[ncell] : 0;
     n_order = n_order < 0 ? 0 : (n_order > nwin ? (int)nwin : n_order);
-    if (t == 0) hardq[0] = 0;  // hard-QP queue of this step's advance phase starts empty
+    if (t == 0) {  // hard-QP queue of this step's advance phase starts empty
+        hardq[0] = 0;
+        hardq[1] = 0;  // blocks of the queue kernel done (the last one empties the queue again)
+    }
     int cell = -1;
     long w = -1;
     double2 p = make_double2(0.0, 0.0);
@@ -601,7 +604,7 @@ __global__ void __launch_bounds__(64) k_lattice_filter_hard(KP P, int row_begin,
                                                             double2* __restrict__ pos_out, double2* __restrict__ u,
                                                             int32_t* __restrict__ status, int32_t* __restrict__ cnt,
                                                             int guard_rows, double* __restrict__ ext_part,
-                                                            const int32_t* __restrict__ hardq) {
+                                                            int32_t* __restrict__ hardq) {
     const int nq = hardq[0];
     const HardRec* q = reinterpret_cast<const HardRec*>(hardq + kHardHeader);
     double e0 = INFINITY, e1 = -INFINITY, e2 = -INFINITY, e3 = INFINITY;
@@ -630,15 +633,8 @@ __global__ void __launch_bounds__(64) k_lattice_filter_hard(KP P, int row_begin,
         if (cnt) cnt[h.k] = E.count;
         ext_accumulate(h.row, row_begin, row_end, guard_rows, pn.y, e0, e1, e2, e3);
     }
-    if (!ext_part) return;
-    const double m0 = wave_min(e0), m1 = wave_max(e1), m2 = wave_max(e2), m3 = wave_min(e3);
-    if (threadIdx.x == 0) {
-        double* o = ext_part + 4l * blockIdx.x;
-        o[0] = m0;
-        o[1] = m1;
-        o[2] = m2;
-        o[3] = m3;
-    }
+    if (ext_part) wave_extents(e0, e1, e2, e3, ext_part, blockIdx.x);
+    hard_queue_done(hardq);
 }
 
 

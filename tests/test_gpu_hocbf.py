@@ -119,3 +119,64 @@ def test_lattice_step_hocbf_vs_oracle(alpha):
         assert np.array_equal(st, ref["status"]), step
         assert np.array_equal(L.u.cpu().numpy(), ref["u"]), step
         assert np.array_equal(L.pos.cpu().numpy(), ref_pos), step
+
+
+@pytest.mark.parametrize("spacing", [0.09, 0.075])
+def test_lattice_hocbf_dense_queue(spacing):
+    """Dense lattices: egos with 9..24 neighbours take the queue + wide kernel
+    (k_lattice_filter_hocbf_wide), more than 24 report NBR_OVERFLOW with u = u0.  Teacher-forced
+    3 steps (the last two replayed from a hipGraph, so the queue is emptied and refilled),
+    bit-exact vs the oracle on every ego the cap admits."""
+    from cbf_amd import scenarios
+    W = H = 40
+    pos = scenarios.lattice(W, H, seed=3, spacing=spacing)
+    L = swarm.LatticeSwarm(pos, W, H, gain=scenarios.LATTICE_GAIN, barrier="euclidean_hocbf")
+    p, hp = po.Params(15), po.HocbfParams(1.0, 1.0)
+    seen_wide = seen_over = 0
+    for step in range(3):
+        if step == 1:
+            L.capture()
+        cur = L.pos.cpu().numpy().copy()
+        L.step()
+        torch.cuda.synchronize()
+        vel = coracle.consensus_lattice(W, H, 0, H, cur, scenarios.LATTICE_GAIN)
+        ref = coracle.filter_swarm_hocbf(p, hp, cur, vel, 0)
+        cnt = L.nbr_count.cpu().numpy()
+        st = L.status.cpu().numpy()
+        u = L.u.cpu().numpy()
+        assert np.array_equal(cnt, ref["cnt"]), step
+        over = cnt > 24
+        seen_wide += int(((cnt > 8) & ~over).sum())
+        seen_over += int(over.sum())
+        assert np.array_equal(st[~over], ref["status"][~over]), step
+        assert ((st[over] & 0xFF) == cbf_amd.STATUS_NBR_OVERFLOW).all()
+        want_u = np.where(over[:, None], vel, ref["u"])
+        assert np.array_equal(u, want_u), step
+        assert np.array_equal(L.pos.cpu().numpy(), coracle.euler(cur, want_u, 1 / 30)), step
+    assert seen_wide > 0
+    if spacing < 0.08:
+        assert seen_over > 0
+
+
+@pytest.mark.parametrize("barrier", ["reference", "euclidean_hocbf"])
+def test_lattice_advance_twice_without_build(barrier):
+    """The queue kernels empty their queue when done: an advance run again on the same build
+    gives the same outputs and counts exactly the same solves (no stale queue entries)."""
+    from cbf_amd import scenarios
+    W = H = 40
+    pos = scenarios.lattice(W, H, seed=5, spacing=0.085)
+    L = swarm.LatticeSwarm(pos, W, H, gain=scenarios.LATTICE_GAIN, barrier=barrier)
+    p0 = L.pos.clone()
+    L.build_phase()
+    outs, counts = [], []
+    for _ in range(3):
+        L.pos.copy_(p0)
+        L.reset_solves()
+        L.advance_phase()
+        torch.cuda.synchronize()
+        outs.append((L.pos.cpu().numpy(), L.u.cpu().numpy(), L.status.cpu().numpy()))
+        counts.append(L.solves_total())
+    assert counts[0] > 0 and counts[0] == counts[1] == counts[2]
+    for o in outs[1:]:
+        for a, b in zip(outs[0], o):
+            assert np.array_equal(a, b)
