@@ -306,6 +306,45 @@ __device__ __forceinline__ void scan_rows_joint(const int (&t0)[3], const int (&
 }
 #endif
 
+#ifndef CBF_SCAN_INLINE
+#define CBF_SCAN_INLINE 0
+#endif
+#ifndef CBF_INLINE_U
+#define CBF_INLINE_U 4
+#endif
+#if CBF_SCAN_U > 0
+// The joint 3-row scan with each candidate's nominal control loaded beside its position and the
+// row assembled in place for hits (no hit list, no per-lane gathers afterwards); same hit
+// order as the list, so the same per-quadrant minima bit for bit.
+template <bool FZ>
+__device__ __forceinline__ void scan_rows_inline(const int (&t0)[3], const int (&t1)[3], const KP& P, Ego& E,
+                                                 const double2* __restrict__ spos,
+                                                 const double2* __restrict__ svel) {
+    const int l0 = t1[0] - t0[0], l01 = l0 + (t1[1] - t0[1]);
+    const int L = l01 + (t1[2] - t0[2]);
+    for (int v = 0; v < L; v += CBF_INLINE_U) {
+        double2 p[CBF_INLINE_U], w[CBF_INLINE_U];
+#pragma unroll
+        for (int q = 0; q < CBF_INLINE_U; ++q) {
+            const int vv = v + q;
+            const int tt = vv < l0 ? t0[0] + vv : (vv < l01 ? t0[1] + (vv - l0) : t0[2] + (vv - l01));
+            if (vv < L) {
+                p[q] = spos[tt];
+                w[q] = svel[tt];
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < CBF_INLINE_U; ++q) {
+            if (v + q < L) {
+                const double e0 = p[q].x - E.r0, e1 = p[q].y - E.r1;
+                const double s = e0 * e0 + e1 * e1;
+                if (s < P.cull_t && s > 0) ego_add<FZ>(P, E, p[q].x, p[q].y, w[q].x, w[q].y);
+            }
+        }
+    }
+}
+#endif
+
 #ifndef CBF_HIT_MASK
 #define CBF_HIT_MASK 0
 #endif

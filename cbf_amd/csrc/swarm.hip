@@ -354,7 +354,11 @@ __device__ __forceinline__ int lattice_ego(const KP& P, const CellGrid& G, int W
         rt0[k] = in ? start[yy * G.nx + xa] : 0;
         rt1[k] = in ? start[yy * G.nx + xb + 1] : 0;
     }
-#if CBF_HIT_MASK && CBF_SCAN_U > 0 && CBF_ABLATE == 0
+#if CBF_SCAN_INLINE && CBF_SCAN_U > 0 && CBF_ABLATE == 0
+    scan_rows_inline<FZ>(rt0, rt1, P, E, spos, svel);
+    (void)hit_lds;
+    (void)spos32;
+#elif CBF_HIT_MASK && CBF_SCAN_U > 0 && CBF_ABLATE == 0
     {
         HitMask Hm;
         if (scan_rows_joint_mask(rt0, rt1, P, E, Hm, spos)) {

@@ -69,6 +69,12 @@ SETS["mask"] = {
     "mask_f2": ["-DCBF_HIT_MASK=1", "-DCBF_FLUSH_U=2"],
     "mask_s8": ["-DCBF_HIT_MASK=1", "-DCBF_SCAN_U=8"],
 }
+SETS["inline"] = {
+    "full": [],
+    "inline4": ["-DCBF_SCAN_INLINE=1"],
+    "inline3": ["-DCBF_SCAN_INLINE=1", "-DCBF_INLINE_U=3"],
+    "inline6": ["-DCBF_SCAN_INLINE=1", "-DCBF_INLINE_U=6"],
+}
 SETS["mc"] = {
     "mc_base": [],
     "mc_screen": ["-DCBF_MC_SCREEN=1"],
