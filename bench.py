@@ -196,7 +196,8 @@ def bench_lattice(args, ws, rank, local):
     codes = np.bincount(status & 0xFF, minlength=5)
     check = full_size_check(S, args) if (ws == 1 and not args.shard and args.barrier == "reference") else None
     achieved = FILTER_BYTES_PER_AGENT * n_local / (k_ms * 1e-3) / 1e9
-    traffic = load_pmc_traffic()
+    traffic = load_pmc_traffic() if args.barrier == "reference" else \
+        load_pmc_traffic(("k_lattice_filter_hocbf", "k_lattice_filter_hocbf_wide"))
     res = {
         "metric": METRIC,
         "value": solves / elapsed,
@@ -225,7 +226,7 @@ def bench_lattice(args, ws, rank, local):
                                       "box_infeasible": codes[3] / len(status)},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS,
-                     "traffic": traffic if args.barrier == "reference" else None,
+                     "traffic": traffic,
                      "kernel": "advance phase: k_lattice_filter + k_lattice_filter_hard" if args.barrier == "reference"
                      else "advance phase: k_lattice_filter_hocbf + k_lattice_filter_hocbf_wide",
                      "kernel_ms": k_ms,

@@ -171,7 +171,10 @@ __device__ __forceinline__ void ego_add(const KP& P, Ego& E, double o0, double o
 
 // Per-lane list of cull hits in LDS (column per lane: conflict-free), flushed into the ego's QP
 // after the scan.  More than kHitCap hits -> the caller rescans with direct assembly.
-constexpr int kHitCap = 16;
+#ifndef CBF_HIT_CAP
+#define CBF_HIT_CAP 16
+#endif
+constexpr int kHitCap = CBF_HIT_CAP;
 struct HitList {
     int n = 0;
     __device__ __forceinline__ void push(int* lds, int t) {

@@ -416,8 +416,16 @@ __device__ __forceinline__ int lattice_ego(const KP& P, const CellGrid& G, int W
 }
 
 // K4: one lane per cell-sorted slot; easy QPs solved in place, hard ones queued.
+#ifndef CBF_FILTER_WPE
+#define CBF_FILTER_WPE 0
+#endif
+#if CBF_FILTER_WPE > 0
+#define CBF_FILTER_BOUNDS __launch_bounds__(kBlock, CBF_FILTER_WPE)
+#else
+#define CBF_FILTER_BOUNDS __launch_bounds__(kBlock)
+#endif
 template <bool FZ>
-__global__ void __launch_bounds__(kBlock) k_lattice_filter(KP P, CellGrid G, int W, int row_begin, int row_end,
+__global__ void CBF_FILTER_BOUNDS k_lattice_filter(KP P, CellGrid G, int W, int row_begin, int row_end,
                                                            int win_row0, long ncell, const double2* __restrict__ spos,
                                                            const double2* __restrict__ svel,
                                                            const int32_t* __restrict__ sidx,

@@ -75,6 +75,14 @@ SETS["inline"] = {
     "inline3": ["-DCBF_SCAN_INLINE=1", "-DCBF_INLINE_U=3"],
     "inline6": ["-DCBF_SCAN_INLINE=1", "-DCBF_INLINE_U=6"],
 }
+SETS["occ"] = {
+    "full": [],
+    "cap12": ["-DCBF_HIT_CAP=12"],
+    "cap10_w8": ["-DCBF_HIT_CAP=10", "-DCBF_FILTER_WPE=8"],
+    "cap12_w7": ["-DCBF_HIT_CAP=12", "-DCBF_FILTER_WPE=7"],
+    "cap16_nobq_w8": ["-DCBF_BQ_LDS=0", "-DCBF_FILTER_WPE=8"],
+    "cap10_nobq_w8": ["-DCBF_HIT_CAP=10", "-DCBF_BQ_LDS=0", "-DCBF_FILTER_WPE=8"],
+}
 SETS["mc"] = {
     "mc_base": [],
     "mc_screen": ["-DCBF_MC_SCREEN=1"],

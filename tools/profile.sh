@@ -2,9 +2,9 @@
 # Profiling recipe run on the GPU box (gpurun): kernel-trace stats + separate PMC passes.
 set -o pipefail
 export TMPDIR=/tmp
-OUT=gpurun_out/prof
+OUT=${PROF_OUT:-gpurun_out/prof}
 mkdir -p $OUT
-B="python3 bench.py --steps 150 --warmup 40 --no-cpu-baseline --kernel-iters 10"
+B="python3 bench.py --steps 150 --warmup 40 --no-cpu-baseline --kernel-iters 10 ${BENCH_EXTRA:-}"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d $OUT/trace -o run -- $B > $OUT/trace.log 2>&1 || exit 1
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -f csv -d $OUT/pmc_fetch -o run -- $B > $OUT/pmc_fetch.log 2>&1 || exit 2
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -f csv -d $OUT/pmc_write -o run -- $B > $OUT/pmc_write.log 2>&1 || exit 3

@@ -59,8 +59,14 @@ def main(prof, rnd):
         summary[k] = e
     with open(os.path.join(ROOT, "profiles", f"{rnd}_pmc.json"), "w") as f:
         json.dump(summary, f, indent=1, sort_keys=True)
-    with open(os.path.join(ROOT, "profiles", "pmc_summary.json"), "w") as f:
-        json.dump({"round": rnd, **summary}, f, indent=1, sort_keys=True)
+    # merged: kernels of an earlier summary that this run did not profile are kept
+    path = os.path.join(ROOT, "profiles", "pmc_summary.json")
+    merged = {}
+    if os.path.exists(path):
+        merged = {k: v for k, v in json.load(open(path)).items() if isinstance(v, dict)}
+    merged.update(summary)
+    with open(path, "w") as f:
+        json.dump({"round": rnd, **merged}, f, indent=1, sort_keys=True)
     for k, e in sorted(summary.items(), key=lambda kv: -(kv[1].get("avg_duration_ns") or 0)):
         print(f"{k:28s} dur={((e.get('avg_duration_ns') or 0) / 1e3):8.2f} us  "
               f"hbm={(e.get('hbm_bytes_per_launch') or 0) / 1e6:8.2f} MB  valu={e.get('SQ_INSTS_VALU', 0):.3g}")
