@@ -451,16 +451,17 @@ __global__ void __launch_bounds__(kBlock) k_lattice_filter_hocbf(
     if (ext_part) wave_extents(e0, e1, e2, e3, ext_part, (long)bx * (kBlock / 64) + (threadIdx.x >> 6));
 }
 
-// The queued egos (kLdsRows < m <= kHocbfCap), 64-lane blocks spread over the CUs: rescan, all
-// rows in this block's LDS, same solve.  The last block to finish empties the queue.
+// The queued egos (kLdsRows < m <= kHocbfCap), 64-lane blocks spread over the CUs (up to
+// kWideBlocks, so a queue of up to 64 k egos is one lane each): rescan, all rows in this
+// block's LDS, same solve.  The last block to finish empties the queue.
 __global__ void __launch_bounds__(64) k_lattice_filter_hocbf_wide(
     KP P, HP H, CellGrid G, int W, int row_begin, int row_end, int win_row0, const double2* __restrict__ spos,
     const double2* __restrict__ svel, const int32_t* __restrict__ sidx, const int32_t* __restrict__ start, double T,
     double2* __restrict__ pos_out, double2* __restrict__ u, int32_t* __restrict__ status, int32_t* __restrict__ cnt,
     int guard_rows, double* __restrict__ ext_part, unsigned long long* __restrict__ solves,
     int32_t* __restrict__ hardq) {
-    __shared__ unsigned long long keys[kHocbfCap * 64];
-    __shared__ double rows[3 * kHocbfCap * 64];
+    __shared__ double rows[3 * kHocbfCap * 64];  // the keys live in its first third until read out
+    unsigned long long* keys = reinterpret_cast<unsigned long long*>(rows);
     const int nq = hardq[0];
     double e0 = INFINITY, e1 = -INFINITY, e2 = -INFINITY, e3 = INFINITY;
     int ns = 0;
@@ -550,7 +551,8 @@ extern "C" int cbf_lattice_advance_hocbf(const cbf_params* p, const cbf_hocbf* h
                        row_end, win_row0, Wk.ncell, Wk.spos, Wk.svel, Wk.sidx, Wk.start, T,
                        reinterpret_cast<double2*>(pos_out), reinterpret_cast<double2*>(u), status, nbr_count,
                        guard_rows, ext_part, reinterpret_cast<unsigned long long*>(solves), Wk.hardq);
-    const int hb = nb < kHardBlocks ? nb : kHardBlocks;
+    const long nw = (n + 63) / 64;
+    const int hb = nw < kWideBlocks ? (int)nw : kWideBlocks;
     hipLaunchKernelGGL(k_lattice_filter_hocbf_wide, dim3(hb), dim3(64), 0, s, make_kp(p), make_hp(hp), G, W,
                        row_begin, row_end, win_row0, Wk.spos, Wk.svel, Wk.sidx, Wk.start, T,
                        reinterpret_cast<double2*>(pos_out), reinterpret_cast<double2*>(u), status, nbr_count,

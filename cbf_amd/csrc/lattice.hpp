@@ -75,7 +75,12 @@ void launch_extents_finalize(int nparts, const double* part, double* out, hipStr
 
 // partial extents: one record per wave of the filter grid, then one per hard-QP block
 inline long lattice_ext_waves(long win_n) { return (win_n + kBlock - 1) / kBlock * (kBlock / 64); }
-inline size_t lattice_ext_bytes(long win_n) { return align256(32 * (size_t)(lattice_ext_waves(win_n) + kHardBlocks)); }
+// grid of the HOCBF wide kernel (64-lane blocks; 4 fit a CU by LDS, so 1024 cover the chip)
+constexpr int kWideBlocks = 1024;
+constexpr int kQueueBlocksMax = kHardBlocks > kWideBlocks ? kHardBlocks : kWideBlocks;
+inline size_t lattice_ext_bytes(long win_n) {
+    return align256(32 * (size_t)(lattice_ext_waves(win_n) + kQueueBlocksMax));
+}
 
 inline int check_lattice(const cbf_params* p, const cbf_grid* grid, int32_t W, int32_t H, int32_t row_begin,
                          int32_t row_end, int32_t win_row0, int32_t win_rows, const double* pos, void* workspace,
