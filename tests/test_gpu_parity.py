@@ -396,6 +396,46 @@ def test_allpairs_nonfinite_coordinates():
     assert np.array_equal(got["u"], ref["u"], equal_nan=True)
 
 
+@pytest.mark.parametrize("offset", [0.0, 37.0, 150.0, 260.0, 1e3, 1e31])
+def test_allpairs_split_screen_exact_at_any_magnitude(offset):
+    """Split all-pairs (scalar-operand screen): the expanded-form fp32 screen (used while
+    16 u M^2 <= cull_t, M <~ 200), the difference form beyond it, and no screen beyond 1e30 all
+    only reject what the exact test rejects.  Pairs straddle the cull radius; a few entities sit
+    at large magnitude so that some waves mix the two forms."""
+    rng = np.random.default_rng(15)
+    p = po.Params(15)
+    fp = swarm.FilterParams()
+    n, n_obs = 2000, 100
+    pos, vel = _random_swarm(rng, n, n_obs, 2.0)
+    for i, d in enumerate([np.nextafter(0.2, 0), 0.2, np.nextafter(0.2, 1), 0.19999999, 0.20000001]):
+        pos[300 + 2 * i + 1] = pos[300 + 2 * i] + [d, 0.0]
+        pos[500 + 2 * i + 1] = pos[500 + 2 * i] + [d * 0.6, d * 0.8]
+        pos[700 + 2 * i + 1] = pos[700 + 2 * i] + [-d * 0.8, d * 0.6]
+    pos = pos + offset
+    pos[1500:1510] += 5e3  # a wave whose egos need the difference form, next to expanded ones
+    pos[1510:1512] = pos[1500:1502] + [0.1, 0.1]
+    ref = coracle.filter_swarm(p, pos, vel, n_obs)
+    out = swarm.filter_swarm(fp, _t(pos), _t(vel), n_obs, method="allpairs")
+    assert np.array_equal(out["nbr_count"].cpu().numpy(), ref["cnt"])
+    assert np.array_equal(out["u"].cpu().numpy(), ref["u"])
+    assert np.array_equal(out["status"].cpu().numpy(), ref["status"])
+
+
+def test_allpairs_split_nonfinite_coordinates():
+    rng = np.random.default_rng(16)
+    p = po.Params(15)
+    fp = swarm.FilterParams()
+    pos, vel = _random_swarm(rng, 700, 30, 0.8)
+    pos[40] = [np.nan, 0.1]
+    pos[41] = [np.inf, 0.0]
+    pos[690] = [0.05, np.nan]
+    ref = coracle.filter_swarm(p, pos, vel, 30)
+    out = swarm.filter_swarm(fp, _t(pos), _t(vel), 30, method="allpairs")
+    assert np.array_equal(out["nbr_count"].cpu().numpy(), ref["cnt"])
+    assert np.array_equal(out["status"].cpu().numpy(), ref["status"])
+    assert np.array_equal(out["u"].cpu().numpy(), ref["u"], equal_nan=True)
+
+
 @pytest.mark.parametrize("n,n_obs,spread", [(40, 10, 0.3), (5000, 1500, 4.0), (20000, 0, 6.0)])
 def test_allpairs_split_vs_oracle(n, n_obs, spread):
     """cbf_filter_allpairs_split (candidate chunks in separate workgroups, merged in order) gives

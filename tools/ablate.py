@@ -19,12 +19,11 @@ sys.path.insert(0, ROOT)
 OUT = os.path.join(ROOT, "tools", "_ablate")
 SETS = {}
 SETS["allpairs"] = {
-    "ap_base": [],
-    "ap_packed": ["-DCBF_AP_PACKED=1"],
-    "ap_packed_s16": ["-DCBF_AP_PACKED=1", "-DCBF_AP_SCREEN=16"],
-    "ap_packed_s16_t1024": ["-DCBF_AP_PACKED=1", "-DCBF_AP_SCREEN=16", "-DCBF_AP_TILE=1024"],
-    "ap_packed_s32_t1024": ["-DCBF_AP_PACKED=1", "-DCBF_AP_SCREEN=32", "-DCBF_AP_TILE=1024"],
-    "ap_s16_t1024": ["-DCBF_AP_SCREEN=16", "-DCBF_AP_TILE=1024"],
+    "ap_lds_diff": [],
+    "ap_lds_expand": ["-DCBF_AP_EXPAND=1"],
+    "ap_lds_diff_packed": ["-DCBF_AP_PACKED=1"],
+    "ap_dpp": ["-DCBF_AP_DPP=1", "-DCBF_AP_EXPAND=1"],
+    "ap_dpp_diff": ["-DCBF_AP_DPP=1"],
 }
 SETS["phases"] = {
     "full": [],

@@ -1,24 +1,26 @@
-"""GPU box: size of the lattice step's hard-QP queue (QPs not solved at the origin) over a run."""
+"""GPU box: size of the lattice step's hard-QP queue over a run.
+
+An ego solved at the origin returns u = clip(u0); the hard queue holds the egos whose QP needed
+the full solve, i.e. (filter ran) and u != clip(u0).  Prints the count every 20 steps.
+"""
 import os, sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-import numpy as np
 import torch
 from cbf_amd import scenarios, swarm
-
-def a256(b):
-    return (b + 255) // 256 * 256
 
 W = H = 1024
 L = swarm.LatticeSwarm(scenarios.lattice(W, H, seed=0), W, H, gain=scenarios.LATTICE_GAIN)
 n = W * H
-nc = L.grid.nx * L.grid.ny
-ntiles = (nc + 2047) // 2048
-off = a256(4 * nc) + a256(4 * (nc + 1)) + a256(8 * ntiles) + 256 + a256(16 * n) + 2 * a256(16 * n) + a256(4 * n) + a256(16 * n) + a256(8 * n)
-for step in range(240):
+ms = 15.0
+for step in range(int(os.environ.get("DIAG_STEPS", "240"))):
     L.step()
-    if step % 20 == 0 or step == 239:
+    if step % 20 == 0:
         torch.cuda.synchronize()
-        hq = int(L.ws[off:off + 4].view(torch.int32).item())
-        st = L.status.cpu().numpy()
-        print(step, "hard queue", hq, "frac", hq / n, "relaxed", float(((st & 0xFF) == 2).mean()),
-              "iters max", int((st >> 8).max()), flush=True)
+        ran = L.nbr_count.view(-1) > 0
+        u0 = L.vel.view(-1, 2).clamp(-ms, ms)
+        hard = ran & (L.u.view(-1, 2) != u0).any(dim=1)
+        st = L.status.view(-1)
+        print(step, "hard", int(hard.sum()), "frac %.5f" % (float(hard.sum()) / n),
+              "relaxed %.4f" % float(((st & 0xFF) == 2).float().mean()),
+              "iters max", int((st >> 8).max()), "nbrs mean %.2f max %d" % (float(L.nbr_count.float().mean()),
+                                                                             int(L.nbr_count.max())), flush=True)
