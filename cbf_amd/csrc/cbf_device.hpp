@@ -666,6 +666,177 @@ __device__ __forceinline__ Sol solve_ego(const KP& P, const Ego& E) {
     return S;
 }
 
+// solve_ego with its loops rolled and the 8 right-hand sides in the lane's own LDS column (a
+// LaneCol: element i of the column at p[i * kBlock], the layout of the hit list, so it never
+// touches another lane's slots; a double occupies elements 2h, 2h + 1): same planes, order,
+// arithmetic and tolerances as solve_planes_reg / solve_ego, so bit-identical results, but about
+// 30 VGPRs instead of ~170, so it can run inside a kernel whose occupancy is set elsewhere (the
+// lattice filter solves its rare hard QPs in place with it).  Plane h's normal comes from a
+// uniform select, never from a runtime-indexed register array (that would be lowered to scratch).
+struct LaneCol {
+    int* p;  // this lane's column: p[i * kBlock]
+    __device__ __forceinline__ double get(int h) const {
+        return __hiloint2double(p[(2 * h + 1) * kBlock], p[2 * h * kBlock]);
+    }
+    __device__ __forceinline__ void set(int h, double v) const {
+        p[2 * h * kBlock] = __double2loint(v);
+        p[(2 * h + 1) * kBlock] = __double2hiint(v);
+    }
+};
+__device__ __forceinline__ void plane_normal(const KP& P, int h, double& a0, double& a1) {
+    switch (h) {
+        case 0: a0 = 1.0, a1 = 0.0; break;
+        case 1: a0 = 0.0, a1 = 1.0; break;
+        case 2: a0 = -1.0, a1 = 0.0; break;
+        case 3: a0 = 0.0, a1 = -1.0; break;
+        case 4: a0 = P.n0[0], a1 = P.n1[0]; break;
+        case 5: a0 = P.n0[1], a1 = P.n1[1]; break;
+        case 6: a0 = P.n0[2], a1 = P.n1[2]; break;
+        default: a0 = P.n0[3], a1 = P.n1[3]; break;
+    }
+}
+
+__device__ __forceinline__ int solve8_lds(const KP& P, const LaneCol& b, unsigned mask, double& xo0, double& xo1) {
+    double x0 = 0.0, x1 = 0.0;
+#pragma unroll 1
+    for (int h = 0; h < 8; ++h) {
+        if (!((mask >> h) & 1u)) continue;
+        double ah0, ah1;
+        plane_normal(P, h, ah0, ah1);
+        const double bh = b.get(h);
+        if ((ah0 * x0 + ah1 * x1) - bh <= FEAS_TOL * pmax(1.0, fabs(bh))) continue;
+        const double n2 = ah0 * ah0 + ah1 * ah1;
+        if (!(n2 > 0)) return h;
+        const double t = bh / n2;
+        const double p0 = t * ah0, p1 = t * ah1;
+        const double d0 = -ah1, d1 = ah0;
+        double rh = 0.0, ah = 0.0, rl = 0.0, al = 0.0;
+        bool has_hi = false, has_lo = false;
+#pragma unroll 1
+        for (int j = 0; j < h; ++j) {
+            if (!((mask >> j) & 1u)) continue;
+            double aj0, aj1;
+            plane_normal(P, j, aj0, aj1);
+            const double ad = aj0 * d0 + aj1 * d1;
+            const double r = b.get(j) - (aj0 * p0 + aj1 * p1);
+            if (ad > 0) {
+                if (!has_hi || r * ah < rh * ad) {
+                    rh = r;
+                    ah = ad;
+                }
+                has_hi = true;
+            } else if (ad < 0) {
+                if (!has_lo || r * al > rl * ad) {
+                    rl = r;
+                    al = ad;
+                }
+                has_lo = true;
+            }
+        }
+        double s = 0.0;
+        bool s_hi = false;
+        if (has_hi && rh < 0) {
+            s = rh / ah;
+            s_hi = true;
+        }
+        if (has_lo && (s_hi ? (rh * al > rl * ah) : (rl < 0))) s = rl / al;
+        x0 = p0 + s * d0;
+        x1 = p1 + s * d1;
+        bool ok = true;
+#pragma unroll 1
+        for (int j = 0; j <= h; ++j) {
+            if (!((mask >> j) & 1u)) continue;
+            double aj0, aj1;
+            plane_normal(P, j, aj0, aj1);
+            const double bj = b.get(j);
+            ok = ok && ((aj0 * x0 + aj1 * x1) - bj <= FEAS_TOL * pmax(1.0, fabs(bj)));
+        }
+        if (!ok) return h;
+    }
+    xo0 = x0;
+    xo1 = x1;
+    return -1;
+}
+
+__device__ __forceinline__ Sol solve_ego_lds(const KP& P, const Ego& E, const LaneCol& b) {
+    const Box B = box_rhs(P, E);
+    b.set(0, pmin(B.S[0], B.S[4]));
+    b.set(1, pmin(B.S[1], B.S[6]));
+    b.set(2, pmin(B.S[2], B.S[5]));
+    b.set(3, pmin(B.S[3], B.S[7]));
+    double q0 = E.bq0, q1 = E.bq1, q2 = E.bq2, q3 = E.bq3;
+    const unsigned mask = 0xFu | (E.present << 4);
+    Sol S;
+    S.status = CBF_STATUS_OPTIMAL;
+    S.iters = 0;
+    S.x0 = S.x1 = 0.0;
+    if ((E.present & 9u) == 9u || (E.present & 6u) == 6u) {  // strip pre-check, as solve_ego
+        for (;;) {
+            bool dead = false;
+            if ((E.present & 9u) == 9u) {
+                const double s = q0 + q3;
+                const double tb = FEAS_TOL * (pmax(1.0, fabs(q0)) + pmax(1.0, fabs(q3)));
+                dead = dead || (s < -tb - 1e-9 * (1.0 + fabs(q0) + fabs(q3)));
+            }
+            if ((E.present & 6u) == 6u) {
+                const double s = q1 + q2;
+                const double tb = FEAS_TOL * (pmax(1.0, fabs(q1)) + pmax(1.0, fabs(q2)));
+                dead = dead || (s < -tb - 1e-9 * (1.0 + fabs(q1) + fabs(q2)));
+            }
+            if (!dead || S.iters >= P.relax_cap) break;
+            q0 = q0 + 1.0;
+            q1 = q1 + 1.0;
+            q2 = q2 + 1.0;
+            q3 = q3 + 1.0;
+            S.iters++;
+        }
+    }
+    for (;;) {
+        b.set(4, q0);
+        b.set(5, q1);
+        b.set(6, q2);
+        b.set(7, q3);
+        const int fail = solve8_lds(P, b, mask, S.x0, S.x1);
+        if (fail < 0) break;
+        if (fail < 4) {  // reported as at the first solve: no relaxation applied
+            S.status = CBF_STATUS_BOX_INFEASIBLE;
+            S.iters = 0;
+            S.x0 = S.x1 = 0.0;
+            q0 = E.bq0;
+            q1 = E.bq1;
+            q2 = E.bq2;
+            q3 = E.bq3;
+            b.set(4, q0);
+            b.set(5, q1);
+            b.set(6, q2);
+            b.set(7, q3);
+            break;
+        }
+        if (S.iters >= P.relax_cap) {
+            S.status = CBF_STATUS_RELAX_CAP;
+            S.x0 = S.x1 = 0.0;
+            break;
+        }
+        q0 = q0 + 1.0;
+        q1 = q1 + 1.0;
+        q2 = q2 + 1.0;
+        q3 = q3 + 1.0;
+        S.iters++;
+    }
+    if (S.status == CBF_STATUS_OPTIMAL && S.iters > 0) S.status = CBF_STATUS_RELAXED;
+    double v = 0.0;
+#pragma unroll 1
+    for (int h = 0; h < 8; ++h)
+        if ((mask >> h) & 1u) {
+            double a0, a1;
+            plane_normal(P, h, a0, a1);
+            const double d = (a0 * S.x0 + a1 * S.x1) - b.get(h);
+            if (d > v) v = d;
+        }
+    S.viol = v;
+    return S;
+}
+
 // The common case of solve_ego without the Seidel machinery: after the strip pre-relaxation the
 // origin satisfies every plane, so solve8 would return x = 0 at its first call.  Same arithmetic
 // as solve_ego on that path (bit-identical Sol); returns false when the full solve is needed.

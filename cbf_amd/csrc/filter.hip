@@ -219,7 +219,7 @@ __device__ __forceinline__ void allpairs_scan(const KP& P, double r0, double r1,
             for (int w = 1; w < kBlock / 64; ++w) mt = pmax(mt, L.smax[w]);
             const double M = pmax(mt, m_ego);
             int t = 0;
-            float te;
+            float te = 0.0f;
             const bool exp_ok = CBF_AP_EXPAND && expand_threshold(P.cull_t, M, ex, ey, te);
             // the form is chosen per wave (both are exact filters; a mixed wave would run both)
             if (__ballot(exp_ok) == __ballot(1)) {

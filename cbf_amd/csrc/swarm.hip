@@ -264,11 +264,18 @@ __global__ void __launch_bounds__(kBlock) k_lattice_scatter_ordered(long nwin, c
 
 // Tail of the lattice filter for one owned ego whose QP rows are accumulated in E: solve at the
 // origin or queue to the hard kernel, clip, Euler, outputs.  Returns 1 (done, *ny = new y) or 2.
+// CBF_HARD_INLINE (off): a QP the origin does not solve is solved in place by solve_ego_lds (rolled
+// loops, right-hand sides in the lane's LDS column `bl`, ~30 VGPRs) instead of being queued for
+// k_lattice_filter_hard, which then is not launched (its launch + queue round trip was ~10 us a
+// step for ~0.3 % of the egos).
+#ifndef CBF_HARD_INLINE
+#define CBF_HARD_INLINE 0  // measured slower: advance 55.7 vs 51.9 us (tools/ablate.py, set hardinline)
+#endif
 template <bool FZ>
 __device__ __forceinline__ int ego_finish(const KP& P, Ego& E, int W, int row_begin, int r, int c, double T,
                                           double2* __restrict__ pos_out, double2* __restrict__ u,
                                           int32_t* __restrict__ status, int32_t* __restrict__ cnt,
-                                          int32_t* __restrict__ hardq, double* ny) {
+                                          int32_t* __restrict__ hardq, double* ny, int* bl = nullptr) {
     const double2 pe = make_double2(E.r0, E.r1);
     const long k = (long)(r - row_begin) * W + c;
     double ux, uy;
@@ -286,7 +293,10 @@ __device__ __forceinline__ int ego_finish(const KP& P, Ego& E, int W, int row_be
         S.viol = E.bq0 + E.bq1 + E.bq2 + E.bq3;
         asm volatile("" ::"v"(S.viol));
 #else
-        if (!solve_easy(P, E, S)) {
+        if (solve_easy(P, E, S)) {
+        } else if (CBF_HARD_INLINE && bl) {
+            S = solve_ego_lds(P, E, LaneCol{bl});
+        } else {
             HardRec* q = reinterpret_cast<HardRec*>(hardq + kHardHeader);
             HardRec& h = q[atomicAdd(&hardq[0], 1)];
             h.r0 = E.r0;
@@ -412,7 +422,10 @@ __device__ __forceinline__ int lattice_ego(const KP& P, const CellGrid& G, int W
 #endif
 #endif
     *nbrs = E.count;
-    return ego_finish<FZ>(P, E, W, row_begin, r, c, T, pos_out, u, status, cnt, hardq, ny);
+    // the lane's LDS column (its hit slots) is free again after the flush: the 8 right-hand sides
+    // of an in-place solve (other lanes' columns may still be in use by their waves)
+    int* bl = CBF_HIT_MASK ? nullptr : hit_lds + threadIdx.x;
+    return ego_finish<FZ>(P, E, W, row_begin, r, c, T, pos_out, u, status, cnt, hardq, ny, bl);
 }
 
 // K4: one lane per cell-sorted slot; easy QPs solved in place, hard ones queued.
@@ -438,6 +451,8 @@ __global__ void CBF_FILTER_BOUNDS k_lattice_filter(KP P, CellGrid G, int W, int 
                                                            const float2* __restrict__ spos32, int cnt_begin,
                                                            int cnt_end) {
     // hit rows + a dummy row (branch-free push) + 4 x fp64 per-quadrant minima (CBF_BQ_LDS)
+    // (>= 16 ints per lane: also the lane's 8 fp64 right-hand sides of an in-place hard solve)
+    static_assert(CBF_HIT_MASK || (kHitCap + 1) + (CBF_BQ_LDS ? 8 : 0) >= 16, "hit LDS too small for solve_ego_lds");
     __shared__ int hit_lds[CBF_HIT_MASK ? 1 : (kHitCap + 1) * kBlock + (CBF_BQ_LDS ? 8 * kBlock : 0)];
     const int bx = xcd_block();
     const int slot = bx * kBlock + threadIdx.x;
@@ -837,9 +852,13 @@ static int lattice_advance(const cbf_params* p, const cbf_grid* grid, int32_t W,
                            po, uo, status, nbr_count, guard_rows, ext_part,
                            reinterpret_cast<unsigned long long*>(solves), Wk.hardq, Wk.spos32, cnt_begin, cnt_end);
     }
-    hipLaunchKernelGGL(k_lattice_filter_hard, dim3(hb), dim3(64), 0, s, kp, row_begin, row_end, T, po, uo, status,
-                       nbr_count, guard_rows, ext_part ? ext_part + 4l * lattice_ext_waves(n) : nullptr, Wk.hardq);
-    if (extents) launch_extents_finalize((int)lattice_ext_waves(n) + hb, ext_part, extents, s);
+    // queue kernel only when the filter queues (CBF_HARD_INLINE solves hard QPs in place)
+    const bool queued = !CBF_HARD_INLINE || CBF_HIT_MASK || (CBF_LDS_STAGE && !ext_part);
+    if (queued)
+        hipLaunchKernelGGL(k_lattice_filter_hard, dim3(hb), dim3(64), 0, s, kp, row_begin, row_end, T, po, uo, status,
+                           nbr_count, guard_rows, ext_part ? ext_part + 4l * lattice_ext_waves(n) : nullptr,
+                           Wk.hardq);
+    if (extents) launch_extents_finalize((int)lattice_ext_waves(n) + (queued ? hb : 0), ext_part, extents, s);
     return (int)hipGetLastError();
 }
 

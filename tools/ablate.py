@@ -25,6 +25,10 @@ SETS["allpairs"] = {
     "ap_dpp": ["-DCBF_AP_DPP=1", "-DCBF_AP_EXPAND=1"],
     "ap_dpp_diff": ["-DCBF_AP_DPP=1"],
 }
+SETS["hardinline"] = {
+    "queue": [],
+    "inline": ["-DCBF_HARD_INLINE=1"],
+}
 SETS["phases"] = {
     "full": [],
     "no_qp": ["-DCBF_ABLATE=1"],
