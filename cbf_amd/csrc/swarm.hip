@@ -98,6 +98,12 @@ __global__ void __launch_bounds__(kBlock) k_euler(int n, double2* __restrict__ p
     pos[i] = make_double2(p.x + T * v.x, p.y + T * v.y);
 }
 
+// CBF_NOMINAL_IN_SCATTER: the Laplacian nominal control is computed by the scatter (K3) instead of
+// K1, so it never makes an HBM round trip (tools/ablate.py, set nominal).
+#ifndef CBF_NOMINAL_IN_SCATTER
+#define CBF_NOMINAL_IN_SCATTER 1
+#endif
+
 // Lattice step K1, temporally coherent form: lanes walk the window agents in the previous step's
 // cell order (identity on the first call), so consecutive lanes mostly share a cell; each run of
 // equal cells in a wave takes its slots with ONE atomic (run length), and the later scatter
@@ -222,11 +228,13 @@ __global__ void __launch_bounds__(kBlock) k_lattice_nominal_bin_ordered(
         bcs[t] = make_int4(-1, 0, (int)w, 0);
         return;
     }
+#if !CBF_NOMINAL_IN_SCATTER
     const int r = win_row0 + (int)(w / W), c = (int)(w % W);
     const double2 a = lattice_sum(pos, w, r, c, W, H);
     const double2 u0 = make_double2(a.x * gain, a.y * gain);
     wvel[w] = u0;
     if (vel_out != wvel && r >= row_begin && r < row_end) vel_out[(long)(r - row_begin) * W + c] = u0;
+#endif
     bcs[t] = make_int4(cell, base + lane - my_leader, (int)w, 0);
 }
 
@@ -239,7 +247,9 @@ __global__ void __launch_bounds__(kBlock) k_lattice_scatter_ordered(long nwin, c
                                                                     int32_t* __restrict__ sidx,
                                                                     float2* __restrict__ spos32,
                                                                     int32_t* __restrict__ order_state, long n,
-                                                                    long ncell, int win_row0, int H) {
+                                                                    long ncell, int win_row0, int H, int W,
+                                                                    int row_begin, int row_end, double gain,
+                                                                    double2* __restrict__ vel_out) {
     const long t = (long)xcd_block() * kBlock + threadIdx.x;
     if (t == 0) {  // the cell order now exists for this window and grid: the next build walks it
         order_state[0] = 1;
@@ -254,7 +264,20 @@ __global__ void __launch_bounds__(kBlock) k_lattice_scatter_ordered(long nwin, c
     const int d = start[b.x] + b.y;
     const double2 p = pos[b.z];
     spos[d] = p;
+#if CBF_NOMINAL_IN_SCATTER
+    // K1's nominal control computed here: the agent's position is loaded anyway and its 4
+    // lattice neighbours are mostly in L2 (cell order ~ lattice order), so the u0 round trip
+    // through HBM (written by K1, gathered back here) disappears
+    const int r = win_row0 + b.z / W, c = b.z % W;
+    const double2 a = lattice_sum(pos, b.z, r, c, W, H);
+    const double2 u0 = make_double2(a.x * gain, a.y * gain);
+    svel[d] = u0;
+    if (r >= row_begin && r < row_end) vel_out[(long)(r - row_begin) * W + c] = u0;
+    (void)wvel;
+#else
     svel[d] = wvel[b.z];
+    (void)W, (void)row_begin, (void)row_end, (void)gain, (void)vel_out;
+#endif
     sidx[d] = b.z;
 #if CBF_SCAN32
     spos32[d] = make_float2((float)p.x, (float)p.y);
@@ -812,7 +835,8 @@ static int lattice_build(const cbf_params* p, const cbf_grid* grid, int32_t W, i
                        Wk.start, Wk.ncell, bcs, Wk.hardq, ext_keys, X);
     launch_scan(Wk, s);
     hipLaunchKernelGGL(k_lattice_scatter_ordered, dim3(nblk(n)), dim3(kBlock), 0, s, n, bcs, Wk.start, p2, wv, Wk.spos,
-                       Wk.svel, Wk.sidx, Wk.spos32, Wk.hardq + 2, n, Wk.ncell, win_row0, H);
+                       Wk.svel, Wk.sidx, Wk.spos32, Wk.hardq + 2, n, Wk.ncell, win_row0, H, W, row_begin, row_end, gain,
+                       reinterpret_cast<double2*>(vel_out));
     return (int)hipGetLastError();
 }
 

@@ -29,6 +29,10 @@ SETS["hardinline"] = {
     "queue": [],
     "inline": ["-DCBF_HARD_INLINE=1"],
 }
+SETS["nominal"] = {
+    "in_scatter": [],
+    "in_bin": ["-DCBF_NOMINAL_IN_SCATTER=0"],
+}
 SETS["phases"] = {
     "full": [],
     "no_qp": ["-DCBF_ABLATE=1"],
