@@ -107,11 +107,11 @@ __global__ void __launch_bounds__(kBlock) k_euler(int n, double2* __restrict__ p
 // Lattice step K1, temporally coherent form: lanes walk the window agents in the previous step's
 // cell order (identity on the first call), so consecutive lanes mostly share a cell; each run of
 // equal cells in a wave takes its slots with ONE atomic (run length), and the later scatter
-// writes nearly sequential slots.  Per-lane result bcs[t] = {cell, slot, agent, -}.
+// writes nearly sequential slots.  Per-lane result bcs[t] = {cell, slot, agent} (12 B).
 __global__ void __launch_bounds__(kBlock) k_lattice_nominal_bin_ordered(
     CellGrid G, int W, int H, int row_begin, int row_end, int win_row0, int win_rows, const double2* __restrict__ pos,
     double gain, double2* __restrict__ wvel, double2* __restrict__ vel_out, int32_t* __restrict__ count,
-    const int32_t* __restrict__ order, const int32_t* __restrict__ start, long ncell, int4* __restrict__ bcs,
+    const int32_t* __restrict__ order, const int32_t* __restrict__ start, long ncell, int3* __restrict__ bcs,
     int32_t* __restrict__ hardq, unsigned long long* __restrict__ ext_keys, ExtSpec X) {
     const long t = (long)xcd_block() * kBlock + threadIdx.x;
     const long nwin = (long)win_rows * W;
@@ -225,7 +225,7 @@ __global__ void __launch_bounds__(kBlock) k_lattice_nominal_bin_ordered(
     base = __shfl(base, my_leader, 64);
     if (t >= nwin) return;
     if (cell < 0) {
-        bcs[t] = make_int4(-1, 0, (int)w, 0);
+        bcs[t] = make_int3(-1, 0, (int)w);
         return;
     }
 #if !CBF_NOMINAL_IN_SCATTER
@@ -235,10 +235,10 @@ __global__ void __launch_bounds__(kBlock) k_lattice_nominal_bin_ordered(
     wvel[w] = u0;
     if (vel_out != wvel && r >= row_begin && r < row_end) vel_out[(long)(r - row_begin) * W + c] = u0;
 #endif
-    bcs[t] = make_int4(cell, base + lane - my_leader, (int)w, 0);
+    bcs[t] = make_int3(cell, base + lane - my_leader, (int)w);
 }
 
-__global__ void __launch_bounds__(kBlock) k_lattice_scatter_ordered(long nwin, const int4* __restrict__ bcs,
+__global__ void __launch_bounds__(kBlock) k_lattice_scatter_ordered(long nwin, const int3* __restrict__ bcs,
                                                                     const int32_t* __restrict__ start,
                                                                     const double2* __restrict__ pos,
                                                                     const double2* __restrict__ wvel,
@@ -259,7 +259,7 @@ __global__ void __launch_bounds__(kBlock) k_lattice_scatter_ordered(long nwin, c
         order_state[4] = H;
     }
     if (t >= nwin) return;
-    const int4 b = bcs[t];
+    const int3 b = bcs[t];
     if (b.x < 0) return;
     const int d = start[b.x] + b.y;
     const double2 p = pos[b.z];
@@ -654,7 +654,8 @@ __global__ void __launch_bounds__(64) k_lattice_filter_hard(KP P, int row_begin,
                                                             double2* __restrict__ pos_out, double2* __restrict__ u,
                                                             int32_t* __restrict__ status, int32_t* __restrict__ cnt,
                                                             int guard_rows, double* __restrict__ ext_part,
-                                                            int32_t* __restrict__ hardq) {
+                                                            int32_t* __restrict__ hardq, int cap) {
+    (void)cap;
     const int nq = hardq[0];
     const HardRec* q = reinterpret_cast<const HardRec*>(hardq + kHardHeader);
     double e0 = INFINITY, e1 = -INFINITY, e2 = -INFINITY, e3 = INFINITY;
@@ -829,7 +830,7 @@ static int lattice_build(const cbf_params* p, const cbf_grid* grid, int32_t W, i
     // unsharded: the window is the owned rows, so the nominal controls go straight to vel_out
     double2* wv = (win_row0 == row_begin && win_rows == row_end - row_begin) ? reinterpret_cast<double2*>(vel_out)
                                                                               : Wk.wvel;
-    int4* bcs = reinterpret_cast<int4*>(Wk.cs);
+    int3* bcs = reinterpret_cast<int3*>(Wk.cs);  // 12 B per agent (the area reserves 16)
     hipLaunchKernelGGL(k_lattice_nominal_bin_ordered, dim3(nblk(n)), dim3(kBlock), 0, s, G, W, H, row_begin, row_end,
                        win_row0, win_rows, p2, gain, wv, reinterpret_cast<double2*>(vel_out), Wk.count, Wk.sidx,
                        Wk.start, Wk.ncell, bcs, Wk.hardq, ext_keys, X);
@@ -881,7 +882,7 @@ static int lattice_advance(const cbf_params* p, const cbf_grid* grid, int32_t W,
     if (queued)
         hipLaunchKernelGGL(k_lattice_filter_hard, dim3(hb), dim3(64), 0, s, kp, row_begin, row_end, T, po, uo, status,
                            nbr_count, guard_rows, ext_part ? ext_part + 4l * lattice_ext_waves(n) : nullptr,
-                           Wk.hardq);
+                           Wk.hardq, (int)n);
     if (extents) launch_extents_finalize((int)lattice_ext_waves(n) + (queued ? hb : 0), ext_part, extents, s);
     return (int)hipGetLastError();
 }

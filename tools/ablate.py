@@ -33,6 +33,7 @@ SETS["nominal"] = {
     "in_scatter": [],
     "in_bin": ["-DCBF_NOMINAL_IN_SCATTER=0"],
 }
+SETS["head"] = {"tree": []}
 SETS["phases"] = {
     "full": [],
     "no_qp": ["-DCBF_ABLATE=1"],
@@ -114,8 +115,12 @@ VARIANTS = {
 
 
 def _variants():
+    rf = os.path.join(OUT, "revs")
+    revs = open(rf).read().split() if os.path.exists(rf) else []
     if os.environ.get("ABLATE_SET"):
-        return {k: (None, d) for k, d in SETS[os.environ["ABLATE_SET"]].items()}
+        v = {k: (None, d) for k, d in SETS[os.environ["ABLATE_SET"]].items()}
+        v.update({f"rev_{rev}": (rev, []) for rev in revs})
+        return v
     """Compile-time ablations of the working tree plus `rev_<git rev>` builds listed in
     tools/_ablate/revs (one revision per line), so a change can be A/B-timed against an
     earlier commit in the same process."""
