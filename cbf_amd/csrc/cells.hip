@@ -24,6 +24,9 @@ __global__ void __launch_bounds__(kBlock) k_bin(CellGrid G, int n, const double2
 // so the critical path is load -> publish/look-back -> store.  The kernel re-zeroes the counts it
 // consumed.  Spins are bounded; a timeout sets sctl[2].
 constexpr unsigned long long kFlagAgg = 1ull << 32, kFlagInc = 2ull << 32;
+#ifndef CBF_SCAN_SUMAGG
+#define CBF_SCAN_SUMAGG 0  // predecessor aggregates summed directly (measured no faster: build 43.0 vs 41.6 us)
+#endif
 
 __device__ __forceinline__ unsigned long long ld_state(const unsigned long long* p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -77,6 +80,37 @@ __global__ void __launch_bounds__(kBlock) k_scan_onepass(int32_t* __restrict__ c
             if (lane == 0) st_state(&tstate[0], ep | kFlagInc | (unsigned)agg);
         } else {
             if (lane == 0) st_state(&tstate[tile], ep | kFlagAgg | (unsigned)agg);
+#if CBF_SCAN_SUMAGG
+            // exclusive prefix = the sum of ALL predecessors' aggregates: their loads are
+            // independent (4 per lane in flight), so the critical path is one publish -> load
+            // round trip instead of a chain of inclusive values through the tiles (no tile
+            // publishes an inclusive value in this form; tile 0's equals its aggregate)
+            int part = 0;
+            long spins = 0;
+            for (int i0 = 0; i0 < tile; i0 += 4 * 64) {
+                unsigned long long v[4];
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const int idx = i0 + k * 64 + lane;
+                    v[k] = idx < tile ? ld_state(&tstate[idx]) : (ep | kFlagAgg);
+                }
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const int idx = i0 + k * 64 + lane;
+                    while ((v[k] & ~((1ull << 34) - 1)) != ep || (v[k] & (3ull << 32)) == 0) {
+                        if (++spins > (1l << 24)) {
+                            sctl[2] = 1;
+                            break;
+                        }
+                        __builtin_amdgcn_s_sleep(1);
+                        v[k] = ld_state(&tstate[idx]);
+                    }
+                    if (idx < tile) part += (int)(unsigned)(v[k] & 0xFFFFFFFFull);
+                }
+            }
+            for (int o = 32; o > 0; o >>= 1) part += __shfl_xor(part, o, 64);
+            excl = part;
+#else
             int top = tile - 1;
             long spins = 0;
             while (true) {
@@ -102,6 +136,7 @@ __global__ void __launch_bounds__(kBlock) k_scan_onepass(int32_t* __restrict__ c
                 top -= 64;
             }
             if (lane == 0) st_state(&tstate[tile], ep | kFlagInc | (unsigned)(excl + agg));
+#endif
         }
         if (lane == 0) {
             s_excl = excl;

@@ -34,6 +34,7 @@ SETS["nominal"] = {
     "in_bin": ["-DCBF_NOMINAL_IN_SCATTER=0"],
 }
 SETS["head"] = {"tree": []}
+SETS["scan"] = {"sumagg": [], "lookback": ["-DCBF_SCAN_SUMAGG=0"]}
 SETS["phases"] = {
     "full": [],
     "no_qp": ["-DCBF_ABLATE=1"],
