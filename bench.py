@@ -441,6 +441,11 @@ def main():
     ap.add_argument("--shard", action="store_true",
                     help="cfg4: run the sharded step (halo pack + collective + unpack) even on one rank")
     args = ap.parse_args()
+    # stdout carries exactly one JSON line: everything else that writes to fd 1 (RCCL prints a
+    # version banner at communicator init) goes to stderr
+    sys.stdout.flush()
+    json_out = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
     ws, rank, local = _dist_env()
     import torch
     if ws > 1 or args.shard:
@@ -478,7 +483,8 @@ def main():
             res["cpu_baseline"] = cpu_baseline_cert(*sample, budget_s=min(args.cpu_budget, 8.0))
         else:
             res["cpu_baseline"] = None
-        print(json.dumps(res), flush=True)
+        json_out.write(json.dumps(res) + "\n")
+        json_out.flush()
     if torch.distributed.is_initialized():
         torch.distributed.destroy_process_group()
 
