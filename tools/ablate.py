@@ -34,6 +34,7 @@ SETS["nominal"] = {
     "in_bin": ["-DCBF_NOMINAL_IN_SCATTER=0"],
 }
 SETS["head"] = {"tree": []}
+SETS["hcert"] = {"cert": [], "nocert": ["-DCBF_HOCBF_CERT=0"]}
 SETS["scan"] = {"sumagg": [], "lookback": ["-DCBF_SCAN_SUMAGG=0"]}
 SETS["phases"] = {
     "full": [],
@@ -176,6 +177,7 @@ def run(rounds, iters, W, H):
     pos0 = scenarios.lattice(W, H, seed=0)
     grid = swarm.grid_for_points(pos0, 0.2)
     cp = _lib.make_params(15)
+    hp = _lib.CbfHocbf(1.0, 1.0)
     ws_bytes = max(L.cbf_lattice_workspace_size(W, H, C.byref(grid)) for L in libs.values())
     st = {}
     for name in names:
@@ -196,9 +198,15 @@ def run(rounds, iters, W, H):
                 _lib.check(L.cbf_lattice_build(cp, C.byref(grid), W, H, 0, H, 0, H, P(s["pos"]), 0.25, P(s["vel"]),
                                                P(s["ws"]), ws_bytes, _lib.stream_handle()), "build")
                 e1.record()
-                _lib.check(L.cbf_lattice_advance(cp, C.byref(grid), W, H, 0, H, 0, H, P(s["pos"]), 1 / 30,
-                                                 P(s["pos"]), P(s["u"]), P(s["status"]), P(s["cnt"]), 0, None, None,
-                                                 P(s["ws"]), ws_bytes, _lib.stream_handle()), "advance")
+                if os.environ.get("ABLATE_HOCBF"):  # the Euclidean HOCBF advance instead
+                    _lib.check(L.cbf_lattice_advance_hocbf(cp, C.byref(hp), C.byref(grid), W, H, 0, H, 0, H,
+                                                           P(s["pos"]), 1 / 30, P(s["pos"]), P(s["u"]),
+                                                           P(s["status"]), P(s["cnt"]), 0, None, None, P(s["ws"]),
+                                                           ws_bytes, _lib.stream_handle()), "advance_hocbf")
+                else:
+                    _lib.check(L.cbf_lattice_advance(cp, C.byref(grid), W, H, 0, H, 0, H, P(s["pos"]), 1 / 30,
+                                                     P(s["pos"]), P(s["u"]), P(s["status"]), P(s["cnt"]), 0, None,
+                                                     None, P(s["ws"]), ws_bytes, _lib.stream_handle()), "advance")
                 e2.record()
                 torch.cuda.synchronize()
                 if r > 0:
