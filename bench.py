@@ -270,8 +270,10 @@ def bench_allpairs(args, ws, rank, local):
             "roofline": {"bound": "valu-fp32", "achieved": pairs * 6 / 1e12, "peak": 157.3, "unit": "TFLOP/s",
                          "frac": pairs * 6 / 1e12 / 157.3, "traffic": None, "kernel": "k_allpairs_partial",
                          "note": "every pair is screened in fp32 (2 sub, 1 mul, 1 fma, 1 min = 6 flops, FMA counted "
-                                 "as 2) against the MI355X FP32 vector peak; candidates the screen passes are "
-                                 "re-tested exactly in fp64 (neighbour sets bit-identical to the oracle)"}}
+                                 "as 2) against the MI355X FP32 vector peak, which counts packed FMAs; the screen "
+                                 "is non-packed (no packed min) and its VALU issue is ~80 % busy (DESIGN.md sec. 4, "
+                                 "profiles/r01_allpairs_dpp_pmc.txt); candidates the screen passes are re-tested "
+                                 "exactly in fp64 (neighbour sets bit-identical to the oracle)"}}
 
 
 def bench_mc(args, ws, rank, local):
