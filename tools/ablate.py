@@ -34,7 +34,7 @@ SETS["nominal"] = {
     "in_bin": ["-DCBF_NOMINAL_IN_SCATTER=0"],
 }
 SETS["head"] = {"tree": []}
-SETS["hcert"] = {"cert": [], "nocert": ["-DCBF_HOCBF_CERT=0"]}
+SETS["hcert"] = {"nocert": [], "cert": ["-DCBF_HOCBF_CERT=1"]}
 SETS["scan"] = {"sumagg": [], "lookback": ["-DCBF_SCAN_SUMAGG=0"]}
 SETS["phases"] = {
     "full": [],
@@ -117,20 +117,14 @@ VARIANTS = {
 
 
 def _variants():
+    """Compile-time ablations of the working tree (the set named by ABLATE_SET, else VARIANTS)
+    plus `rev_<git rev>` builds listed in tools/_ablate/revs (one revision per line), so a change
+    can be A/B-timed against an earlier commit in the same process."""
     rf = os.path.join(OUT, "revs")
     revs = open(rf).read().split() if os.path.exists(rf) else []
-    if os.environ.get("ABLATE_SET"):
-        v = {k: (None, d) for k, d in SETS[os.environ["ABLATE_SET"]].items()}
-        v.update({f"rev_{rev}": (rev, []) for rev in revs})
-        return v
-    """Compile-time ablations of the working tree plus `rev_<git rev>` builds listed in
-    tools/_ablate/revs (one revision per line), so a change can be A/B-timed against an
-    earlier commit in the same process."""
-    v = {k: (None, d) for k, d in VARIANTS.items()}
-    rf = os.path.join(OUT, "revs")
-    if os.path.exists(rf):
-        for rev in open(rf).read().split():
-            v[f"rev_{rev}"] = (rev, [])
+    sel = SETS[os.environ["ABLATE_SET"]] if os.environ.get("ABLATE_SET") else VARIANTS
+    v = {k: (None, d) for k, d in sel.items()}
+    v.update({f"rev_{rev}": (rev, []) for rev in revs})
     return v
 
 
