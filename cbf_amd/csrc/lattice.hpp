@@ -59,10 +59,11 @@ __device__ __forceinline__ void ext_accumulate(int r, int row_begin, int row_end
 }
 
 // End of a 64-lane queue kernel (every block has read hardq[0]): the last block to finish
-// empties the queue, so an advance run again without a build starts from an empty queue.
+// empties the queue, so an advance run again without a build starts from an empty queue.  No
+// fence: the block is one wave whose load of hardq[0] has returned (the loop used it) before
+// lane 0's atomic, and nothing the reset could race with is written by the queue kernels.
 __device__ __forceinline__ void hard_queue_done(int32_t* hardq) {
     if (threadIdx.x == 0) {
-        __threadfence();
         if (atomicAdd(&hardq[1], 1) == (int)gridDim.x - 1) {
             hardq[0] = 0;
             hardq[1] = 0;
