@@ -14,9 +14,12 @@ namespace cbf {
 
 constexpr int kScanTile = 2048;  // 256 threads x 8 cells
 #ifndef CBF_HARD_BLOCKS
-#define CBF_HARD_BLOCKS 256
+#define CBF_HARD_BLOCKS 128
 #endif
-constexpr int kHardBlocks = CBF_HARD_BLOCKS;  // grid (64-lane blocks) of the hard-QP kernel of the lattice step
+// grid (64-lane blocks) of the hard-QP kernel of the lattice step: 8 k lanes cover the ~3 k queued
+// QPs of cfg4 one per lane; each block ends with an atomic on the done counter, so fewer blocks
+// end sooner (advance 50.2 us at 128 blocks, 51.0 at 256, 59.8 at 1024; tools/ablate.py set hard)
+constexpr int kHardBlocks = CBF_HARD_BLOCKS;
 constexpr int kHardHeader = 16;  // int32 words ahead of the hard-QP records (count + padding)
 
 // A QP the filter kernel could not solve at the origin, queued with its assembled state.

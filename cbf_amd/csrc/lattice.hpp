@@ -76,8 +76,13 @@ void launch_extents_finalize(int nparts, const double* part, double* out, hipStr
 
 // partial extents: one record per wave of the filter grid, then one per hard-QP block
 inline long lattice_ext_waves(long win_n) { return (win_n + kBlock - 1) / kBlock * (kBlock / 64); }
-// grid of the HOCBF wide kernel (64-lane blocks; 4 fit a CU by LDS, so 1024 cover the chip)
-constexpr int kWideBlocks = 1024;
+// grid of the HOCBF wide kernel (64-lane blocks): 256 x 64 lanes cover the ~10 k queued egos of
+// cfg4 one per lane; every block ends with one atomic on the done counter, so a larger grid only
+// lengthens that serialised chain (1024 blocks: advance 231 vs 221 us, tools/ablate.py set wide)
+#ifndef CBF_WIDE_BLOCKS
+#define CBF_WIDE_BLOCKS 256
+#endif
+constexpr int kWideBlocks = CBF_WIDE_BLOCKS;
 constexpr int kQueueBlocksMax = kHardBlocks > kWideBlocks ? kHardBlocks : kWideBlocks;
 inline size_t lattice_ext_bytes(long win_n) {
     return align256(32 * (size_t)(lattice_ext_waves(win_n) + kQueueBlocksMax));

@@ -34,6 +34,7 @@ SETS["nominal"] = {
     "in_bin": ["-DCBF_NOMINAL_IN_SCATTER=0"],
 }
 SETS["head"] = {"tree": []}
+SETS["wide"] = {"w1024": [], "w256": ["-DCBF_WIDE_BLOCKS=256"], "w128": ["-DCBF_WIDE_BLOCKS=128"]}
 SETS["hcert"] = {"nocert": [], "cert": ["-DCBF_HOCBF_CERT=1"]}
 SETS["scan"] = {"sumagg": [], "lookback": ["-DCBF_SCAN_SUMAGG=0"]}
 SETS["phases"] = {
@@ -60,9 +61,9 @@ SETS["scan32"] = {
 }
 SETS["hard"] = {
     "full": [],
+    "hard64": ["-DCBF_HARD_BLOCKS=64"],
+    "hard128": ["-DCBF_HARD_BLOCKS=128"],
     "hard1024": ["-DCBF_HARD_BLOCKS=1024"],
-    "hard2048": ["-DCBF_HARD_BLOCKS=2048"],
-    "hard4096": ["-DCBF_HARD_BLOCKS=4096"],
 }
 SETS["xcd"] = {
     "full": [],
