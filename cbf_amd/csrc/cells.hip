@@ -6,8 +6,10 @@ namespace cbf {
 namespace {
 
 __global__ void __launch_bounds__(kBlock) k_bin(CellGrid G, int n, const double2* __restrict__ pos,
-                                                int32_t* __restrict__ count, int2* __restrict__ cs) {
+                                                int32_t* __restrict__ count, int2* __restrict__ cs,
+                                                int32_t* __restrict__ sctl) {
     const int i = blockIdx.x * kBlock + threadIdx.x;
+    if (CBF_SCAN_EPOCH_BIN && i == 0) scan_epoch_advance(sctl);
     if (i >= n) return;
     const double2 p = pos[i];
     const int c = cell_coord(p.y, G.y0, G.inv_h, G.ny) * G.nx + cell_coord(p.x, G.x0, G.inv_h, G.nx);
@@ -19,7 +21,7 @@ __global__ void __launch_bounds__(kBlock) k_bin(CellGrid G, int n, const double2
 // dispatcher hands out workgroups in increasing order, so a tile only waits on tiles whose blocks
 // are already resident.  Tile status is one 64-bit word {epoch:30 | flag:2 | value:32} written
 // and read with agent-scope relaxed atomics (the payload travels inside the flag word, so no
-// fence is needed); the epoch (bumped by the last tile to finish) makes words of earlier
+// fence is needed); the epoch (advanced before each scan, CBF_SCAN_EPOCH_BIN) makes words of earlier
 // launches invisible without a reset pass.  The epoch load and the count loads are independent,
 // so the critical path is load -> publish/look-back -> store.  The kernel re-zeroes the counts it
 // consumed.  Spins are bounded; a timeout sets sctl[2].
@@ -142,7 +144,7 @@ __global__ void __launch_bounds__(kBlock) k_scan_onepass(int32_t* __restrict__ c
             s_excl = excl;
             if (tile == ntiles - 1) start[ncell] = excl + agg;
             // the last block to finish bumps the epoch: every block has read it by then
-            if (atomicAdd(&sctl[0], 1) == ntiles - 1) {
+            if (!CBF_SCAN_EPOCH_BIN && atomicAdd(&sctl[0], 1) == ntiles - 1) {
                 sctl[0] = 0;
                 __hip_atomic_store(&sctl[1], (int)((epoch + 1) & 0x3FFFFFFFu), __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_AGENT);
@@ -194,7 +196,7 @@ int scan_and_scatter(const CellGrid& G, const CellWs& W, int n, const double2* p
 
 int build_cells(const CellGrid& G, const CellWs& W, int n, const double2* pos, const double2* vel, const int32_t*,
                 hipStream_t s) {
-    hipLaunchKernelGGL(k_bin, dim3(nblk(n)), dim3(kBlock), 0, s, G, n, pos, W.count, W.cs);
+    hipLaunchKernelGGL(k_bin, dim3(nblk(n)), dim3(kBlock), 0, s, G, n, pos, W.count, W.cs, W.sctl);
     return scan_and_scatter(G, W, n, pos, vel, s);
 }
 

@@ -102,4 +102,15 @@ int scan_and_scatter(const CellGrid& G, const CellWs& W, int n, const double2* p
 // Exclusive scan of W.count into W.start (and re-zeroes W.count).
 void launch_scan(const CellWs& W, hipStream_t s);
 
+// CBF_SCAN_EPOCH_BIN: the scan's tile-state epoch is advanced by thread 0 of the bin kernel that
+// precedes every scan (stream order makes it visible), instead of by the last scan block to
+// finish -- that needed a returning atomic on one counter from each of the ~270 scan blocks, a
+// serialised chain at the end of the scan.
+#ifndef CBF_SCAN_EPOCH_BIN
+#define CBF_SCAN_EPOCH_BIN 1
+#endif
+__device__ __forceinline__ void scan_epoch_advance(int32_t* sctl) {
+    sctl[1] = (sctl[1] + 1) & 0x3FFFFFFF;  // one thread, before the scan kernel starts
+}
+
 }  // namespace cbf

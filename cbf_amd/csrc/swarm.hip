@@ -112,8 +112,9 @@ __global__ void __launch_bounds__(kBlock) k_lattice_nominal_bin_ordered(
     CellGrid G, int W, int H, int row_begin, int row_end, int win_row0, int win_rows, const double2* __restrict__ pos,
     double gain, double2* __restrict__ wvel, double2* __restrict__ vel_out, int32_t* __restrict__ count,
     const int32_t* __restrict__ order, const int32_t* __restrict__ start, long ncell, int3* __restrict__ bcs,
-    int32_t* __restrict__ hardq, unsigned long long* __restrict__ ext_keys, ExtSpec X) {
+    int32_t* __restrict__ hardq, unsigned long long* __restrict__ ext_keys, ExtSpec X, int32_t* __restrict__ sctl) {
     const long t = (long)xcd_block() * kBlock + threadIdx.x;
+    if (CBF_SCAN_EPOCH_BIN && t == 0) scan_epoch_advance(sctl);
     const long nwin = (long)win_rows * W;
     // hardq[2..4]: the previous build left a cell order for this window size and grid (else
     // identity); the order only permutes the work, so a stale one costs speed, never results
@@ -833,7 +834,7 @@ static int lattice_build(const cbf_params* p, const cbf_grid* grid, int32_t W, i
     int3* bcs = reinterpret_cast<int3*>(Wk.cs);  // 12 B per agent (the area reserves 16)
     hipLaunchKernelGGL(k_lattice_nominal_bin_ordered, dim3(nblk(n)), dim3(kBlock), 0, s, G, W, H, row_begin, row_end,
                        win_row0, win_rows, p2, gain, wv, reinterpret_cast<double2*>(vel_out), Wk.count, Wk.sidx,
-                       Wk.start, Wk.ncell, bcs, Wk.hardq, ext_keys, X);
+                       Wk.start, Wk.ncell, bcs, Wk.hardq, ext_keys, X, Wk.sctl);
     launch_scan(Wk, s);
     hipLaunchKernelGGL(k_lattice_scatter_ordered, dim3(nblk(n)), dim3(kBlock), 0, s, n, bcs, Wk.start, p2, wv, Wk.spos,
                        Wk.svel, Wk.sidx, Wk.spos32, Wk.hardq + 2, n, Wk.ncell, win_row0, H, W, row_begin, row_end, gain,
