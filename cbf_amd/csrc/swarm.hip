@@ -292,6 +292,9 @@ __global__ void __launch_bounds__(kBlock) k_lattice_scatter_ordered(long nwin, c
 // loops, right-hand sides in the lane's LDS column `bl`, ~30 VGPRs) instead of being queued for
 // k_lattice_filter_hard, which then is not launched (its launch + queue round trip was ~10 us a
 // step for ~0.3 % of the egos).
+#ifndef CBF_NT_STORES
+#define CBF_NT_STORES 0
+#endif
 #ifndef CBF_HARD_INLINE
 #define CBF_HARD_INLINE 0  // measured slower: advance 55.7 vs 51.9 us (tools/ablate.py, set hardinline)
 #endif
@@ -344,10 +347,21 @@ __device__ __forceinline__ int ego_finish(const KP& P, Ego& E, int W, int row_be
         st = pack_status(S);
     }
     const double2 pn = make_double2(pe.x + T * ux, pe.y + T * uy);
+#if CBF_NT_STORES
+    // outputs are not read again by this kernel: non-temporal stores keep them from displacing
+    // the cell-sorted candidate lines in L2
+    __builtin_nontemporal_store(pn.x, &pos_out[k].x);
+    __builtin_nontemporal_store(pn.y, &pos_out[k].y);
+    __builtin_nontemporal_store(ux, &u[k].x);
+    __builtin_nontemporal_store(uy, &u[k].y);
+    __builtin_nontemporal_store(st, &status[k]);
+    if (cnt) __builtin_nontemporal_store(E.count, &cnt[k]);
+#else
     pos_out[k] = pn;
     u[k] = make_double2(ux, uy);
     status[k] = st;
     if (cnt) cnt[k] = E.count;
+#endif
     *ny = pn.y;
     return 1;
 }
