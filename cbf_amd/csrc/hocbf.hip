@@ -369,6 +369,11 @@ __global__ void __launch_bounds__(kBlock) k_hocbf_indexed(KP P, HP H, const doub
 // rows recomputed from the cell-sorted state during the solve; clip, Euler, outputs as
 // k_lattice_filter.  More than kHocbfCap neighbours: CBF_STATUS_NBR_OVERFLOW, u = u0.
 constexpr int kHocbfCap = 24;
+// CBF_HSORT_REG: the main HOCBF lattice kernel appends hits unsorted and sorts its <= 8 keys in
+// registers instead of keeping the LDS list sorted by insertion (tools/ablate.py set hsort)
+#ifndef CBF_HSORT_REG
+#define CBF_HSORT_REG 1
+#endif
 #ifndef CBF_HSCAN_U
 #define CBF_HSCAN_U 6
 #endif
@@ -376,6 +381,10 @@ constexpr int kHScan = CBF_HSCAN_U;  // candidates in flight per lane in the HOC
 
 // Neighbour scan of one ego (slot) over its 3x3 cells; hits go into the ascending-entity key
 // list keys[i * ks + lane] (first kHocbfCap of them).  Returns the hit count m.
+// SORTED: keep the list sorted by insertion (all kHocbfCap slots); otherwise append the first
+// kLdsRows hits unsorted (the main kernel sorts them in registers, hocbf_sort8; egos with more
+// hits are queued and rescanned sorted by the wide kernel).
+template <bool SORTED = true>
 __device__ __forceinline__ int hocbf_scan(const KP& P, const CellGrid& G, const Ego& E, const double2* __restrict__ spos,
                                           const int32_t* __restrict__ sidx, const int32_t* __restrict__ start,
                                           unsigned long long* keys, int ks, int lane) {
@@ -414,7 +423,9 @@ __device__ __forceinline__ int hocbf_scan(const KP& P, const CellGrid& G, const 
             const double sq = q0 * q0 + q1 * q1;
             if (!(sq < P.cull_t && sq > 0)) continue;  // agents only (cross_and_rescue.py:147-150)
             const unsigned long long key = ((unsigned long long)(unsigned)iq[q] << 32) | (unsigned)tq[q];
-            if (m < kHocbfCap) {  // insertion into the sorted list
+            if (!SORTED) {
+                if (m < kLdsRows) keys[m * ks + lane] = key;
+            } else if (m < kHocbfCap) {  // insertion into the sorted list
                 int j = m;
                 while (j > 0 && keys[(j - 1) * ks + lane] > key) {
                     keys[j * ks + lane] = keys[(j - 1) * ks + lane];
@@ -428,15 +439,36 @@ __device__ __forceinline__ int hocbf_scan(const KP& P, const CellGrid& G, const 
     return m;
 }
 
+// Ascending sort of 8 keys in registers (Batcher odd-even merge network, 19 compare-exchanges;
+// keys are unique, so the order equals the insertion-sorted list's).
+__device__ __forceinline__ void cas(unsigned long long& a, unsigned long long& b) {
+    const unsigned long long lo = a < b ? a : b, hi = a < b ? b : a;
+    a = lo;
+    b = hi;
+}
+__device__ __forceinline__ void hocbf_sort8(unsigned long long (&k)[8]) {
+    cas(k[0], k[1]); cas(k[2], k[3]); cas(k[4], k[5]); cas(k[6], k[7]);
+    cas(k[0], k[2]); cas(k[1], k[3]); cas(k[4], k[6]); cas(k[5], k[7]);
+    cas(k[1], k[2]); cas(k[5], k[6]);
+    cas(k[0], k[4]); cas(k[1], k[5]); cas(k[2], k[6]); cas(k[3], k[7]);
+    cas(k[2], k[4]); cas(k[3], k[5]);
+    cas(k[1], k[2]); cas(k[3], k[4]); cas(k[5], k[6]);
+}
+
 // Rows of the m <= cap sorted keys computed once into lds[(3i + c) * ks + lane] (the keys are
-// read out first when the row area aliases the key area), then the relaxation loop.
-template <int CAP>
+// read out first when the row area aliases the key area), then the relaxation loop.  SORT: the
+// keys were appended unsorted (cap = 8): sort them in registers first (absent slots = ~0 sort last).
+template <int CAP, bool SORT = false>
 __device__ __forceinline__ Sol hocbf_solve_lds(const KP& P, const HP& H, const Ego& E, const double2* __restrict__ spos,
                                                const double2* __restrict__ svel, const unsigned long long* keys,
                                                double* rl, int ks, int lane, int m) {
     unsigned long long kr[CAP];
 #pragma unroll
-    for (int i = 0; i < CAP; ++i) kr[i] = i < m ? keys[i * ks + lane] : 0ull;
+    for (int i = 0; i < CAP; ++i) kr[i] = i < m ? keys[i * ks + lane] : ~0ull;
+    if constexpr (SORT) {
+        static_assert(CAP == 8, "hocbf_sort8 sorts 8 keys");
+        hocbf_sort8(kr);
+    }
 #pragma unroll
     for (int i = 0; i < CAP; ++i) {
         if (i < m) {
@@ -498,12 +530,12 @@ __global__ void __launch_bounds__(kBlock) k_lattice_filter_hocbf(
             const double2 pe = spos[slot], ve = svel[slot];
             Ego E;
             ego_init(P, E, pe.x, pe.y, ve.x, ve.y, ve.x, ve.y);
-            const int m = hocbf_scan(P, G, E, spos, sidx, start, keys, kBlock, threadIdx.x);
+            const int m = hocbf_scan<!CBF_HSORT_REG>(P, G, E, spos, sidx, start, keys, kBlock, threadIdx.x);
             E.count = m;
             if (m > kLdsRows && m <= kHocbfCap) {
                 hardq[kHardHeader + atomicAdd(&hardq[0], 1)] = slot;
             } else if (m > 0 && m <= kLdsRows) {
-                const Sol S = hocbf_solve_lds<kLdsRows>(P, H, E, spos, svel, keys, reinterpret_cast<double*>(keys),
+                const Sol S = hocbf_solve_lds<kLdsRows, CBF_HSORT_REG>(P, H, E, spos, svel, keys, reinterpret_cast<double*>(keys),
                                                         kBlock, threadIdx.x, m);
                 solved = true;
                 hocbf_finish(P, &S, E, m, W, row_begin, row_end, r, c, T, pos_out, u, status, cnt, guard_rows, e0,

@@ -34,6 +34,7 @@ SETS["nominal"] = {
     "in_bin": ["-DCBF_NOMINAL_IN_SCATTER=0"],
 }
 SETS["head"] = {"tree": []}
+SETS["hsort"] = {"reg": [], "insertion": ["-DCBF_HSORT_REG=0"]}
 SETS["nt"] = {"plain": [], "nt": ["-DCBF_NT_STORES=1"]}
 SETS["wide"] = {"w1024": [], "w256": ["-DCBF_WIDE_BLOCKS=256"], "w128": ["-DCBF_WIDE_BLOCKS=128"]}
 SETS["hcert"] = {"nocert": [], "cert": ["-DCBF_HOCBF_CERT=1"]}
