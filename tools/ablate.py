@@ -39,6 +39,7 @@ SETS["nt"] = {"plain": [], "nt": ["-DCBF_NT_STORES=1"]}
 SETS["wide"] = {"w1024": [], "w256": ["-DCBF_WIDE_BLOCKS=256"], "w128": ["-DCBF_WIDE_BLOCKS=128"]}
 SETS["hcert"] = {"nocert": [], "cert": ["-DCBF_HOCBF_CERT=1"]}
 SETS["scan"] = {"sumagg": [], "lookback": ["-DCBF_SCAN_SUMAGG=0"]}
+SETS["scanst"] = {"vst": [], "scalar": ["-DCBF_SCAN_VST=0"]}
 SETS["phases"] = {
     "full": [],
     "no_qp": ["-DCBF_ABLATE=1"],
