@@ -49,24 +49,26 @@ __global__ void __launch_bounds__(kBlock) k_scan_onepass(int32_t* __restrict__ c
     const int tile = blockIdx.x;
     const unsigned epoch = (unsigned)__hip_atomic_load(&sctl[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const unsigned long long ep = (unsigned long long)(epoch & 0x3FFFFFFFu) << 34;
-    const long base = (long)tile * kScanTile + threadIdx.x * 8;
-    int c[8];
+    constexpr int kPer = kScanTile / kBlock;  // cells per lane, a multiple of 4
+    const long base = (long)tile * kScanTile + threadIdx.x * kPer;
+    int c[kPer];
     int tot = 0;
-    if (base + 8 <= ncell) {  // 2 x 16-B loads (base is a multiple of 8 ints)
-        const int4 a = *reinterpret_cast<const int4*>(count + base);
-        const int4 b = *reinterpret_cast<const int4*>(count + base + 4);
-        c[0] = a.x, c[1] = a.y, c[2] = a.z, c[3] = a.w, c[4] = b.x, c[5] = b.y, c[6] = b.z, c[7] = b.w;
-        *reinterpret_cast<int4*>(count + base) = make_int4(0, 0, 0, 0);  // zeroed for the next build
-        *reinterpret_cast<int4*>(count + base + 4) = make_int4(0, 0, 0, 0);
+    if (base + kPer <= ncell) {  // 16-B loads (base is a multiple of kPer ints)
+#pragma unroll
+        for (int v = 0; v < kPer / 4; ++v) {
+            const int4 a = *reinterpret_cast<const int4*>(count + base + 4 * v);
+            c[4 * v] = a.x, c[4 * v + 1] = a.y, c[4 * v + 2] = a.z, c[4 * v + 3] = a.w;
+            *reinterpret_cast<int4*>(count + base + 4 * v) = make_int4(0, 0, 0, 0);  // zeroed for the next build
+        }
     } else {
 #pragma unroll
-        for (int k = 0; k < 8; ++k) {
+        for (int k = 0; k < kPer; ++k) {
             c[k] = (base + k < ncell) ? count[base + k] : 0;
             if (base + k < ncell) count[base + k] = 0;
         }
     }
 #pragma unroll
-    for (int k = 0; k < 8; ++k) tot += c[k];
+    for (int k = 0; k < kPer; ++k) tot += c[k];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     int inc = tot;
     for (int o = 1; o < 64; o <<= 1) {
@@ -159,20 +161,21 @@ __global__ void __launch_bounds__(kBlock) k_scan_onepass(int32_t* __restrict__ c
     for (int w = 0; w < wid; ++w) wpre += wtot[w];
     int run = s_excl + wpre + inc - tot;
 #if CBF_SCAN_VST
-    if (base + 8 <= ncell) {  // full tile: the lane's 8 starts as 2 x 16-B stores, like the loads
-        int o[8];
+    if (base + kPer <= ncell) {  // full tile: the lane's starts as 16-B stores, like the loads
+        int o[kPer];
 #pragma unroll
-        for (int k = 0; k < 8; ++k) {
+        for (int k = 0; k < kPer; ++k) {
             o[k] = run;
             run += c[k];
         }
-        *reinterpret_cast<int4*>(start + base) = make_int4(o[0], o[1], o[2], o[3]);
-        *reinterpret_cast<int4*>(start + base + 4) = make_int4(o[4], o[5], o[6], o[7]);
+#pragma unroll
+        for (int v = 0; v < kPer / 4; ++v)
+            *reinterpret_cast<int4*>(start + base + 4 * v) = make_int4(o[4 * v], o[4 * v + 1], o[4 * v + 2], o[4 * v + 3]);
         return;
     }
 #endif
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
+    for (int k = 0; k < kPer; ++k) {
         if (base + k < ncell) start[base + k] = run;
         run += c[k];
     }

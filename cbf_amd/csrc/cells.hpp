@@ -12,7 +12,10 @@
 
 namespace cbf {
 
-constexpr int kScanTile = 2048;  // 256 threads x 8 cells
+#ifndef CBF_SCAN_PER
+#define CBF_SCAN_PER 8  // cells per scan lane (a multiple of 4)
+#endif
+constexpr int kScanTile = 256 * CBF_SCAN_PER;  // 256 threads x CBF_SCAN_PER cells
 #ifndef CBF_HARD_BLOCKS
 #define CBF_HARD_BLOCKS 128
 #endif

@@ -40,6 +40,7 @@ SETS["wide"] = {"w1024": [], "w256": ["-DCBF_WIDE_BLOCKS=256"], "w128": ["-DCBF_
 SETS["hcert"] = {"nocert": [], "cert": ["-DCBF_HOCBF_CERT=1"]}
 SETS["scan"] = {"sumagg": [], "lookback": ["-DCBF_SCAN_SUMAGG=0"]}
 SETS["scanst"] = {"vst": [], "scalar": ["-DCBF_SCAN_VST=0"]}
+SETS["scanper"] = {"per8": [], "per16": ["-DCBF_SCAN_PER=16"], "per4": ["-DCBF_SCAN_PER=4"]}
 SETS["phases"] = {
     "full": [],
     "no_qp": ["-DCBF_ABLATE=1"],
