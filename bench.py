@@ -46,92 +46,56 @@ def load_pmc_traffic(kernels=("k_lattice_filter", "k_lattice_filter_hard")):
         return None
 
 
-def cpu_baseline_lattice(W, H, seed, budget_s=12.0):
-    """The reference's CPU path on a bounded sample of the cfg4 workload, one host core:
-    the per-agent loop of cross_and_rescue.py:135-160 restated line by line in Python (O(N)
-    Python cull per ego, cbf.py rows, cvxopt's coneqp restated in numpy: oracle/refloop.py).
-    Beside it, ``c_port``: the same loop in the C oracle (exact 2-D solver instead of cvxopt)."""
-    from cbf_amd import scenarios
-    from oracle import coracle, pyoracle as po, refloop
-    pos = scenarios.lattice(W, H, seed=seed)
-    vel = coracle.consensus_lattice(W, H, 0, H, pos, scenarios.LATTICE_GAIN)
-    p = po.Params(15)
-    order = np.random.default_rng(123).permutation(W * H)
-    done, solves, dt = refloop.loop_sample(p, pos, vel, 0, (int(e) for e in order), budget_s)
-    # C port of the same loop
-    t0 = time.perf_counter()
-    cdone = csolves = 0
-    while time.perf_counter() - t0 < budget_s / 2 and cdone < len(order):
-        e = int(order[cdone])
-        o = coracle.filter_swarm(p, pos, vel, 0, e, e + 1)
-        csolves += int(o["cnt"][0] > 0)
-        cdone += 1
-    cdt = time.perf_counter() - t0
-    return {"value": solves / dt, "unit": "agent-QP solves/s", "cores": 1, "kind": "port",
-            "sample": f"{done} random egos of cfg4 (N={W * H}) through a line-by-line Python restatement of the "
-                      f"reference loop (cross_and_rescue.py:135-160: Python cull of every agent, cbf.py:38-92 rows "
-                      f"+ cvxopt coneqp restated in numpy, maxiters 600), {dt:.1f} s on one core; cvxopt itself "
-                      f"is absent from the image",
-            "c_port": {"value": csolves / cdt, "unit": "agent-QP solves/s", "cores": 1,
-                       "sample": f"{cdone} random egos, same loop in the C oracle (O(N) cull + exact 2-D QP), "
-                                 f"{cdt:.1f} s"}}
-
-
-def _cport_worker(arg):
-    """One process of the parallel C-port baseline: the reference loop's per-ego work (O(N) cull
-    over every agent, rows, exact QP, clip) for a slice of random egos, until the budget."""
-    W, H, seed, egos, budget_s = arg
-    sys.path.insert(0, ROOT)
-    from cbf_amd import scenarios
-    from oracle import coracle, pyoracle as po
-    pos = scenarios.lattice(W, H, seed=seed)
-    vel = coracle.consensus_lattice(W, H, 0, H, pos, scenarios.LATTICE_GAIN)
-    p = po.Params(15)
-    t0 = time.perf_counter()
-    done = solves = 0
-    for e in egos:
-        if time.perf_counter() - t0 >= budget_s:
-            break
-        o = coracle.filter_swarm(p, pos, vel, 0, int(e), int(e) + 1)
-        solves += int(o["cnt"][0] > 0)
-        done += 1
-    return done, solves, time.perf_counter() - t0
-
-
-def cpu_baseline_parallel(W, H, seed, budget_s, procs):
-    """The C port spread over `procs` host processes (spawned, so no child inherits the GPU
-    context); agents are independent, so the rates add."""
-    import multiprocessing as mp
-    order = np.random.default_rng(321).permutation(W * H)
-    chunks = [(W, H, seed, order[i::procs][:200000], budget_s) for i in range(procs)]
-    with mp.get_context("spawn").Pool(procs) as pool:
-        res = pool.map(_cport_worker, chunks)
-    done = sum(r[0] for r in res)
-    solves = sum(r[1] for r in res)
-    dt = max(r[2] for r in res)
-    return {"value": solves / dt, "unit": "agent-QP solves/s", "cores": procs,
-            "sample": f"{done} random egos over {procs} processes, the C oracle's loop (O(N) cull + exact 2-D QP), "
-                      f"{dt:.1f} s"}
+def cpu_baseline_lattice(W, H, seed, budget_s, spacing, gain, procs=None):
+    """The reference's CPU loop (oracle/refloop.py: cross_and_rescue.py:135-160 restated, with
+    cvxopt's coneqp restated) on every core of this job's host share (oracle/cpu_baseline.py):
+    random egos of this workload (O(N) Python cull per ego, as the reference does at this N), and
+    beside it the QP-dominated cfg2 shape (N = 100)."""
+    from oracle import cpu_baseline
+    res = cpu_baseline.run("cfg4", budget_s, procs=procs, shape=(W, H, seed, spacing, gain))
+    res["qp_dominated_cfg2"] = cpu_baseline.run("qp", budget_s, procs=procs)
+    return res
 
 
 def full_size_check(S, args):
     """After the timed run (untimed): one more fused step of the full swarm against the separate
     cell-list filter (cbf_filter_cells with diagnostics) on the same input state -- controls
-    bit-identical, and the largest row violation over the solved QPs (north star: <= 1e-7)."""
+    bit-identical, and the largest row violation over the OPTIMAL QPs (the ones whose answer the
+    reference defines; north star: <= 1e-7)."""
     import torch
-    from cbf_amd import scenarios, swarm
+    from cbf_amd import swarm
     pos0 = S.pos.clone()
     S.step()
     torch.cuda.synchronize()
-    vel = swarm.consensus_lattice(pos0, S.W, S.H, scenarios.LATTICE_GAIN)
+    vel = swarm.consensus_lattice(pos0, S.W, S.H, S.gain)
     out = swarm.filter_swarm(S.params, pos0, vel, 0, method="cells", grid=S.grid, diag=True)
     st = out["status"]
-    solved = ((st & 0xFF) == 1) | ((st & 0xFF) == 2)
-    viol = float(out["viol"][solved].max().item()) if bool(solved.any()) else 0.0
+    opt = (st & 0xFF) == 1
+    viol = float(out["viol"][opt].max().item()) if bool(opt.any()) else 0.0
     return {"agents": int(pos0.shape[0]), "u_bit_identical_to_cell_filter": bool(torch.equal(out["u"], S.u)),
-            "status_identical": bool(torch.equal(st, S.status)), "max_row_violation": viol,
+            "status_identical": bool(torch.equal(st, S.status)), "max_row_violation_optimal": viol,
+            "optimal_fraction": float(opt.float().mean().item()),
             "relaxed_fraction": float(((st & 0xFF) == 2).float().mean().item()),
             "max_relaxations": int((st >> 8).max().item())}
+
+
+def safety_report(st, steps):
+    """The rollout's safety and parity record from the device statistics of the timed steps
+    (include/cbf_amd.h CBF_STAT_*).  feasible_fraction = OPTIMAL solves / solves: the share whose
+    output the reference defines (an exact QP minimiser; cvxopt's iterate for an infeasible QP is
+    arbitrary, cbf.py:81-87).  max_violation_optimal is the north star's "max barrier violation"
+    over those; the RELAXED ones violate their original rows by construction and are reported
+    separately, with the rollout's minimum distance between culled neighbours."""
+    n = max(st["solves"], 1)
+    d2 = st["min_dist2"]
+    return {"steps": steps, "solves": st["solves"],
+            "feasible_fraction": st["optimal"] / n, "relaxed_fraction": st["relaxed"] / n,
+            "infeasible_fraction": st["infeasible"] / n, "seidel_fraction": st["seidel"] / n,
+            "max_violation_optimal": st["viol_optimal"],
+            "max_violation_original_rows_relaxed": st["viol_original_relaxed"],
+            "min_pairwise_distance": None if d2 is None else float(np.sqrt(d2)),
+            "min_pairwise_distance_note": "over neighbour pairs the reference culls (0 < d < 0.2, "
+                                          "cross_and_rescue.py:147-150); None = no pair closer than 0.2"}
 
 
 def bench_lattice(args, ws, rank, local):
@@ -141,10 +105,10 @@ def bench_lattice(args, ws, rank, local):
     rows = args.rows
     if ws > 1 or args.shard:
         from cbf_amd.shard import ShardedLattice
-        S = ShardedLattice(W, rows, seed=args.seed, substeps=args.substeps)
+        S = ShardedLattice(W, rows, seed=args.seed, substeps=args.substeps, spacing=args.spacing, gain=args.gain)
     else:
-        pos = scenarios.lattice(W, rows, seed=args.seed)
-        S = swarm.LatticeSwarm(pos, W, rows, gain=scenarios.LATTICE_GAIN, barrier=args.barrier)
+        pos = scenarios.lattice(W, rows, seed=args.seed, spacing=args.spacing)
+        S = swarm.LatticeSwarm(pos, W, rows, gain=args.gain, barrier=args.barrier)
     # the sharded path stays eager: per-sub-step graph replays measured slower than eager
     # launches (110 vs 104 us per step at one rank, 4 sub-steps per exchange)
     use_graph = not args.eager and not (ws > 1 or args.shard)
@@ -180,6 +144,21 @@ def bench_lattice(args, ws, rank, local):
         S.check_guard()
     else:
         n_total = n_local
+    # the timed rollout's safety record, before the kernel-timing launches below add to it
+    stat = S.stats_summary()
+    if ws > 1:
+        import torch.distributed as dist
+        keys = ("solves", "optimal", "relaxed", "infeasible", "seidel")
+        c = torch.tensor([stat[k] for k in keys], dtype=torch.float64, device="cuda")
+        m = torch.tensor([stat["viol_optimal"], stat["viol_original_relaxed"],
+                          -(stat["min_dist2"] if stat["min_dist2"] is not None else np.inf)],
+                         dtype=torch.float64, device="cuda")
+        dist.all_reduce(c)
+        dist.all_reduce(m, op=dist.ReduceOp.MAX)
+        stat.update({k: int(v) for k, v in zip(keys, c.tolist())})
+        stat.update(viol_optimal=float(m[0]), viol_original_relaxed=float(m[1]),
+                    min_dist2=None if not np.isfinite(m[2].item()) else -float(m[2]))
+    safety = safety_report(stat, args.steps) if args.barrier == "reference" else None
     # dominant kernel (filter + clip + Euler) timed alone with HIP events on the launch stream
     kt = []
     for _ in range(args.kernel_iters):
@@ -211,15 +190,17 @@ def bench_lattice(args, ws, rank, local):
         "vs_baseline": None,
         "dtype": "f64",
         "data": "synthetic",
-        "config": {"workload": f"cfg4: {W}x{rows * ws} jittered lattice swarm (spacing 0.145), lattice-Laplacian "
-                               "consensus + radius-0.2 cell-list cull + CBF QP + clip + Euler, one fused timestep "
-                               "per step", "barrier": args.barrier,
+        "config": {"workload": f"{args.config}: {W}x{rows * ws} jittered lattice swarm (spacing {args.spacing}), "
+                               f"lattice-Laplacian consensus (gain {args.gain}) + radius-0.2 cell-list cull + CBF QP "
+                               "+ clip + Euler, one fused timestep per step", "barrier": args.barrier,
                    "agents_total": n_total, "agents_per_gpu": n_local,
                    "parallelism": f"row-stripe shards x{ws}, 1 RCCL all-gather of ghost-row slabs per "
                                   f"{args.substeps} steps" if (ws > 1 or args.shard) else "single GPU",
                    "graph": use_graph},
         "timesteps_per_s": args.steps / elapsed,
         "solves_per_step": solves / args.steps,
+        "feasible_fraction": safety["feasible_fraction"] if safety else None,
+        "safety": safety,
         "full_size_check": check,
         "status_fraction_last_step": {"idle": codes[0] / len(status), "optimal": codes[1] / len(status),
                                       "relaxed": codes[2] / len(status),
@@ -417,7 +398,11 @@ def _reduce(elapsed, solves, ws):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--config", default="cfg4", choices=["cfg4", "cfg3", "cfg5", "cert"])
+    ap.add_argument("--config", default="cfg4", choices=["cfg4", "cfg4f", "cfg3", "cfg5", "cert"],
+                    help="cfg4f: the cfg4 swarm at spacing 0.2 (= dmin), where most QPs are feasible and "
+                         "barrier rows bind (the exact QP path at scale)")
+    ap.add_argument("--spacing", type=float, default=None, help="lattice spacing (cfg4 0.145, cfg4f 0.2)")
+    ap.add_argument("--gain", type=float, default=None, help="lattice consensus gain (default 0.25)")
     ap.add_argument("--cert-scenarios", type=int, default=100000)
     ap.add_argument("--cert-agents", type=int, default=16)
     ap.add_argument("--mc-scenarios", type=int, default=100000)
@@ -433,9 +418,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--barrier", default="reference", choices=["reference", "euclidean_hocbf"],
                     help="cfg4 single-GPU: the reference's L1 barrier rows or the Euclidean HOCBF mode")
-    ap.add_argument("--cpu-budget", type=float, default=12.0)
-    ap.add_argument("--cpu-procs", type=int, default=min(16, os.cpu_count() or 1),
-                    help="host processes for the parallel C-port baseline (1 = skip)")
+    ap.add_argument("--cpu-budget", type=float, default=10.0, help="seconds per CPU-baseline process and shape")
+    ap.add_argument("--cpu-procs", type=int, default=None,
+                    help="CPU-baseline processes (default: this job's host cores, oracle/cpu_baseline.py)")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="torch.distributed backend for N > 1 (nccl = RCCL; gloo = host-staged rehearsal)")
     ap.add_argument("--substeps", type=int, default=4,
@@ -443,6 +428,11 @@ def main():
     ap.add_argument("--shard", action="store_true",
                     help="cfg4: run the sharded step (halo pack + collective + unpack) even on one rank")
     args = ap.parse_args()
+    from cbf_amd import scenarios as _sc
+    if args.spacing is None:
+        args.spacing = 0.2 if args.config == "cfg4f" else _sc.LATTICE_SPACING
+    if args.gain is None:
+        args.gain = _sc.LATTICE_GAIN
     # stdout carries exactly one JSON line: everything else that writes to fd 1 (RCCL prints a
     # version banner at communicator init) goes to stderr
     sys.stdout.flush()
@@ -476,11 +466,9 @@ def main():
         res = bench_lattice(args, ws, rank, local)
     if rank == 0:
         sample = res.pop("_cert_sample", None)
-        if ws == 1 and not args.no_cpu_baseline and args.config == "cfg4":
-            res["cpu_baseline"] = cpu_baseline_lattice(args.width, args.rows, args.seed, args.cpu_budget)
-            if args.cpu_procs > 1:
-                res["cpu_baseline"]["c_port_parallel"] = cpu_baseline_parallel(
-                    args.width, args.rows, args.seed, min(args.cpu_budget, 6.0), args.cpu_procs)
+        if ws == 1 and not args.no_cpu_baseline and args.config in ("cfg4", "cfg4f"):
+            res["cpu_baseline"] = cpu_baseline_lattice(args.width, args.rows, args.seed, args.cpu_budget,
+                                                       args.spacing, args.gain, args.cpu_procs)
         elif ws == 1 and not args.no_cpu_baseline and args.config == "cert":
             res["cpu_baseline"] = cpu_baseline_cert(*sample, budget_s=min(args.cpu_budget, 8.0))
         else:

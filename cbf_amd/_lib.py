@@ -15,8 +15,14 @@ PKG = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(PKG, "libcbf_amd.so")
 
 CBF_EINVAL = -1
+ABI_VERSION = 2  # include/cbf_amd.h CBF_ABI_VERSION
 STATUS_IDLE, STATUS_OPTIMAL, STATUS_RELAXED, STATUS_BOX_INFEASIBLE, STATUS_RELAX_CAP = 0, 1, 2, 3, 4
 STATUS_NBR_OVERFLOW = 5
+STATUS_WORKSPACE_ERROR = 6
+# words of a lattice-step statistics slot (include/cbf_amd.h CBF_STAT_*)
+(STAT_SOLVES, STAT_OPTIMAL, STAT_RELAXED, STAT_INFEASIBLE, STAT_SEIDEL, STAT_VIOL_OPTIMAL, STAT_VIOL_ORIGINAL,
+ STAT_MIN_DIST2, STAT_ERRORS) = range(9)
+_DIST_KEY_TOP = 0x7FF0000000000000
 
 
 class CbfParams(C.Structure):
@@ -84,7 +90,7 @@ SIGNATURES = {
                                       _i32, _vp, _vp, _vp, _sz, _vp]),
     "cbf_lattice_advance_hocbf": (C.c_int, [_P, _HP, _G, _i32, _i32, _i32, _i32, _i32, _i32, _vp, _d, _vp, _vp, _vp,
                                             _vp, _i32, _vp, _vp, _vp, _sz, _vp]),
-    "cbf_mc_rollout": (C.c_int, [_P, _i32, _i32, _i32, _i32, _d, _d, _d, _d, _d, _vp, _vp, _vp, _vp]),
+    "cbf_mc_rollout": (C.c_int, [_P, _i32, _i32, _i32, _i32, _d, _d, _d, _d, _d, _vp, _vp, _vp, _vp, _vp]),
     "cbf_halo_guard": (C.c_int, [_vp, C.c_int64, _i32, _i32, _d, _vp, _vp]),
     "cbf_halo_ext_bytes": (_sz, [_i32]),
     "cbf_halo_ext_reset": (C.c_int, [_vp, _i32, _vp]),
@@ -105,11 +111,19 @@ if not os.path.exists(LIB_PATH):
     raise ImportError(f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
                       "(there is no CPU fallback)")
 
+# torch first: its bundled HIP runtime (soname libamdhip64.so.7) is then the one this library binds
+# to.  Loaded the other way round, /opt/rocm's runtime and torch's would both be live in the process
+# and torch's device calls fail (hipErrorNoDevice).
+import torch  # noqa: E402,F401
+
 lib = C.CDLL(LIB_PATH)
 for _name, (_res, _args) in SIGNATURES.items():
     _fn = getattr(lib, _name)
     _fn.restype = _res
     _fn.argtypes = _args
+if lib.cbf_abi_version() != ABI_VERSION:
+    raise ImportError(f"{LIB_PATH} has ABI version {lib.cbf_abi_version()}, this package expects {ABI_VERSION}: "
+                      "rebuild it")
 
 
 class CbfError(RuntimeError):
@@ -132,6 +146,21 @@ def make_params(max_speed, dmin=0.2, k=1.0, f=None, g=None, safety_distance=0.2)
                              float(safety_distance))
     check(rc, "cbf_params_init")
     return p
+
+
+def decode_stats(words) -> dict:
+    """Host summary of a lattice-step statistics array (uint64[1024] as int64 numpy/torch values:
+    64 slots of 16 words, include/cbf_amd.h CBF_STAT_*)."""
+    w = np.asarray(words).astype(np.int64).view(np.uint64).reshape(64, 16)
+    cnt = {k: int(w[:, i].sum()) for k, i in (("solves", STAT_SOLVES), ("optimal", STAT_OPTIMAL),
+                                               ("relaxed", STAT_RELAXED), ("infeasible", STAT_INFEASIBLE),
+                                               ("seidel", STAT_SEIDEL), ("errors", STAT_ERRORS))}
+    vo = w[:, STAT_VIOL_OPTIMAL].max().reshape(1).view(np.float64)[0]
+    vr = w[:, STAT_VIOL_ORIGINAL].max().reshape(1).view(np.float64)[0]
+    key = int(w[:, STAT_MIN_DIST2].max())
+    d2 = None if key == 0 else float(np.array([_DIST_KEY_TOP - key], dtype=np.uint64).view(np.float64)[0])
+    cnt.update(viol_optimal=float(vo), viol_original_relaxed=float(vr), min_dist2=d2)
+    return cnt
 
 
 def require_gpu():

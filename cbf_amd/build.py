@@ -20,17 +20,21 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("CBF_OFFLOAD_ARCH", "gfx950")
 FLAGS = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-Wall", "-Wno-unused-function",
          f"--offload-arch={ARCH}", "-I", os.path.join(ROOT, "include"), "-I", CSRC]
+# A/B builds only (tools/_ab): extra -D switches from the environment; the shipped build sets none
+FLAGS += [f"-D{d}" for d in os.environ.get("CBF_EXTRA_DEFS", "").split()]
 
 
-def _compile(src: str) -> str:
-    out = os.path.join(BUILD, os.path.splitext(src)[0] + ".o")
+def _compile(src: str, variant: str = "", defines=()) -> str:
+    bdir = os.path.join(BUILD, variant) if variant else BUILD
+    os.makedirs(bdir, exist_ok=True)
+    out = os.path.join(bdir, os.path.splitext(src)[0] + ".o")
     path = os.path.join(CSRC, src)
     deps = [path] + [os.path.join(CSRC, h) for h in os.listdir(CSRC) if h.endswith(".hpp")] + \
         [os.path.join(ROOT, "include", "cbf_amd.h")]
     if os.path.exists(out) and os.path.getmtime(out) >= max(os.path.getmtime(d) for d in deps):
         return out
     lang = ["-x", "hip"] if src.endswith(".hip") else []
-    cmd = [HIPCC] + FLAGS + lang + ["-c", path, "-o", out]
+    cmd = [HIPCC] + FLAGS + [f"-D{d}" for d in defines] + lang + ["-c", path, "-o", out]
     subprocess.run(cmd, check=True)
     return out
 
@@ -45,6 +49,25 @@ def build(verbose: bool = False) -> str:
     if verbose:
         print(f"built {LIB}")
     return LIB
+
+
+# Test-only builds of the library with a compile switch flipped in some sources (never loaded by
+# the package): name -> (sources, defines).  CBF_SCAN_TEST_TIMEOUT makes every scan look-back give
+# up, so tests/test_gpu_parity.py can check that the failure is reported, not silent.
+TEST_VARIANTS = {"scantimeout": (["cells.hip"], ["CBF_SCAN_TEST_TIMEOUT=1"])}
+TEST_LIB_DIR = os.path.join(ROOT, "tests", "_lib")
+
+
+def build_test_variants(verbose: bool = False) -> None:
+    os.makedirs(TEST_LIB_DIR, exist_ok=True)
+    base = {src: _compile(src) for src in SOURCES}
+    for name, (srcs, defines) in TEST_VARIANTS.items():
+        objs = [(_compile(src, name, defines) if src in srcs else base[src]) for src in SOURCES]
+        out = os.path.join(TEST_LIB_DIR, f"libcbf_{name}.so")
+        if not os.path.exists(out) or os.path.getmtime(out) < max(os.path.getmtime(o) for o in objs):
+            subprocess.run([HIPCC, "-shared", f"--offload-arch={ARCH}", "-o", out] + objs, check=True)
+        if verbose:
+            print(f"built {out}")
 
 
 if __name__ == "__main__":

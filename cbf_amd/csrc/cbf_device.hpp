@@ -15,35 +15,13 @@
 
 #include "cbf_amd.h"
 
-// Ablation builds only (tools/ablate.py): 1 = skip the QP, 2 = also skip row assembly,
-// 3 = also skip the candidate scan.  The shipped library is built with 0.
-#ifndef CBF_ABLATE
-#define CBF_ABLATE 0
-#endif
-// Loads in flight per lane in the lattice filter's hit flush and joint candidate scan
-// (tools/ablate.py times the choices).
 #ifndef CBF_FLUSH_U
 #define CBF_FLUSH_U 4
 #endif
 #ifndef CBF_SCAN_U
 #define CBF_SCAN_U 6
 #endif
-// Lattice filter variants (tools/ablate.py): CBF_PUSH_BF = branch-free hit push (one LDS store per
-// candidate into the hit row or a dummy row); CBF_BQ_LDS = per-quadrant minima kept in LDS
-// (one read-compare-write per hit instead of four register compare-selects).
-#ifndef CBF_PUSH_BF
-#define CBF_PUSH_BF 0
-#endif
-#ifndef CBF_BQ_LDS
-#define CBF_BQ_LDS 1
-#endif
-// CBF_SCAN32 = the lattice filter's candidate scan reads fp32 positions (8 B instead of 16 B per
-// candidate through the vector memory pipe) and screens with screen_threshold(); every candidate
-// the screen lets through is re-tested exactly in fp64 in the flush.
-#ifndef CBF_SCAN32
-#define CBF_SCAN32 0
-#endif
-
+static_assert(CBF_FLUSH_U >= 1 && CBF_SCAN_U >= 1, "loads in flight per lane");
 namespace cbf {
 
 constexpr double FEAS_TOL = 1e-12;
@@ -181,16 +159,11 @@ struct HitList {
         if (n < kHitCap) lds[n * kBlock + threadIdx.x] = t;
         ++n;
     }
-    // branch-free form: lds has kHitCap + 1 rows, row kHitCap takes the non-hits
-    __device__ __forceinline__ void push_if(int* lds, int t, bool hit) {
-        const int row = (hit && n < kHitCap) ? n : kHitCap;
-        lds[row * kBlock + threadIdx.x] = t;
-        n += hit ? 1 : 0;
-    }
     __device__ __forceinline__ bool overflowed() const { return n > kHitCap; }
-    // flush with the per-quadrant minima in LDS (bq[q * kBlock + lane], preset to +inf by the
-    // caller and read back into E after); same rows, same order, same minimum
-    template <bool FZ = false, bool EXACT = false>
+    // flush into the per-quadrant minima kept in LDS (bq[q * kBlock + lane], preset to +inf by
+    // the caller and read back into E after): one read-compare-write per hit instead of four
+    // register compare-selects; same rows, same minimum
+    template <bool FZ = false>
     __device__ __forceinline__ void flush_bq(const int* lds, double* bq, const KP& P, Ego& E,
                                              const double2* __restrict__ pos, const double2* __restrict__ vel) {
         for (int i = 0; i < n; i += CBF_FLUSH_U) {
@@ -205,13 +178,7 @@ struct HitList {
             }
 #pragma unroll
             for (int q = 0; q < CBF_FLUSH_U; ++q) {
-                bool keep = i + q < n;
-                if (EXACT && keep) {  // screened candidate: the exact agent cull test
-                    const double e0 = pj[q].x - E.r0, e1 = pj[q].y - E.r1;
-                    const double s = e0 * e0 + e1 * e1;
-                    keep = s < P.cull_t && s > 0;
-                }
-                if (keep) {
+                if (i + q < n) {
                     int qd;
                     const double b = row_b<FZ>(P, E, pj[q].x, pj[q].y, vj[q].x, vj[q].y, qd);
                     double* slot = bq + qd * kBlock + threadIdx.x;
@@ -224,64 +191,15 @@ struct HitList {
         }
         n = 0;
     }
-    template <bool FZ = false, bool EXACT = false>
-    __device__ __forceinline__ void flush(const int* lds, const KP& P, Ego& E, const double2* __restrict__ pos,
-                                          const double2* __restrict__ vel) {
-        // CBF_FLUSH_U hits' loads in flight per lane (same assembly order as one at a time)
-        for (int i = 0; i < n; i += CBF_FLUSH_U) {
-            double2 pj[CBF_FLUSH_U], vj[CBF_FLUSH_U];
-#pragma unroll
-            for (int q = 0; q < CBF_FLUSH_U; ++q) {
-                if (i + q < n) {
-                    const int t = lds[(i + q) * kBlock + threadIdx.x];
-                    pj[q] = pos[t];
-                    vj[q] = vel[t];
-                }
-            }
-#pragma unroll
-            for (int q = 0; q < CBF_FLUSH_U; ++q) {
-                bool keep = i + q < n;
-                if (EXACT && keep) {  // screened candidate: the exact agent cull test
-                    const double e0 = pj[q].x - E.r0, e1 = pj[q].y - E.r1;
-                    const double s = e0 * e0 + e1 * e1;
-                    keep = s < P.cull_t && s > 0;
-                }
-                if (keep) ego_add<FZ>(P, E, pj[q].x, pj[q].y, vj[q].x, vj[q].y);
-            }
-        }
-        n = 0;
-    }
 };
 
-// Cull test over cell-sorted candidate slots [t0, t1) for an agent ego (0 < s < cull_t),
-// 4 candidates' loads in flight per lane.
-__device__ __forceinline__ void scan_range(int t0, int t1, const KP& P, const Ego& E, HitList& H, int* lds,
-                                           const double2* __restrict__ spos) {
-    int t = t0;
-    for (; t + 4 <= t1; t += 4) {
-        double2 p[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) p[u] = spos[t + u];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            const double e0 = p[u].x - E.r0, e1 = p[u].y - E.r1;
-            const double s = e0 * e0 + e1 * e1;
-            if (s < P.cull_t && s > 0) H.push(lds, t + u);
-        }
-    }
-    for (; t < t1; ++t) {
-        const double2 pj = spos[t];
-        const double e0 = pj.x - E.r0, e1 = pj.y - E.r1;
-        const double s = e0 * e0 + e1 * e1;
-        if (s < P.cull_t && s > 0) H.push(lds, t);
-    }
-}
-
-#if CBF_SCAN_U > 0
 // The three cell-row ranges of an ego scanned as one sequence, CBF_SCAN_U candidates' loads in
-// flight per lane (pushes in the same order as three scan_range calls).
+// flight per lane; hits (0 < s < cull_t, cross_and_rescue.py:147-150) go to the hit list in
+// sequence order.  smin tracks the smallest hit distance^2 (the rollout's minimum pairwise
+// distance, a reported statistic only).
 __device__ __forceinline__ void scan_rows_joint(const int (&t0)[3], const int (&t1)[3], const KP& P, const Ego& E,
-                                                HitList& H, int* lds, const double2* __restrict__ spos) {
+                                                HitList& H, int* lds, const double2* __restrict__ spos,
+                                                double& smin) {
     const int l0 = t1[0] - t0[0], l01 = l0 + (t1[1] - t0[1]);
     const int L = l01 + (t1[2] - t0[2]);
     for (int v = 0; v < L; v += CBF_SCAN_U) {
@@ -298,179 +216,14 @@ __device__ __forceinline__ void scan_rows_joint(const int (&t0)[3], const int (&
             if (v + q < L) {
                 const double e0 = p[q].x - E.r0, e1 = p[q].y - E.r1;
                 const double s = e0 * e0 + e1 * e1;
-#if CBF_PUSH_BF
-                H.push_if(lds, tt[q], s < P.cull_t && s > 0);
-#else
-                if (s < P.cull_t && s > 0) H.push(lds, tt[q]);
-#endif
+                if (s < P.cull_t && s > 0) {
+                    H.push(lds, tt[q]);
+                    smin = pmin(smin, s);
+                }
             }
         }
     }
 }
-#endif
-
-#ifndef CBF_SCAN_INLINE
-#define CBF_SCAN_INLINE 0
-#endif
-#ifndef CBF_INLINE_U
-#define CBF_INLINE_U 4
-#endif
-#if CBF_SCAN_U > 0
-// The joint 3-row scan with each candidate's nominal control loaded beside its position and the
-// row assembled in place for hits (no hit list, no per-lane gathers afterwards); same hit
-// order as the list, so the same per-quadrant minima bit for bit.
-template <bool FZ>
-__device__ __forceinline__ void scan_rows_inline(const int (&t0)[3], const int (&t1)[3], const KP& P, Ego& E,
-                                                 const double2* __restrict__ spos,
-                                                 const double2* __restrict__ svel) {
-    const int l0 = t1[0] - t0[0], l01 = l0 + (t1[1] - t0[1]);
-    const int L = l01 + (t1[2] - t0[2]);
-    for (int v = 0; v < L; v += CBF_INLINE_U) {
-        double2 p[CBF_INLINE_U], w[CBF_INLINE_U];
-#pragma unroll
-        for (int q = 0; q < CBF_INLINE_U; ++q) {
-            const int vv = v + q;
-            const int tt = vv < l0 ? t0[0] + vv : (vv < l01 ? t0[1] + (vv - l0) : t0[2] + (vv - l01));
-            if (vv < L) {
-                p[q] = spos[tt];
-                w[q] = svel[tt];
-            }
-        }
-#pragma unroll
-        for (int q = 0; q < CBF_INLINE_U; ++q) {
-            if (v + q < L) {
-                const double e0 = p[q].x - E.r0, e1 = p[q].y - E.r1;
-                const double s = e0 * e0 + e1 * e1;
-                if (s < P.cull_t && s > 0) ego_add<FZ>(P, E, p[q].x, p[q].y, w[q].x, w[q].y);
-            }
-        }
-    }
-}
-#endif
-
-#ifndef CBF_HIT_MASK
-#define CBF_HIT_MASK 0
-#endif
-#if CBF_SCAN_U > 0
-// Hits of the joint 3-row candidate sequence as a 96-bit mask in registers (bit v = candidate v
-// of the sequence) instead of an LDS index list; returns false when the sequence is longer than
-// 96 (the caller takes the direct path).
-struct HitMask {
-    unsigned m0 = 0u, m1 = 0u, m2 = 0u;
-    int l0 = 0, l01 = 0, L = 0;
-    __device__ __forceinline__ void set(int v) {
-        const unsigned b = 1u << (v & 31);
-        if (v < 32) m0 |= b;
-        else if (v < 64) m1 |= b;
-        else m2 |= b;
-    }
-    // next set bit (ascending), -1 when none
-    __device__ __forceinline__ int pop() {
-        if (m0) {
-            const int b = __ffs((int)m0) - 1;
-            m0 &= m0 - 1u;
-            return b;
-        }
-        if (m1) {
-            const int b = __ffs((int)m1) - 1;
-            m1 &= m1 - 1u;
-            return 32 + b;
-        }
-        if (m2) {
-            const int b = __ffs((int)m2) - 1;
-            m2 &= m2 - 1u;
-            return 64 + b;
-        }
-        return -1;
-    }
-};
-
-__device__ __forceinline__ bool scan_rows_joint_mask(const int (&t0)[3], const int (&t1)[3], const KP& P,
-                                                     const Ego& E, HitMask& H, const double2* __restrict__ spos) {
-    H.l0 = t1[0] - t0[0];
-    H.l01 = H.l0 + (t1[1] - t0[1]);
-    H.L = H.l01 + (t1[2] - t0[2]);
-    if (H.L > 96) return false;
-    const int l0 = H.l0, l01 = H.l01, L = H.L;
-    for (int v = 0; v < L; v += CBF_SCAN_U) {
-        double2 p[CBF_SCAN_U];
-#pragma unroll
-        for (int q = 0; q < CBF_SCAN_U; ++q) {
-            const int vv = v + q;
-            const int tt = vv < l0 ? t0[0] + vv : (vv < l01 ? t0[1] + (vv - l0) : t0[2] + (vv - l01));
-            if (vv < L) p[q] = spos[tt];
-        }
-#pragma unroll
-        for (int q = 0; q < CBF_SCAN_U; ++q) {
-            if (v + q < L) {
-                const double e0 = p[q].x - E.r0, e1 = p[q].y - E.r1;
-                const double s = e0 * e0 + e1 * e1;
-                if (s < P.cull_t && s > 0) H.set(v + q);
-            }
-        }
-    }
-    return true;
-}
-
-// Row assembly over the masked hits, CBF_FLUSH_U hits' loads in flight per lane.
-template <bool FZ>
-__device__ __forceinline__ void flush_mask(HitMask& H, const int (&t0)[3], const KP& P, Ego& E,
-                                           const double2* __restrict__ spos, const double2* __restrict__ svel) {
-    for (;;) {
-        int tt[CBF_FLUSH_U];
-        bool any = false;
-#pragma unroll
-        for (int q = 0; q < CBF_FLUSH_U; ++q) {
-            const int v = H.pop();
-            tt[q] = v < 0 ? -1 : (v < H.l0 ? t0[0] + v : (v < H.l01 ? t0[1] + (v - H.l0) : t0[2] + (v - H.l01)));
-            any = any || v >= 0;
-        }
-        if (!any) break;
-        double2 pj[CBF_FLUSH_U], vj[CBF_FLUSH_U];
-#pragma unroll
-        for (int q = 0; q < CBF_FLUSH_U; ++q)
-            if (tt[q] >= 0) {
-                pj[q] = spos[tt[q]];
-                vj[q] = svel[tt[q]];
-            }
-#pragma unroll
-        for (int q = 0; q < CBF_FLUSH_U; ++q)
-            if (tt[q] >= 0) ego_add<FZ>(P, E, pj[q].x, pj[q].y, vj[q].x, vj[q].y);
-    }
-}
-#endif
-
-#if CBF_SCAN_U > 0
-// scan_rows_joint over fp32 positions with the screen threshold t32 (pushes candidates that
-// may be neighbours, including the ego itself; the flush decides exactly).
-__device__ __forceinline__ void scan_rows_joint32(const int (&t0)[3], const int (&t1)[3], float t32, float ex,
-                                                  float ey, HitList& H, int* lds, const float2* __restrict__ spos32) {
-    const int l0 = t1[0] - t0[0], l01 = l0 + (t1[1] - t0[1]);
-    const int L = l01 + (t1[2] - t0[2]);
-    for (int v = 0; v < L; v += CBF_SCAN_U) {
-        float2 p[CBF_SCAN_U];
-        int tt[CBF_SCAN_U];
-#pragma unroll
-        for (int q = 0; q < CBF_SCAN_U; ++q) {
-            const int vv = v + q;
-            tt[q] = vv < l0 ? t0[0] + vv : (vv < l01 ? t0[1] + (vv - l0) : t0[2] + (vv - l01));
-            if (vv < L) p[q] = spos32[tt[q]];
-        }
-#pragma unroll
-        for (int q = 0; q < CBF_SCAN_U; ++q) {
-            if (v + q < L) {
-                const float d0 = p[q].x - ex, d1 = p[q].y - ey;
-                const float sq = __builtin_fmaf(d0, d0, d1 * d1);
-#if CBF_PUSH_BF
-                H.push_if(lds, tt[q], sq < t32);
-#else
-                if (sq < t32) H.push(lds, tt[q]);
-#endif
-            }
-        }
-    }
-}
-#endif
 
 // Direct (uncompacted) cull + assembly over [t0, t1): the overflow path.
 template <bool FZ = false>
@@ -588,8 +341,26 @@ struct Sol {
     double x0, x1;
     int status;
     int iters;
-    double viol;
+    double viol;       // max(0, a.x - b) over the rows of the QP actually solved (relaxed rhs)
+    double viol_orig;  // the same over the ORIGINAL rows (cbf.py:58-59 before any +1, box rows)
 };
+
+// max(0, max_i a_i.x - b_i) over an ego's original rows: the merged box rows and the per-quadrant
+// barrier minima before relaxation.  Equal to Sol::viol for an OPTIMAL QP; for a RELAXED one it is
+// how far the returned control violates the barrier the reference asked for (a reported
+// statistic).
+__device__ __forceinline__ double orig_violation(const KP& P, const Ego& E, const Box& B, double x0, double x1) {
+    double v = 0.0;
+    const double bb[4] = {pmin(B.S[0], B.S[4]), pmin(B.S[1], B.S[6]), pmin(B.S[2], B.S[5]), pmin(B.S[3], B.S[7])};
+    const double ab[4] = {x0, x1, -x0, -x1};
+#pragma unroll
+    for (int h = 0; h < 4; ++h) v = pmax(v, ab[h] - bb[h]);
+    const double bq[4] = {E.bq0, E.bq1, E.bq2, E.bq3};
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+        if ((E.present >> q) & 1u) v = pmax(v, (P.n0[q] * x0 + P.n1[q] * x1) - bq[q]);
+    return v;
+}
 
 // The QP of cbf.py:62-87 for an ego: merged box rows + per-quadrant CBF rows, with the
 // reference's +1 relaxation (cbf.py:84-87) applied while infeasible.
@@ -663,177 +434,7 @@ __device__ __forceinline__ Sol solve_ego(const KP& P, const Ego& E) {
             if (d > v) v = d;
         }
     S.viol = v;
-    return S;
-}
-
-// solve_ego with its loops rolled and the 8 right-hand sides in the lane's own LDS column (a
-// LaneCol: element i of the column at p[i * kBlock], the layout of the hit list, so it never
-// touches another lane's slots; a double occupies elements 2h, 2h + 1): same planes, order,
-// arithmetic and tolerances as solve_planes_reg / solve_ego, so bit-identical results, but about
-// 30 VGPRs instead of ~170, so it can run inside a kernel whose occupancy is set elsewhere (the
-// lattice filter solves its rare hard QPs in place with it).  Plane h's normal comes from a
-// uniform select, never from a runtime-indexed register array (that would be lowered to scratch).
-struct LaneCol {
-    int* p;  // this lane's column: p[i * kBlock]
-    __device__ __forceinline__ double get(int h) const {
-        return __hiloint2double(p[(2 * h + 1) * kBlock], p[2 * h * kBlock]);
-    }
-    __device__ __forceinline__ void set(int h, double v) const {
-        p[2 * h * kBlock] = __double2loint(v);
-        p[(2 * h + 1) * kBlock] = __double2hiint(v);
-    }
-};
-__device__ __forceinline__ void plane_normal(const KP& P, int h, double& a0, double& a1) {
-    switch (h) {
-        case 0: a0 = 1.0, a1 = 0.0; break;
-        case 1: a0 = 0.0, a1 = 1.0; break;
-        case 2: a0 = -1.0, a1 = 0.0; break;
-        case 3: a0 = 0.0, a1 = -1.0; break;
-        case 4: a0 = P.n0[0], a1 = P.n1[0]; break;
-        case 5: a0 = P.n0[1], a1 = P.n1[1]; break;
-        case 6: a0 = P.n0[2], a1 = P.n1[2]; break;
-        default: a0 = P.n0[3], a1 = P.n1[3]; break;
-    }
-}
-
-__device__ __forceinline__ int solve8_lds(const KP& P, const LaneCol& b, unsigned mask, double& xo0, double& xo1) {
-    double x0 = 0.0, x1 = 0.0;
-#pragma unroll 1
-    for (int h = 0; h < 8; ++h) {
-        if (!((mask >> h) & 1u)) continue;
-        double ah0, ah1;
-        plane_normal(P, h, ah0, ah1);
-        const double bh = b.get(h);
-        if ((ah0 * x0 + ah1 * x1) - bh <= FEAS_TOL * pmax(1.0, fabs(bh))) continue;
-        const double n2 = ah0 * ah0 + ah1 * ah1;
-        if (!(n2 > 0)) return h;
-        const double t = bh / n2;
-        const double p0 = t * ah0, p1 = t * ah1;
-        const double d0 = -ah1, d1 = ah0;
-        double rh = 0.0, ah = 0.0, rl = 0.0, al = 0.0;
-        bool has_hi = false, has_lo = false;
-#pragma unroll 1
-        for (int j = 0; j < h; ++j) {
-            if (!((mask >> j) & 1u)) continue;
-            double aj0, aj1;
-            plane_normal(P, j, aj0, aj1);
-            const double ad = aj0 * d0 + aj1 * d1;
-            const double r = b.get(j) - (aj0 * p0 + aj1 * p1);
-            if (ad > 0) {
-                if (!has_hi || r * ah < rh * ad) {
-                    rh = r;
-                    ah = ad;
-                }
-                has_hi = true;
-            } else if (ad < 0) {
-                if (!has_lo || r * al > rl * ad) {
-                    rl = r;
-                    al = ad;
-                }
-                has_lo = true;
-            }
-        }
-        double s = 0.0;
-        bool s_hi = false;
-        if (has_hi && rh < 0) {
-            s = rh / ah;
-            s_hi = true;
-        }
-        if (has_lo && (s_hi ? (rh * al > rl * ah) : (rl < 0))) s = rl / al;
-        x0 = p0 + s * d0;
-        x1 = p1 + s * d1;
-        bool ok = true;
-#pragma unroll 1
-        for (int j = 0; j <= h; ++j) {
-            if (!((mask >> j) & 1u)) continue;
-            double aj0, aj1;
-            plane_normal(P, j, aj0, aj1);
-            const double bj = b.get(j);
-            ok = ok && ((aj0 * x0 + aj1 * x1) - bj <= FEAS_TOL * pmax(1.0, fabs(bj)));
-        }
-        if (!ok) return h;
-    }
-    xo0 = x0;
-    xo1 = x1;
-    return -1;
-}
-
-__device__ __forceinline__ Sol solve_ego_lds(const KP& P, const Ego& E, const LaneCol& b) {
-    const Box B = box_rhs(P, E);
-    b.set(0, pmin(B.S[0], B.S[4]));
-    b.set(1, pmin(B.S[1], B.S[6]));
-    b.set(2, pmin(B.S[2], B.S[5]));
-    b.set(3, pmin(B.S[3], B.S[7]));
-    double q0 = E.bq0, q1 = E.bq1, q2 = E.bq2, q3 = E.bq3;
-    const unsigned mask = 0xFu | (E.present << 4);
-    Sol S;
-    S.status = CBF_STATUS_OPTIMAL;
-    S.iters = 0;
-    S.x0 = S.x1 = 0.0;
-    if ((E.present & 9u) == 9u || (E.present & 6u) == 6u) {  // strip pre-check, as solve_ego
-        for (;;) {
-            bool dead = false;
-            if ((E.present & 9u) == 9u) {
-                const double s = q0 + q3;
-                const double tb = FEAS_TOL * (pmax(1.0, fabs(q0)) + pmax(1.0, fabs(q3)));
-                dead = dead || (s < -tb - 1e-9 * (1.0 + fabs(q0) + fabs(q3)));
-            }
-            if ((E.present & 6u) == 6u) {
-                const double s = q1 + q2;
-                const double tb = FEAS_TOL * (pmax(1.0, fabs(q1)) + pmax(1.0, fabs(q2)));
-                dead = dead || (s < -tb - 1e-9 * (1.0 + fabs(q1) + fabs(q2)));
-            }
-            if (!dead || S.iters >= P.relax_cap) break;
-            q0 = q0 + 1.0;
-            q1 = q1 + 1.0;
-            q2 = q2 + 1.0;
-            q3 = q3 + 1.0;
-            S.iters++;
-        }
-    }
-    for (;;) {
-        b.set(4, q0);
-        b.set(5, q1);
-        b.set(6, q2);
-        b.set(7, q3);
-        const int fail = solve8_lds(P, b, mask, S.x0, S.x1);
-        if (fail < 0) break;
-        if (fail < 4) {  // reported as at the first solve: no relaxation applied
-            S.status = CBF_STATUS_BOX_INFEASIBLE;
-            S.iters = 0;
-            S.x0 = S.x1 = 0.0;
-            q0 = E.bq0;
-            q1 = E.bq1;
-            q2 = E.bq2;
-            q3 = E.bq3;
-            b.set(4, q0);
-            b.set(5, q1);
-            b.set(6, q2);
-            b.set(7, q3);
-            break;
-        }
-        if (S.iters >= P.relax_cap) {
-            S.status = CBF_STATUS_RELAX_CAP;
-            S.x0 = S.x1 = 0.0;
-            break;
-        }
-        q0 = q0 + 1.0;
-        q1 = q1 + 1.0;
-        q2 = q2 + 1.0;
-        q3 = q3 + 1.0;
-        S.iters++;
-    }
-    if (S.status == CBF_STATUS_OPTIMAL && S.iters > 0) S.status = CBF_STATUS_RELAXED;
-    double v = 0.0;
-#pragma unroll 1
-    for (int h = 0; h < 8; ++h)
-        if ((mask >> h) & 1u) {
-            double a0, a1;
-            plane_normal(P, h, a0, a1);
-            const double d = (a0 * S.x0 + a1 * S.x1) - b.get(h);
-            if (d > v) v = d;
-        }
-    S.viol = v;
+    S.viol_orig = S.iters > 0 ? orig_violation(P, E, B, S.x0, S.x1) : v;
     return S;
 }
 
@@ -885,6 +486,7 @@ __device__ __forceinline__ bool solve_easy(const KP& P, const Ego& E, Sol& S) {
     S.iters = iters;
     S.status = iters > 0 ? CBF_STATUS_RELAXED : CBF_STATUS_OPTIMAL;
     S.viol = v;
+    S.viol_orig = iters > 0 ? orig_violation(P, E, B, x0, x1) : v;
     return true;
 }
 

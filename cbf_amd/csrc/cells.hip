@@ -9,7 +9,7 @@ __global__ void __launch_bounds__(kBlock) k_bin(CellGrid G, int n, const double2
                                                 int32_t* __restrict__ count, int2* __restrict__ cs,
                                                 int32_t* __restrict__ sctl) {
     const int i = blockIdx.x * kBlock + threadIdx.x;
-    if (CBF_SCAN_EPOCH_BIN && i == 0) scan_epoch_advance(sctl);
+    if (i == 0) build_begin(sctl, n, (long)G.nx * G.ny);
     if (i >= n) return;
     const double2 p = pos[i];
     const int c = cell_coord(p.y, G.y0, G.inv_h, G.ny) * G.nx + cell_coord(p.x, G.x0, G.inv_h, G.nx);
@@ -21,16 +21,19 @@ __global__ void __launch_bounds__(kBlock) k_bin(CellGrid G, int n, const double2
 // dispatcher hands out workgroups in increasing order, so a tile only waits on tiles whose blocks
 // are already resident.  Tile status is one 64-bit word {epoch:30 | flag:2 | value:32} written
 // and read with agent-scope relaxed atomics (the payload travels inside the flag word, so no
-// fence is needed); the epoch (advanced before each scan, CBF_SCAN_EPOCH_BIN) makes words of earlier
-// launches invisible without a reset pass.  The epoch load and the count loads are independent,
-// so the critical path is load -> publish/look-back -> store.  The kernel re-zeroes the counts it
-// consumed.  Spins are bounded; a timeout sets sctl[2].
+// fence is needed); the epoch (advanced before each scan by the bin kernel) makes words of
+// earlier launches invisible without a reset pass.  The epoch load and the count loads are
+// independent, so the critical path is load -> publish/look-back -> store.  The kernel re-zeroes
+// the counts it consumed.  Spins are bounded: a look-back that gives up sets sctl[2], which the
+// filter kernels turn into CBF_STATUS_WORKSPACE_ERROR for every ego of that step (the cell starts
+// are then wrong); the next bin kernel clears it (build_begin).  CBF_SCAN_TEST_TIMEOUT = 1 (a test build only)
+// makes every look-back give up at once, so the reporting path can be tested deterministically.
 constexpr unsigned long long kFlagAgg = 1ull << 32, kFlagInc = 2ull << 32;
-#ifndef CBF_SCAN_VST
-#define CBF_SCAN_VST 1  // full-tile starts written as 16-B vector stores (start is 256-B aligned)
+#ifndef CBF_SCAN_SPIN_LIMIT
+#define CBF_SCAN_SPIN_LIMIT (1l << 24)
 #endif
-#ifndef CBF_SCAN_SUMAGG
-#define CBF_SCAN_SUMAGG 0  // predecessor aggregates summed directly (measured no faster: build 43.0 vs 41.6 us)
+#ifndef CBF_SCAN_TEST_TIMEOUT
+#define CBF_SCAN_TEST_TIMEOUT 0
 #endif
 
 __device__ __forceinline__ unsigned long long ld_state(const unsigned long long* p) {
@@ -87,37 +90,6 @@ __global__ void __launch_bounds__(kBlock) k_scan_onepass(int32_t* __restrict__ c
             if (lane == 0) st_state(&tstate[0], ep | kFlagInc | (unsigned)agg);
         } else {
             if (lane == 0) st_state(&tstate[tile], ep | kFlagAgg | (unsigned)agg);
-#if CBF_SCAN_SUMAGG
-            // exclusive prefix = the sum of ALL predecessors' aggregates: their loads are
-            // independent (4 per lane in flight), so the critical path is one publish -> load
-            // round trip instead of a chain of inclusive values through the tiles (no tile
-            // publishes an inclusive value in this form; tile 0's equals its aggregate)
-            int part = 0;
-            long spins = 0;
-            for (int i0 = 0; i0 < tile; i0 += 4 * 64) {
-                unsigned long long v[4];
-#pragma unroll
-                for (int k = 0; k < 4; ++k) {
-                    const int idx = i0 + k * 64 + lane;
-                    v[k] = idx < tile ? ld_state(&tstate[idx]) : (ep | kFlagAgg);
-                }
-#pragma unroll
-                for (int k = 0; k < 4; ++k) {
-                    const int idx = i0 + k * 64 + lane;
-                    while ((v[k] & ~((1ull << 34) - 1)) != ep || (v[k] & (3ull << 32)) == 0) {
-                        if (++spins > (1l << 24)) {
-                            sctl[2] = 1;
-                            break;
-                        }
-                        __builtin_amdgcn_s_sleep(1);
-                        v[k] = ld_state(&tstate[idx]);
-                    }
-                    if (idx < tile) part += (int)(unsigned)(v[k] & 0xFFFFFFFFull);
-                }
-            }
-            for (int o = 32; o > 0; o >>= 1) part += __shfl_xor(part, o, 64);
-            excl = part;
-#else
             int top = tile - 1;
             long spins = 0;
             while (true) {
@@ -128,8 +100,8 @@ __global__ void __launch_bounds__(kBlock) k_scan_onepass(int32_t* __restrict__ c
                 const unsigned long long im = __ballot(incl), nr = __ballot(!ready);
                 const int stop = im ? __ffsll((long long)im) - 1 : 63;  // lanes 0..stop are needed
                 const unsigned long long need = stop == 63 ? ~0ull : ((1ull << (stop + 1)) - 1);
-                if (nr & need) {
-                    if (++spins > (1l << 24)) {
+                if (CBF_SCAN_TEST_TIMEOUT || (nr & need)) {
+                    if (CBF_SCAN_TEST_TIMEOUT || ++spins > CBF_SCAN_SPIN_LIMIT) {
                         if (lane == 0) sctl[2] = 1;
                         break;
                     }
@@ -143,24 +115,16 @@ __global__ void __launch_bounds__(kBlock) k_scan_onepass(int32_t* __restrict__ c
                 top -= 64;
             }
             if (lane == 0) st_state(&tstate[tile], ep | kFlagInc | (unsigned)(excl + agg));
-#endif
         }
         if (lane == 0) {
             s_excl = excl;
             if (tile == ntiles - 1) start[ncell] = excl + agg;
-            // the last block to finish bumps the epoch: every block has read it by then
-            if (!CBF_SCAN_EPOCH_BIN && atomicAdd(&sctl[0], 1) == ntiles - 1) {
-                sctl[0] = 0;
-                __hip_atomic_store(&sctl[1], (int)((epoch + 1) & 0x3FFFFFFFu), __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
-            }
         }
     }
     __syncthreads();
     int wpre = 0;
     for (int w = 0; w < wid; ++w) wpre += wtot[w];
     int run = s_excl + wpre + inc - tot;
-#if CBF_SCAN_VST
     if (base + kPer <= ncell) {  // full tile: the lane's starts as 16-B stores, like the loads
         int o[kPer];
 #pragma unroll
@@ -173,7 +137,6 @@ __global__ void __launch_bounds__(kBlock) k_scan_onepass(int32_t* __restrict__ c
             *reinterpret_cast<int4*>(start + base + 4 * v) = make_int4(o[4 * v], o[4 * v + 1], o[4 * v + 2], o[4 * v + 3]);
         return;
     }
-#endif
 #pragma unroll
     for (int k = 0; k < kPer; ++k) {
         if (base + k < ncell) start[base + k] = run;
@@ -181,16 +144,19 @@ __global__ void __launch_bounds__(kBlock) k_scan_onepass(int32_t* __restrict__ c
     }
 }
 
+// Scatter into the cell-sorted copies.  Skipped entirely when the build is flagged unusable
+// (sctl[2]: the starts cannot be trusted), and every slot is bounds-checked.
 __global__ void __launch_bounds__(kBlock) k_scatter(int n, const int2* __restrict__ cs,
                                                     const int32_t* __restrict__ start,
                                                     const double2* __restrict__ pos, const double2* __restrict__ vel,
                                                     double2* __restrict__ spos, double2* __restrict__ svel,
-                                                    int32_t* __restrict__ sidx) {
+                                                    int32_t* __restrict__ sidx, const int32_t* __restrict__ sctl) {
     const int i = blockIdx.x * kBlock + threadIdx.x;
-    if (i >= n) return;
+    if (i >= n || sctl[2] != 0) return;
     const int2 c = cs[i];
     if (c.x < 0) return;
     const int d = start[c.x] + c.y;
+    if (d < 0 || d >= n) return;
     spos[d] = pos[i];
     svel[d] = vel[i];
     sidx[d] = i;
@@ -209,7 +175,7 @@ int scan_and_scatter(const CellGrid& G, const CellWs& W, int n, const double2* p
                      hipStream_t s) {
     launch_scan(W, s);
     hipLaunchKernelGGL(k_scatter, dim3(nblk(n)), dim3(kBlock), 0, s, n, W.cs, W.start, pos, vel, W.spos, W.svel,
-                       W.sidx);
+                       W.sidx, W.sctl);
     return (int)hipGetLastError();
 }
 

@@ -13,18 +13,19 @@
 namespace cbf {
 
 #ifndef CBF_SCAN_PER
-#define CBF_SCAN_PER 8  // cells per scan lane (a multiple of 4)
+#define CBF_SCAN_PER 8  // cells per scan lane
 #endif
+static_assert(CBF_SCAN_PER >= 4 && CBF_SCAN_PER % 4 == 0, "the scan moves its cells as 16-B int4 vectors");
 constexpr int kScanTile = 256 * CBF_SCAN_PER;  // 256 threads x CBF_SCAN_PER cells
-#ifndef CBF_HARD_BLOCKS
-#define CBF_HARD_BLOCKS 128
-#endif
-// grid (64-lane blocks) of the hard-QP kernel of the lattice step: 8 k lanes cover the ~3 k queued
-// QPs of cfg4 one per lane; each block ends with an atomic on the done counter, so fewer blocks
-// end sooner (advance 50.2 us at 128 blocks, 51.0 at 256, 59.8 at 1024; tools/ablate.py set hard)
-constexpr int kHardBlocks = CBF_HARD_BLOCKS;
-constexpr int kHardHeader = 16;  // int32 words ahead of the hard-QP records (count + padding)
-
+// Hard-QP queues of the lattice step: kSubQ sub-queues; filter block b appends the QPs it cannot
+// finish at the origin to sub-queue b % kSubQ (one wave-aggregated atomic per wave on that
+// sub-queue's counter), so the entries of a sub-queue are contiguous and the queue kernel runs
+// them in full waves.  One chip-wide counter serialised ~16 k wave atomics a step at the memory
+// side (the filter ran 200 us instead of 43 at cfg4f); 64 counters on separate 128-B lines take
+// ~256 each, in parallel.  Header: [2..7] the cell-order state of the last build; [32 (1 + q)]
+// sub-queue q's length; [32 (1 + kSubQ + q)] its done counter (queue kernel).
+constexpr int kSubQ = 64;
+constexpr int kHardHeader = 32 * (1 + 2 * kSubQ);
 // A QP the filter kernel could not solve at the origin, queued with its assembled state.
 struct HardRec {
     double r0, r1, r2, r3, u0x, u0y, bq0, bq1, bq2, bq3;
@@ -48,38 +49,44 @@ inline CellGrid make_grid(const cbf_grid* g) {
 
 inline size_t align256(size_t b) { return (b + 255) & ~size_t(255); }
 
-// Workspace carve-up (all segments 256-byte aligned).
+// Workspace carve-up (all segments 256-byte aligned).  The control words come first, at a fixed
+// offset, so that the shape signature they hold can be checked whatever shape a call assumes.
 struct CellWs {
+    int32_t* sctl;    // [64] control: [1] scan epoch, [2] error flag of this build (scan look-back
+                      // gave up, or workspace shape mismatch), [4] n, [5] ncell: the shape the
+                      // workspace is bound to (0 = fresh)
     int32_t* count;   // [ncell]
     int32_t* start;   // [ncell + 1]
     unsigned long long* tstate;  // [ntiles] scan tile status {epoch:30 | flag:2 | value:32}
-    int32_t* sctl;    // [64] scan control: [0] finished-tile counter, [1] epoch, [2] error flag
-    int2* cs;        // [n] (cell, slot), cell < 0: not binned; 16 B/entry reserved (lattice: int4)
+    int2* cs;         // [n] (cell, slot), cell < 0: not binned; 16 B/entry reserved (lattice: int3)
     double2* spos;    // [n] cell-sorted positions
     double2* svel;    // [n] cell-sorted velocities / nominal controls
     int32_t* sidx;    // [n] entity index of each sorted slot
-    double2* wvel;    // [n] scratch velocities (lattice step: nominal of window agents)
-    float2* spos32;   // [n] fp32 copy of spos (lattice step: the filter's distance screen)
-    int32_t* hardq;   // lattice step: [0] = count, records (HardRec) from word kHardHeader
+    double2* wvel;    // [n] scratch velocities
+    int32_t* hardq;   // lattice step: header (kHardHeader words)
+    HardRec* qrec;    // [kSubQ * qcap] sub-queue q at qrec + q * qcap (HOCBF: int slots)
     long ncell;
     int ntiles;
+    long qcap;
 
     static int tiles(long ncell) { return (int)((ncell + kScanTile - 1) / kScanTile); }
+    // capacity of a sub-queue: the egos of the filter blocks that append to it
+    static long subq_cap(long n) { return ((n + kBlock - 1) / kBlock + kSubQ - 1) / kSubQ * kBlock; }
     static size_t bytes(long n, long ncell) {
-        return align256(4 * ncell) + align256(4 * (ncell + 1)) + align256(8 * (size_t)tiles(ncell)) + 256 +
-               align256(16 * n) + 2 * align256(16 * n) + align256(4 * n) + align256(16 * n) + align256(8 * n) +
-               align256(4 * kHardHeader + sizeof(HardRec) * (size_t)n);
+        return 256 + align256(4 * ncell) + align256(4 * (ncell + 1)) + align256(8 * (size_t)tiles(ncell)) +
+               align256(16 * n) + 2 * align256(16 * n) + align256(4 * n) + align256(16 * n) +
+               align256(4 * kHardHeader) + align256(sizeof(HardRec) * (size_t)(kSubQ * subq_cap(n)));
     }
-    CellWs(void* base, long n, long nc) : ncell(nc), ntiles(tiles(nc)) {
+    CellWs(void* base, long n, long nc) : ncell(nc), ntiles(tiles(nc)), qcap(subq_cap(n)) {
         char* p = (char*)base;
+        sctl = (int32_t*)p;
+        p += 256;
         count = (int32_t*)p;
         p += align256(4 * nc);
         start = (int32_t*)p;
         p += align256(4 * (nc + 1));
         tstate = (unsigned long long*)p;
         p += align256(8 * (size_t)ntiles);
-        sctl = (int32_t*)p;
-        p += 256;
         cs = (int2*)p;
         p += align256(16 * n);
         spos = (double2*)p;
@@ -90,9 +97,9 @@ struct CellWs {
         p += align256(4 * n);
         wvel = (double2*)p;
         p += align256(16 * n);
-        spos32 = (float2*)p;
-        p += align256(8 * n);
         hardq = (int32_t*)p;
+        p += align256(4 * kHardHeader);
+        qrec = (HardRec*)p;
     }
 };
 
@@ -105,15 +112,23 @@ int scan_and_scatter(const CellGrid& G, const CellWs& W, int n, const double2* p
 // Exclusive scan of W.count into W.start (and re-zeroes W.count).
 void launch_scan(const CellWs& W, hipStream_t s);
 
-// CBF_SCAN_EPOCH_BIN: the scan's tile-state epoch is advanced by thread 0 of the bin kernel that
-// precedes every scan (stream order makes it visible), instead of by the last scan block to
-// finish -- that needed a returning atomic on one counter from each of the ~270 scan blocks, a
-// serialised chain at the end of the scan.
-#ifndef CBF_SCAN_EPOCH_BIN
-#define CBF_SCAN_EPOCH_BIN 1
-#endif
-__device__ __forceinline__ void scan_epoch_advance(int32_t* sctl) {
-    sctl[1] = (sctl[1] + 1) & 0x3FFFFFFF;  // one thread, before the scan kernel starts
+// Start of a build, by thread 0 of the bin kernel that precedes every scan (stream order makes it
+// visible): advance the scan's tile-state epoch (rather than by the last scan block to finish,
+// which needed a returning atomic from each of the ~270 scan blocks: a serialised chain), clear
+// the error flag, and check the workspace's shape binding.  A workspace holds counts, starts and
+// tile words whose offsets depend on (n, ncell); reused for another shape without re-zeroing, those
+// would corrupt the cell list, so a mismatch sets the error flag (every ego of the step reports
+// CBF_STATUS_WORKSPACE_ERROR) and stays bound to the old shape, so later calls fail the same way
+// until the caller zero-fills the workspace.
+__device__ __forceinline__ void build_begin(int32_t* sctl, long n, long ncell) {
+    sctl[1] = (sctl[1] + 1) & 0x3FFFFFFF;
+    const bool fresh = sctl[4] == 0 && sctl[5] == 0;
+    const bool same = sctl[4] == (int32_t)n && sctl[5] == (int32_t)ncell;
+    sctl[2] = (fresh || same) ? 0 : 1;
+    if (fresh) {
+        sctl[4] = (int32_t)n;
+        sctl[5] = (int32_t)ncell;
+    }
 }
 
 }  // namespace cbf

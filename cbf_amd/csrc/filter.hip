@@ -132,17 +132,10 @@ __device__ __forceinline__ void ap_exact(const KP& P, Ego& E, const double2* sp,
 #ifndef CBF_AP_SCREEN
 #define CBF_AP_SCREEN 8   // candidates per screen step
 #endif
-#ifndef CBF_AP_PACKED
-#define CBF_AP_PACKED 0   // packed-fp32 difference-form screen (tools/ablate.py times it)
-#endif
-#ifndef CBF_AP_EXPAND
-#define CBF_AP_EXPAND 0   // expanded-form screen (2 FMAs per pair) where its bound holds; measured no faster
-#endif
-typedef float pf2 __attribute__((ext_vector_type(2)));
 
 // The all-pairs candidate loop of one ego over entities [c0, c1): tiles of CBF_AP_TILE entities
-// staged in LDS (fp64 state plus fp32 copies of the positions and of |p|^2, SoA, so one 16-B LDS
-// read brings 4 consecutive candidates) and read by broadcast (every lane reads the same
+// staged in LDS (fp64 state plus fp32 copies of the positions, SoA, so one 16-B LDS read brings 4
+// consecutive candidates) and read by broadcast (every lane reads the same
 // candidate), ascending index order (= reference order).  CBF_AP_SCREEN candidates per screen
 // step; the exact test and row assembly run only for candidates the screen lets through.  Every
 // lane of the block must call it (it synchronises the block).
@@ -151,33 +144,8 @@ struct ApLds {
     double2 sv[CBF_AP_TILE];
     float xs32[CBF_AP_TILE];
     float ys32[CBF_AP_TILE];
-    float qs32[CBF_AP_TILE];  // fl(fma(x, x, fl(y * y))): the candidate's |p|^2 for the expanded screen
     double smax[kBlock / 64];
 };
-
-// Expanded-form fp32 screen: S' = fl(fma(px, -2ex, fl(fma(py, -2ey, q)))), q = fl(fma(px, px,
-// fl(py*py))), is |p - e|^2 - |e|^2 up to rounding, 2 FMAs per pair instead of the difference
-// form's 2 subtractions + mul + fma.  Bound (all fp32 coordinates |.| <= M1 = M(1+u), u = 2^-24):
-// |q - Q| <= 2.001uQ and the two FMAs add u|py b + q| + u|px a + py b + q|(1+u), so
-// |S' - (D32 - EE)| <= 14.1 u M1^2 with D32 = |p - e|^2 (real) and EE = ex^2 + ey^2 (exact in
-// fp64).  A candidate passing the exact fp64 test has |P - E| <= r and, with componentwise
-// rounding of 2uM, D32 <= rho^2, rho = r + 2 sqrt2 uM.  So S' < T = rho^2 + 16 u M1^2 - EE (with
-// slack, rounded up to fp32).  Only used while 16 u M1^2 <= cull_t (M up to ~200 at cull_t =
-// 0.04), else the difference form; like it, the screen only rejects.
-__device__ __forceinline__ bool expand_threshold(double cull_t, double M, float ex, float ey, float& t) {
-    const double u = 0x1p-24;
-    const double M1 = M * (1.0 + 2.0 * u) + 1e-30;
-    const double slack = 16.5 * u * M1 * M1;
-    if (!(M <= 1e30) || !(slack <= cull_t)) return false;
-    const double r = sqrt(cull_t) * (1.0 + 1e-12) + 1e-35;
-    const double rho = r + 2.0 * 1.4142135623730951 * u * M * (1.0 + 1e-12);
-    const double ee = (double)ex * (double)ex + (double)ey * (double)ey;
-    const double T = (rho * rho + slack) * (1.0 + 1e-12) - ee * (1.0 - 1e-15) + 1e-30;
-    float t32 = (float)T;
-    if ((double)t32 < T) t32 = nextafterf(t32, INFINITY);
-    t = t32;
-    return true;
-}
 
 template <class Hit>
 __device__ __forceinline__ void allpairs_scan(const KP& P, double r0, double r1, bool active, int c0, int c1,
@@ -187,7 +155,6 @@ __device__ __forceinline__ void allpairs_scan(const KP& P, double r0, double r1,
     constexpr int kTile = CBF_AP_TILE;
     constexpr int kPer = kTile / kBlock;
     const float ex = (float)r0, ey = (float)r1;
-    const float ea = -2.0f * ex, eb = -2.0f * ey;  // exact
     double m_ego = absmax2(make_double2(r0, r1));
     if (m_ego != m_ego) m_ego = INFINITY;
     for (int base = c0; base < c1; base += kTile) {
@@ -203,7 +170,6 @@ __device__ __forceinline__ void allpairs_scan(const KP& P, double r0, double r1,
                 const float x = (float)pj.x, y = (float)pj.y;
                 L.xs32[tl] = x;
                 L.ys32[tl] = y;
-                L.qs32[tl] = __builtin_fmaf(x, x, y * y);
                 double a = absmax2(pj);
                 if (a != a) a = INFINITY;  // NaN coordinate: screen off for this tile
                 mj = pmax(mj, a);
@@ -219,69 +185,30 @@ __device__ __forceinline__ void allpairs_scan(const KP& P, double r0, double r1,
             for (int w = 1; w < kBlock / 64; ++w) mt = pmax(mt, L.smax[w]);
             const double M = pmax(mt, m_ego);
             int t = 0;
-            float te = 0.0f;
-            const bool exp_ok = CBF_AP_EXPAND && expand_threshold(P.cull_t, M, ex, ey, te);
-            // the form is chosen per wave (both are exact filters; a mixed wave would run both)
-            if (__ballot(exp_ok) == __ballot(1)) {
+            // fp32 difference-form screen; it only rejects (screen_threshold), and it is off for
+            // tiles with huge or non-finite coordinates (every candidate then takes the exact test)
+            const float t32 = screen_threshold(P.cull_t, M);
+            if (t32 > 0.0f) {
                 for (; t + kScreen <= m; t += kScreen) {
                     float sq[kScreen];
 #pragma unroll
                     for (int q = 0; q < kScreen; q += 4) {
                         const float4 X = *reinterpret_cast<const float4*>(&L.xs32[t + q]);
                         const float4 Y = *reinterpret_cast<const float4*>(&L.ys32[t + q]);
-                        const float4 Q = *reinterpret_cast<const float4*>(&L.qs32[t + q]);
-                        sq[q] = __builtin_fmaf(X.x, ea, __builtin_fmaf(Y.x, eb, Q.x));
-                        sq[q + 1] = __builtin_fmaf(X.y, ea, __builtin_fmaf(Y.y, eb, Q.y));
-                        sq[q + 2] = __builtin_fmaf(X.z, ea, __builtin_fmaf(Y.z, eb, Q.z));
-                        sq[q + 3] = __builtin_fmaf(X.w, ea, __builtin_fmaf(Y.w, eb, Q.w));
+                        const float xs[4] = {X.x, X.y, X.z, X.w}, ys[4] = {Y.x, Y.y, Y.z, Y.w};
+#pragma unroll
+                        for (int k = 0; k < 4; ++k) {
+                            const float d0 = xs[k] - ex, d1 = ys[k] - ey;
+                            sq[q + k] = __builtin_fmaf(d0, d0, d1 * d1);
+                        }
                     }
                     float mn = sq[0];
 #pragma unroll
                     for (int q = 1; q < kScreen; ++q) mn = fminf(mn, sq[q]);
-                    if (mn < te) {
+                    if (mn < t32) {
 #pragma unroll
                         for (int q = 0; q < kScreen; ++q)
-                            if (sq[q] < te) hit(base, t + q);
-                    }
-                }
-            } else {
-                const float t32 = screen_threshold(P.cull_t, M);
-                if (t32 > 0.0f) {
-                    for (; t + kScreen <= m; t += kScreen) {
-                        float sq[kScreen];
-#pragma unroll
-                        for (int q = 0; q < kScreen; q += 4) {
-                            const float4 X = *reinterpret_cast<const float4*>(&L.xs32[t + q]);
-                            const float4 Y = *reinterpret_cast<const float4*>(&L.ys32[t + q]);
-#if CBF_AP_PACKED
-                            // two candidates per packed fp32 op: same arithmetic per candidate as
-                            // the scalar form, fma(d0, d0, d1 * d1)
-                            const pf2 e2x = {ex, ex}, e2y = {ey, ey};
-                            const pf2 dxa = pf2{X.x, X.y} - e2x, dxb = pf2{X.z, X.w} - e2x;
-                            const pf2 dya = pf2{Y.x, Y.y} - e2y, dyb = pf2{Y.z, Y.w} - e2y;
-                            const pf2 sa = __builtin_elementwise_fma(dxa, dxa, dya * dya);
-                            const pf2 sb = __builtin_elementwise_fma(dxb, dxb, dyb * dyb);
-                            sq[q] = sa.x;
-                            sq[q + 1] = sa.y;
-                            sq[q + 2] = sb.x;
-                            sq[q + 3] = sb.y;
-#else
-                            const float xs[4] = {X.x, X.y, X.z, X.w}, ys[4] = {Y.x, Y.y, Y.z, Y.w};
-#pragma unroll
-                            for (int k = 0; k < 4; ++k) {
-                                const float d0 = xs[k] - ex, d1 = ys[k] - ey;
-                                sq[q + k] = __builtin_fmaf(d0, d0, d1 * d1);
-                            }
-#endif
-                        }
-                        float mn = sq[0];
-#pragma unroll
-                        for (int q = 1; q < kScreen; ++q) mn = fminf(mn, sq[q]);
-                        if (mn < t32) {
-#pragma unroll
-                            for (int q = 0; q < kScreen; ++q)
-                                if (sq[q] < t32) hit(base, t + q);
-                        }
+                            if (sq[q] < t32) hit(base, t + q);
                     }
                 }
             }
@@ -414,196 +341,6 @@ __global__ void __launch_bounds__(kBlock) k_allpairs_partial(KP P, int n, int n_
     part[(long)blockIdx.y * (ego_end - ego_begin) + k] = o;
 }
 
-// Split all-pairs, register-broadcast form (CBF_AP_DPP): the chunk's candidates are staged once
-// per call by k_ap_stage as fp32 {x, y, |p|^2, 0} records; every 16-lane row of a wave loads the
-// same 16 candidates (one 16-B load per lane per 16 candidates, from L1/L2), and DPP
-// row_newbcast:k hands candidate k to all 16 lanes of each row inside the VALU instruction that
-// uses it.  So the screen of one pair is v_mov_dpp + 2 v_fmac_dpp (+ half a v_min3), with no LDS
-// traffic and no block barriers: the LDS-staged form is bound by its broadcast ds_reads (6 per 8
-// candidates per wave).  Candidates the screen lets through are re-tested exactly from the fp64
-// state in global memory (a wave-uniform address).  Same exact tests, same per-quadrant minima.
-#ifndef CBF_AP_DPP
-#define CBF_AP_DPP 0  // measured slower than the LDS form (618 vs 579 us at cfg3)
-#endif
-constexpr int kApStage = 256;  // entities per k_ap_stage tile (tile max |coord| granularity)
-
-inline size_t ap_stage_bytes(long n) {
-    const long nt = (n + kApStage - 1) / kApStage;
-    return align256(sizeof(float4) * (size_t)(nt * kApStage)) + align256(sizeof(double) * (size_t)nt);
-}
-
-__global__ void __launch_bounds__(kApStage) k_ap_stage(int n, const double2* __restrict__ pos,
-                                                       float4* __restrict__ cand, double* __restrict__ tmax) {
-    __shared__ double wm[kApStage / 64];
-    const int j = blockIdx.x * kApStage + threadIdx.x;
-    float x = 0.0f, y = 0.0f;
-    double a = 0.0;
-    if (j < n) {
-        const double2 p = pos[j];
-        x = (float)p.x;
-        y = (float)p.y;
-        a = absmax2(p);
-        if (a != a) a = INFINITY;  // NaN coordinate: screen off for this tile
-    }
-    cand[j] = make_float4(x, y, __builtin_fmaf(x, x, y * y), 0.0f);  // padding (j >= n) never screened
-    for (int o = 32; o > 0; o >>= 1) a = pmax(a, __shfl_xor(a, o, 64));
-    if ((threadIdx.x & 63) == 0) wm[threadIdx.x >> 6] = a;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        double m = wm[0];
-        for (int w = 1; w < kApStage / 64; ++w) m = pmax(m, wm[w]);
-        tmax[blockIdx.x] = m;
-    }
-}
-
-// candidate K of the lane's 16-lane row, expanded form: fma(x, ea, fma(y, eb, q)) (v_fmac is fused)
-template <int K>
-__device__ __forceinline__ float dpp_expand(const float4& c, float ea, float eb) {
-    float acc;
-    // a VALU write of a DPP source needs 2 wait states before the DPP read; the compiler does not
-    // track hazards into inline asm, so the first broadcast of a group waits them out itself
-    if constexpr (K == 0)
-        asm("s_nop 1\n\tv_mov_b32_dpp %0, %1 row_newbcast:%2 row_mask:0xf bank_mask:0xf" : "=v"(acc) : "v"(c.z), "n"(K));
-    else
-        asm("v_mov_b32_dpp %0, %1 row_newbcast:%2 row_mask:0xf bank_mask:0xf" : "=v"(acc) : "v"(c.z), "n"(K));
-    asm("v_fmac_f32_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf" : "+v"(acc) : "v"(c.y), "v"(eb), "n"(K));
-    asm("v_fmac_f32_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf" : "+v"(acc) : "v"(c.x), "v"(ea), "n"(K));
-    return acc;
-}
-template <int K>
-__device__ __forceinline__ float dpp_bcast(float v) {
-    return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x150 + K, 0xF, 0xF, true));
-}
-
-template <int K>
-__device__ __forceinline__ void dpp_expand_all(const float4& c, float ea, float eb, float (&sq)[16]) {
-    if constexpr (K < 16) {
-        sq[K] = dpp_expand<K>(c, ea, eb);
-        dpp_expand_all<K + 1>(c, ea, eb, sq);
-    }
-}
-// mixed waves: per lane the expanded form (exp) or the difference form
-template <int K>
-__device__ __forceinline__ void dpp_mixed_all(const float4& c, bool exp, float ea, float eb, float ex, float ey,
-                                              float (&sq)[16]) {
-    if constexpr (K < 16) {
-        const float x = dpp_bcast<K>(c.x), y = dpp_bcast<K>(c.y), q = dpp_bcast<K>(c.z);
-        const float d0 = x - ex, d1 = y - ey;
-        sq[K] = exp ? __builtin_fmaf(x, ea, __builtin_fmaf(y, eb, q)) : __builtin_fmaf(d0, d0, d1 * d1);
-        dpp_mixed_all<K + 1>(c, exp, ea, eb, ex, ey, sq);
-    }
-}
-
-// Every lane of the wave must call it with the same [c0, c1) (DPP reads other lanes: EXEC full).
-template <class Hit>
-__device__ __forceinline__ void allpairs_scan_dpp(const KP& P, double r0, double r1, bool active, int c0, int c1,
-                                                  const float4* __restrict__ cand, const double* __restrict__ tmax,
-                                                  Hit& hit) {
-    const float ex = (float)r0, ey = (float)r1;
-    const float ea = -2.0f * ex, eb = -2.0f * ey;  // exact
-    const int row_lane = threadIdx.x & 15;
-    double m_ego = absmax2(make_double2(r0, r1));
-    if (m_ego != m_ego) m_ego = INFINITY;
-    // c0 is a multiple of kApStage (chunks are whole tiles)
-    for (int base = c0; base < c1; base += kApStage) {
-        const int m = min(kApStage, c1 - base);
-        const double M = pmax(tmax[base / kApStage], m_ego);
-        float te = 0.0f;
-        const bool exp_ok = !active || (CBF_AP_EXPAND && expand_threshold(P.cull_t, M, ex, ey, te));
-        const float t32 = exp_ok ? 0.0f : screen_threshold(P.cull_t, M);
-        const bool screen = exp_ok || t32 > 0.0f;
-        const float thr = exp_ok ? te : t32;
-        int t = 0;
-        if (__ballot(!exp_ok) == 0) {  // the whole wave screens in the expanded form
-            float4 c = cand[base + row_lane];  // (staged records are padded to whole tiles)
-            for (; t + 16 <= m; t += 16) {
-                const int tn = t + 32 <= m ? t + 16 : t;
-                const float4 cn = cand[base + tn + row_lane];  // next group in flight
-                float sq[16];
-                dpp_expand_all<0>(c, ea, eb, sq);
-                // min tree in asm: fminf on asm results would canonicalise every input first
-                float m4[4];
-#pragma unroll
-                for (int q = 0; q < 4; ++q)
-                    asm("v_min3_f32 %0, %1, %2, %3\n\tv_min_f32 %0, %0, %4"
-                        : "=&v"(m4[q])
-                        : "v"(sq[4 * q]), "v"(sq[4 * q + 1]), "v"(sq[4 * q + 2]), "v"(sq[4 * q + 3]));
-                float mn;
-                asm("v_min3_f32 %0, %1, %2, %3\n\tv_min_f32 %0, %0, %4"
-                    : "=&v"(mn)
-                    : "v"(m4[0]), "v"(m4[1]), "v"(m4[2]), "v"(m4[3]));
-                if (active && mn < te) {
-#pragma unroll
-                    for (int q = 0; q < 16; ++q)
-                        if (sq[q] < te) hit(base, t + q);
-                }
-                c = cn;
-            }
-        } else if (__ballot(screen) == __ballot(1)) {  // difference form for some lanes
-            for (; t + 16 <= m; t += 16) {
-                const float4 c = cand[base + t + row_lane];
-                float sq[16];
-                dpp_mixed_all<0>(c, exp_ok, ea, eb, ex, ey, sq);
-                float mn = sq[0];
-#pragma unroll
-                for (int q = 1; q < 16; ++q) mn = fminf(mn, sq[q]);
-                if (active && mn < thr) {
-#pragma unroll
-                    for (int q = 0; q < 16; ++q)
-                        if (sq[q] < thr) hit(base, t + q);
-                }
-            }
-        }
-        // tail, and every candidate of a wave with a lane whose screen is off: exact test
-        if (active)
-            for (; t < m; ++t) hit(base, t);
-    }
-}
-
-__global__ void __launch_bounds__(kBlock) k_allpairs_partial_dpp(KP P, int n, int n_obs,
-                                                                 const double2* __restrict__ pos,
-                                                                 const double2* __restrict__ vel, int ego_begin,
-                                                                 int ego_end, int chunk, ApPart* __restrict__ part,
-                                                                 const float4* __restrict__ cand,
-                                                                 const double* __restrict__ tmax) {
-    const int e = ego_begin + blockIdx.x * kBlock + threadIdx.x;
-    const bool active = e < ego_end;
-    Ego E;
-    {
-        const double2 pe = active ? pos[e] : make_double2(0, 0);
-        const double2 ve = active ? vel[e] : make_double2(0, 0);
-        ego_init(P, E, pe.x, pe.y, ve.x, ve.y, ve.x, ve.y);
-    }
-    const int c0 = blockIdx.y * chunk;
-    const int c1 = min(n, c0 + chunk);
-    const int k = e - ego_begin;
-    const cbf_diag D0 = {};
-    // candidates in global memory: entity base + t at pos + base + t
-    struct {
-        const KP& P;
-        Ego& E;
-        const double2* pos;
-        const double2* vel;
-        int n_obs;
-        const cbf_diag& D;
-        int k;
-        int recorded;
-        __device__ __forceinline__ void operator()(int base, int t) {
-            ap_exact(P, E, pos + base, vel + base, base, t, n_obs, D, k, recorded);
-        }
-    } hit{P, E, pos, vel, n_obs, D0, k, 0};
-    allpairs_scan_dpp(P, E.r0, E.r1, active, c0, c1, cand, tmax, hit);
-    if (!active) return;
-    ApPart o;
-    o.bq0 = E.bq0;
-    o.bq1 = E.bq1;
-    o.bq2 = E.bq2;
-    o.bq3 = E.bq3;
-    o.present = (int)E.present;
-    o.count = E.count;
-    part[(long)blockIdx.y * (ego_end - ego_begin) + k] = o;
-}
-
 __global__ void __launch_bounds__(kBlock) k_allpairs_finish(KP P, int nchunk, const double2* __restrict__ pos,
                                                             const double2* __restrict__ vel, int ego_begin,
                                                             int ego_end, const ApPart* __restrict__ part,
@@ -638,9 +375,19 @@ __global__ void __launch_bounds__(kBlock) k_filter_cells(KP P, CellGrid G, int n
                                                          int ego_end, double* __restrict__ u,
                                                          int32_t* __restrict__ status, int32_t* __restrict__ cnt,
                                                          const double2* __restrict__ pos,
-                                                         const double2* __restrict__ vel, cbf_diag D) {
+                                                         const double2* __restrict__ vel, cbf_diag D,
+                                                         const int32_t* __restrict__ sctl) {
     const int slot = blockIdx.x * kBlock + threadIdx.x;
     if (slot >= n) return;
+    if (sctl[2] != 0) {  // the cell list of this call is unusable (cells.hpp build_begin, cells.hip scan):
+        const int e = slot;  // touch none of it; every ego reports the error, unfiltered
+        if (e < ego_begin || e >= ego_end) return;
+        const int k = e - ego_begin;
+        reinterpret_cast<double2*>(u)[k] = vel[e];
+        status[k] = CBF_STATUS_WORKSPACE_ERROR;
+        if (cnt) cnt[k] = 0;
+        return;
+    }
     const int e = sidx[slot];
     if (e < ego_begin || e >= ego_end) return;
     const double2 pe = spos[slot], ve = svel[slot];
@@ -754,8 +501,7 @@ extern "C" int cbf_cull_allpairs(const cbf_params* p, int32_t n, int32_t n_obs, 
 
 extern "C" size_t cbf_allpairs_workspace_size(int32_t n, int32_t n_ego) {
     if (n < 0 || n_ego < 0) return 0;
-    return align256(sizeof(ApPart) * (size_t)ap_chunks(n, n_ego) * (size_t)(n_ego > 0 ? n_ego : 1)) +
-           (CBF_AP_DPP ? ap_stage_bytes(n) : 0);
+    return align256(sizeof(ApPart) * (size_t)ap_chunks(n, n_ego) * (size_t)(n_ego > 0 ? n_ego : 1));
 }
 
 extern "C" int cbf_filter_allpairs_split(const cbf_params* p, int32_t n, int32_t n_obs, const double* pos,
@@ -774,18 +520,8 @@ extern "C" int cbf_filter_allpairs_split(const cbf_params* p, int32_t n, int32_t
     hipStream_t st = (hipStream_t)stream;
     const double2* p2 = reinterpret_cast<const double2*>(pos);
     const double2* v2 = reinterpret_cast<const double2*>(vel);
-    if (CBF_AP_DPP) {
-        const size_t pb = align256(sizeof(ApPart) * (size_t)s * (size_t)ne);
-        const long nt = (n + kApStage - 1) / kApStage;
-        float4* cand = reinterpret_cast<float4*>((char*)workspace + pb);
-        double* tmax = reinterpret_cast<double*>((char*)cand + align256(sizeof(float4) * (size_t)(nt * kApStage)));
-        hipLaunchKernelGGL(k_ap_stage, dim3(nt), dim3(kApStage), 0, st, n, p2, cand, tmax);
-        hipLaunchKernelGGL(k_allpairs_partial_dpp, dim3(grid_for(ne), s), dim3(kBlock), 0, st, kp, n, n_obs, p2, v2,
-                           ego_begin, ego_end, (int)chunk, part, cand, tmax);
-    } else {
-        hipLaunchKernelGGL(k_allpairs_partial, dim3(grid_for(ne), s), dim3(kBlock), 0, st, kp, n, n_obs, p2, v2,
-                           ego_begin, ego_end, (int)chunk, part);
-    }
+    hipLaunchKernelGGL(k_allpairs_partial, dim3(grid_for(ne), s), dim3(kBlock), 0, st, kp, n, n_obs, p2, v2,
+                       ego_begin, ego_end, (int)chunk, part);
     hipLaunchKernelGGL(k_allpairs_finish, dim3(grid_for(ne)), dim3(kBlock), 0, st, kp, s, p2, v2, ego_begin, ego_end,
                        part, u, status, nbr_count);
     return (int)hipGetLastError();
@@ -816,6 +552,6 @@ extern "C" int cbf_filter_cells(const cbf_params* p, const cbf_grid* grid, int32
     hipLaunchKernelGGL(k_filter_cells, dim3(grid_for(n)), dim3(kBlock), 0, s, make_kp(p), G, n, n_obs, W.spos, W.svel,
                        W.sidx, W.start, ego_begin, ego_end, u, status, nbr_count,
                        reinterpret_cast<const double2*>(pos), reinterpret_cast<const double2*>(vel),
-                       diag_or_empty(diag));
+                       diag_or_empty(diag), W.sctl);
     return (int)hipGetLastError();
 }

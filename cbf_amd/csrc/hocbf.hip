@@ -172,73 +172,6 @@ __device__ __forceinline__ int solve_rows(const double (&bb)[4], const Src& R, d
     return -1;
 }
 
-// CBF_HOCBF_CERT: skip the first solve of a QP that a Farkas certificate proves infeasible.
-// In the dense cfg4 swarm ~90 % of the HOCBF QPs relax exactly once (tools/diag_hocbf_iters.py),
-// so the solve at iteration 0 is a full O(m^2) pass that is certain to fail.  Certificate from
-// three barrier rows: i = the row most violated at the origin (b_i / |a_i|_1 most negative),
-// j and k = the rows angularly closest to -a_i on either side; lam_j a_j + lam_k a_k = -a_i
-// (Cramer) with lam >= 0 gives sum lam a = r (a rounding residual).  An x the solver accepts
-// satisfies every row within its tolerance 1e-12 max(1, |b|) plus the rounding of a.x - b, and
-// |x| <= max(bb) + tol by the box planes, so sum lam b >= -(sum lam (tol + rounding) + |r|_1 |x|);
-// if sum lam b lies below that (with a generous margin) the solve at iteration 0 must fail.  With
-// the box planes satisfied at the origin (all bb >= 0) it fails at a barrier row, so the oracle
-// relaxes once: we apply the same +1 (R.relax()) and continue the loop -- bit-identical.
-// Measured slower (advance 262.7 vs 239.0 us at cfg4, bit-identical): the failing first solve
-// stops at an early barrier row, so it is cheaper than the two certificate passes.  Off.
-#ifndef CBF_HOCBF_CERT
-#define CBF_HOCBF_CERT 0
-#endif
-template <class Src>
-__device__ __forceinline__ bool hocbf_certainly_infeasible(const Src& R, const double (&bb)[4]) {
-    if (R.m < 3 || !(bb[0] >= 0.0 && bb[1] >= 0.0 && bb[2] >= 0.0 && bb[3] >= 0.0)) return false;
-    int iw = -1;
-    double best = 0.0, ai0 = 0.0, ai1 = 0.0, bi = 0.0;
-    for (int i = 0; i < R.m; ++i) {
-        double a0, a1, b;
-        R.row(i, a0, a1, b);
-        const double n1 = fabs(a0) + fabs(a1);
-        if (!(n1 > 0.0) || !(b < 0.0)) continue;
-        const double q = b / n1;
-        if (iw < 0 || q < best) {
-            iw = i;
-            best = q;
-            ai0 = a0;
-            ai1 = a1;
-            bi = b;
-        }
-    }
-    if (iw < 0) return false;
-    const double c0 = -ai0, c1 = -ai1;
-    int jw = -1, kw = -1;
-    double cj = -INFINITY, ck = -INFINITY, aj0 = 0, aj1 = 0, bj = 0, ak0 = 0, ak1 = 0, bk = 0;
-    for (int i = 0; i < R.m; ++i) {
-        if (i == iw) continue;
-        double a0, a1, b;
-        R.row(i, a0, a1, b);
-        const double n2 = sqrt(a0 * a0 + a1 * a1);
-        if (!(n2 > 0.0)) continue;
-        const double cs = (c0 * a0 + c1 * a1) / n2;  // |c| cos(angle to -a_i); |c| is common
-        const double cr = c0 * a1 - c1 * a0;
-        if (cr > 0.0 && cs > cj) {
-            cj = cs, jw = i, aj0 = a0, aj1 = a1, bj = b;
-        } else if (cr < 0.0 && cs > ck) {
-            ck = cs, kw = i, ak0 = a0, ak1 = a1, bk = b;
-        }
-    }
-    if (jw < 0 || kw < 0) return false;
-    const double det = aj0 * ak1 - aj1 * ak0;
-    const double lj = (c0 * ak1 - c1 * ak0) / det, lk = (aj0 * c1 - aj1 * c0) / det;
-    if (!(lj >= 0.0 && lk >= 0.0 && lj < 1e12 && lk < 1e12)) return false;  // also rejects NaN / inf
-    const double r0 = (ai0 + lj * aj0) + lk * ak0, r1 = (ai1 + lj * aj1) + lk * ak1;
-    const double X = pmax(pmax(bb[0], bb[1]), pmax(bb[2], bb[3])) * (1.0 + 1e-9) + 1e-6;
-    const double sb = (bi + lj * bj) + lk * bk;
-    const double e_i = 1e-12 * pmax(1.0, fabs(bi)) + 1e-13 * ((fabs(ai0) + fabs(ai1)) * X + fabs(bi));
-    const double e_j = 1e-12 * pmax(1.0, fabs(bj)) + 1e-13 * ((fabs(aj0) + fabs(aj1)) * X + fabs(bj));
-    const double e_k = 1e-12 * pmax(1.0, fabs(bk)) + 1e-13 * ((fabs(ak0) + fabs(ak1)) * X + fabs(bk));
-    const double margin = 2.0 * ((e_i + lj * e_j) + lk * e_k) + (fabs(r0) + fabs(r1)) * X + 1e-12;
-    return sb < -margin;
-}
-
 // oracle/cbf_oracle.c:solve_hocbf -- +1 relaxation of every barrier row while infeasible
 template <class Src>
 __device__ __forceinline__ Sol solve_hocbf(const KP& P, const Ego& E, Src& R) {
@@ -249,11 +182,6 @@ __device__ __forceinline__ Sol solve_hocbf(const KP& P, const Ego& E, Src& R) {
     S.iters = 0;
     S.x0 = S.x1 = 0.0;
     S.viol = 0.0;
-    if (CBF_HOCBF_CERT && P.relax_cap > 0 && hocbf_certainly_infeasible(R, bb)) {
-        R.relax();  // the solve at iteration 0 would fail at a barrier row (see above)
-        S.iters = 1;
-        S.status = CBF_STATUS_RELAXED;
-    }
     for (;;) {
         const int fail = solve_rows(bb, R, S.x0, S.x1);
         if (fail < 0) break;
@@ -369,15 +297,9 @@ __global__ void __launch_bounds__(kBlock) k_hocbf_indexed(KP P, HP H, const doub
 // rows recomputed from the cell-sorted state during the solve; clip, Euler, outputs as
 // k_lattice_filter.  More than kHocbfCap neighbours: CBF_STATUS_NBR_OVERFLOW, u = u0.
 constexpr int kHocbfCap = 24;
-// CBF_HSORT_REG: the main HOCBF lattice kernel appends hits unsorted and sorts its <= 8 keys in
-// registers instead of keeping the LDS list sorted by insertion (tools/ablate.py set hsort)
-#ifndef CBF_HSORT_REG
-#define CBF_HSORT_REG 1
-#endif
-#ifndef CBF_HSCAN_U
-#define CBF_HSCAN_U 6
-#endif
-constexpr int kHScan = CBF_HSCAN_U;  // candidates in flight per lane in the HOCBF scan
+// The main HOCBF lattice kernel appends hits unsorted and sorts its <= 8 keys in registers
+// (hocbf_sort8) instead of keeping the LDS list sorted by insertion: advance 196.5 vs 219.9 us.
+constexpr int kHScan = 6;  // candidates in flight per lane in the HOCBF scan
 
 // Neighbour scan of one ego (slot) over its 3x3 cells; hits go into the ascending-entity key
 // list keys[i * ks + lane] (first kHocbfCap of them).  Returns the hit count m.
@@ -512,14 +434,20 @@ __device__ __forceinline__ void hocbf_finish(const KP& P, const Sol* S, const Eg
 // kLdsRows neighbours are queued (their slot, hardq) for k_lattice_filter_hocbf_wide, so the
 // long tail does not hold whole waves; more than kHocbfCap: CBF_STATUS_NBR_OVERFLOW, u = u0.
 __global__ void __launch_bounds__(kBlock) k_lattice_filter_hocbf(
-    KP P, HP H, CellGrid G, int W, int row_begin, int row_end, int win_row0, long ncell,
+    KP P, HP H, CellGrid G, int W, int row_begin, int row_end, int win_row0, long nwin, long ncell,
     const double2* __restrict__ spos, const double2* __restrict__ svel, const int32_t* __restrict__ sidx,
     const int32_t* __restrict__ start, double T, double2* __restrict__ pos_out, double2* __restrict__ u,
     int32_t* __restrict__ status, int32_t* __restrict__ cnt, int guard_rows, double* __restrict__ ext_part,
-    unsigned long long* __restrict__ solves, int32_t* __restrict__ hardq) {
+    unsigned long long* __restrict__ solves, int32_t* __restrict__ hardq, int32_t* __restrict__ qslot, long qcap,
+    const int32_t* __restrict__ sctl) {
     __shared__ unsigned long long keys[kHocbfCap * kBlock];
     const int bx = xcd_block();
     const int slot = bx * kBlock + threadIdx.x;
+    if (sctl[2] != 0) {  // unusable cell list (build_begin / scan timeout): touch none of it
+        lattice_error_tail(W, row_begin, row_end, win_row0, nwin, slot, u, status, cnt, solves, ext_part,
+                           (long)bx * (kBlock / 64) + (threadIdx.x >> 6));
+        return;
+    }
     const int total = start[ncell];
     double e0 = INFINITY, e1 = -INFINITY, e2 = -INFINITY, e3 = INFINITY;
     bool solved = false;
@@ -530,12 +458,12 @@ __global__ void __launch_bounds__(kBlock) k_lattice_filter_hocbf(
             const double2 pe = spos[slot], ve = svel[slot];
             Ego E;
             ego_init(P, E, pe.x, pe.y, ve.x, ve.y, ve.x, ve.y);
-            const int m = hocbf_scan<!CBF_HSORT_REG>(P, G, E, spos, sidx, start, keys, kBlock, threadIdx.x);
+            const int m = hocbf_scan<false>(P, G, E, spos, sidx, start, keys, kBlock, threadIdx.x);
             E.count = m;
             if (m > kLdsRows && m <= kHocbfCap) {
-                hardq[kHardHeader + atomicAdd(&hardq[0], 1)] = slot;
+                qslot[(long)(bx % kSubQ) * qcap + subq_append(hardq, bx % kSubQ)] = slot;
             } else if (m > 0 && m <= kLdsRows) {
-                const Sol S = hocbf_solve_lds<kLdsRows, CBF_HSORT_REG>(P, H, E, spos, svel, keys, reinterpret_cast<double*>(keys),
+                const Sol S = hocbf_solve_lds<kLdsRows, true>(P, H, E, spos, svel, keys, reinterpret_cast<double*>(keys),
                                                         kBlock, threadIdx.x, m);
                 solved = true;
                 hocbf_finish(P, &S, E, m, W, row_begin, row_end, r, c, T, pos_out, u, status, cnt, guard_rows, e0,
@@ -555,22 +483,20 @@ __global__ void __launch_bounds__(kBlock) k_lattice_filter_hocbf(
     if (ext_part) wave_extents(e0, e1, e2, e3, ext_part, (long)bx * (kBlock / 64) + (threadIdx.x >> 6));
 }
 
-// The queued egos (kLdsRows < m <= kHocbfCap), 64-lane blocks spread over the CUs (up to
-// kWideBlocks, so a queue of up to 64 k egos is one lane each): rescan, all rows in this
-// block's LDS, same solve.  The last block to finish empties the queue.
+// The queued egos (kLdsRows < m <= kHocbfCap), the sub-queues drained in full waves (drain_subq):
+// rescan, all rows in this block's LDS, same solve.
 __global__ void __launch_bounds__(64) k_lattice_filter_hocbf_wide(
     KP P, HP H, CellGrid G, int W, int row_begin, int row_end, int win_row0, const double2* __restrict__ spos,
     const double2* __restrict__ svel, const int32_t* __restrict__ sidx, const int32_t* __restrict__ start, double T,
     double2* __restrict__ pos_out, double2* __restrict__ u, int32_t* __restrict__ status, int32_t* __restrict__ cnt,
     int guard_rows, double* __restrict__ ext_part, unsigned long long* __restrict__ solves,
-    int32_t* __restrict__ hardq) {
+    int32_t* __restrict__ hardq, const int32_t* __restrict__ qslot, long qcap) {
     __shared__ double rows[3 * kHocbfCap * 64];  // the keys live in its first third until read out
     unsigned long long* keys = reinterpret_cast<unsigned long long*>(rows);
-    const int nq = hardq[0];
     double e0 = INFINITY, e1 = -INFINITY, e2 = -INFINITY, e3 = INFINITY;
     int ns = 0;
-    for (int i = blockIdx.x * 64 + threadIdx.x; i < nq; i += gridDim.x * 64) {
-        const int slot = hardq[kHardHeader + i];
+    drain_subq(hardq, kWidePerQ, [&](int q, int i) {
+        const int slot = qslot[(long)q * qcap + i];
         const int w = sidx[slot];
         const int r = win_row0 + w / W, c = w % W;
         const double2 pe = spos[slot], ve = svel[slot];
@@ -582,14 +508,13 @@ __global__ void __launch_bounds__(64) k_lattice_filter_hocbf_wide(
         ++ns;
         hocbf_finish(P, &S, E, m, W, row_begin, row_end, r, c, T, pos_out, u, status, cnt, guard_rows, e0, e1, e2,
                      e3);
-    }
+    });
     if (solves) {
         int t = (int)ns;
         for (int o = 32; o > 0; o >>= 1) t += __shfl_xor(t, o, 64);
         if (threadIdx.x == 0 && t) atomicAdd(&solves[16 * (blockIdx.x & 63)], (unsigned long long)t);
     }
     if (ext_part) wave_extents(e0, e1, e2, e3, ext_part, blockIdx.x);
-    hard_queue_done(hardq);
 }
 
 inline int nblocks(long n) { return (int)((n + kBlock - 1) / kBlock); }
@@ -652,16 +577,17 @@ extern "C" int cbf_lattice_advance_hocbf(const cbf_params* p, const cbf_hocbf* h
     double* ext_part = extents ? (double*)((char*)workspace + CellWs::bytes(n, Wk.ncell)) : nullptr;
     const int nb = nblocks(n);
     hipLaunchKernelGGL(k_lattice_filter_hocbf, dim3(nb), dim3(kBlock), 0, s, make_kp(p), make_hp(hp), G, W, row_begin,
-                       row_end, win_row0, Wk.ncell, Wk.spos, Wk.svel, Wk.sidx, Wk.start, T,
+                       row_end, win_row0, n, Wk.ncell, Wk.spos, Wk.svel, Wk.sidx, Wk.start, T,
                        reinterpret_cast<double2*>(pos_out), reinterpret_cast<double2*>(u), status, nbr_count,
-                       guard_rows, ext_part, reinterpret_cast<unsigned long long*>(solves), Wk.hardq);
-    const long nw = (n + 63) / 64;
-    const int hb = nw < kWideBlocks ? (int)nw : kWideBlocks;
+                       guard_rows, ext_part, reinterpret_cast<unsigned long long*>(solves), Wk.hardq,
+                       reinterpret_cast<int32_t*>(Wk.qrec), Wk.qcap, Wk.sctl);
+    const int hb = lattice_wide_blocks(n);
     hipLaunchKernelGGL(k_lattice_filter_hocbf_wide, dim3(hb), dim3(64), 0, s, make_kp(p), make_hp(hp), G, W,
                        row_begin, row_end, win_row0, Wk.spos, Wk.svel, Wk.sidx, Wk.start, T,
                        reinterpret_cast<double2*>(pos_out), reinterpret_cast<double2*>(u), status, nbr_count,
                        guard_rows, ext_part ? ext_part + 4l * lattice_ext_waves(n) : nullptr,
-                       reinterpret_cast<unsigned long long*>(solves), Wk.hardq);
+                       reinterpret_cast<unsigned long long*>(solves), Wk.hardq,
+                       reinterpret_cast<const int32_t*>(Wk.qrec), Wk.qcap);
     if (extents) launch_extents_finalize((int)lattice_ext_waves(n) + hb, ext_part, extents, s);
     return (int)hipGetLastError();
 }

@@ -58,16 +58,122 @@ __device__ __forceinline__ void ext_accumulate(int r, int row_begin, int row_end
     if (r >= row_begin + guard_rows) e3 = pmin(e3, ny);
 }
 
-// End of a 64-lane queue kernel (every block has read hardq[0]): the last block to finish
-// empties the queue, so an advance run again without a build starts from an empty queue.  No
-// fence: the block is one wave whose load of hardq[0] has returned (the loop used it) before
-// lane 0's atomic, and nothing the reset could race with is written by the queue kernels.
-__device__ __forceinline__ void hard_queue_done(int32_t* hardq) {
-    if (threadIdx.x == 0) {
-        if (atomicAdd(&hardq[1], 1) == (int)gridDim.x - 1) {
-            hardq[0] = 0;
-            hardq[1] = 0;
+// This lane's entry in sub-queue q (length at hardq[32 (1 + q)]); every active lane of the wave
+// that calls it appends one entry, with one atomic per wave.
+__device__ __forceinline__ int subq_append(int32_t* hardq, int q) {
+    const unsigned long long m = __ballot(1);
+    const int lane = threadIdx.x & 63;
+    const int leader = __ffsll((long long)m) - 1;
+    int base = 0;
+    if (lane == leader) base = atomicAdd(&hardq[32 * (1 + q)], __popcll(m));
+    base = __shfl(base, leader, 64);
+    return base + __popcll(m & ((1ull << lane) - 1ull));
+}
+
+// The queue kernels: 64-lane blocks, block g serving sub-queue g % kSubQ as its (g / kSubQ)-th of
+// per_q blocks.  Of a sub-queue of length nq, nwork = min(per_q, ceil(nq / 64)) blocks work, lane
+// i of the k-th taking entries k 64 + i, then + nwork 64, ...; visit(entry) per entry.  The working
+// blocks of a sub-queue then count themselves done; the last empties the sub-queue (length and
+// done counter), so the next advance starts from empty queues with no extra launch.  A chain of
+// <= per_q returning atomics per sub-queue line, the 64 lines in parallel.  No fence: a block is
+// one wave whose load of the length has returned before lane 0's atomic, and nothing the reset
+// races with is written by the queue kernels.  A block k >= nwork that reads the length after the
+// reset sees 0 and is still idle (any smaller length gives it no work either).
+template <class Visit>
+__device__ __forceinline__ void drain_subq(int32_t* __restrict__ hardq, int per_q, Visit&& visit) {
+    const int q = blockIdx.x % kSubQ, k = blockIdx.x / kSubQ;
+    const int nq = hardq[32 * (1 + q)];
+    const int need = (nq + 63) / 64;
+    const int nwork = need < per_q ? need : per_q;
+    if (k >= nwork) return;
+    for (int i = k * 64 + threadIdx.x; i < nq; i += nwork * 64) visit(q, i);
+    if (threadIdx.x == 0 && atomicAdd(&hardq[32 * (1 + kSubQ + q)], 1) == nwork - 1) {
+        hardq[32 * (1 + q)] = 0;
+        hardq[32 * (1 + kSubQ + q)] = 0;
+    }
+}
+
+// Rollout statistics of the lattice step (`stats`, device uint64[1024] = 64 slots of 16 words,
+// one 128-B line each; a wave adds into slot (its index & 63), the host sums or maxes over the
+// slots).  Counted over the egos of the counted rows.  The two violations are the bits of
+// non-negative doubles (monotone as uint64, so atomicMax is an exact maximum); the smallest
+// neighbour distance^2 is kept as kDistKeyTop - bits(s) under atomicMax, so a zero-filled array
+// reads as "no neighbour pair".  Word layout: cbf_amd.h (CBF_STAT_*).
+constexpr unsigned long long kDistKeyTop = 0x7FF0000000000000ull;
+
+__device__ __forceinline__ unsigned long long dbits(double v) { return (unsigned long long)__double_as_longlong(v); }
+
+// One wave's contribution.  solved: an agent-QP ran for this lane's ego (>= 1 neighbour);
+// seidel: its QP went to the full solve (queued); fin: its status code is final here (code,
+// viol = violation of the solved rows, vorig = violation of the original rows); d2: smallest
+// neighbour distance^2 of the ego (+inf if none).  Every lane of the wave must call it.
+__device__ __forceinline__ void wave_stats(unsigned long long* __restrict__ st, long wave, bool solved, bool seidel,
+                                           bool fin, int code, double viol, double vorig, double d2) {
+    const bool opt = fin && code == CBF_STATUS_OPTIMAL, rel = fin && code == CBF_STATUS_RELAXED;
+    const bool inf = fin && (code == CBF_STATUS_BOX_INFEASIBLE || code == CBF_STATUS_RELAX_CAP);
+    const unsigned long long m_sol = __ballot(solved), m_sei = __ballot(seidel), m_opt = __ballot(opt),
+                             m_rel = __ballot(rel), m_inf = __ballot(inf);
+    double vo = 0.0, vr = 0.0, dm = INFINITY;
+    if (__ballot(opt && viol > 0.0)) vo = wave_max(opt ? viol : 0.0);
+    if (__ballot(rel && vorig > 0.0)) vr = wave_max(rel ? vorig : 0.0);
+    if (__ballot(d2 < INFINITY)) dm = wave_min(d2);
+    if ((threadIdx.x & 63) == 0) {
+        unsigned long long* s = st + 16 * (wave & 63);
+        if (m_sol) atomicAdd(&s[CBF_STAT_SOLVES], (unsigned long long)__popcll(m_sol));
+        if (m_opt) atomicAdd(&s[CBF_STAT_OPTIMAL], (unsigned long long)__popcll(m_opt));
+        if (m_rel) atomicAdd(&s[CBF_STAT_RELAXED], (unsigned long long)__popcll(m_rel));
+        if (m_inf) atomicAdd(&s[CBF_STAT_INFEASIBLE], (unsigned long long)__popcll(m_inf));
+        if (m_sei) atomicAdd(&s[CBF_STAT_SEIDEL], (unsigned long long)__popcll(m_sei));
+        if (vo > 0.0) atomicMax(&s[CBF_STAT_VIOL_OPTIMAL], dbits(vo));
+        if (vr > 0.0) atomicMax(&s[CBF_STAT_VIOL_ORIGINAL], dbits(vr));
+        if (dm < INFINITY) atomicMax(&s[CBF_STAT_MIN_DIST2], kDistKeyTop - dbits(dm));
+    }
+}
+
+// The lattice filters' path when the build is flagged unusable: window agent slot (identity order,
+// the cell-sorted copies are not read) reports CBF_STATUS_WORKSPACE_ERROR for an owned agent, with
+// u = 0 and no neighbours; positions are left as they are; the step counts as one error.
+__device__ __forceinline__ void lattice_error_tail(int W, int row_begin, int row_end, int win_row0, long nwin,
+                                                   long slot, double2* __restrict__ u, int32_t* __restrict__ status,
+                                                   int32_t* __restrict__ cnt, unsigned long long* __restrict__ stats,
+                                                   double* __restrict__ ext_part, long wave) {
+    if (slot < nwin) {
+        const int r = win_row0 + (int)(slot / W), c = (int)(slot % W);
+        if (r >= row_begin && r < row_end) {
+            const long k = (long)(r - row_begin) * W + c;
+            u[k] = make_double2(0.0, 0.0);
+            status[k] = CBF_STATUS_WORKSPACE_ERROR;
+            if (cnt) cnt[k] = 0;
         }
+    }
+    if (stats && slot == 0) atomicAdd(&stats[CBF_STAT_ERRORS], 1ull);
+    if (ext_part && (threadIdx.x & 63) == 0) {
+        double* o = ext_part + 4 * wave;
+        o[0] = INFINITY;
+        o[1] = -INFINITY;
+        o[2] = -INFINITY;
+        o[3] = INFINITY;
+    }
+}
+
+// Per-lane status counts and violation maxima of a queue kernel, summed over the wave (every lane
+// of the wave must call it, after its loop).
+__device__ __forceinline__ void wave_stats_counts(unsigned long long* __restrict__ st, long wave, int n_opt, int n_rel,
+                                                  int n_inf, double vo, double vr) {
+    for (int o = 32; o > 0; o >>= 1) {
+        n_opt += __shfl_xor(n_opt, o, 64);
+        n_rel += __shfl_xor(n_rel, o, 64);
+        n_inf += __shfl_xor(n_inf, o, 64);
+    }
+    vo = wave_max(vo);
+    vr = wave_max(vr);
+    if ((threadIdx.x & 63) == 0) {
+        unsigned long long* s = st + 16 * (wave & 63);
+        if (n_opt) atomicAdd(&s[CBF_STAT_OPTIMAL], (unsigned long long)n_opt);
+        if (n_rel) atomicAdd(&s[CBF_STAT_RELAXED], (unsigned long long)n_rel);
+        if (n_inf) atomicAdd(&s[CBF_STAT_INFEASIBLE], (unsigned long long)n_inf);
+        if (vo > 0.0) atomicMax(&s[CBF_STAT_VIOL_OPTIMAL], dbits(vo));
+        if (vr > 0.0) atomicMax(&s[CBF_STAT_VIOL_ORIGINAL], dbits(vr));
     }
 }
 
@@ -76,16 +182,20 @@ void launch_extents_finalize(int nparts, const double* part, double* out, hipStr
 
 // partial extents: one record per wave of the filter grid, then one per hard-QP block
 inline long lattice_ext_waves(long win_n) { return (win_n + kBlock - 1) / kBlock * (kBlock / 64); }
-// grid of the HOCBF wide kernel (64-lane blocks): 256 x 64 lanes cover the ~10 k queued egos of
-// cfg4 one per lane; every block ends with one atomic on the done counter, so a larger grid only
-// lengthens that serialised chain (1024 blocks: advance 231 vs 221 us, tools/ablate.py set wide)
-#ifndef CBF_WIDE_BLOCKS
-#define CBF_WIDE_BLOCKS 256
+// the HOCBF wide kernel: kWidePerQ 64-lane blocks per sub-queue (~10 k queued egos at cfg4,
+// ~160 per sub-queue)
+constexpr int kWidePerQ = 4;
+inline int lattice_wide_blocks(long) { return kSubQ * kWidePerQ; }
+// the hard-QP kernel of the lattice step: kHardPerQ 64-lane blocks per sub-queue (2048 lanes: the
+// ~4.6 k entries per sub-queue at cfg4f in ~2 passes, the ~50 at cfg4 in one block)
+#ifndef CBF_HARD_PER_Q
+#define CBF_HARD_PER_Q 32
 #endif
-constexpr int kWideBlocks = CBF_WIDE_BLOCKS;
-constexpr int kQueueBlocksMax = kHardBlocks > kWideBlocks ? kHardBlocks : kWideBlocks;
+constexpr int kHardPerQ = CBF_HARD_PER_Q;
+inline int lattice_hard_blocks(long) { return kSubQ * kHardPerQ; }
 inline size_t lattice_ext_bytes(long win_n) {
-    return align256(32 * (size_t)(lattice_ext_waves(win_n) + kQueueBlocksMax));
+    const long hb = lattice_hard_blocks(win_n), wb = lattice_wide_blocks(win_n);
+    return align256(32 * (size_t)(lattice_ext_waves(win_n) + (hb > wb ? hb : wb)));
 }
 
 inline int check_lattice(const cbf_params* p, const cbf_grid* grid, int32_t W, int32_t H, int32_t row_begin,

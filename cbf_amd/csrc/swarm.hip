@@ -13,13 +13,7 @@ namespace {
 inline int nblk(long n) { return (int)((n + kBlock - 1) / kBlock); }
 
 constexpr int kExtSlotWords = 16;  // one 128-B line per extents slot (6 keys used)
-#ifndef CBF_EXT_SLOTS
-#define CBF_EXT_SLOTS 64
-#endif
-#ifndef CBF_EXT_WAVE
-#define CBF_EXT_WAVE 0
-#endif
-constexpr int kExtSlots = CBF_EXT_SLOTS;  // slots per sub-step set (tools/ablate.py times the choices)
+constexpr int kExtSlots = 64;      // extents slots per sub-step set
 constexpr int kExtVals = 6;        // {ego min, ego max, owned max below guard, owned min above guard, owned min, max}
 __host__ __device__ constexpr bool ext_is_min(int q) { return q == 0 || q == 3 || q == 4; }
 
@@ -98,34 +92,25 @@ __global__ void __launch_bounds__(kBlock) k_euler(int n, double2* __restrict__ p
     pos[i] = make_double2(p.x + T * v.x, p.y + T * v.y);
 }
 
-// CBF_NOMINAL_IN_SCATTER: the Laplacian nominal control is computed by the scatter (K3) instead of
-// K1, so it never makes an HBM round trip (tools/ablate.py, set nominal).
-#ifndef CBF_NOMINAL_IN_SCATTER
-#define CBF_NOMINAL_IN_SCATTER 1
-#endif
-
 // Lattice step K1, temporally coherent form: lanes walk the window agents in the previous step's
 // cell order (identity on the first call), so consecutive lanes mostly share a cell; each run of
 // equal cells in a wave takes its slots with ONE atomic (run length), and the later scatter
 // writes nearly sequential slots.  Per-lane result bcs[t] = {cell, slot, agent} (12 B).
 __global__ void __launch_bounds__(kBlock) k_lattice_nominal_bin_ordered(
     CellGrid G, int W, int H, int row_begin, int row_end, int win_row0, int win_rows, const double2* __restrict__ pos,
-    double gain, double2* __restrict__ wvel, double2* __restrict__ vel_out, int32_t* __restrict__ count,
-    const int32_t* __restrict__ order, const int32_t* __restrict__ start, long ncell, int3* __restrict__ bcs,
-    int32_t* __restrict__ hardq, unsigned long long* __restrict__ ext_keys, ExtSpec X, int32_t* __restrict__ sctl) {
+    int32_t* __restrict__ count, const int32_t* __restrict__ order, const int32_t* __restrict__ start, long ncell,
+    int3* __restrict__ bcs, int32_t* __restrict__ hardq, unsigned long long* __restrict__ ext_keys, ExtSpec X,
+    int32_t* __restrict__ sctl) {
     const long t = (long)xcd_block() * kBlock + threadIdx.x;
-    if (CBF_SCAN_EPOCH_BIN && t == 0) scan_epoch_advance(sctl);
     const long nwin = (long)win_rows * W;
-    // hardq[2..4]: the previous build left a cell order for this window size and grid (else
-    // identity); the order only permutes the work, so a stale one costs speed, never results
+    if (t == 0) build_begin(sctl, nwin, ncell);
+    // hardq[2..7]: the previous build left a cell order for exactly this window and grid (else
+    // identity).  The order only permutes the work; it must list every window agent once, which
+    // holds when window size, width, first row, lattice height and cell count all match.
     const bool ordered = hardq[2] == 1 && hardq[3] == (int)nwin && hardq[4] == (int)ncell && hardq[5] == win_row0 &&
-                         hardq[6] == H;
+                         hardq[6] == H && hardq[7] == W;
     int n_order = ordered ? start[ncell] : 0;
     n_order = n_order < 0 ? 0 : (n_order > nwin ? (int)nwin : n_order);
-    if (t == 0) {  // hard-QP queue of this step's advance phase starts empty
-        hardq[0] = 0;
-        hardq[1] = 0;  // blocks of the queue kernel done (the last one empties the queue again)
-    }
     int cell = -1;
     long w = -1;
     double2 p = make_double2(0.0, 0.0);
@@ -184,17 +169,6 @@ __global__ void __launch_bounds__(kBlock) k_lattice_nominal_bin_ordered(
 #pragma unroll
             for (int q = 0; q < 6; ++q) e[q] = ext_is_min(q) ? wave_min(e[q]) : wave_max(e[q]);
         }
-#if CBF_EXT_WAVE
-        // per wave: lane 0 of every wave with an agent in range does the atomics (no block barrier)
-        if (__ballot(any) && lane == 0) {
-            unsigned long long* k = ext_keys + kExtSlotWords * ((t >> 6) & (kExtSlots - 1));
-#pragma unroll
-            for (int q = 0; q < 6; ++q) {
-                if (ext_is_min(q)) atomicMin(&k[q], dkey(e[q]));
-                else atomicMax(&k[q], dkey(e[q]));
-            }
-        }
-#else
         const int wid = threadIdx.x >> 6;
         if (lane == 0)
 #pragma unroll
@@ -211,7 +185,6 @@ __global__ void __launch_bounds__(kBlock) k_lattice_nominal_bin_ordered(
                 else atomicMax(&k[q], dkey(e[q]));
             }
         }
-#endif
     }
     // runs of equal cells inside the wave: one atomic per run
     int cprev = __shfl_up(cell, 1, 64);
@@ -229,103 +202,78 @@ __global__ void __launch_bounds__(kBlock) k_lattice_nominal_bin_ordered(
         bcs[t] = make_int3(-1, 0, (int)w);
         return;
     }
-#if !CBF_NOMINAL_IN_SCATTER
-    const int r = win_row0 + (int)(w / W), c = (int)(w % W);
-    const double2 a = lattice_sum(pos, w, r, c, W, H);
-    const double2 u0 = make_double2(a.x * gain, a.y * gain);
-    wvel[w] = u0;
-    if (vel_out != wvel && r >= row_begin && r < row_end) vel_out[(long)(r - row_begin) * W + c] = u0;
-#endif
     bcs[t] = make_int3(cell, base + lane - my_leader, (int)w);
 }
 
+// Lattice step K3: counting-sort scatter of the binned window agents into the cell-sorted copies,
+// with each agent's lattice-Laplacian nominal control (cross_and_rescue.py:121-125 shape) computed
+// here: the agent's position is loaded anyway and its 4 lattice neighbours are mostly L2 hits
+// (cell order ~ lattice order), so the control never makes an HBM round trip.
 __global__ void __launch_bounds__(kBlock) k_lattice_scatter_ordered(long nwin, const int3* __restrict__ bcs,
                                                                     const int32_t* __restrict__ start,
                                                                     const double2* __restrict__ pos,
-                                                                    const double2* __restrict__ wvel,
                                                                     double2* __restrict__ spos,
                                                                     double2* __restrict__ svel,
                                                                     int32_t* __restrict__ sidx,
-                                                                    float2* __restrict__ spos32,
-                                                                    int32_t* __restrict__ order_state, long n,
-                                                                    long ncell, int win_row0, int H, int W,
-                                                                    int row_begin, int row_end, double gain,
-                                                                    double2* __restrict__ vel_out) {
+                                                                    int32_t* __restrict__ order_state, long ncell,
+                                                                    int win_row0, int H, int W, int row_begin,
+                                                                    int row_end, double gain,
+                                                                    double2* __restrict__ vel_out,
+                                                                    const int32_t* __restrict__ sctl) {
     const long t = (long)xcd_block() * kBlock + threadIdx.x;
-    if (t == 0) {  // the cell order now exists for this window and grid: the next build walks it
+    if (t == 0 && sctl[2] == 0) {  // the cell order now exists for this window and grid: the next build walks it
         order_state[0] = 1;
-        order_state[1] = (int)n;
+        order_state[1] = (int)nwin;
         order_state[2] = (int)ncell;
         order_state[3] = win_row0;
         order_state[4] = H;
+        order_state[5] = W;
     }
-    if (t >= nwin) return;
+    if (t >= nwin || sctl[2] != 0) return;  // an unusable build (build_begin / scan timeout): no scatter
     const int3 b = bcs[t];
     if (b.x < 0) return;
     const int d = start[b.x] + b.y;
+    if (d < 0 || d >= nwin) return;
     const double2 p = pos[b.z];
     spos[d] = p;
-#if CBF_NOMINAL_IN_SCATTER
-    // K1's nominal control computed here: the agent's position is loaded anyway and its 4
-    // lattice neighbours are mostly in L2 (cell order ~ lattice order), so the u0 round trip
-    // through HBM (written by K1, gathered back here) disappears
     const int r = win_row0 + b.z / W, c = b.z % W;
     const double2 a = lattice_sum(pos, b.z, r, c, W, H);
     const double2 u0 = make_double2(a.x * gain, a.y * gain);
     svel[d] = u0;
     if (r >= row_begin && r < row_end) vel_out[(long)(r - row_begin) * W + c] = u0;
-    (void)wvel;
-#else
-    svel[d] = wvel[b.z];
-    (void)W, (void)row_begin, (void)row_end, (void)gain, (void)vel_out;
-#endif
     sidx[d] = b.z;
-#if CBF_SCAN32
-    spos32[d] = make_float2((float)p.x, (float)p.y);
-#endif
 }
 
+// Per-ego outcome of the lattice filter for the statistics.
+struct EgoOut {
+    int res;          // 0 not an owned ego, 1 done (outputs written), 2 queued for the full solve
+    int row;          // lattice row
+    int nbrs;         // neighbours
+    int code;         // final status code (res == 1)
+    double viol, vorig, d2, ny;
+};
 
 // Tail of the lattice filter for one owned ego whose QP rows are accumulated in E: solve at the
-// origin or queue to the hard kernel, clip, Euler, outputs.  Returns 1 (done, *ny = new y) or 2.
-// CBF_HARD_INLINE (off): a QP the origin does not solve is solved in place by solve_ego_lds (rolled
-// loops, right-hand sides in the lane's LDS column `bl`, ~30 VGPRs) instead of being queued for
-// k_lattice_filter_hard, which then is not launched (its launch + queue round trip was ~10 us a
-// step for ~0.3 % of the egos).
-#ifndef CBF_NT_STORES
-#define CBF_NT_STORES 0
-#endif
-#ifndef CBF_HARD_INLINE
-#define CBF_HARD_INLINE 0  // measured slower: advance 55.7 vs 51.9 us (tools/ablate.py, set hardinline)
-#endif
+// origin (solve_easy) or queue to the hard kernel (sub-queue q: header hardq, records qr), clip,
+// Euler, outputs.
 template <bool FZ>
-__device__ __forceinline__ int ego_finish(const KP& P, Ego& E, int W, int row_begin, int r, int c, double T,
-                                          double2* __restrict__ pos_out, double2* __restrict__ u,
-                                          int32_t* __restrict__ status, int32_t* __restrict__ cnt,
-                                          int32_t* __restrict__ hardq, double* ny, int* bl = nullptr) {
-    const double2 pe = make_double2(E.r0, E.r1);
+__device__ __forceinline__ void ego_finish(const KP& P, Ego& E, int W, int row_begin, int r, int c, double T,
+                                           double2* __restrict__ pos_out, double2* __restrict__ u,
+                                           int32_t* __restrict__ status, int32_t* __restrict__ cnt,
+                                           int32_t* __restrict__ hardq, int q, HardRec* __restrict__ qr,
+                                           EgoOut& O) {
     const long k = (long)(r - row_begin) * W + c;
     double ux, uy;
     int32_t st;
+    O.code = CBF_STATUS_IDLE;
     if (E.count == 0) {
         ux = E.u0x;
         uy = E.u0y;
         st = CBF_STATUS_IDLE;
     } else {
         Sol S;
-#if CBF_ABLATE >= 1
-        S.x0 = S.x1 = 0.0;
-        S.status = CBF_STATUS_OPTIMAL;
-        S.iters = 0;
-        S.viol = E.bq0 + E.bq1 + E.bq2 + E.bq3;
-        asm volatile("" ::"v"(S.viol));
-#else
-        if (solve_easy(P, E, S)) {
-        } else if (CBF_HARD_INLINE && bl) {
-            S = solve_ego_lds(P, E, LaneCol{bl});
-        } else {
-            HardRec* q = reinterpret_cast<HardRec*>(hardq + kHardHeader);
-            HardRec& h = q[atomicAdd(&hardq[0], 1)];
+        if (!solve_easy(P, E, S)) {
+            HardRec& h = qr[subq_append(hardq, q)];
             h.r0 = E.r0;
             h.r1 = E.r1;
             h.r2 = E.r2;
@@ -340,50 +288,41 @@ __device__ __forceinline__ int ego_finish(const KP& P, Ego& E, int W, int row_be
             h.count = E.count;
             h.k = (int)k;
             h.row = r;
-            return 2;
+            O.res = 2;
+            return;
         }
-#endif
         clip_u(P, S, E, ux, uy);
         st = pack_status(S);
+        O.code = S.status;
+        O.viol = S.viol;
+        O.vorig = S.viol_orig;
     }
-    const double2 pn = make_double2(pe.x + T * ux, pe.y + T * uy);
-#if CBF_NT_STORES
-    // outputs are not read again by this kernel: non-temporal stores keep them from displacing
-    // the cell-sorted candidate lines in L2
-    __builtin_nontemporal_store(pn.x, &pos_out[k].x);
-    __builtin_nontemporal_store(pn.y, &pos_out[k].y);
-    __builtin_nontemporal_store(ux, &u[k].x);
-    __builtin_nontemporal_store(uy, &u[k].y);
-    __builtin_nontemporal_store(st, &status[k]);
-    if (cnt) __builtin_nontemporal_store(E.count, &cnt[k]);
-#else
+    const double2 pn = make_double2(E.r0 + T * ux, E.r1 + T * uy);
     pos_out[k] = pn;
     u[k] = make_double2(ux, uy);
     status[k] = st;
     if (cnt) cnt[k] = E.count;
-#endif
-    *ny = pn.y;
-    return 1;
+    O.ny = pn.y;
+    O.res = 1;
 }
 
-// Lattice step K4: filter + clip + Euler for one owned agent at cell-sorted slot `slot`.
-// QPs that the origin does not solve (after the strip pre-relaxation) are not solved here but
-// appended, with their assembled state, to the hard queue: one such lane would otherwise make
-// its whole wave run the Seidel path (and hold the registers for it); K5 solves them.
-// Returns 0 (not an owned agent), 1 (done: outputs written, *ny = new y), 2 (queued).
+// Lattice step K4 for one cell-sorted slot: 3x3-cell cull (the three cell rows scanned as one
+// sequence, hits compacted into the lane's LDS column), row assembly for the hits only (so
+// divergent lanes do not pay assembly for every candidate iteration of the wave), then the tail.
 template <bool FZ>
-__device__ __forceinline__ int lattice_ego(const KP& P, const CellGrid& G, int W, int row_begin, int row_end,
-                                           int win_row0, int slot, const double2* __restrict__ spos,
-                                           const double2* __restrict__ svel, const int32_t* __restrict__ sidx,
-                                           const int32_t* __restrict__ start, double T, double2* __restrict__ pos_out,
-                                           double2* __restrict__ u, int32_t* __restrict__ status,
-                                           int32_t* __restrict__ cnt, int32_t* __restrict__ hardq, int* hit_lds,
-                                           const float2* __restrict__ spos32, double* ny, int* row, int* nbrs) {
+__device__ __forceinline__ void lattice_ego(const KP& P, const CellGrid& G, int W, int row_begin, int row_end,
+                                            int win_row0, int slot, const double2* __restrict__ spos,
+                                            const double2* __restrict__ svel, const int32_t* __restrict__ sidx,
+                                            const int32_t* __restrict__ start, double T,
+                                            double2* __restrict__ pos_out, double2* __restrict__ u,
+                                            int32_t* __restrict__ status, int32_t* __restrict__ cnt,
+                                            int32_t* __restrict__ hardq, int q, HardRec* __restrict__ qr,
+                                            int* hit_lds, EgoOut& O) {
     const int w = sidx[slot];
     const int r = win_row0 + w / W;
     const int c = w % W;
-    *row = r;
-    if (!(r >= row_begin && r < row_end)) return 0;
+    O.row = r;
+    if (!(r >= row_begin && r < row_end)) return;
     const double2 pe = spos[slot], ve = svel[slot];
     Ego E;
     ego_init(P, E, pe.x, pe.y, ve.x, ve.y, ve.x, ve.y);
@@ -391,9 +330,6 @@ __device__ __forceinline__ int lattice_ego(const KP& P, const CellGrid& G, int W
     const int cy = cell_coord(pe.y, G.y0, G.inv_h, G.ny);
     const int xa = cx > 0 ? cx - 1 : 0;
     const int xb = cx < G.nx - 1 ? cx + 1 : G.nx - 1;
-    // pass 1: cheap cull test over the 3x3 cells, hits compacted into a per-lane LDS list;
-    // pass 2: row assembly only for hits (keeps divergent lanes from paying assembly for
-    // every candidate iteration of the wave)
     int rt0[3], rt1[3];
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
@@ -402,280 +338,91 @@ __device__ __forceinline__ int lattice_ego(const KP& P, const CellGrid& G, int W
         rt0[k] = in ? start[yy * G.nx + xa] : 0;
         rt1[k] = in ? start[yy * G.nx + xb + 1] : 0;
     }
-#if CBF_SCAN_INLINE && CBF_SCAN_U > 0 && CBF_ABLATE == 0
-    scan_rows_inline<FZ>(rt0, rt1, P, E, spos, svel);
-    (void)hit_lds;
-    (void)spos32;
-#elif CBF_HIT_MASK && CBF_SCAN_U > 0 && CBF_ABLATE == 0
-    {
-        HitMask Hm;
-        if (scan_rows_joint_mask(rt0, rt1, P, E, Hm, spos)) {
-            flush_mask<FZ>(Hm, rt0, P, E, spos, svel);
-        } else {
-#pragma unroll
-            for (int k = 0; k < 3; ++k) scan_range_direct<FZ>(rt0[k], rt1[k], P, E, spos, svel);
-        }
-        (void)hit_lds;
-        (void)spos32;
-    }
-#elif CBF_ABLATE < 3
     HitList Hl;
-#if CBF_SCAN32
-    // screen bound from the ego's own magnitude: a true neighbour lies within r of it
-    const float t32 = screen_threshold(P.cull_t, pmax(fabs(E.r0), fabs(E.r1)) + sqrt(P.cull_t));
-    constexpr bool kExact = true;
-    if (t32 > 0.0f)
-        scan_rows_joint32(rt0, rt1, t32, (float)E.r0, (float)E.r1, Hl, hit_lds, spos32);
-    else
-        Hl.n = kHitCap + 1;  // screen off (non-finite or huge coordinates): the exact direct scan
-#elif CBF_SCAN_U > 0
-    constexpr bool kExact = false;
-    scan_rows_joint(rt0, rt1, P, E, Hl, hit_lds, spos);
-#else
-    constexpr bool kExact = false;
-#pragma unroll
-    for (int k = 0; k < 3; ++k) scan_range(rt0[k], rt1[k], P, E, Hl, hit_lds, spos);
-#endif
-#if CBF_ABLATE < 2
+    double d2 = INFINITY;
+    scan_rows_joint(rt0, rt1, P, E, Hl, hit_lds, spos, d2);
     if (!Hl.overflowed()) {
-#if CBF_BQ_LDS
-        double* bq = reinterpret_cast<double*>(hit_lds + (kHitCap + 1) * kBlock);
+        double* bq = reinterpret_cast<double*>(hit_lds + kHitCap * kBlock);
 #pragma unroll
         for (int q = 0; q < 4; ++q) bq[q * kBlock + threadIdx.x] = INFINITY;
-        Hl.template flush_bq<FZ, kExact>(hit_lds, bq, P, E, spos, svel);
+        Hl.template flush_bq<FZ>(hit_lds, bq, P, E, spos, svel);
         E.bq0 = bq[threadIdx.x];
         E.bq1 = bq[kBlock + threadIdx.x];
         E.bq2 = bq[2 * kBlock + threadIdx.x];
         E.bq3 = bq[3 * kBlock + threadIdx.x];
-#else
-        Hl.template flush<FZ, kExact>(hit_lds, P, E, spos, svel);
-#endif
     } else {
 #pragma unroll
         for (int k = 0; k < 3; ++k) scan_range_direct<FZ>(rt0[k], rt1[k], P, E, spos, svel);
     }
-#else
-    E.count = Hl.n;
-    asm volatile("" ::"v"(E.count));
-#endif
-#endif
-    *nbrs = E.count;
-    // the lane's LDS column (its hit slots) is free again after the flush: the 8 right-hand sides
-    // of an in-place solve (other lanes' columns may still be in use by their waves)
-    int* bl = CBF_HIT_MASK ? nullptr : hit_lds + threadIdx.x;
-    return ego_finish<FZ>(P, E, W, row_begin, r, c, T, pos_out, u, status, cnt, hardq, ny, bl);
+    O.nbrs = E.count;
+    O.d2 = d2;
+    ego_finish<FZ>(P, E, W, row_begin, r, c, T, pos_out, u, status, cnt, hardq, q, qr, O);
 }
 
-// K4: one lane per cell-sorted slot; easy QPs solved in place, hard ones queued.
-#ifndef CBF_FILTER_WPE
-#define CBF_FILTER_WPE 0
-#endif
-#if CBF_FILTER_WPE > 0
-#define CBF_FILTER_BOUNDS __launch_bounds__(kBlock, CBF_FILTER_WPE)
-#else
-#define CBF_FILTER_BOUNDS __launch_bounds__(kBlock)
-#endif
+// K4: one lane per cell-sorted slot; QPs the origin solves (after the strip pre-relaxation) are
+// finished in place, the others are appended with their assembled state to the hard queue: one
+// such lane would otherwise make its whole wave run the Seidel path (and hold the registers for
+// it, 167 VGPRs against 68); K5 solves them.
 template <bool FZ>
-__global__ void CBF_FILTER_BOUNDS k_lattice_filter(KP P, CellGrid G, int W, int row_begin, int row_end,
-                                                           int win_row0, long ncell, const double2* __restrict__ spos,
+__global__ void __launch_bounds__(kBlock) k_lattice_filter(KP P, CellGrid G, int W, int row_begin, int row_end,
+                                                           int win_row0, long nwin, long ncell,
+                                                           const double2* __restrict__ spos,
                                                            const double2* __restrict__ svel,
                                                            const int32_t* __restrict__ sidx,
-                                                           const int32_t* __restrict__ start, double T,
+                                                           const int32_t* __restrict__ start,
+                                                           const int32_t* __restrict__ sctl, double T,
                                                            double2* __restrict__ pos_out, double2* __restrict__ u,
                                                            int32_t* __restrict__ status, int32_t* __restrict__ cnt,
                                                            int guard_rows, double* __restrict__ ext_part,
-                                                           unsigned long long* __restrict__ solves,
-                                                           int32_t* __restrict__ hardq,
-                                                           const float2* __restrict__ spos32, int cnt_begin,
-                                                           int cnt_end) {
-    // hit rows + a dummy row (branch-free push) + 4 x fp64 per-quadrant minima (CBF_BQ_LDS)
-    // (>= 16 ints per lane: also the lane's 8 fp64 right-hand sides of an in-place hard solve)
-    static_assert(CBF_HIT_MASK || (kHitCap + 1) + (CBF_BQ_LDS ? 8 : 0) >= 16, "hit LDS too small for solve_ego_lds");
-    __shared__ int hit_lds[CBF_HIT_MASK ? 1 : (kHitCap + 1) * kBlock + (CBF_BQ_LDS ? 8 * kBlock : 0)];
+                                                           unsigned long long* __restrict__ stats,
+                                                           int32_t* __restrict__ hardq, HardRec* __restrict__ qrec,
+                                                           long qcap, int cnt_begin, int cnt_end) {
+    // hit rows + 4 x fp64 per-quadrant minima, one column per lane
+    __shared__ int hit_lds[kHitCap * kBlock + 8 * kBlock];
     const int bx = xcd_block();
     const int slot = bx * kBlock + threadIdx.x;
+    if (sctl[2] != 0) {  // unusable cell list (build_begin / scan timeout): touch none of it
+        lattice_error_tail(W, row_begin, row_end, win_row0, nwin, slot, u, status, cnt, stats, ext_part,
+                           (long)bx * (kBlock / 64) + (threadIdx.x >> 6));
+        return;
+    }
     const int total = start[ncell];
     double e0 = INFINITY, e1 = -INFINITY, e2 = -INFINITY, e3 = INFINITY;
-    bool solved = false;
+    EgoOut O;
+    O.res = 0;
+    O.row = -1;
+    O.nbrs = 0;
+    O.code = CBF_STATUS_IDLE;
+    O.viol = O.vorig = 0.0;
+    O.d2 = INFINITY;
     if (slot < total) {
-        double ny;
-        int r, nb = 0;
-        const int res = lattice_ego<FZ>(P, G, W, row_begin, row_end, win_row0, slot, spos, svel, sidx, start,
-                                               T, pos_out, u, status, cnt, hardq, hit_lds, spos32, &ny, &r, &nb);
-        solved = res != 0 && nb > 0 && r >= cnt_begin && r < cnt_end;
-        if (res == 1) ext_accumulate(r, row_begin, row_end, guard_rows, ny, e0, e1, e2, e3);
+        lattice_ego<FZ>(P, G, W, row_begin, row_end, win_row0, slot, spos, svel, sidx, start, T, pos_out, u,
+                        status, cnt, hardq, bx % kSubQ, qrec + (long)(bx % kSubQ) * qcap, hit_lds, O);
+        if (O.res == 1) ext_accumulate(O.row, row_begin, row_end, guard_rows, O.ny, e0, e1, e2, e3);
     }
-    if (solves) {  // wave-aggregated, spread over 64 counters on separate 128-B lines
-        const unsigned long long m = __ballot(solved);
-        if ((threadIdx.x & 63) == 0 && m)
-            atomicAdd(&solves[16 * ((bx * (kBlock / 64) + (threadIdx.x >> 6)) & 63)],
-                      (unsigned long long)__popcll(m));
+    if (stats) {
+        const bool counted = O.res != 0 && O.row >= cnt_begin && O.row < cnt_end;
+        wave_stats(stats, (long)bx * (kBlock / 64) + (threadIdx.x >> 6), counted && O.nbrs > 0,
+                   counted && O.res == 2, counted && O.res == 1, O.code, O.viol, O.vorig, counted ? O.d2 : INFINITY);
     }
     if (ext_part) wave_extents(e0, e1, e2, e3, ext_part, (long)bx * (kBlock / 64) + (threadIdx.x >> 6));
 }
 
-// K4, LDS-staged form (CBF_LDS_STAGE): the egos of a wave are consecutive cell-sorted slots, so
-// the union of their three cell-row candidate ranges is three short contiguous slot segments
-// (~210 agents at the cfg4 density).  The wave loads that union once, coalesced, into its own
-// LDS region (positions and nominal controls), then every lane culls and assembles its own ~17
-// candidates from LDS: no per-lane gathers, no hit list, no flush.  A wave whose union exceeds
-// kStageCap (a sparse or wrapped region) takes the direct path from global memory.  Same rows,
-// same per-quadrant minima as k_lattice_filter (the minimum is order-independent).
-#ifndef CBF_LDS_STAGE
-#define CBF_LDS_STAGE 0
-#endif
-constexpr int kStageCap = 256;
-
-template <bool FZ>
-__global__ void __launch_bounds__(kBlock) k_lattice_filter_lds(KP P, CellGrid G, int W, int row_begin, int row_end,
-                                                               int win_row0, long ncell,
-                                                               const double2* __restrict__ spos,
-                                                               const double2* __restrict__ svel,
-                                                               const int32_t* __restrict__ sidx,
-                                                               const int32_t* __restrict__ start, double T,
-                                                               double2* __restrict__ pos_out, double2* __restrict__ u,
-                                                               int32_t* __restrict__ status, int32_t* __restrict__ cnt,
-                                                               unsigned long long* __restrict__ solves,
-                                                               int32_t* __restrict__ hardq, int cnt_begin,
-                                                               int cnt_end) {
-    __shared__ double2 st_pos[kBlock / 64][kStageCap];
-    __shared__ double2 st_vel[kBlock / 64][kStageCap];
-    const int bx = xcd_block();
-    const int slot = bx * kBlock + threadIdx.x;
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    const int total = start[ncell];
-    bool act = false;
-    int r = 0, c = 0;
-    Ego E;
-    int rt0[3] = {0, 0, 0}, rt1[3] = {0, 0, 0};
-    if (slot < total) {
-        const int w = sidx[slot];
-        r = win_row0 + w / W;
-        c = w % W;
-        if (r >= row_begin && r < row_end) {
-            act = true;
-            const double2 pe = spos[slot], ve = svel[slot];
-            ego_init(P, E, pe.x, pe.y, ve.x, ve.y, ve.x, ve.y);
-            const int cx = cell_coord(pe.x, G.x0, G.inv_h, G.nx);
-            const int cy = cell_coord(pe.y, G.y0, G.inv_h, G.ny);
-            const int xa = cx > 0 ? cx - 1 : 0;
-            const int xb = cx < G.nx - 1 ? cx + 1 : G.nx - 1;
-#pragma unroll
-            for (int k = 0; k < 3; ++k) {
-                const int yy = cy + k - 1;
-                if (yy >= 0 && yy < G.ny) {
-                    rt0[k] = start[yy * G.nx + xa];
-                    rt1[k] = start[yy * G.nx + xb + 1];
-                }
-            }
-        }
-    }
-    // wave union of the three row ranges
-    int lo[3], len[3];
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-        const bool ne = act && rt1[k] > rt0[k];
-        int a = ne ? rt0[k] : 0x7FFFFFFF, b = ne ? rt1[k] : -1;
-        for (int o = 32; o > 0; o >>= 1) {
-            const int a2 = __shfl_xor(a, o, 64), b2 = __shfl_xor(b, o, 64);
-            a = a2 < a ? a2 : a;
-            b = b2 > b ? b2 : b;
-        }
-        lo[k] = a;
-        len[k] = b > a ? b - a : 0;
-    }
-    const int off1 = len[0], off2 = len[0] + len[1], L = off2 + len[2];
-    if (L <= kStageCap) {
-#pragma unroll
-        for (int j = 0; j < kStageCap / 64; ++j) {
-            const int i = lane + 64 * j;
-            if (i < L) {
-                const int g = i >= off2 ? lo[2] + (i - off2) : (i >= off1 ? lo[1] + (i - off1) : lo[0] + i);
-                st_pos[wid][i] = spos[g];
-                st_vel[wid][i] = svel[g];
-            }
-        }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        if (act) {
-#if CBF_LDS_STAGE == 2
-            // pass 1: cull test only, hits as a bit mask per row range; pass 2: assembly per hit
-            // (the wave iterates max-hits times instead of max-candidates times)
-            unsigned m[3] = {0u, 0u, 0u};
-            bool wide = false;
-#pragma unroll
-            for (int k = 0; k < 3; ++k) {
-                const int base = (k == 0 ? 0 : (k == 1 ? off1 : off2)) - lo[k];
-                wide = wide || rt1[k] - rt0[k] > 32;
-                const int te = rt1[k] - rt0[k] > 32 ? rt0[k] + 32 : rt1[k];
-                for (int t = rt0[k]; t < te; ++t) {
-                    const double2 pj = st_pos[wid][base + t];
-                    const double e0 = pj.x - E.r0, e1 = pj.y - E.r1;
-                    const double s = e0 * e0 + e1 * e1;
-                    if (s < P.cull_t && s > 0) m[k] |= 1u << (t - rt0[k]);
-                }
-            }
-            if (!wide) {
-#pragma unroll
-                for (int k = 0; k < 3; ++k) {
-                    const int base = (k == 0 ? 0 : (k == 1 ? off1 : off2)) - lo[k] + rt0[k];
-                    while (m[k]) {
-                        const int b = __ffs((int)m[k]) - 1;
-                        m[k] &= m[k] - 1u;
-                        const double2 pj = st_pos[wid][base + b];
-                        const double2 vj = st_vel[wid][base + b];
-                        ego_add<FZ>(P, E, pj.x, pj.y, vj.x, vj.y);
-                    }
-                }
-            } else {
-#pragma unroll
-                for (int k = 0; k < 3; ++k) scan_range_direct<FZ>(rt0[k], rt1[k], P, E, spos, svel);
-            }
-#else
-#pragma unroll
-            for (int k = 0; k < 3; ++k) {
-                const int base = (k == 0 ? 0 : (k == 1 ? off1 : off2)) - lo[k];
-                for (int t = rt0[k]; t < rt1[k]; ++t) {
-                    const double2 pj = st_pos[wid][base + t];
-                    const double e0 = pj.x - E.r0, e1 = pj.y - E.r1;
-                    const double s = e0 * e0 + e1 * e1;
-                    if (!(s < P.cull_t && s > 0)) continue;
-                    const double2 vj = st_vel[wid][base + t];
-                    ego_add<FZ>(P, E, pj.x, pj.y, vj.x, vj.y);
-                }
-            }
-#endif
-        }
-    } else if (act) {
-#pragma unroll
-        for (int k = 0; k < 3; ++k) scan_range_direct<FZ>(rt0[k], rt1[k], P, E, spos, svel);
-    }
-    bool solved = false;
-    if (act) {
-        double ny;
-        const int res = ego_finish<FZ>(P, E, W, row_begin, r, c, T, pos_out, u, status, cnt, hardq, &ny);
-        solved = res != 0 && E.count > 0 && r >= cnt_begin && r < cnt_end;
-    }
-    if (solves) {
-        const unsigned long long m = __ballot(solved);
-        if (lane == 0 && m)
-            atomicAdd(&solves[16 * ((bx * (kBlock / 64) + wid) & 63)], (unsigned long long)__popcll(m));
-    }
-}
-
-// K5: the queued hard QPs (state assembled by K4), 64-lane blocks spread over the CUs.
+// K5: the queued hard QPs (state assembled by K4): the exact Seidel solve, one per lane, the
+// sub-queues drained in full waves (drain_subq).
 __global__ void __launch_bounds__(64) k_lattice_filter_hard(KP P, int row_begin, int row_end, double T,
                                                             double2* __restrict__ pos_out, double2* __restrict__ u,
                                                             int32_t* __restrict__ status, int32_t* __restrict__ cnt,
                                                             int guard_rows, double* __restrict__ ext_part,
-                                                            int32_t* __restrict__ hardq, int cap) {
-    (void)cap;
-    const int nq = hardq[0];
-    const HardRec* q = reinterpret_cast<const HardRec*>(hardq + kHardHeader);
+                                                            unsigned long long* __restrict__ stats,
+                                                            int32_t* __restrict__ hardq,
+                                                            const HardRec* __restrict__ qrec, long qcap, int cnt_begin,
+                                                            int cnt_end) {
     double e0 = INFINITY, e1 = -INFINITY, e2 = -INFINITY, e3 = INFINITY;
-    for (int i = blockIdx.x * 64 + threadIdx.x; i < nq; i += gridDim.x * 64) {
-        const HardRec& h = q[i];
+    int n_opt = 0, n_rel = 0, n_inf = 0;
+    double vo = 0.0, vr = 0.0;
+    drain_subq(hardq, kHardPerQ, [&](int q, int i) {
+        const HardRec& h = qrec[(long)q * qcap + i];
         Ego E;
         E.r0 = h.r0;
         E.r1 = h.r1;
@@ -698,11 +445,21 @@ __global__ void __launch_bounds__(64) k_lattice_filter_hard(KP P, int row_begin,
         status[h.k] = pack_status(S);
         if (cnt) cnt[h.k] = E.count;
         ext_accumulate(h.row, row_begin, row_end, guard_rows, pn.y, e0, e1, e2, e3);
-    }
+        if (h.row >= cnt_begin && h.row < cnt_end) {
+            if (S.status == CBF_STATUS_OPTIMAL) {
+                ++n_opt;
+                vo = pmax(vo, S.viol);
+            } else if (S.status == CBF_STATUS_RELAXED) {
+                ++n_rel;
+                vr = pmax(vr, S.viol_orig);
+            } else {
+                ++n_inf;
+            }
+        }
+    });
+    if (stats) wave_stats_counts(stats, blockIdx.x, n_opt, n_rel, n_inf, vo, vr);
     if (ext_part) wave_extents(e0, e1, e2, e3, ext_part, blockIdx.x);
-    hard_queue_done(hardq);
 }
-
 
 constexpr int kFinBlock = 1024;
 __global__ void __launch_bounds__(kFinBlock) k_extents_finalize(int nparts, const double* __restrict__ part,
@@ -842,17 +599,14 @@ static int lattice_build(const cbf_params* p, const cbf_grid* grid, int32_t W, i
     const CellGrid G = make_grid(grid);
     CellWs Wk(workspace, n, (long)G.nx * G.ny);
     const double2* p2 = reinterpret_cast<const double2*>(pos);
-    // unsharded: the window is the owned rows, so the nominal controls go straight to vel_out
-    double2* wv = (win_row0 == row_begin && win_rows == row_end - row_begin) ? reinterpret_cast<double2*>(vel_out)
-                                                                              : Wk.wvel;
     int3* bcs = reinterpret_cast<int3*>(Wk.cs);  // 12 B per agent (the area reserves 16)
     hipLaunchKernelGGL(k_lattice_nominal_bin_ordered, dim3(nblk(n)), dim3(kBlock), 0, s, G, W, H, row_begin, row_end,
-                       win_row0, win_rows, p2, gain, wv, reinterpret_cast<double2*>(vel_out), Wk.count, Wk.sidx,
-                       Wk.start, Wk.ncell, bcs, Wk.hardq, ext_keys, X, Wk.sctl);
+                       win_row0, win_rows, p2, Wk.count, Wk.sidx, Wk.start, Wk.ncell, bcs, Wk.hardq, ext_keys, X,
+                       Wk.sctl);
     launch_scan(Wk, s);
-    hipLaunchKernelGGL(k_lattice_scatter_ordered, dim3(nblk(n)), dim3(kBlock), 0, s, n, bcs, Wk.start, p2, wv, Wk.spos,
-                       Wk.svel, Wk.sidx, Wk.spos32, Wk.hardq + 2, n, Wk.ncell, win_row0, H, W, row_begin, row_end, gain,
-                       reinterpret_cast<double2*>(vel_out));
+    hipLaunchKernelGGL(k_lattice_scatter_ordered, dim3(nblk(n)), dim3(kBlock), 0, s, n, bcs, Wk.start, p2, Wk.spos,
+                       Wk.svel, Wk.sidx, Wk.hardq + 2, Wk.ncell, win_row0, H, W, row_begin, row_end, gain,
+                       reinterpret_cast<double2*>(vel_out), Wk.sctl);
     return (int)hipGetLastError();
 }
 
@@ -866,7 +620,7 @@ extern "C" int cbf_lattice_build(const cbf_params* p, const cbf_grid* grid, int3
 static int lattice_advance(const cbf_params* p, const cbf_grid* grid, int32_t W, int32_t H, int32_t row_begin,
                            int32_t row_end, int32_t win_row0, int32_t win_rows, const double* pos, double T,
                            double* pos_out, double* u, int32_t* status, int32_t* nbr_count, int32_t guard_rows,
-                           double* extents, uint64_t* solves, void* workspace, size_t workspace_bytes,
+                           double* extents, uint64_t* stats, void* workspace, size_t workspace_bytes,
                            int32_t cnt_begin, int32_t cnt_end, void* stream) {
     int rc = check_lattice(p, grid, W, H, row_begin, row_end, win_row0, win_rows, pos, workspace, workspace_bytes);
     if (rc) return rc;
@@ -877,57 +631,48 @@ static int lattice_advance(const cbf_params* p, const cbf_grid* grid, int32_t W,
     CellWs Wk(workspace, n, (long)G.nx * G.ny);
     double* ext_part = extents ? (double*)((char*)workspace + CellWs::bytes(n, Wk.ncell)) : nullptr;
     const int nb = nblk(n);
-    const int hb = nb < kHardBlocks ? nb : kHardBlocks;
+    const int hb = lattice_hard_blocks(n);
     const KP kp = make_kp(p);
     double2* po = reinterpret_cast<double2*>(pos_out);
     double2* uo = reinterpret_cast<double2*>(u);
-    if (CBF_LDS_STAGE && !ext_part) {
-        hipLaunchKernelGGL(p->f_is_zero ? k_lattice_filter_lds<true> : k_lattice_filter_lds<false>, dim3(nb),
-                           dim3(kBlock), 0, s, kp, G, W, row_begin, row_end, win_row0, Wk.ncell, Wk.spos, Wk.svel,
-                           Wk.sidx, Wk.start, T, po, uo, status, nbr_count,
-                           reinterpret_cast<unsigned long long*>(solves), Wk.hardq, cnt_begin, cnt_end);
-    } else {
-        hipLaunchKernelGGL(p->f_is_zero ? k_lattice_filter<true> : k_lattice_filter<false>, dim3(nb), dim3(kBlock), 0,
-                           s, kp, G, W, row_begin, row_end, win_row0, Wk.ncell, Wk.spos, Wk.svel, Wk.sidx, Wk.start, T,
-                           po, uo, status, nbr_count, guard_rows, ext_part,
-                           reinterpret_cast<unsigned long long*>(solves), Wk.hardq, Wk.spos32, cnt_begin, cnt_end);
-    }
-    // queue kernel only when the filter queues (CBF_HARD_INLINE solves hard QPs in place)
-    const bool queued = !CBF_HARD_INLINE || CBF_HIT_MASK || (CBF_LDS_STAGE && !ext_part);
-    if (queued)
-        hipLaunchKernelGGL(k_lattice_filter_hard, dim3(hb), dim3(64), 0, s, kp, row_begin, row_end, T, po, uo, status,
-                           nbr_count, guard_rows, ext_part ? ext_part + 4l * lattice_ext_waves(n) : nullptr,
-                           Wk.hardq, (int)n);
-    if (extents) launch_extents_finalize((int)lattice_ext_waves(n) + (queued ? hb : 0), ext_part, extents, s);
+    unsigned long long* st = reinterpret_cast<unsigned long long*>(stats);
+    hipLaunchKernelGGL(p->f_is_zero ? k_lattice_filter<true> : k_lattice_filter<false>, dim3(nb), dim3(kBlock), 0, s,
+                       kp, G, W, row_begin, row_end, win_row0, n, Wk.ncell, Wk.spos, Wk.svel, Wk.sidx, Wk.start, Wk.sctl,
+                       T, po, uo, status, nbr_count, guard_rows, ext_part, st, Wk.hardq, Wk.qrec, Wk.qcap, cnt_begin,
+                       cnt_end);
+    hipLaunchKernelGGL(k_lattice_filter_hard, dim3(hb), dim3(64), 0, s, kp, row_begin, row_end, T, po, uo, status,
+                       nbr_count, guard_rows, ext_part ? ext_part + 4l * lattice_ext_waves(n) : nullptr, st, Wk.hardq,
+                       Wk.qrec, Wk.qcap, cnt_begin, cnt_end);
+    if (extents) launch_extents_finalize((int)lattice_ext_waves(n) + hb, ext_part, extents, s);
     return (int)hipGetLastError();
 }
 
 extern "C" int cbf_lattice_advance(const cbf_params* p, const cbf_grid* grid, int32_t W, int32_t H,
                                    int32_t row_begin, int32_t row_end, int32_t win_row0, int32_t win_rows,
                                    const double* pos, double T, double* pos_out, double* u, int32_t* status,
-                                   int32_t* nbr_count, int32_t guard_rows, double* extents, uint64_t* solves,
+                                   int32_t* nbr_count, int32_t guard_rows, double* extents, uint64_t* stats,
                                    void* workspace, size_t workspace_bytes, void* stream) {
     return lattice_advance(p, grid, W, H, row_begin, row_end, win_row0, win_rows, pos, T, pos_out, u, status, nbr_count,
-                           guard_rows, extents, solves, workspace, workspace_bytes, row_begin, row_end, stream);
+                           guard_rows, extents, stats, workspace, workspace_bytes, row_begin, row_end, stream);
 }
 
 extern "C" int cbf_lattice_step(const cbf_params* p, const cbf_grid* grid, int32_t W, int32_t H, int32_t row_begin,
                                 int32_t row_end, int32_t win_row0, int32_t win_rows, const double* pos, double gain,
                                 double T, double* pos_out, double* vel_out, double* u, int32_t* status,
-                                int32_t* nbr_count, int32_t guard_rows, double* extents, uint64_t* solves,
+                                int32_t* nbr_count, int32_t guard_rows, double* extents, uint64_t* stats,
                                 void* workspace, size_t workspace_bytes, void* stream) {
     int rc = cbf_lattice_build(p, grid, W, H, row_begin, row_end, win_row0, win_rows, pos, gain, vel_out, workspace,
                                workspace_bytes, stream);
     if (rc) return rc;
     return cbf_lattice_advance(p, grid, W, H, row_begin, row_end, win_row0, win_rows, pos, T, pos_out, u, status,
-                               nbr_count, guard_rows, extents, solves, workspace, workspace_bytes, stream);
+                               nbr_count, guard_rows, extents, stats, workspace, workspace_bytes, stream);
 }
 
 extern "C" int cbf_lattice_step_sharded(const cbf_params* p, const cbf_grid* grid, int32_t W, int32_t H,
                                         int32_t row_begin, int32_t row_end, int32_t own_begin, int32_t own_end,
                                         int32_t win_row0, int32_t win_rows, const double* pos, double gain, double T,
                                         double* pos_out, double* vel_out, double* u, int32_t* status,
-                                        int32_t* nbr_count, int32_t guard_rows, uint64_t* ext_keys, uint64_t* solves,
+                                        int32_t* nbr_count, int32_t guard_rows, uint64_t* ext_keys, uint64_t* stats,
                                         void* workspace, size_t workspace_bytes, void* stream) {
     if (!ext_keys || guard_rows < 0 || own_begin < row_begin || own_end > row_end || own_begin >= own_end)
         return CBF_EINVAL;
@@ -936,7 +681,7 @@ extern "C" int cbf_lattice_step_sharded(const cbf_params* p, const cbf_grid* gri
                            ExtSpec{own_begin, own_end, guard_rows}, stream);
     if (rc) return rc;
     return lattice_advance(p, grid, W, H, row_begin, row_end, win_row0, win_rows, pos, T, pos_out, u, status, nbr_count,
-                           guard_rows, nullptr, solves, workspace, workspace_bytes, own_begin, own_end, stream);
+                           guard_rows, nullptr, stats, workspace, workspace_bytes, own_begin, own_end, stream);
 }
 
 // ---- halo exchange of the row-sharded step -----------------------------------------

@@ -91,6 +91,9 @@ class HipBackend:
         # one workspace per sub-step: each keeps the cell order of its own window across cycles
         self.wss = [torch.zeros((self.ws_bytes,), dtype=torch.uint8, device=self.dev) for _ in range(nsub)]
         self.flag = torch.zeros((1,), dtype=torch.int32, device=self.dev)
+        # the guard flag is read back asynchronously after every exchange: a pinned host copy per
+        # exchange in flight, polled (never waited on) at the next exchanges
+        self._pending = []
         self.set_words = _lib.lib.cbf_halo_ext_bytes(1) // 8
         self.ext_keys = torch.empty((nsub * self.set_words,), dtype=torch.int64, device=self.dev)
         _lib.check(_lib.lib.cbf_halo_ext_reset(_lib.ptr(self.ext_keys), nsub, _lib.stream_handle()),
@@ -116,7 +119,7 @@ class HipBackend:
         L.check(L.lib.cbf_lattice_step_sharded(
             self.cp, L.C.byref(self.grid), W, self.H, sub.a, sub.b, S.rb, S.re, sub.w0, sub.w1 - sub.w0,
             P(S.wpos[(sub.w0 - S.w0) * W:]), self.gain, self.T, P(S.wpos[o:]), P(S.wvel[o:]), P(S.wu[o:]),
-            P(S.wstatus[o:]), P(S.wcnt[o:]), sub.guard, P(self.ext_keys[s * self.set_words:]), P(S.solves),
+            P(S.wstatus[o:]), P(S.wcnt[o:]), sub.guard, P(self.ext_keys[s * self.set_words:]), P(S.stats),
             P(self.wss[s]), self.ws_bytes, L.stream_handle()), "cbf_lattice_step_sharded")
 
     def lattice_build(self, S):
@@ -131,8 +134,25 @@ class HipBackend:
         sub = S.subs[-1]
         L.check(L.lib.cbf_lattice_advance(self.cp, L.C.byref(self.grid), self.W, self.H, S.rb, S.re, sub.w0,
                                           sub.w1 - sub.w0, P(S.wpos[(sub.w0 - S.w0) * self.W:]), self.T, P(S.own),
-                                          P(S.u), P(S.status), P(S.nbr_count), sub.guard, None, P(S.solves),
+                                          P(S.u), P(S.status), P(S.nbr_count), sub.guard, None, P(S.stats),
                                           P(self.wss[-1]), self.ws_bytes, L.stream_handle()), "cbf_lattice_advance")
+
+    def arm_guard_readback(self):
+        """Queue a copy of the guard flag to pinned host memory behind this exchange's unpack."""
+        torch = self.torch
+        host = torch.empty((1,), dtype=torch.int32, pin_memory=True)
+        host.copy_(self.flag, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        self._pending.append((ev, host))
+
+    def poll_guard(self) -> bool:
+        """True once a completed exchange's guard has failed (does not wait for the GPU)."""
+        while self._pending and self._pending[0][0].query():
+            _, host = self._pending.pop(0)
+            if int(host[0]):
+                return True
+        return False
 
     def guard_failed(self) -> bool:
         return bool(self.flag.item())
@@ -142,7 +162,7 @@ class ShardedLattice:
     """One rank's stripe of a W x (rows_per_rank * world) lattice swarm (see module docstring)."""
 
     def __init__(self, W, rows_per_rank, seed=0, halo=4, substeps=4, gain=scenarios.LATTICE_GAIN, T=scenarios.T,
-                 params=None, backend=None, group=None, pos_global=None):
+                 params=None, backend=None, group=None, pos_global=None, spacing=scenarios.LATTICE_SPACING):
         import torch
         import torch.distributed as dist
         from .swarm import FilterParams, make_grid
@@ -165,9 +185,9 @@ class ShardedLattice:
             self.subs.append(Sub(a, b, max(0, a - halo), min(self.H, b + halo), d + halo - 1))
         self.params = params or FilterParams()
         if pos_global is None:
-            pos_global = scenarios.lattice(W, self.H, seed=seed)
+            pos_global = scenarios.lattice(W, self.H, seed=seed, spacing=spacing)
         win = pos_global[self.w0 * W:self.w1 * W]
-        a = scenarios.LATTICE_SPACING
+        a = spacing
         grid = make_grid(-1.0 - a, self.w0 * a - 1.0 - a, W * a + 1.0, self.w1 * a + 1.0,
                          self.params.safety_distance * 1.02)
         if backend is None:
@@ -188,7 +208,7 @@ class ShardedLattice:
         self.u = self.wu[o0:o0 + self.n_owned]
         self.status = self.wstatus[o0:o0 + self.n_owned]
         self.nbr_count = self.wcnt[o0:o0 + self.n_owned]
-        self.solves = t(np.zeros(1024, np.int64))
+        self.stats = t(np.zeros(1024, np.int64))  # rollout statistics, include/cbf_amd.h CBF_STAT_*
         # send slab: [first G rows | last G rows | k guard records of 8 doubles] doubles
         self.slab = 2 * self.G * W * 2
         self.stride = self.slab + 8 * substeps
@@ -213,9 +233,18 @@ class ShardedLattice:
             self.dist.all_gather_into_tensor(self.recv, self.send, group=self.group)
 
     def exchange(self):
+        # the guard of the sub-steps certified at earlier exchanges, read back without waiting:
+        # a breach stops the rollout one or two cycles after it happened, not at the end
+        if self.be.poll_guard():
+            raise RuntimeError(self._guard_msg())
         self.be.pack(self)
         self._gather()
         self.be.unpack_guard(self)
+        self.be.arm_guard_readback()
+
+    def _guard_msg(self):
+        return (f"rank {self.rank}: halo guard failed -- an agent moved within the cull radius of a stripe from "
+                f"outside the {self.halo}-row halo; raise halo")
 
     def step(self):
         if self.sub == 0:
@@ -249,18 +278,25 @@ class ShardedLattice:
         return graphs
 
     def reset_solves(self):
-        self.solves.zero_()
+        self.stats.zero_()
+
+    def stats_summary(self) -> dict:
+        """This rank's rollout statistics over its owned rows (include/cbf_amd.h CBF_STAT_*)."""
+        from . import _lib
+        st = _lib.decode_stats(self.stats.cpu().numpy())
+        if st["errors"]:
+            raise _lib.CbfError(f"rank {self.rank}: {st['errors']} step(s) ran on an unusable cell list")
+        return st
 
     def solves_total(self) -> int:
-        return int(self.solves.view(64, 16)[:, 0].sum().item())
+        return self.stats_summary()["solves"]
 
     def check_guard(self):
         """Certify the sub-steps since the last exchange (one more exchange, which also refreshes
         the ghost rows) and raise if any sub-step's guard failed."""
         self.exchange()
         if self.be.guard_failed():
-            raise RuntimeError(f"rank {self.rank}: halo guard failed -- an agent moved within the cull radius of "
-                               f"a stripe from outside the {self.halo}-row halo; raise halo")
+            raise RuntimeError(self._guard_msg())
 
     def owned_positions(self):
         return self.own

@@ -87,7 +87,9 @@ def filter_swarm_hocbf(params, pos, vel, n_obs, ego_begin=None, ego_end=None, al
 def filter_swarm(params, pos, vel, n_obs, ego_begin=None, ego_end=None, method="auto", grid=None, kmax=0,
                  diag=False, workspace=None):
     """cross_and_rescue.py:135-160 for every ego in [ego_begin, ego_end).  Returns a dict of
-    CUDA tensors: u (n_ego,2), status, nbr_count [, nbr_idx, nbr_active, box_active, x, viol]."""
+    CUDA tensors: u (n_ego,2), status, nbr_count [, nbr_idx, nbr_active, box_active, x, viol].
+    workspace (method "cells"): a zero-filled uint8 tensor bound to one (n, grid) shape on first
+    use (include/cbf_amd.h); pass the same grid with it, or leave it None for a fresh one."""
     torch = _lib.require_gpu()
     n = pos.shape[0]
     eb = n_obs if ego_begin is None else ego_begin
@@ -259,7 +261,9 @@ class LatticeSwarm:
         self.nbr_count = torch.empty((n,), dtype=torch.int32, device=self.dev)
         self.ws_bytes = lib.cbf_lattice_workspace_size(W, H, _lib.C.byref(self.grid))
         self.ws = torch.zeros((self.ws_bytes,), dtype=torch.uint8, device=self.dev)
-        self.solves = torch.zeros((1024,), dtype=torch.int64, device=self.dev)
+        # rollout statistics of the fused step (include/cbf_amd.h CBF_STAT_*: solves, status counts,
+        # violations, minimum neighbour distance), accumulated on device by every step
+        self.stats = torch.zeros((1024,), dtype=torch.int64, device=self.dev)
         self.ap_ws = torch.empty((lib.cbf_allpairs_workspace_size(n, n) if method == "allpairs" else 1,),
                                  dtype=torch.uint8, device=self.dev)
         self.graph = None
@@ -272,7 +276,7 @@ class LatticeSwarm:
                                                 ptr(self.ap_ws), self.ap_ws.numel(), stream_handle()),
                   "cbf_filter_allpairs_split")
             euler(self.pos, self.u, self.T)
-            self.solves[0] += (self.nbr_count > 0).sum()
+            self.stats[_lib.STAT_SOLVES] += (self.nbr_count > 0).sum()
             return
         if self.barrier == "euclidean_hocbf":
             self.build_phase()
@@ -280,7 +284,7 @@ class LatticeSwarm:
             return
         check(lib.cbf_lattice_step(self.cp, _lib.C.byref(self.grid), self.W, self.H, 0, self.H, 0, self.H,
                                    ptr(self.pos), self.gain, self.T, ptr(self.pos), ptr(self.vel), ptr(self.u),
-                                   ptr(self.status), ptr(self.nbr_count), 0, None, ptr(self.solves), ptr(self.ws),
+                                   ptr(self.status), ptr(self.nbr_count), 0, None, ptr(self.stats), ptr(self.ws),
                                    self.ws_bytes, stream_handle()), "cbf_lattice_step")
 
     def build_phase(self):
@@ -295,19 +299,27 @@ class LatticeSwarm:
             check(lib.cbf_lattice_advance_hocbf(self.cp, _lib.C.byref(self.hp), _lib.C.byref(self.grid), self.W,
                                                 self.H, 0, self.H, 0, self.H, ptr(self.pos), self.T, ptr(self.pos),
                                                 ptr(self.u), ptr(self.status), ptr(self.nbr_count), 0, None,
-                                                ptr(self.solves), ptr(self.ws), self.ws_bytes, stream_handle()),
+                                                ptr(self.stats), ptr(self.ws), self.ws_bytes, stream_handle()),
                   "cbf_lattice_advance_hocbf")
             return
         check(lib.cbf_lattice_advance(self.cp, _lib.C.byref(self.grid), self.W, self.H, 0, self.H, 0, self.H,
                                       ptr(self.pos), self.T, ptr(self.pos), ptr(self.u), ptr(self.status),
-                                      ptr(self.nbr_count), 0, None, ptr(self.solves), ptr(self.ws), self.ws_bytes,
+                                      ptr(self.nbr_count), 0, None, ptr(self.stats), ptr(self.ws), self.ws_bytes,
                                       stream_handle()), "cbf_lattice_advance")
 
+    def stats_summary(self) -> dict:
+        """Rollout statistics since the last reset (host sync); raises if a step's cell list was
+        unusable (CBF_STATUS_WORKSPACE_ERROR)."""
+        st = _lib.decode_stats(self.stats.cpu().numpy())
+        if st["errors"]:
+            raise _lib.CbfError(f"{st['errors']} lattice step(s) ran on an unusable cell list (scan gave up)")
+        return st
+
     def solves_total(self) -> int:
-        return int(self.solves.view(64, 16)[:, 0].sum().item())
+        return self.stats_summary()["solves"]
 
     def reset_solves(self):
-        self.solves.zero_()
+        self.stats.zero_()
 
     def capture(self):
         """Capture one step into a hipGraph (replayed by step())."""
@@ -331,9 +343,11 @@ class LatticeSwarm:
             self._launch()
 
 
-def mc_rollout(params, pos, n_o, n_a, steps, T=1 / 30, theta=None, so=1.0, ga=1.0):
+def mc_rollout(params, pos, n_o, n_a, steps, T=1 / 30, theta=None, so=1.0, ga=1.0, safety=False):
     """SURVEY cfg5: pos (n_scen, n_o+n_a, 2) CUDA float64, advanced in place by `steps` steps.
-    Returns (counters int64 (n_scen,4), maxviol (n_scen,))."""
+    Returns (counters int64 (n_scen,4) = {filter calls, relaxed, box-infeasible, relax-cap},
+    maxviol (n_scen,) = max row violation over OPTIMAL solves[, safety (n_scen, 2) = {max violation
+    of the original barrier rows over RELAXED solves, min neighbour distance^2}])."""
     torch = _lib.require_gpu()
     theta = -math.pi / n_o if theta is None else theta
     rc, rs = float(np.cos(theta)), float(np.sin(theta))
@@ -341,7 +355,8 @@ def mc_rollout(params, pos, n_o, n_a, steps, T=1 / 30, theta=None, so=1.0, ga=1.
     assert pos.is_contiguous() and pos.dtype == torch.float64 and pos.shape[1] == n_o + n_a
     cnt = torch.empty((n_scen, 4), dtype=torch.int64, device=pos.device)
     mv = torch.empty((n_scen,), dtype=torch.float64, device=pos.device)
+    sf = torch.empty((n_scen, 2), dtype=torch.float64, device=pos.device) if safety else None
     cp = params.c() if isinstance(params, FilterParams) else params
     check(lib.cbf_mc_rollout(cp, n_scen, n_o, n_a, steps, float(T), rc, rs, float(so), float(ga), ptr(pos), ptr(cnt),
-                             ptr(mv), stream_handle()), "cbf_mc_rollout")
-    return cnt, mv
+                             ptr(mv), ptr(sf), stream_handle()), "cbf_mc_rollout")
+    return (cnt, mv, sf) if safety else (cnt, mv)

@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define CBF_ABI_VERSION 1
+#define CBF_ABI_VERSION 2
 
 #define CBF_EINVAL (-1)
 
@@ -50,6 +50,21 @@ extern "C" {
 #define CBF_STATUS_BOX_INFEASIBLE 3 /* the 8 box rows alone are infeasible; x = 0 */
 #define CBF_STATUS_RELAX_CAP 4      /* relaxation cap reached; x = 0 */
 #define CBF_STATUS_NBR_OVERFLOW 5   /* indexed HOCBF filter: more neighbours than kmax; u = u0, not filtered */
+#define CBF_STATUS_WORKSPACE_ERROR 6 /* the cell list of this step is unusable (its scan gave up waiting,
+                                        which no correct launch should hit); u = u0, not filtered */
+
+/* Rollout statistics of the lattice step (`stats`, device uint64[1024] zero-filled by the caller:
+ * 64 slots of 16 words, slot i at stats + 16 i; sum the counts and take the maximum of the other
+ * words over the slots).  Counted over the egos of the counted rows. */
+#define CBF_STAT_SOLVES 0        /* agent-QP solves (egos with >= 1 neighbour) */
+#define CBF_STAT_OPTIMAL 1       /* ... with status OPTIMAL (the reference's QP is feasible) */
+#define CBF_STAT_RELAXED 2       /* ... RELAXED (infeasible as posed; the cbf.py:84-87 rule applied) */
+#define CBF_STAT_INFEASIBLE 3    /* ... BOX_INFEASIBLE or RELAX_CAP */
+#define CBF_STAT_SEIDEL 4        /* QPs whose origin was infeasible after the strip pre-relaxation (full solve) */
+#define CBF_STAT_VIOL_OPTIMAL 5  /* max row violation over OPTIMAL QPs (bits of a double >= 0) */
+#define CBF_STAT_VIOL_ORIGINAL 6 /* max violation of the ORIGINAL barrier rows over RELAXED QPs (bits) */
+#define CBF_STAT_MIN_DIST2 7     /* 0x7FF0000000000000 - bits(min neighbour distance^2); 0 = no pair */
+#define CBF_STAT_ERRORS 8        /* steps whose cell list was unusable (CBF_STATUS_WORKSPACE_ERROR) */
 
 /* ControlBarrierFunction state (cbf.py:6-16) + the callers' dynamics and cull radius. */
 typedef struct cbf_params {
@@ -162,8 +177,12 @@ typedef struct cbf_grid {
     int32_t nx, ny; /* cells per axis */
 } cbf_grid;
 
-/* Workspaces (cells and lattice) must be zero-filled before their first use; every call leaves
- * them zero-filled again, so one workspace can be reused by any sequence of calls on a stream. */
+/* Workspaces (cells and lattice) must be zero-filled before their first use.  The first call binds
+ * a workspace to its shape (the number of binned entities -- n, or W x win_rows -- and the grid's
+ * cell count); it may then be reused by any sequence of calls of that shape on one stream (the
+ * kernels restore what they consume: cell counts, queue counts, scan epochs).  A call with another
+ * shape is detected on the device: every ego of it reports CBF_STATUS_WORKSPACE_ERROR (and the
+ * lattice step counts it in CBF_STAT_ERRORS) until the workspace is zero-filled again. */
 size_t cbf_cells_workspace_size(int32_t n, const cbf_grid* grid);
 
 int cbf_filter_cells(const cbf_params* p, const cbf_grid* grid, int32_t n, int32_t n_obs, const double* pos,
@@ -288,12 +307,15 @@ int cbf_lattice_step_sharded(const cbf_params* p, const cbf_grid* grid, int32_t 
  * n_o pursuit obstacles (ring i -> i+1, rotation (rc, rs), scale so) then n_a free agents
  * (complete-graph consensus, gain ga; only they are filtered), `steps` Euler steps of T.
  * pos [n_scen][n_o + n_a][2] is updated in place.  counters [n_scen][4] int64 = {filter calls,
- * relaxed, box-infeasible, relax-cap}; maxviol [n_scen] = max row violation over feasible
- * solves.  One workgroup runs several scenarios for all steps with the state in LDS.
+ * relaxed, box-infeasible, relax-cap}; maxviol [n_scen] = max row violation over the OPTIMAL
+ * (feasible) solves; safety [n_scen][2] (nullable) = {max violation of the ORIGINAL barrier rows over
+ * the RELAXED solves, min distance^2 from an agent to a culled neighbour (+inf if none)}.  One
+ * workgroup runs several scenarios for all steps with the state in LDS.
  * Requires 1 <= n_o, n_a and n_o + n_a <= 256.
  */
 int cbf_mc_rollout(const cbf_params* p, int32_t n_scen, int32_t n_o, int32_t n_a, int32_t steps, double T, double rc,
-                   double rs, double so, double ga, double* pos, int64_t* counters, double* maxviol, void* stream);
+                   double rs, double so, double ga, double* pos, int64_t* counters, double* maxviol, double* safety,
+                   void* stream);
 
 /*
  * robotarium-lite: the rps calls the reference scripts wrap around the

@@ -238,6 +238,26 @@ int orc_filter_one(const orc_params* p, const double r[4], int m, const double* 
     return st;
 }
 
+/* max(0, a.x - b) over the ego's ORIGINAL rows (merged box rows, per-quadrant barrier minima before
+ * any relaxation): the violation of the barrier the reference asked for (a reported statistic;
+ * same evaluation order as cbf_device.hpp:orig_violation). */
+static double orig_violation(const orc_params* p, const double r[4], const double u0[2], const double bq[4],
+                             const int present[4], const double x[2]) {
+    double S[8];
+    box_rhs(p, r, u0, S);
+    const double bb[4] = {py_min(S[0], S[4]), py_min(S[1], S[6]), py_min(S[2], S[5]), py_min(S[3], S[7])};
+    const double ab[4] = {x[0], x[1], -x[0], -x[1]};
+    double v = 0.0;
+    for (int h = 0; h < 4; ++h) v = py_max(v, ab[h] - bb[h]);
+    for (int q = 0; q < 4; ++q)
+        if (present[q]) {
+            double nq[2];
+            quadrant_normal(p, q, nq);
+            v = py_max(v, (nq[0] * x[0] + nq[1] * x[1]) - bq[q]);
+        }
+    return v;
+}
+
 static double relaxed(double b, int iters) {
     for (int i = 0; i < iters; ++i) b = b + 1.0;
     return b;
@@ -252,7 +272,7 @@ static double relaxed(double b, int iters) {
  */
 void orc_filter_swarm(const orc_params* p, int n, int n_obs, const double* pos, const double* vel, int ego_begin,
                       int ego_end, double* u, int32_t* status, int32_t* cnt, int32_t* nbr_idx, uint8_t* nbr_active,
-                      int kmax, uint8_t* box_active, double* xdev, double* viol) {
+                      int kmax, uint8_t* box_active, double* xdev, double* viol, double* viol_orig, double* d2min) {
     for (int e = ego_begin; e < ego_end; ++e) {
         int k = e - ego_begin;
         double r[4] = {pos[2 * e], pos[2 * e + 1], vel[2 * e], vel[2 * e + 1]};
@@ -260,10 +280,12 @@ void orc_filter_swarm(const orc_params* p, int n, int n_obs, const double* pos, 
         double bq[4] = {0, 0, 0, 0};
         int present[4] = {0, 0, 0, 0};
         int m = 0;
+        double dm = INFINITY;
         for (int j = 0; j < n; ++j) {
             double e0 = pos[2 * j] - r[0], e1 = pos[2 * j + 1] - r[1];
             double s = (0.0 + e0 * e0) + e1 * e1;
             if (!(s < p->cull_t && (j < n_obs || s > 0))) continue;
+            dm = py_min(dm, s);
             double o[4] = {pos[2 * j], pos[2 * j + 1], vel[2 * j], vel[2 * j + 1]};
             int q;
             double b = row_b(p, r, o, u0, &q);
@@ -273,6 +295,7 @@ void orc_filter_swarm(const orc_params* p, int n, int n_obs, const double* pos, 
             m++;
         }
         cnt[k] = m;
+        if (d2min) d2min[k] = dm;
         if (nbr_idx)
             for (int t = m; t < kmax; ++t) nbr_idx[(size_t)k * kmax + t] = -1;
         if (m == 0) {
@@ -281,6 +304,7 @@ void orc_filter_swarm(const orc_params* p, int n, int n_obs, const double* pos, 
             status[k] = ST_IDLE;
             if (xdev) xdev[2 * k] = xdev[2 * k + 1] = 0.0;
             if (viol) viol[k] = 0.0;
+            if (viol_orig) viol_orig[k] = 0.0;
             if (box_active) box_active[k] = 0;
             if (nbr_active)
                 for (int t = 0; t < kmax; ++t) nbr_active[(size_t)k * kmax + t] = 0;
@@ -300,6 +324,7 @@ void orc_filter_swarm(const orc_params* p, int n, int n_obs, const double* pos, 
             xdev[2 * k + 1] = x[1];
         }
         if (viol) viol[k] = v;
+        if (viol_orig) viol_orig[k] = iters > 0 ? orig_violation(p, r, u0, bq, present, x) : v;
         if (box_active) {
             double S[8];
             box_rhs(p, r, u0, S);
@@ -385,21 +410,23 @@ void orc_euler(int n, double* pos, const double* vel, double T) {
  * per scenario, n_o pursuit obstacles (ring Laplacian i -> i+1, rotation (rc,rs), scale so)
  * followed by n_a free agents (complete-graph consensus, gain ga); only agents are filtered.
  * pos: [n_scen][n_o+n_a][2], updated in place over `steps` Euler steps of length T.
- * counters: [n_scen][4] int64 = {filter calls, relaxed, box-infeasible, relax-cap}; maxviol [n_scen].
+ * counters: [n_scen][4] int64 = {filter calls, relaxed, box-infeasible, relax-cap}; maxviol [n_scen] = max
+ * row violation over OPTIMAL solves; safety [n_scen][2] (nullable) = {max violation of the original rows
+ * over RELAXED solves, min neighbour distance^2 of an agent}.
  */
 void orc_mc_rollout(const orc_params* p, int n_scen, int n_o, int n_a, int steps, double T, double rc, double rs,
-                    double so, double ga, double* pos, int64_t* counters, double* maxviol) {
+                    double so, double ga, double* pos, int64_t* counters, double* maxviol, double* safety) {
     int n = n_o + n_a;
     double vel[2 * 512];
     double u[2 * 256];
     int32_t st[256], cnt[256];
-    double viol[256];
+    double viol[256], vorig[256], d2[256];
     int32_t ring_ptr[2] = {0, 1};
     for (int s = 0; s < n_scen; ++s) {
         double* P = pos + (size_t)s * n * 2;
         int64_t* C = counters + (size_t)s * 4;
         C[0] = C[1] = C[2] = C[3] = 0;
-        double mv = 0.0;
+        double mv = 0.0, mvo = 0.0, dmin = INFINITY;
         for (int t = 0; t < steps; ++t) {
             for (int i = 0; i < n_o; ++i) {
                 int32_t col = (i + 1) % n_o;
@@ -413,21 +440,27 @@ void orc_mc_rollout(const orc_params* p, int n_scen, int n_o, int n_a, int steps
                 int32_t rp[2] = {0, m};
                 orc_consensus_csr(1, i, n_a, P + 2 * n_o, 0, rp, cols, 0, 1.0, 0.0, ga, vel + 2 * (n_o + i));
             }
-            orc_filter_swarm(p, n, n_o, P, vel, n_o, n, u, st, cnt, 0, 0, 0, 0, 0, viol);
+            orc_filter_swarm(p, n, n_o, P, vel, n_o, n, u, st, cnt, 0, 0, 0, 0, 0, viol, vorig, d2);
             for (int i = 0; i < n_a; ++i) {
+                dmin = py_min(dmin, d2[i]);
                 if (cnt[i] == 0) continue;
                 C[0]++;
                 int code = st[i] & 0xff;
                 if (code == ST_RELAXED) C[1]++;
                 if (code == ST_BOX_INFEASIBLE) C[2]++;
                 if (code == ST_RELAX_CAP) C[3]++;
-                if (code == ST_OPTIMAL || code == ST_RELAXED) mv = viol[i] > mv ? viol[i] : mv;
+                if (code == ST_OPTIMAL) mv = viol[i] > mv ? viol[i] : mv;
+                if (code == ST_RELAXED) mvo = vorig[i] > mvo ? vorig[i] : mvo;
                 vel[2 * (n_o + i)] = u[2 * i];
                 vel[2 * (n_o + i) + 1] = u[2 * i + 1];
             }
             orc_euler(n, P, vel, T);
         }
         maxviol[s] = mv;
+        if (safety) {
+            safety[2 * s] = mvo;
+            safety[2 * s + 1] = dmin;
+        }
     }
 }
 

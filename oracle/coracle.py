@@ -42,13 +42,14 @@ def lib():
         L.orc_filter_one.argtypes = [P, dp, C.c_int, dp, dp, dp, dp, C.POINTER(C.c_int)]
         L.orc_filter_one.restype = C.c_int
         L.orc_filter_swarm.argtypes = [P, C.c_int, C.c_int, dp, dp, C.c_int, C.c_int, dp, ip, ip,
-                                       C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p]
+                                       C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p,
+                                       C.c_void_p, C.c_void_p]
         L.orc_consensus_csr.argtypes = [C.c_int, C.c_int, C.c_int, dp, C.c_void_p, ip, ip, C.c_int, C.c_double,
                                         C.c_double, C.c_double, dp]
         L.orc_consensus_lattice.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int, dp, C.c_double, dp]
         L.orc_euler.argtypes = [C.c_int, dp, dp, C.c_double]
         L.orc_mc_rollout.argtypes = [P, C.c_int, C.c_int, C.c_int, C.c_int, C.c_double, C.c_double, C.c_double,
-                                     C.c_double, C.c_double, dp, i64p, dp]
+                                     C.c_double, C.c_double, dp, i64p, dp, C.c_void_p]
         L.orc_filter_one_hocbf.argtypes = [P, C.c_double, C.c_double, dp, C.c_int, dp, dp, dp, dp,
                                            C.POINTER(C.c_int)]
         L.orc_filter_one_hocbf.restype = C.c_int
@@ -87,7 +88,10 @@ def filter_one(p, r, obs, u0):
     return dict(u=u, x=x, status=st, iters=it.value)
 
 
-def filter_swarm(p, pos, vel, n_obs, ego_begin=None, ego_end=None, kmax=0, diag=False):
+def filter_swarm(p, pos, vel, n_obs, ego_begin=None, ego_end=None, kmax=0, diag=False, stats=False):
+    """cross_and_rescue.py:135-160 for egos [ego_begin, ego_end).  diag: neighbour indices / active
+    flags, box bits, x, viol (solved rows); stats: viol_orig (original rows) and d2min (smallest
+    neighbour distance^2, +inf if none)."""
     pos = _c(pos).reshape(-1, 2); vel = _c(vel).reshape(-1, 2)
     n = pos.shape[0]
     eb = n_obs if ego_begin is None else ego_begin
@@ -95,7 +99,7 @@ def filter_swarm(p, pos, vel, n_obs, ego_begin=None, ego_end=None, kmax=0, diag=
     ne = ee - eb
     u = np.zeros((ne, 2)); st = np.zeros(ne, np.int32); cnt = np.zeros(ne, np.int32)
     out = dict(u=u, status=st, cnt=cnt)
-    ptrs = [None] * 5
+    ptrs = [None] * 7
     if kmax:
         out["nbr_idx"] = np.zeros((ne, kmax), np.int32)
         ptrs[0] = out["nbr_idx"].ctypes.data
@@ -106,8 +110,11 @@ def filter_swarm(p, pos, vel, n_obs, ego_begin=None, ego_end=None, kmax=0, diag=
         out["box_active"] = np.zeros(ne, np.uint8); ptrs[2] = out["box_active"].ctypes.data
         out["x"] = np.zeros((ne, 2)); ptrs[3] = out["x"].ctypes.data
         out["viol"] = np.zeros(ne); ptrs[4] = out["viol"].ctypes.data
+    if stats:
+        out["viol_orig"] = np.zeros(ne); ptrs[5] = out["viol_orig"].ctypes.data
+        out["d2min"] = np.zeros(ne); ptrs[6] = out["d2min"].ctypes.data
     lib().orc_filter_swarm(C.byref(params(p)), n, n_obs, pos, vel, eb, ee, u, st, cnt, ptrs[0], ptrs[1], kmax,
-                           ptrs[2], ptrs[3], ptrs[4])
+                           ptrs[2], ptrs[3], ptrs[4], ptrs[5], ptrs[6])
     return out
 
 
@@ -136,12 +143,16 @@ def euler(pos, vel, T):
     return pos
 
 
-def mc_rollout(p, pos, n_o, n_a, steps, T, rot, so, ga):
+def mc_rollout(p, pos, n_o, n_a, steps, T, rot, so, ga, safety=False):
+    """Returns (pos, counters, maxviol[, safety (n_scen, 2) = {max original-row violation over
+    RELAXED solves, min neighbour distance^2}])."""
     pos = _c(pos).copy()
     n_scen = pos.shape[0]
     counters = np.zeros((n_scen, 4), np.int64); mv = np.zeros(n_scen)
-    lib().orc_mc_rollout(C.byref(params(p)), n_scen, n_o, n_a, steps, T, rot[0], rot[1], so, ga, pos, counters, mv)
-    return pos, counters, mv
+    sf = np.zeros((n_scen, 2)) if safety else None
+    lib().orc_mc_rollout(C.byref(params(p)), n_scen, n_o, n_a, steps, T, rot[0], rot[1], so, ga, pos, counters, mv,
+                         None if sf is None else sf.ctypes.data)
+    return (pos, counters, mv, sf) if safety else (pos, counters, mv)
 
 
 def filter_one_hocbf(p, hp, r, obs, u0):

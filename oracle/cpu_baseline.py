@@ -1,0 +1,128 @@
+"""The reference's CPU path timed on the host's cores, for bench.py's ``cpu_baseline`` leg.
+
+TEST INFRASTRUCTURE ONLY (imported by bench.py's cpu_baseline leg and tests/, never by cbf_amd).
+
+What is timed is ``oracle/refloop.py``: /root/reference/cross_and_rescue.py:135-160 restated line
+by line (a Python cull over every entity per ego, the rows of cbf.py:38-80, cvxopt's coneqp of
+cbf.py:75-87 restated in numpy since the cvxopt binary is absent, de-bias and clip).  Agents are
+independent within a step (the loop is a Jacobi update over the packed nominal states,
+cross_and_rescue.py:133), so the egos are split over one single-threaded process per host core
+(OMP / OPENBLAS / MKL threads pinned to 1) and the rates add.
+
+Two shapes, both on the same inputs the GPU runs:
+  * ``qp``   -- cfg2 (meet_at_center.py:76-153 at N = 100: 50 pursuit obstacles, 50 agents), where
+                the interior-point QP dominates each agent-QP;
+  * ``cfg4`` -- random egos of the 1M-agent lattice, where the reference's O(N) Python cull per
+                ego dominates (that is what its loop does at that N).
+"""
+from __future__ import annotations
+
+import multiprocessing as mp
+import os
+import sys
+import time
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+
+
+def host_cores():
+    """(cores, how) available to this job: the cgroup CPU quota, the affinity mask and the
+    launcher's OMP_NUM_THREADS share, whichever is smallest (os.cpu_count() is the whole machine,
+    which several GPU jobs share)."""
+    cands = {}
+    try:
+        cands["affinity"] = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        cands["cpu_count"] = os.cpu_count() or 1
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        if q != "max":
+            cands["cgroup_quota"] = max(1, int(int(q) // int(per)))
+    except (OSError, ValueError):
+        pass
+    omp = os.environ.get("OMP_NUM_THREADS")
+    if omp and omp.isdigit() and int(omp) > 0:
+        cands["OMP_NUM_THREADS"] = int(omp)
+    how = min(cands, key=cands.get)
+    return cands[how], f"{how}={cands[how]} (all: {cands}, machine cpu_count={os.cpu_count()})"
+
+
+def _scenarios():
+    """cbf_amd/scenarios.py (plain numpy) loaded by path: the package __init__ would load the HIP
+    library into every worker process."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("_cbf_scenarios", os.path.join(ROOT, "cbf_amd", "scenarios.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def _pin_blas():
+    for v in ("OMP_NUM_THREADS", "OPENBLAS_NUM_THREADS", "MKL_NUM_THREADS"):
+        os.environ[v] = "1"
+
+
+def _cfg2_state():
+    """cfg2's packed states at step 0: positions and nominal controls (meet_at_center.py:86-116)."""
+    from oracle import coracle
+    pos, n_obs, groups = _scenarios().meet_at_center(100)
+    vel = np.zeros_like(pos)
+    for (b, e, rows, anc, rot, scale) in groups:
+        rp = np.concatenate([[0], np.cumsum([len(r) for r in rows])]).astype(np.int32)
+        col = np.array([j for r in rows for j in r], np.int32)
+        vel[b:e] = coracle.consensus_csr(pos[b:e], rp, col, 0, e - b, anchors=anc, rot=rot, scale=scale)
+    return pos, vel, n_obs
+
+
+def _cfg4_state(W, H, seed, spacing, gain):
+    from oracle import coracle
+    pos = _scenarios().lattice(W, H, seed=seed, spacing=spacing)
+    return pos, coracle.consensus_lattice(W, H, 0, H, pos, gain), 0
+
+
+def _worker(arg):
+    kind, shape, rank, procs, budget_s = arg
+    _pin_blas()
+    if ROOT not in sys.path:
+        sys.path.insert(0, ROOT)
+    from oracle import pyoracle as po, refloop
+    if kind == "qp":
+        pos, vel, n_obs = _cfg2_state()
+        n_ego = pos.shape[0] - n_obs
+        egos = (i % n_ego for i in range(rank, 1 << 40, procs))        # the 50 agents, cyclically
+    else:
+        pos, vel, n_obs = _cfg4_state(*shape)
+        order = np.random.default_rng(321).permutation(pos.shape[0] - n_obs)
+        egos = (int(e) for e in order[rank::procs])
+    done, solves, dt = refloop.loop_sample(po.Params(15), pos, vel, n_obs, egos, budget_s)
+    return done, solves, dt
+
+
+def run(kind, budget_s, procs=None, shape=None):
+    """Times the restated reference loop on `procs` processes (default: host_cores()) for about
+    budget_s seconds each.  Returns the cpu_baseline record."""
+    cores, how = host_cores()
+    procs = procs or cores
+    args = [(kind, shape, r, procs, budget_s) for r in range(procs)]
+    t0 = time.perf_counter()
+    with mp.get_context("spawn").Pool(procs) as pool:
+        res = pool.map(_worker, args)
+    wall = time.perf_counter() - t0
+    done = sum(r[0] for r in res)
+    solves = sum(r[1] for r in res)
+    dt = max(r[2] for r in res)
+    what = ("cfg2 (meet_at_center.py at N=100: 50 obstacles + 50 agents, step-0 states), every agent-QP "
+            "one cvxopt-coneqp solve" if kind == "qp" else
+            f"random egos of the {shape[0]}x{shape[1]} lattice (spacing {shape[3]}), each an O(N) Python cull "
+            "+ cvxopt-coneqp solve")
+    return {"value": solves / dt, "unit": "agent-QP solves/s", "cores": procs, "kind": "port",
+            "per_core": solves / dt / procs,
+            "sample": f"{done} egos of {what}, through oracle/refloop.py (cross_and_rescue.py:135-160 restated "
+                      f"line by line; cbf.py's cvxopt coneqp restated in numpy, maxiters 600; cvxopt itself is "
+                      f"absent from the image), {procs} single-threaded processes x {dt:.1f} s "
+                      f"({wall:.1f} s wall incl. start-up)",
+            "cores_source": how}

@@ -27,7 +27,7 @@ def test_library_loads_and_exports_every_declared_symbol():
         assert hasattr(_lib.lib, n), n
         assert n in _lib.SIGNATURES, n
     assert set(_lib.SIGNATURES) == set(names)
-    assert _lib.lib.cbf_abi_version() == 1
+    assert _lib.lib.cbf_abi_version() == _lib.ABI_VERSION == 2
 
 
 def test_library_is_gfx950_code_object():
@@ -73,7 +73,7 @@ def test_argument_validation_without_launch():
     assert L.cbf_lattice_step(cp, C.byref(g), 8, 8, 2, 4, 2, 2, 1, 0.25, 0.1, 1, 1, 1, 1, null, 0, null, null, 1,
                               1 << 24, null) == _lib.CBF_EINVAL
     # mc: too many entities per scenario
-    assert L.cbf_mc_rollout(cp, 4, 200, 100, 1, 0.1, 1.0, 0.0, 1.0, 1.0, 1, 1, 1, null) == _lib.CBF_EINVAL
+    assert L.cbf_mc_rollout(cp, 4, 200, 100, 1, 0.1, 1.0, 0.0, 1.0, 1.0, 1, 1, 1, null, null) == _lib.CBF_EINVAL
     # sharded halo exchange: bad geometry is refused before any launch
     assert L.cbf_halo_ext_bytes(0) == 0 and L.cbf_halo_ext_bytes(4) == 4 * L.cbf_halo_ext_bytes(1)
     assert L.cbf_halo_pack(8, 4, 16, 1, 1, 1, 1, null) == _lib.CBF_EINVAL          # fewer owned rows than 2 halos
@@ -96,6 +96,27 @@ def test_argument_validation_without_launch():
     assert L.cbf_euler(0, null, null, 0.1, null) == 0
     assert L.cbf_si_barrier_cert(C.byref(cc), 0, 4, null, null, null, null, null, null, null) == 0
     assert L.cbf_get_safe_control_batch(cp, 0, null, null, null, null, null, null, null, null) == 0
+
+
+def test_decode_stats():
+    """Host decoding of the lattice-step statistics words (include/cbf_amd.h CBF_STAT_*)."""
+    from cbf_amd import _lib
+    w = np.zeros(1024, np.uint64)
+    assert _lib.decode_stats(w.view(np.int64)) == {"solves": 0, "optimal": 0, "relaxed": 0, "infeasible": 0,
+                                                   "seidel": 0, "errors": 0, "viol_optimal": 0.0,
+                                                   "viol_original_relaxed": 0.0, "min_dist2": None}
+    s = w.reshape(64, 16)
+    s[3, _lib.STAT_SOLVES] = 5
+    s[60, _lib.STAT_SOLVES] = 7
+    s[1, _lib.STAT_OPTIMAL] = 4
+    s[2, _lib.STAT_VIOL_OPTIMAL] = np.array([1e-17]).view(np.uint64)[0]
+    s[9, _lib.STAT_VIOL_OPTIMAL] = np.array([3e-18]).view(np.uint64)[0]
+    s[4, _lib.STAT_VIOL_ORIGINAL] = np.array([0.25]).view(np.uint64)[0]
+    for slot, d2 in ((5, 0.01), (6, 0.0049), (7, 0.03)):
+        s[slot, _lib.STAT_MIN_DIST2] = np.uint64(0x7FF0000000000000) - np.array([d2]).view(np.uint64)[0]
+    d = _lib.decode_stats(w.view(np.int64))
+    assert d["solves"] == 12 and d["optimal"] == 4
+    assert d["viol_optimal"] == 1e-17 and d["viol_original_relaxed"] == 0.25 and d["min_dist2"] == 0.0049
 
 
 def test_workspace_sizes():

@@ -222,19 +222,59 @@ def _oracle_lattice_step(pos, W, H, gain, T):
     return coracle.euler(pos, out["u"], T), vel, out
 
 
-def test_lattice_step_vs_oracle():
+def _oracle_stats(outs):
+    """The rollout statistics (include/cbf_amd.h CBF_STAT_*) restated from oracle outputs."""
+    st = {"solves": 0, "optimal": 0, "relaxed": 0, "infeasible": 0, "viol_optimal": 0.0,
+          "viol_original_relaxed": 0.0, "min_dist2": np.inf, "min_seidel": 0}
+    for o in outs:
+        code = o["status"] & 0xFF
+        solved = o["cnt"] > 0
+        st["solves"] += int(solved.sum())
+        st["optimal"] += int((code == 1).sum())
+        st["relaxed"] += int((code == 2).sum())
+        st["infeasible"] += int(((code == 3) | (code == 4)).sum())
+        st["viol_optimal"] = max(st["viol_optimal"], float(o["viol"][code == 1].max(initial=0.0)))
+        st["viol_original_relaxed"] = max(st["viol_original_relaxed"],
+                                          float(o["viol_orig"][code == 2].max(initial=0.0)))
+        st["min_dist2"] = min(st["min_dist2"], float(o["d2min"].min(initial=np.inf)))
+        # an OPTIMAL QP whose minimiser is not the origin cannot be finished at the origin
+        st["min_seidel"] += int(((code == 1) & (np.abs(o["x"]).max(axis=1) > 0)).sum())
+    return st
+
+
+def _check_stats(got, want):
+    for k in ("solves", "optimal", "relaxed", "infeasible", "viol_optimal", "viol_original_relaxed"):
+        assert got[k] == want[k], (k, got[k], want[k])
+    assert (got["min_dist2"] if got["min_dist2"] is not None else np.inf) == want["min_dist2"]
+    assert want["min_seidel"] <= got["seidel"] <= got["solves"]
+    assert got["errors"] == 0
+
+
+@pytest.mark.parametrize("spacing", [scenarios.LATTICE_SPACING, 0.2])
+def test_lattice_step_vs_oracle(spacing):
+    """Fused lattice steps == oracle steps bit for bit, and the device rollout statistics (status
+    counts, OPTIMAL-only and original-row violations, minimum neighbour distance) equal the same
+    quantities restated from the oracle's outputs.  Spacing 0.2 is the feasible regime (cfg4f)."""
     W, H = 48, 40
-    pos = scenarios.lattice(W, H, seed=5)
+    pos = scenarios.lattice(W, H, seed=5, spacing=spacing)
     L = swarm.LatticeSwarm(pos, W, H, gain=0.25)
     ref = pos.copy()
+    outs = []
     for step in range(8):
         L.step()
-        ref, vel, out = _oracle_lattice_step(ref, W, H, 0.25, 1 / 30)
+        vel = coracle.consensus_lattice(W, H, 0, H, ref, 0.25)
+        out = coracle.filter_swarm(po.Params(15), ref, vel, 0, diag=True, stats=True)
+        ref = coracle.euler(ref, out["u"], 1 / 30)
+        outs.append(out)
         assert np.array_equal(L.vel.cpu().numpy(), vel), step
         assert np.array_equal(L.u.cpu().numpy(), out["u"]), step
         assert np.array_equal(L.status.cpu().numpy(), out["status"]), step
         assert np.array_equal(L.nbr_count.cpu().numpy(), out["cnt"]), step
         assert np.array_equal(L.pos.cpu().numpy(), ref), step
+    want = _oracle_stats(outs)
+    _check_stats(L.stats_summary(), want)
+    if spacing == 0.2:
+        assert want["optimal"] > 0.5 * want["solves"] and want["min_seidel"] > 0.1 * want["solves"]
 
 
 def test_lattice_graph_replay_matches_eager():
@@ -290,18 +330,105 @@ def test_lattice_full_size_cfg4():
     assert np.abs(u[cnt > 0]).max() <= 15.0
 
 
+def _min_pair_dist2(pos, cull_t):
+    """Exact smallest s = dx^2 + dy^2 over pairs with 0 < s < cull_t (the GPU's and the oracle's
+    arithmetic: the pair's two egos compute the same s, negation being exact)."""
+    from scipy.spatial import cKDTree
+    pr = cKDTree(pos).query_pairs(0.2 * (1 + 1e-9), output_type="ndarray")
+    d = pos[pr[:, 1]] - pos[pr[:, 0]]
+    s = d[:, 0] * d[:, 0] + d[:, 1] * d[:, 1]
+    s = s[(s < cull_t) & (s > 0)]
+    return float(s.min()) if s.size else np.inf
+
+
+@pytest.mark.parametrize("spacing", [scenarios.LATTICE_SPACING, 0.2])
+def test_lattice_full_size_safety_stats(spacing):
+    """cfg4 (and the feasible-regime cfg4f) at full size, 1024 x 1024, over a 3-step rollout: the
+    OPTIMAL-only row violation is <= 1e-12 (north star <= 1e-7), the device statistics count every
+    agent-QP once and agree with the statuses, and the minimum neighbour distance equals the exact
+    minimum over all culled pairs of the steps' input states."""
+    W = H = 1024
+    pos = scenarios.lattice(W, H, seed=0, spacing=spacing)
+    L = swarm.LatticeSwarm(pos, W, H)
+    cull_t = float(swarm.FilterParams().c().cull_t)
+    d2 = []
+    codes = np.zeros(8, np.int64)
+    for _ in range(3):
+        d2.append(_min_pair_dist2(L.pos.cpu().numpy(), cull_t))
+        L.step()
+        st = L.status.cpu().numpy() & 0xFF
+        codes += np.bincount(st, minlength=8)
+    got = L.stats_summary()
+    assert got["errors"] == 0
+    assert got["solves"] == codes[1] + codes[2] + codes[3] + codes[4]
+    assert (got["optimal"], got["relaxed"], got["infeasible"]) == (codes[1], codes[2], codes[3] + codes[4])
+    assert got["viol_optimal"] <= 1e-12
+    assert got["min_dist2"] == min(d2)
+    if spacing == 0.2:   # the feasible regime: most QPs feasible, the exact solve busy
+        assert got["optimal"] > 0.6 * got["solves"] and got["seidel"] > 0.15 * got["solves"]
+    else:
+        assert got["relaxed"] > 0.9 * got["solves"] and got["viol_original_relaxed"] > 0
+
+
+def test_lattice_full_size_cfg3_allpairs():
+    """cfg3 at full size (256 x 256 = 65,536 agents, every pair tested): one step, 256 sampled egos
+    against the O(N) reference cull of the oracle, plus size-independent properties."""
+    W = H = 256
+    pos = scenarios.lattice(W, H, seed=0)
+    L = swarm.LatticeSwarm(pos, W, H, gain=scenarios.LATTICE_GAIN, method="allpairs")
+    L.step()
+    torch.cuda.synchronize()
+    vel = coracle.consensus_lattice(W, H, 0, H, pos, scenarios.LATTICE_GAIN)
+    assert np.array_equal(L.vel.cpu().numpy(), vel)
+    u, st, cnt = L.u.cpu().numpy(), L.status.cpu().numpy(), L.nbr_count.cpu().numpy()
+    idx = np.random.default_rng(3).choice(W * H, 256, replace=False)
+    for e, (ru, rst, rc) in zip(idx, _sample_oracle(pos, vel, idx)):
+        assert np.array_equal(u[e], ru) and st[e] == rst and cnt[e] == rc, e
+    assert np.array_equal(L.pos.cpu().numpy(), coracle.euler(pos, u, 1 / 30))
+    code = st & 0xFF
+    assert np.array_equal(code == 0, cnt == 0)
+    assert np.array_equal(u[cnt == 0], vel[cnt == 0])
+    # the cell-list filter (a different cull) agrees on the whole swarm
+    out = swarm.filter_swarm(swarm.FilterParams(), _t(pos), _t(vel), 0, method="cells")
+    assert np.array_equal(out["u"].cpu().numpy(), u) and np.array_equal(out["status"].cpu().numpy(), st)
+
+
 def test_mc_rollout_vs_oracle():
     p = po.Params(15)
     n_scen, n_o, n_a, steps = 40, 16, 16, 60
     pos0 = scenarios.mc_scenarios(n_scen, n_o, n_a, seed=4)
     P = _t(pos0)
-    cnt, mv = swarm.mc_rollout(swarm.FilterParams(), P, n_o, n_a, steps, ga=scenarios.MC_GAIN)
-    rp, rc, rm = coracle.mc_rollout(p, pos0, n_o, n_a, steps, 1 / 30, (np.cos(-np.pi / n_o), np.sin(-np.pi / n_o)),
-                                    1.0, scenarios.MC_GAIN)
+    cnt, mv, sf = swarm.mc_rollout(swarm.FilterParams(), P, n_o, n_a, steps, ga=scenarios.MC_GAIN, safety=True)
+    rp, rc, rm, rs = coracle.mc_rollout(p, pos0, n_o, n_a, steps, 1 / 30,
+                                        (np.cos(-np.pi / n_o), np.sin(-np.pi / n_o)), 1.0, scenarios.MC_GAIN,
+                                        safety=True)
     assert np.array_equal(P.cpu().numpy(), rp)
     assert np.array_equal(cnt.cpu().numpy(), rc)
     assert np.array_equal(mv.cpu().numpy(), rm)
-    assert rc[:, 0].sum() > 0
+    assert np.array_equal(sf.cpu().numpy(), rs)
+    assert rc[:, 0].sum() > 0 and rm.max() <= 1e-12
+
+
+def test_mc_rollout_full_batch_cfg5():
+    """cfg5 at full size: 100,000 scenarios x 32 entities, 10 steps in one launch; 64 sampled
+    scenarios checked bit for bit against the oracle's rollout (positions, counters, violations,
+    distances), and the whole batch's OPTIMAL-only violation <= 1e-12."""
+    p = po.Params(15)
+    n_scen, n_o, n_a, steps = 100_000, 16, 16, 10
+    pos0 = scenarios.mc_scenarios(n_scen, n_o, n_a, seed=0)
+    P = _t(pos0)
+    cnt, mv, sf = swarm.mc_rollout(swarm.FilterParams(), P, n_o, n_a, steps, ga=scenarios.MC_GAIN, safety=True)
+    got_p, got_c, got_m, got_s = P.cpu().numpy(), cnt.cpu().numpy(), mv.cpu().numpy(), sf.cpu().numpy()
+    idx = np.sort(np.random.default_rng(5).choice(n_scen, 64, replace=False))
+    rp, rc, rm, rs = coracle.mc_rollout(p, pos0[idx], n_o, n_a, steps, 1 / 30,
+                                        (np.cos(-np.pi / n_o), np.sin(-np.pi / n_o)), 1.0, scenarios.MC_GAIN,
+                                        safety=True)
+    assert np.array_equal(got_p[idx], rp)
+    assert np.array_equal(got_c[idx], rc)
+    assert np.array_equal(got_m[idx], rm)
+    assert np.array_equal(got_s[idx], rs)
+    assert got_c[:, 0].sum() > 0 and got_m.max() <= 1e-12
+    assert np.isfinite(got_p).all()
 
 
 def test_mc_rollout_shipped_meet_at_center_shape():
@@ -462,3 +589,55 @@ def test_lattice_allpairs_step_vs_oracle():
     ref = coracle.filter_swarm(po.Params(15), pos, vel, 0)
     assert np.array_equal(L.u.cpu().numpy(), ref["u"])
     assert np.array_equal(L.pos.cpu().numpy(), coracle.euler(pos, ref["u"], 1 / 30))
+
+
+def test_workspace_bound_to_its_shape():
+    """A cells workspace reused with another grid is refused on the device (every ego reports
+    CBF_STATUS_WORKSPACE_ERROR, unfiltered) until it is zero-filled again (include/cbf_amd.h)."""
+    rng = np.random.default_rng(21)
+    p = po.Params(15)
+    fp = swarm.FilterParams()
+    pos, vel = _random_swarm(rng, 3000, 0, 2.5)
+    ref = coracle.filter_swarm(p, pos, vel, 0)
+    g1 = swarm.grid_for_points(pos, 0.2)
+    g2 = swarm.grid_for_points(pos, 0.2, margin=3.0)
+    from cbf_amd import _lib
+    need = max(_lib.lib.cbf_cells_workspace_size(3000, _lib.C.byref(g)) for g in (g1, g2))
+    ws = torch.zeros((need,), dtype=torch.uint8, device=DEV)
+    a = swarm.filter_swarm(fp, _t(pos), _t(vel), 0, method="cells", grid=g1, workspace=ws)
+    assert np.array_equal(a["u"].cpu().numpy(), ref["u"])
+    b = swarm.filter_swarm(fp, _t(pos), _t(vel), 0, method="cells", grid=g1, workspace=ws)   # same shape: fine
+    assert np.array_equal(b["status"].cpu().numpy(), ref["status"])
+    for _ in range(2):   # another grid: refused, and stays refused
+        c = swarm.filter_swarm(fp, _t(pos), _t(vel), 0, method="cells", grid=g2, workspace=ws)
+        assert (c["status"].cpu().numpy() == _lib.STATUS_WORKSPACE_ERROR).all()
+        assert np.array_equal(c["u"].cpu().numpy(), vel)
+    ws.zero_()
+    d = swarm.filter_swarm(fp, _t(pos), _t(vel), 0, method="cells", grid=g2, workspace=ws)
+    assert np.array_equal(d["u"].cpu().numpy(), ref["u"])
+
+
+def test_scan_timeout_is_reported():
+    """A scan look-back that gives up (forced in every tile by the test-only build
+    tests/_lib/libcbf_scantimeout.so, CBF_SCAN_TEST_TIMEOUT) is reported, not silent: every ego of
+    the step gets CBF_STATUS_WORKSPACE_ERROR and the statistics count the step in CBF_STAT_ERRORS.
+    The kernels after the scan do not read the unusable cell list (no scatter, identity order)."""
+    import ctypes as C
+    import os
+    from cbf_amd import _lib
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "libcbf_scantimeout.so")
+    L = C.CDLL(path)
+    fn = L.cbf_lattice_step
+    fn.restype, fn.argtypes = _lib.SIGNATURES["cbf_lattice_step"]
+    W, H = 512, 512   # > one scan tile of cells, so some tile has a predecessor to wait for
+    S = swarm.LatticeSwarm(scenarios.lattice(W, H, seed=1), W, H)
+    vel = torch.empty_like(S.pos)
+    rc = fn(S.cp, C.byref(S.grid), W, H, 0, H, 0, H, _lib.ptr(S.pos), S.gain, S.T, _lib.ptr(S.pos), _lib.ptr(vel),
+            _lib.ptr(S.u), _lib.ptr(S.status), _lib.ptr(S.nbr_count), 0, None, _lib.ptr(S.stats), _lib.ptr(S.ws),
+            S.ws_bytes, _lib.stream_handle())
+    assert rc == 0
+    torch.cuda.synchronize()
+    assert (S.status.cpu().numpy() == _lib.STATUS_WORKSPACE_ERROR).all()
+    with pytest.raises(cbf_amd.CbfError):
+        S.stats_summary()
+    assert _lib.decode_stats(S.stats.cpu().numpy())["errors"] == 1

@@ -78,7 +78,13 @@ class OracleBackend:
         S.wvel[o:o + n].copy_(torch.as_tensor(vel[eb:ee])); S.wu[o:o + n].copy_(torch.as_tensor(out["u"]))
         S.wstatus[o:o + n].copy_(torch.as_tensor(out["status"])); S.wcnt[o:o + n].copy_(torch.as_tensor(out["cnt"]))
         oe, of = (S.rb - sub.a) * W, (S.re - sub.a) * W
-        S.solves[0] += int((out["cnt"][oe:of] > 0).sum())
+        S.stats[0] += int((out["cnt"][oe:of] > 0).sum())
+
+    def arm_guard_readback(self):
+        pass
+
+    def poll_guard(self):
+        return bool(self.flag)
 
     def guard_failed(self):
         return bool(self.flag)
@@ -101,7 +107,7 @@ def _worker(rank, ws, port, W, R, steps, halo, q, k=1):
     for _ in range(steps):
         S.step()
     S.check_guard()
-    q.put((rank, S.own.numpy().copy(), S.u.numpy().copy(), S.status.numpy().copy(), int(S.solves[0])))
+    q.put((rank, S.own.numpy().copy(), S.u.numpy().copy(), S.status.numpy().copy(), int(S.stats[0])))
     dist.barrier()
     dist.destroy_process_group()
 

@@ -1,6 +1,6 @@
 """Sharded lattice step on the HIP path: 2 and 3 ranks rehearsed on one GPU (gloo, host-staged
 exchange), with 1 and 4 sub-steps per exchange (6 steps: the last cycle is partial), compared
-bit-for-bit with the single-GPU step of the whole lattice."""
+bit-for-bit with the CPU oracle's rollout of the whole lattice (and with the single-GPU step)."""
 import os
 import socket
 
@@ -38,7 +38,7 @@ def _worker(rank, ws, port, W, R, steps, q, k=4, graph=False):
         S.step()
     torch.cuda.synchronize()
     S.check_guard()
-    q.put((rank, S.own.cpu().numpy(), S.status.cpu().numpy(), S.solves_total()))
+    q.put((rank, S.own.cpu().numpy(), S.status.cpu().numpy(), S.u.cpu().numpy(), S.stats_summary()))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -58,11 +58,59 @@ def test_sharded_equals_single_gpu(ws, k, graph):
         p.join(timeout=120)
         assert p.exitcode == 0
     H = R * ws
+    # the oracle's rollout of the whole lattice (test infrastructure, oracle/)
+    from oracle import coracle, pyoracle as po
+    pos = scenarios.lattice(W, H, seed=7)
+    solves = optimal = relaxed = 0
+    for _ in range(steps):
+        vel = coracle.consensus_lattice(W, H, 0, H, pos, scenarios.LATTICE_GAIN)
+        out = coracle.filter_swarm(po.Params(15), pos, vel, 0)
+        pos = coracle.euler(pos, out["u"], scenarios.T)
+        solves += int((out["cnt"] > 0).sum())
+        optimal += int(((out["status"] & 0xFF) == 1).sum())
+        relaxed += int(((out["status"] & 0xFF) == 2).sum())
+    assert np.array_equal(np.concatenate([r[1] for r in res]), pos)
+    assert np.array_equal(np.concatenate([r[2] for r in res]), out["status"])
+    assert np.array_equal(np.concatenate([r[3] for r in res]), out["u"])
+    assert sum(r[4]["solves"] for r in res) == solves
+    assert sum(r[4]["optimal"] for r in res) == optimal and sum(r[4]["relaxed"] for r in res) == relaxed
+    # and the single-GPU fused step of the whole lattice
     L = swarm.LatticeSwarm(scenarios.lattice(W, H, seed=7), W, H)
-    L.reset_solves()
     for _ in range(steps):
         L.step()
     torch.cuda.synchronize()
-    assert np.array_equal(np.concatenate([r[1] for r in res]), L.pos.cpu().numpy())
-    assert np.array_equal(np.concatenate([r[2] for r in res]), L.status.cpu().numpy())
-    assert sum(r[3] for r in res) == L.solves_total()
+    assert np.array_equal(L.pos.cpu().numpy(), pos)
+
+
+def _worker_breach(rank, ws, port, q):
+    import datetime
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    # a rank that stops at a breach leaves its peer in the next collective: a short timeout ends it
+    dist.init_process_group("gloo", rank=rank, world_size=ws, timeout=datetime.timedelta(seconds=20))
+    from cbf_amd.shard import ShardedLattice
+    S = ShardedLattice(48, 16, seed=3, halo=2, substeps=1)   # halo 2 is too small for spacing 0.145
+    done = 0
+    try:
+        for _ in range(40):
+            S.step()
+            done += 1
+            torch.cuda.synchronize()   # let the guard read-back of each exchange land
+        q.put((rank, "not caught", done))
+    except RuntimeError as e:
+        q.put((rank, "raised" if "halo guard" in str(e) else "peer stopped", done))
+
+
+def test_halo_breach_stops_the_rollout_early():
+    """A halo that is too small is caught at an exchange during the rollout (the guard flag is read
+    back after every exchange), not only by check_guard() at the end."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_breach, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=300) for _ in range(2)])
+    for p in procs:
+        p.join(timeout=120)
+    assert any(r[1] == "raised" and r[2] < 5 for r in res), res

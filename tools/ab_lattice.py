@@ -1,0 +1,39 @@
+"""A/B timing of the fused lattice step for two source trees (tools/_ab/<tree>): the same
+jittered lattice, hipGraph replay, step time and advance-phase time by HIP events.
+Usage: python tools/ab_lattice.py <tree-root> <spacing> [steps]"""
+import sys
+import time
+
+root, spacing = sys.argv[1], float(sys.argv[2])
+steps = int(sys.argv[3]) if len(sys.argv) > 3 else 100
+sys.path.insert(0, root)
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+from cbf_amd import scenarios, swarm  # noqa: E402
+
+W = H = 1024
+rng = np.random.default_rng(0)
+r, c = np.divmod(np.arange(W * H), W)
+pos = np.stack([c * spacing, r * spacing], axis=1).astype(np.float64)
+pos += rng.uniform(-spacing / 2, spacing / 2, size=pos.shape)
+L = swarm.LatticeSwarm(pos, W, H, gain=0.25)
+L.capture()
+for _ in range(20):
+    L.step()
+torch.cuda.synchronize()
+t0 = time.perf_counter()
+for _ in range(steps):
+    L.step()
+torch.cuda.synchronize()
+dt = (time.perf_counter() - t0) / steps
+ks = []
+for _ in range(10):
+    L.build_phase()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    L.advance_phase()
+    b.record()
+    ks.append((a, b))
+torch.cuda.synchronize()
+adv = np.mean([a.elapsed_time(b) for a, b in ks]) * 1e3
+print(f"{root} spacing {spacing}: step {dt * 1e6:.1f} us, advance {adv:.1f} us")
