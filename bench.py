@@ -90,7 +90,8 @@ def safety_report(st, steps):
     d2 = st["min_dist2"]
     return {"steps": steps, "solves": st["solves"],
             "feasible_fraction": st["optimal"] / n, "relaxed_fraction": st["relaxed"] / n,
-            "infeasible_fraction": st["infeasible"] / n, "seidel_fraction": st["seidel"] / n,
+            "infeasible_fraction": st["infeasible"] / n, "binding_fraction": st["binding"] / n,
+            "seidel_fraction": st["seidel"] / n,
             "max_violation_optimal": st["viol_optimal"],
             "max_violation_original_rows_relaxed": st["viol_original_relaxed"],
             "min_pairwise_distance": None if d2 is None else float(np.sqrt(d2)),
@@ -148,7 +149,7 @@ def bench_lattice(args, ws, rank, local):
     stat = S.stats_summary()
     if ws > 1:
         import torch.distributed as dist
-        keys = ("solves", "optimal", "relaxed", "infeasible", "seidel")
+        keys = ("solves", "optimal", "relaxed", "infeasible", "seidel", "binding")
         c = torch.tensor([stat[k] for k in keys], dtype=torch.float64, device="cuda")
         m = torch.tensor([stat["viol_optimal"], stat["viol_original_relaxed"],
                           -(stat["min_dist2"] if stat["min_dist2"] is not None else np.inf)],

@@ -21,7 +21,7 @@ STATUS_NBR_OVERFLOW = 5
 STATUS_WORKSPACE_ERROR = 6
 # words of a lattice-step statistics slot (include/cbf_amd.h CBF_STAT_*)
 (STAT_SOLVES, STAT_OPTIMAL, STAT_RELAXED, STAT_INFEASIBLE, STAT_SEIDEL, STAT_VIOL_OPTIMAL, STAT_VIOL_ORIGINAL,
- STAT_MIN_DIST2, STAT_ERRORS) = range(9)
+ STAT_MIN_DIST2, STAT_ERRORS, STAT_BINDING) = range(10)
 _DIST_KEY_TOP = 0x7FF0000000000000
 
 
@@ -154,7 +154,8 @@ def decode_stats(words) -> dict:
     w = np.asarray(words).astype(np.int64).view(np.uint64).reshape(64, 16)
     cnt = {k: int(w[:, i].sum()) for k, i in (("solves", STAT_SOLVES), ("optimal", STAT_OPTIMAL),
                                                ("relaxed", STAT_RELAXED), ("infeasible", STAT_INFEASIBLE),
-                                               ("seidel", STAT_SEIDEL), ("errors", STAT_ERRORS))}
+                                               ("seidel", STAT_SEIDEL), ("errors", STAT_ERRORS),
+                                               ("binding", STAT_BINDING))}
     vo = w[:, STAT_VIOL_OPTIMAL].max().reshape(1).view(np.float64)[0]
     vr = w[:, STAT_VIOL_ORIGINAL].max().reshape(1).view(np.float64)[0]
     key = int(w[:, STAT_MIN_DIST2].max())

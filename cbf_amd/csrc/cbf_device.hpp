@@ -438,10 +438,16 @@ __device__ __forceinline__ Sol solve_ego(const KP& P, const Ego& E) {
     return S;
 }
 
-// The common case of solve_ego without the Seidel machinery: after the strip pre-relaxation the
-// origin satisfies every plane, so solve8 would return x = 0 at its first call.  Same arithmetic
-// as solve_ego on that path (bit-identical Sol); returns false when the full solve is needed.
-__device__ __forceinline__ bool solve_easy(const KP& P, const Ego& E, Sol& S) {
+// The common cases of solve_ego without the full Seidel machinery, bit-identical to it.  After the
+// strip pre-relaxation, solve_ego's first solve8 call either finds the origin feasible (no plane
+// violated: x = 0), or meets exactly one violated plane h whose projection p = (b_h / |a_h|^2) a_h
+// is not moved along the line (every earlier plane j with a_j.d != 0 has b_j - a_j.p >= 0, so the
+// 1-D bound search keeps s = 0) and satisfies every plane within tolerance, so that solve8 returns
+// x = p + 0 d there.  Both are decided with solve8's own expressions; anything else (a second
+// event, a bound that moves x, an infeasible prefix, non-finite data) returns false and the caller
+// runs solve_ego.  Measured: 57 % (cfg4) and 89 % (cfg4f) of the QPs the origin does not solve are
+// one such event (tools).
+__device__ __forceinline__ bool solve_fast(const KP& P, const Ego& E, Sol& S) {
     const Box B = box_rhs(P, E);
     const double a0[8] = {1.0, 0.0, -1.0, 0.0, P.n0[0], P.n0[1], P.n0[2], P.n0[3]};
     const double a1[8] = {0.0, 1.0, 0.0, -1.0, P.n1[0], P.n1[1], P.n1[2], P.n1[3]};
@@ -449,7 +455,7 @@ __device__ __forceinline__ bool solve_easy(const KP& P, const Ego& E, Sol& S) {
                    E.bq0, E.bq1, E.bq2, E.bq3};
     const unsigned mask = 0xFu | (E.present << 4);
     int iters = 0;
-    if ((E.present & 9u) == 9u || (E.present & 6u) == 6u) {
+    if ((E.present & 9u) == 9u || (E.present & 6u) == 6u) {  // strip pre-check, as solve_ego
         for (;;) {
             bool dead = false;
             if ((E.present & 9u) == 9u) {
@@ -470,14 +476,46 @@ __device__ __forceinline__ bool solve_easy(const KP& P, const Ego& E, Sol& S) {
             iters++;
         }
     }
-    const double x0 = 0.0, x1 = 0.0;
+    // the first plane violated at the origin (solve8's test at x = 0)
+    int h = -1;
+#pragma unroll
+    for (int j = 7; j >= 0; --j)
+        if (((mask >> j) & 1u) && !((a0[j] * 0.0 + a1[j] * 0.0) - b[j] <= FEAS_TOL * pmax(1.0, fabs(b[j])))) h = j;
+    double x0 = 0.0, x1 = 0.0;
+    if (h >= 0) {
+        double ah0 = 0.0, ah1 = 0.0, bh = 0.0;
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+            if (j == h) {
+                ah0 = a0[j];
+                ah1 = a1[j];
+                bh = b[j];
+            }
+        const double n2 = ah0 * ah0 + ah1 * ah1;
+        if (!(n2 > 0)) return false;
+        const double t = bh / n2;
+        const double p0 = t * ah0, p1 = t * ah1;
+        const double d0 = -ah1, d1 = ah0;
+        bool stay = true;  // the 1-D bound search over planes j < h keeps s = 0
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            if (j >= h || !((mask >> j) & 1u)) continue;
+            const double ad = a0[j] * d0 + a1[j] * d1;
+            const double r = b[j] - (a0[j] * p0 + a1[j] * p1);
+            if ((ad > 0 || ad < 0) && !(r >= 0)) stay = false;
+        }
+        if (!stay) return false;
+        const double s0 = 0.0;
+        x0 = p0 + s0 * d0;
+        x1 = p1 + s0 * d1;
+    }
     bool ok = true;
     double v = 0.0;
 #pragma unroll
-    for (int h = 0; h < 8; ++h)
-        if ((mask >> h) & 1u) {
-            const double d = (a0[h] * x0 + a1[h] * x1) - b[h];
-            ok = ok && (d <= FEAS_TOL * pmax(1.0, fabs(b[h])));
+    for (int j = 0; j < 8; ++j)
+        if ((mask >> j) & 1u) {
+            const double d = (a0[j] * x0 + a1[j] * x1) - b[j];
+            ok = ok && (d <= FEAS_TOL * pmax(1.0, fabs(b[j])));
             if (d > v) v = d;
         }
     if (!ok) return false;

@@ -108,11 +108,11 @@ __device__ __forceinline__ unsigned long long dbits(double v) { return (unsigned
 // viol = violation of the solved rows, vorig = violation of the original rows); d2: smallest
 // neighbour distance^2 of the ego (+inf if none).  Every lane of the wave must call it.
 __device__ __forceinline__ void wave_stats(unsigned long long* __restrict__ st, long wave, bool solved, bool seidel,
-                                           bool fin, int code, double viol, double vorig, double d2) {
+                                           bool fin, int code, bool binding, double viol, double vorig, double d2) {
     const bool opt = fin && code == CBF_STATUS_OPTIMAL, rel = fin && code == CBF_STATUS_RELAXED;
     const bool inf = fin && (code == CBF_STATUS_BOX_INFEASIBLE || code == CBF_STATUS_RELAX_CAP);
     const unsigned long long m_sol = __ballot(solved), m_sei = __ballot(seidel), m_opt = __ballot(opt),
-                             m_rel = __ballot(rel), m_inf = __ballot(inf);
+                             m_rel = __ballot(rel), m_inf = __ballot(inf), m_bnd = __ballot(fin && binding);
     double vo = 0.0, vr = 0.0, dm = INFINITY;
     if (__ballot(opt && viol > 0.0)) vo = wave_max(opt ? viol : 0.0);
     if (__ballot(rel && vorig > 0.0)) vr = wave_max(rel ? vorig : 0.0);
@@ -124,6 +124,7 @@ __device__ __forceinline__ void wave_stats(unsigned long long* __restrict__ st, 
         if (m_rel) atomicAdd(&s[CBF_STAT_RELAXED], (unsigned long long)__popcll(m_rel));
         if (m_inf) atomicAdd(&s[CBF_STAT_INFEASIBLE], (unsigned long long)__popcll(m_inf));
         if (m_sei) atomicAdd(&s[CBF_STAT_SEIDEL], (unsigned long long)__popcll(m_sei));
+        if (m_bnd) atomicAdd(&s[CBF_STAT_BINDING], (unsigned long long)__popcll(m_bnd));
         if (vo > 0.0) atomicMax(&s[CBF_STAT_VIOL_OPTIMAL], dbits(vo));
         if (vr > 0.0) atomicMax(&s[CBF_STAT_VIOL_ORIGINAL], dbits(vr));
         if (dm < INFINITY) atomicMax(&s[CBF_STAT_MIN_DIST2], kDistKeyTop - dbits(dm));
@@ -159,11 +160,12 @@ __device__ __forceinline__ void lattice_error_tail(int W, int row_begin, int row
 // Per-lane status counts and violation maxima of a queue kernel, summed over the wave (every lane
 // of the wave must call it, after its loop).
 __device__ __forceinline__ void wave_stats_counts(unsigned long long* __restrict__ st, long wave, int n_opt, int n_rel,
-                                                  int n_inf, double vo, double vr) {
+                                                  int n_inf, int n_bnd, double vo, double vr) {
     for (int o = 32; o > 0; o >>= 1) {
         n_opt += __shfl_xor(n_opt, o, 64);
         n_rel += __shfl_xor(n_rel, o, 64);
         n_inf += __shfl_xor(n_inf, o, 64);
+        n_bnd += __shfl_xor(n_bnd, o, 64);
     }
     vo = wave_max(vo);
     vr = wave_max(vr);
@@ -172,6 +174,7 @@ __device__ __forceinline__ void wave_stats_counts(unsigned long long* __restrict
         if (n_opt) atomicAdd(&s[CBF_STAT_OPTIMAL], (unsigned long long)n_opt);
         if (n_rel) atomicAdd(&s[CBF_STAT_RELAXED], (unsigned long long)n_rel);
         if (n_inf) atomicAdd(&s[CBF_STAT_INFEASIBLE], (unsigned long long)n_inf);
+        if (n_bnd) atomicAdd(&s[CBF_STAT_BINDING], (unsigned long long)n_bnd);
         if (vo > 0.0) atomicMax(&s[CBF_STAT_VIOL_OPTIMAL], dbits(vo));
         if (vr > 0.0) atomicMax(&s[CBF_STAT_VIOL_ORIGINAL], dbits(vr));
     }

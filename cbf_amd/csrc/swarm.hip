@@ -250,11 +250,12 @@ struct EgoOut {
     int row;          // lattice row
     int nbrs;         // neighbours
     int code;         // final status code (res == 1)
+    bool binding;     // the minimiser is not the origin (res == 1)
     double viol, vorig, d2, ny;
 };
 
-// Tail of the lattice filter for one owned ego whose QP rows are accumulated in E: solve at the
-// origin (solve_easy) or queue to the hard kernel (sub-queue q: header hardq, records qr), clip,
+// Tail of the lattice filter for one owned ego whose QP rows are accumulated in E: solve in place
+// when solve_fast can (origin, or one Seidel event that stays put) or queue to the hard kernel (sub-queue q: header hardq, records qr), clip,
 // Euler, outputs.
 template <bool FZ>
 __device__ __forceinline__ void ego_finish(const KP& P, Ego& E, int W, int row_begin, int r, int c, double T,
@@ -272,7 +273,7 @@ __device__ __forceinline__ void ego_finish(const KP& P, Ego& E, int W, int row_b
         st = CBF_STATUS_IDLE;
     } else {
         Sol S;
-        if (!solve_easy(P, E, S)) {
+        if (!solve_fast(P, E, S)) {
             HardRec& h = qr[subq_append(hardq, q)];
             h.r0 = E.r0;
             h.r1 = E.r1;
@@ -294,6 +295,7 @@ __device__ __forceinline__ void ego_finish(const KP& P, Ego& E, int W, int row_b
         clip_u(P, S, E, ux, uy);
         st = pack_status(S);
         O.code = S.status;
+        O.binding = S.x0 != 0.0 || S.x1 != 0.0;
         O.viol = S.viol;
         O.vorig = S.viol_orig;
     }
@@ -359,10 +361,10 @@ __device__ __forceinline__ void lattice_ego(const KP& P, const CellGrid& G, int 
     ego_finish<FZ>(P, E, W, row_begin, r, c, T, pos_out, u, status, cnt, hardq, q, qr, O);
 }
 
-// K4: one lane per cell-sorted slot; QPs the origin solves (after the strip pre-relaxation) are
-// finished in place, the others are appended with their assembled state to the hard queue: one
-// such lane would otherwise make its whole wave run the Seidel path (and hold the registers for
-// it, 167 VGPRs against 68); K5 solves them.
+// K4: one lane per cell-sorted slot; QPs that solve_fast settles (the origin, or one Seidel event
+// that stays put) are finished in place, the others are appended with their assembled state to
+// the hard queue: one such lane would otherwise make its whole wave run the full Seidel path (and
+// hold the registers for it, ~180 VGPRs against ~75); K5 solves them.
 template <bool FZ>
 __global__ void __launch_bounds__(kBlock) k_lattice_filter(KP P, CellGrid G, int W, int row_begin, int row_end,
                                                            int win_row0, long nwin, long ncell,
@@ -393,6 +395,7 @@ __global__ void __launch_bounds__(kBlock) k_lattice_filter(KP P, CellGrid G, int
     O.row = -1;
     O.nbrs = 0;
     O.code = CBF_STATUS_IDLE;
+    O.binding = false;
     O.viol = O.vorig = 0.0;
     O.d2 = INFINITY;
     if (slot < total) {
@@ -403,7 +406,8 @@ __global__ void __launch_bounds__(kBlock) k_lattice_filter(KP P, CellGrid G, int
     if (stats) {
         const bool counted = O.res != 0 && O.row >= cnt_begin && O.row < cnt_end;
         wave_stats(stats, (long)bx * (kBlock / 64) + (threadIdx.x >> 6), counted && O.nbrs > 0,
-                   counted && O.res == 2, counted && O.res == 1, O.code, O.viol, O.vorig, counted ? O.d2 : INFINITY);
+                   counted && O.res == 2, counted && O.res == 1, O.code, O.binding, O.viol, O.vorig,
+                   counted ? O.d2 : INFINITY);
     }
     if (ext_part) wave_extents(e0, e1, e2, e3, ext_part, (long)bx * (kBlock / 64) + (threadIdx.x >> 6));
 }
@@ -419,7 +423,7 @@ __global__ void __launch_bounds__(64) k_lattice_filter_hard(KP P, int row_begin,
                                                             const HardRec* __restrict__ qrec, long qcap, int cnt_begin,
                                                             int cnt_end) {
     double e0 = INFINITY, e1 = -INFINITY, e2 = -INFINITY, e3 = INFINITY;
-    int n_opt = 0, n_rel = 0, n_inf = 0;
+    int n_opt = 0, n_rel = 0, n_inf = 0, n_bnd = 0;
     double vo = 0.0, vr = 0.0;
     drain_subq(hardq, kHardPerQ, [&](int q, int i) {
         const HardRec& h = qrec[(long)q * qcap + i];
@@ -446,6 +450,7 @@ __global__ void __launch_bounds__(64) k_lattice_filter_hard(KP P, int row_begin,
         if (cnt) cnt[h.k] = E.count;
         ext_accumulate(h.row, row_begin, row_end, guard_rows, pn.y, e0, e1, e2, e3);
         if (h.row >= cnt_begin && h.row < cnt_end) {
+            n_bnd += (S.x0 != 0.0 || S.x1 != 0.0) ? 1 : 0;
             if (S.status == CBF_STATUS_OPTIMAL) {
                 ++n_opt;
                 vo = pmax(vo, S.viol);
@@ -457,7 +462,7 @@ __global__ void __launch_bounds__(64) k_lattice_filter_hard(KP P, int row_begin,
             }
         }
     });
-    if (stats) wave_stats_counts(stats, blockIdx.x, n_opt, n_rel, n_inf, vo, vr);
+    if (stats) wave_stats_counts(stats, blockIdx.x, n_opt, n_rel, n_inf, n_bnd, vo, vr);
     if (ext_part) wave_extents(e0, e1, e2, e3, ext_part, blockIdx.x);
 }
 

@@ -60,11 +60,12 @@ extern "C" {
 #define CBF_STAT_OPTIMAL 1       /* ... with status OPTIMAL (the reference's QP is feasible) */
 #define CBF_STAT_RELAXED 2       /* ... RELAXED (infeasible as posed; the cbf.py:84-87 rule applied) */
 #define CBF_STAT_INFEASIBLE 3    /* ... BOX_INFEASIBLE or RELAX_CAP */
-#define CBF_STAT_SEIDEL 4        /* QPs whose origin was infeasible after the strip pre-relaxation (full solve) */
+#define CBF_STAT_SEIDEL 4        /* QPs queued for the full Seidel solve (neither the origin nor one projection) */
 #define CBF_STAT_VIOL_OPTIMAL 5  /* max row violation over OPTIMAL QPs (bits of a double >= 0) */
 #define CBF_STAT_VIOL_ORIGINAL 6 /* max violation of the ORIGINAL barrier rows over RELAXED QPs (bits) */
 #define CBF_STAT_MIN_DIST2 7     /* 0x7FF0000000000000 - bits(min neighbour distance^2); 0 = no pair */
 #define CBF_STAT_ERRORS 8        /* steps whose cell list was unusable (CBF_STATUS_WORKSPACE_ERROR) */
+#define CBF_STAT_BINDING 9       /* QPs whose minimiser is not the origin (a barrier or box row binds) */
 
 /* ControlBarrierFunction state (cbf.py:6-16) + the callers' dynamics and cull radius. */
 typedef struct cbf_params {

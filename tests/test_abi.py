@@ -103,7 +103,7 @@ def test_decode_stats():
     from cbf_amd import _lib
     w = np.zeros(1024, np.uint64)
     assert _lib.decode_stats(w.view(np.int64)) == {"solves": 0, "optimal": 0, "relaxed": 0, "infeasible": 0,
-                                                   "seidel": 0, "errors": 0, "viol_optimal": 0.0,
+                                                   "seidel": 0, "errors": 0, "binding": 0, "viol_optimal": 0.0,
                                                    "viol_original_relaxed": 0.0, "min_dist2": None}
     s = w.reshape(64, 16)
     s[3, _lib.STAT_SOLVES] = 5
