@@ -33,17 +33,21 @@ def _dist_env():
     return ws, rank, local
 
 
-def load_pmc_traffic(kernels=("k_lattice_filter", "k_lattice_filter_hard")):
-    """HBM bytes per launch of the advance phase (sum over its kernels) from the committed PMC
-    summary (profiles/pmc_summary.json, written by tools/summarize_profile.py), if present."""
-    path = os.path.join(ROOT, "profiles", "pmc_summary.json")
+def load_pmc(config):
+    """This config's section of the committed PMC summary (profiles/pmc_summary.json, written by
+    tools/summarize_profile.py from tools/profile.sh runs), or {}."""
     try:
-        with open(path) as f:
-            d = json.load(f)
-        vals = [d.get(k, {}).get("hbm_bytes_per_launch") for k in kernels]
-        return None if any(v is None for v in vals) else float(sum(vals))
-    except (OSError, ValueError):
-        return None
+        with open(os.path.join(ROOT, "profiles", "pmc_summary.json")) as f:
+            return json.load(f).get(config, {})
+    except (OSError, ValueError, AttributeError):
+        return {}
+
+
+def load_pmc_traffic(config, kernels=("k_lattice_filter", "k_lattice_filter_hard")):
+    """HBM bytes per launch of the advance phase (sum over its kernels) for this config, if profiled."""
+    d = load_pmc(config)
+    vals = [d.get(k, {}).get("hbm_bytes_per_launch") for k in kernels]
+    return None if any(v is None for v in vals) else float(sum(vals))
 
 
 def cpu_baseline_lattice(W, H, seed, budget_s, spacing, gain, procs=None):
@@ -176,8 +180,8 @@ def bench_lattice(args, ws, rank, local):
     codes = np.bincount(status & 0xFF, minlength=5)
     check = full_size_check(S, args) if (ws == 1 and not args.shard and args.barrier == "reference") else None
     achieved = FILTER_BYTES_PER_AGENT * n_local / (k_ms * 1e-3) / 1e9
-    traffic = load_pmc_traffic() if args.barrier == "reference" else \
-        load_pmc_traffic(("k_lattice_filter_hocbf", "k_lattice_filter_hocbf_wide"))
+    traffic = load_pmc_traffic(args.config) if args.barrier == "reference" else \
+        load_pmc_traffic(args.config + "_hocbf", ("k_lattice_filter_hocbf", "k_lattice_filter_hocbf_wide"))
     res = {
         "metric": METRIC,
         "value": solves / elapsed,
@@ -259,56 +263,64 @@ def bench_allpairs(args, ws, rank, local):
 
 
 def bench_mc(args, ws, rank, local):
-    """cfg5: batched Monte-Carlo rendezvous, scenarios sharded across ranks (strong scaling),
-    counters combined with one all_reduce at the end."""
+    """cfg5: batched Monte-Carlo rendezvous, scenarios sharded across ranks (strong scaling: the
+    100k-scenario batch is split), no per-step traffic, totals combined by all-reduces at the end
+    (cbf_amd/montecarlo.py)."""
     import torch
-    from cbf_amd import scenarios, swarm
-    n_o = n_a = 16
-    per = (args.mc_scenarios + ws - 1) // ws
-    lo = rank * per
-    hi = min(args.mc_scenarios, lo + per)
-    pos0 = scenarios.mc_scenarios(args.mc_scenarios, n_o, n_a, seed=args.seed)[lo:hi]
-    P = torch.tensor(pos0, device="cuda")
-    fp = swarm.FilterParams()
-    tot = torch.zeros(4, dtype=torch.int64, device="cuda")
-    mv = torch.zeros(1, dtype=torch.float64, device="cuda")
-    for _ in range(max(1, args.warmup)):  # the same ops as a timed step (loads torch's kernels too)
-        cnt, m = swarm.mc_rollout(fp, P, n_o, n_a, args.mc_inner, ga=scenarios.MC_GAIN)
-        tot += cnt.sum(0)
-        mv = torch.maximum(mv, m.max().reshape(1))
-    tot.zero_()
-    mv.zero_()
+    from cbf_amd.montecarlo import MonteCarlo
+    mc = MonteCarlo(args.mc_scenarios, 16, 16, seed=args.seed)
+    for _ in range(max(1, args.warmup)):  # the same launches as a timed step
+        mc.run(args.mc_inner)
+    torch.cuda.synchronize()
+    mc.reset_totals()
     if ws > 1:
         torch.distributed.barrier()
     torch.cuda.synchronize()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
+    ev0.record()
     for _ in range(args.steps):
-        cnt, m = swarm.mc_rollout(fp, P, n_o, n_a, args.mc_inner, ga=scenarios.MC_GAIN)
-        tot += cnt.sum(0)
-        mv = torch.maximum(mv, m.max().reshape(1))
+        mc.run(args.mc_inner)
+    ev1.record()
     torch.cuda.synchronize()
     if ws > 1:
         torch.distributed.barrier()
     elapsed = time.perf_counter() - t0
-    if ws > 1:
-        torch.distributed.all_reduce(tot)
-        torch.distributed.all_reduce(mv, op=torch.distributed.ReduceOp.MAX)
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
-        elapsed = float(t[0])
-    c = tot.cpu().numpy()
-    return {"metric": METRIC, "value": c[0] / elapsed, "unit": "agent-QP solves/s", "n_gpus": ws,
+    kernel_ms = ev0.elapsed_time(ev1) / args.steps
+    elapsed, _ = _reduce(elapsed, 0, ws)
+    tot = mc.totals()
+    scen_steps = args.mc_scenarios * args.mc_inner * args.steps
+    return {"metric": METRIC, "value": tot["calls"] / elapsed, "unit": "agent-QP solves/s", "n_gpus": ws,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
             "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f64",
             "data": "synthetic",
             "config": {"workload": f"cfg5: {args.mc_scenarios} independent 16+16 rendezvous scenarios, "
                                    f"{args.mc_inner} timesteps per step, scenario-sharded",
                        "parallelism": f"scenario shards x{ws}" if ws > 1 else "single GPU"},
-            "scenario_timesteps_per_s": args.mc_scenarios * args.mc_inner * args.steps / elapsed,
-            "relaxed_fraction": c[1] / max(c[0], 1), "box_infeasible": int(c[2]), "relax_cap": int(c[3]),
-            "max_violation": float(mv.item()),
-            "roofline": {"bound": "valu-fp64", "achieved": None, "peak": 78.6, "unit": "TFLOP/s", "frac": None,
-                         "traffic": None, "note": "state lives in LDS for the whole rollout; no HBM traffic per step"}}
+            "scenario_timesteps_per_s": scen_steps / elapsed,
+            "feasible_fraction": tot["feasible_fraction"],
+            "safety": {"solves": tot["calls"], "feasible_fraction": tot["feasible_fraction"],
+                       "relaxed_fraction": tot["relaxed"] / max(tot["calls"], 1),
+                       "box_infeasible": tot["box_infeasible"], "relax_cap": tot["relax_cap"],
+                       "max_violation_optimal": tot["max_violation_optimal"],
+                       "max_violation_original_rows_relaxed": tot["max_violation_original_rows_relaxed"],
+                       "min_pairwise_distance": tot["min_pairwise_distance"]},
+            "roofline": mc_roofline(kernel_ms, args.mc_scenarios // ws, args.mc_inner)}
+
+
+def mc_roofline(kernel_ms, n_scen, inner):
+    """cfg5's kernel keeps every scenario in LDS for the whole rollout (no HBM traffic per step), so
+    its bound is the VALU: the VALU busy fraction of k_mc_rollout from the committed rocprof
+    counters (profiles/pmc_summary.json "cfg5", tools/summarize_profile.py: SQ_ACTIVE_INST_VALU x 4 /
+    (SIMDs x GRBM_GUI_ACTIVE)), measured on the same launch shape."""
+    e = load_pmc("cfg5").get("k_mc_rollout", {})
+    out = {"bound": "valu", "unit": "fraction of VALU issue cycles", "peak": 1.0, "kernel": "k_mc_rollout",
+           "kernel_ms": kernel_ms, "traffic": None}
+    busy = e.get("valu_busy")
+    out.update(achieved=busy, frac=busy,
+               source="profiles/pmc_summary.json cfg5 (rocprofv3 --pmc, tools/profile.sh)" if busy is not None
+               else "not profiled")
+    return out
 
 
 def cert_scenarios(B, N, seed=0):

@@ -1,7 +1,8 @@
 """Build libcbf_amd.so (hand-written HIP for gfx950) in-tree with hipcc.
 
-No torch extension: the product boundary is a plain C ABI (include/cbf_amd.h) that Python
-reaches through ctypes with device pointers from torch tensors.
+The product boundary is a plain C ABI (include/cbf_amd.h): non-torch callers bind it directly
+(ctypes, cgo, ...); cbf_amd/_lib.py uses ctypes, and the thin PyTorch-ROCm extension
+(csrc/torch_ops.cpp -> libcbf_amd_torch.so) registers torch.ops.cbf_amd.* over it.
 """
 from __future__ import annotations
 
@@ -49,6 +50,32 @@ def build(verbose: bool = False) -> str:
     if verbose:
         print(f"built {LIB}")
     return LIB
+
+
+TORCH_SRC = os.path.join(CSRC, "torch_ops.cpp")
+TORCH_LIB = os.path.join(PKG, "libcbf_amd_torch.so")
+
+
+def build_torch_ops(verbose: bool = False) -> str:
+    """The thin PyTorch-ROCm extension (torch.ops.cbf_amd.*, csrc/torch_ops.cpp): host C++ over the
+    C ABI, linked against libcbf_amd.so (rpath $ORIGIN) and torch's own libraries, built in-tree."""
+    import torch
+    from torch.utils import cpp_extension as ce
+    deps = [TORCH_SRC, os.path.join(ROOT, "include", "cbf_amd.h"), LIB]
+    if os.path.exists(TORCH_LIB) and os.path.getmtime(TORCH_LIB) >= max(os.path.getmtime(d) for d in deps):
+        return TORCH_LIB
+    tlib = os.path.join(os.path.dirname(torch.__file__), "lib")
+    abi = int(torch._C._GLIBCXX_USE_CXX11_ABI)
+    cmd = (["g++", "-O2", "-std=c++17", "-fPIC", "-shared", TORCH_SRC, "-o", TORCH_LIB, "-I", os.path.join(ROOT, "include"),
+            f"-D_GLIBCXX_USE_CXX11_ABI={abi}", "-D__HIP_PLATFORM_AMD__=1", "-DUSE_ROCM=1",
+            "-DTORCH_EXTENSION_NAME=cbf_amd_torch", "-Wno-deprecated-declarations"] +
+           [f"-I{p}" for p in ce.include_paths("cuda")] +
+           ["-L", tlib, "-lc10", "-lc10_hip", "-ltorch_cpu", "-ltorch", f"-Wl,-rpath,{tlib}",
+            "-L", PKG, "-lcbf_amd", "-Wl,-rpath,$ORIGIN"])
+    subprocess.run(cmd, check=True)
+    if verbose:
+        print(f"built {TORCH_LIB}")
+    return TORCH_LIB
 
 
 # Test-only builds of the library with a compile switch flipped in some sources (never loaded by

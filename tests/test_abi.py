@@ -142,3 +142,19 @@ def test_product_path_has_no_cpu_fallback():
         with pytest.raises(cbf_amd.CbfError):
             cbf_amd.ControlBarrierFunction(15).get_safe_control(np.zeros(4), np.zeros((1, 4)), np.zeros((4, 4)),
                                                                 0.1 * np.eye(4, 2), [0.0, 0.0])
+
+
+def test_torch_extension_registers_ops():
+    """The thin PyTorch-ROCm extension (torch.ops.cbf_amd, csrc/torch_ops.cpp) loads, exposes the
+    reference call surface over the C ABI, and has no CPU kernels (no fallback)."""
+    import torch
+    from cbf_amd import _lib, swarm, torch_ops
+    o = torch_ops.ops()
+    for name in ("get_safe_control_batch", "filter_swarm", "lattice_step", "lattice_workspace_size", "abi_version"):
+        assert hasattr(o, name), name
+    assert o.abi_version() == _lib.ABI_VERSION
+    g = swarm.make_grid(-1.0, -1.0, 20.0, 30.0, 0.204)
+    assert o.lattice_workspace_size(96, 128, g.x0, g.y0, 1 / g.inv_h, g.nx, g.ny) == \
+        _lib.lib.cbf_lattice_workspace_size(96, 128, C.byref(g))
+    with pytest.raises((NotImplementedError, RuntimeError)):
+        o.filter_swarm(torch.zeros(4, 2, dtype=torch.float64), torch.zeros(4, 2, dtype=torch.float64), 0, 15.0)
