@@ -133,6 +133,41 @@ __device__ __forceinline__ double row_b(const KP& P, const Ego& E, double o0, do
     return (P.gamma * (H - P.dmin) + Lf) + c;
 }
 
+// row_b's quadrant term c (the g(x) u0 part of cbf.py:55-59) for sign quadrant q, same expression.
+__device__ __forceinline__ double quad_c(const KP& P, const Ego& E, int q) {
+    const double sx = (q & 1) ? -1.0 : 1.0, sy = (q & 2) ? -1.0 : 1.0;
+    const double ksx = P.k * sx, ksy = P.k * sy;
+    return fma(ksy, E.gu3, fma(ksx, E.gu2, fma(sy, E.gu1, sx * E.gu0)));
+}
+
+// row_b without the quadrant term c, for a neighbour whose position differs from the ego's
+// ((d0, d1) != 0; every agent hit has s > 0): gamma (H - dmin) [+ L_f], so that row_b =
+// row_g + c.  Bit for bit row_b's H: with s = sign(d), s d0 = |d0| up to the sign of a zero, and
+// a zero's sign cannot reach |d0| + |d1| once either is nonzero; k s is k or -k exactly.  The
+// per-quadrant minimum can then be taken over row_g and c added once per quadrant: x -> x + c
+// rounds monotonically, so min_j (g_j + c) = (min_j g_j) + c exactly whenever c is finite (the
+// caller checks that; a NaN g_j is skipped by both minima).
+template <bool FZ = false>
+__device__ __forceinline__ double row_g(const KP& P, const Ego& E, double o0, double o1, double o2, double o3,
+                                        int& q) {
+    const double d0 = E.r0 - o0, d1 = E.r1 - o1, d2 = E.r2 - o2, d3 = E.r3 - o3;
+    const bool nx = d0 < 0, ny = d1 < 0;
+    const double ksx = nx ? -P.k : P.k, ksy = ny ? -P.k : P.k;
+    const double H = fma(ksy, d3, fma(ksx, d2, fabs(d0) + fabs(d1)));
+    q = (nx ? 1 : 0) | (ny ? 2 : 0);
+    if (FZ) return P.gamma * (H - P.dmin);
+    double Lf = 0.0;
+    if (!P.f_zero) {
+        const double sx = nx ? -1.0 : 1.0, sy = ny ? -1.0 : 1.0;
+        double fd[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+            fd[i] = ((P.f[4 * i] * d0 + P.f[4 * i + 1] * d1) + P.f[4 * i + 2] * d2) + P.f[4 * i + 3] * d3;
+        Lf = fma(ksy, fd[3], fma(ksx, fd[2], fma(sy, fd[1], sx * fd[0])));
+    }
+    return P.gamma * (H - P.dmin) + Lf;
+}
+
 template <bool FZ = false>
 __device__ __forceinline__ void ego_add(const KP& P, Ego& E, double o0, double o1, double o2, double o3) {
     int q;
@@ -152,6 +187,12 @@ __device__ __forceinline__ void ego_add(const KP& P, Ego& E, double o0, double o
 #ifndef CBF_HIT_CAP
 #define CBF_HIT_CAP 16
 #endif
+// Slot t of a cell-sorted array through a 32-bit byte offset from the (uniform) base: one address
+// instruction per load instead of a 64-bit multiply-add.  The lattice entry points bound windows
+// to < 2^28 slots (check_lattice), so 16 t fits in 32 bits.
+__device__ __forceinline__ double2 ld_slot(const double2* __restrict__ a, int t) {
+    return *reinterpret_cast<const double2*>(reinterpret_cast<const char*>(a) + ((uint32_t)t << 4));
+}
 constexpr int kHitCap = CBF_HIT_CAP;
 struct HitList {
     int n = 0;
@@ -160,11 +201,12 @@ struct HitList {
         ++n;
     }
     __device__ __forceinline__ bool overflowed() const { return n > kHitCap; }
-    // flush into the per-quadrant minima kept in LDS (bq[q * kBlock + lane], preset to +inf by
-    // the caller and read back into E after): one read-compare-write per hit instead of four
-    // register compare-selects; same rows, same minimum
+    // flush into the per-quadrant minima of row_g kept in LDS (gq[q * kBlock + lane], preset to
+    // +inf by the caller, which adds the quadrant terms c after): one read-compare-write per hit
+    // instead of four register compare-selects; same rows, same minimum (row_g).  Agent hits only
+    // (s > 0).
     template <bool FZ = false>
-    __device__ __forceinline__ void flush_bq(const int* lds, double* bq, const KP& P, Ego& E,
+    __device__ __forceinline__ void flush_gq(const int* lds, double* gq, const KP& P, Ego& E,
                                              const double2* __restrict__ pos, const double2* __restrict__ vel) {
         for (int i = 0; i < n; i += CBF_FLUSH_U) {
             double2 pj[CBF_FLUSH_U], vj[CBF_FLUSH_U];
@@ -172,23 +214,23 @@ struct HitList {
             for (int q = 0; q < CBF_FLUSH_U; ++q) {
                 if (i + q < n) {
                     const int t = lds[(i + q) * kBlock + threadIdx.x];
-                    pj[q] = pos[t];
-                    vj[q] = vel[t];
+                    pj[q] = ld_slot(pos, t);
+                    vj[q] = ld_slot(vel, t);
                 }
             }
 #pragma unroll
             for (int q = 0; q < CBF_FLUSH_U; ++q) {
                 if (i + q < n) {
                     int qd;
-                    const double b = row_b<FZ>(P, E, pj[q].x, pj[q].y, vj[q].x, vj[q].y, qd);
-                    double* slot = bq + qd * kBlock + threadIdx.x;
+                    const double g = row_g<FZ>(P, E, pj[q].x, pj[q].y, vj[q].x, vj[q].y, qd);
+                    double* slot = gq + qd * kBlock + threadIdx.x;
                     const double cur = *slot;
-                    *slot = (b < cur) ? b : cur;
+                    *slot = (g < cur) ? g : cur;
                     E.present |= 1u << qd;
-                    E.count++;
                 }
             }
         }
+        E.count += n;
         n = 0;
     }
 };
@@ -209,7 +251,7 @@ __device__ __forceinline__ void scan_rows_joint(const int (&t0)[3], const int (&
         for (int q = 0; q < CBF_SCAN_U; ++q) {
             const int vv = v + q;
             tt[q] = vv < l0 ? t0[0] + vv : (vv < l01 ? t0[1] + (vv - l0) : t0[2] + (vv - l01));
-            if (vv < L) p[q] = spos[tt[q]];
+            if (vv < L) p[q] = ld_slot(spos, tt[q]);
         }
 #pragma unroll
         for (int q = 0; q < CBF_SCAN_U; ++q) {
@@ -476,13 +518,27 @@ __device__ __forceinline__ bool solve_fast(const KP& P, const Ego& E, Sol& S) {
             iters++;
         }
     }
-    // the first plane violated at the origin (solve8's test at x = 0)
+    // the first plane violated at the origin (solve8's test at x = 0), and the origin's violation
     int h = -1;
+    double v0 = 0.0;
 #pragma unroll
     for (int j = 7; j >= 0; --j)
-        if (((mask >> j) & 1u) && !((a0[j] * 0.0 + a1[j] * 0.0) - b[j] <= FEAS_TOL * pmax(1.0, fabs(b[j])))) h = j;
+        if ((mask >> j) & 1u) {
+            const double d = (a0[j] * 0.0 + a1[j] * 0.0) - b[j];
+            if (!(d <= FEAS_TOL * pmax(1.0, fabs(b[j])))) h = j;
+            if (d > v0) v0 = d;
+        }
+    if (h < 0) {  // solve8 returns the origin; the final check below would repeat the test above
+        S.x0 = 0.0;
+        S.x1 = 0.0;
+        S.iters = iters;
+        S.status = iters > 0 ? CBF_STATUS_RELAXED : CBF_STATUS_OPTIMAL;
+        S.viol = v0;
+        S.viol_orig = iters > 0 ? orig_violation(P, E, B, 0.0, 0.0) : v0;
+        return true;
+    }
     double x0 = 0.0, x1 = 0.0;
-    if (h >= 0) {
+    {
         double ah0 = 0.0, ah1 = 0.0, bh = 0.0;
 #pragma unroll
         for (int j = 0; j < 8; ++j)

@@ -58,6 +58,39 @@ __device__ __forceinline__ void ext_accumulate(int r, int row_begin, int row_end
     if (r >= row_begin + guard_rows) e3 = pmin(e3, ny);
 }
 
+// The row tests of the reference-barrier lattice filter as bounds on the window index
+// w = (r - win_row0) W + c (0 <= c < W): r < X <=> w < (X - win_row0) W and r >= Y <=>
+// w >= (Y - win_row0) W, so the kernels never divide by W.
+struct WinBounds {
+    int own_lo, own_hi;  // owned rows [row_begin, row_end); output index k = w - own_lo
+    int cnt_lo, cnt_hi;  // rows whose solves are counted
+    int g_hi;            // rows < row_end - guard_rows (halo-guard extents)
+    int g_lo;            // rows >= row_begin + guard_rows
+};
+inline int win_bound(long row, int win_row0, int W, long nwin) {
+    const long v = (row - win_row0) * (long)W;  // clamped to [-1, nwin + 1]: same answers for w in [0, nwin)
+    return (int)(v < -1 ? -1 : (v > nwin + 1 ? nwin + 1 : v));
+}
+inline WinBounds make_win_bounds(int W, int win_row0, long nwin, int row_begin, int row_end, int cnt_begin,
+                                 int cnt_end, int guard_rows) {
+    WinBounds B;
+    B.own_lo = win_bound(row_begin, win_row0, W, nwin);
+    B.own_hi = win_bound(row_end, win_row0, W, nwin);
+    B.cnt_lo = win_bound(cnt_begin, win_row0, W, nwin);
+    B.cnt_hi = win_bound(cnt_end, win_row0, W, nwin);
+    B.g_hi = win_bound((long)row_end - guard_rows, win_row0, W, nwin);
+    B.g_lo = win_bound((long)row_begin + guard_rows, win_row0, W, nwin);
+    return B;
+}
+// ext_accumulate for an owned agent given by its window index
+__device__ __forceinline__ void ext_accumulate_w(int w, const WinBounds& B, double ny, double& e0, double& e1,
+                                                 double& e2, double& e3) {
+    e0 = pmin(e0, ny);
+    e1 = pmax(e1, ny);
+    if (w < B.g_hi) e2 = pmax(e2, ny);
+    if (w >= B.g_lo) e3 = pmin(e3, ny);
+}
+
 // This lane's entry in sub-queue q (length at hardq[32 (1 + q)]); every active lane of the wave
 // that calls it appends one entry, with one atomic per wave.
 __device__ __forceinline__ int subq_append(int32_t* hardq, int q) {
@@ -103,20 +136,44 @@ constexpr unsigned long long kDistKeyTop = 0x7FF0000000000000ull;
 
 __device__ __forceinline__ unsigned long long dbits(double v) { return (unsigned long long)__double_as_longlong(v); }
 
+}  // namespace cbf
+extern "C" __device__ __attribute__((const)) unsigned int __ockl_wfred_max_u32(unsigned int);
+extern "C" __device__ __attribute__((const)) unsigned int __ockl_wfred_min_u32(unsigned int);
+namespace cbf {
+
+// Wave-wide max / min of 64-bit keys as two 32-bit DPP reductions (high words, then the low words
+// of the lanes holding the extreme high word): about half the instructions of a 64-bit shuffle
+// tree.  Every lane of the wave must call them; all lanes get the result.
+__device__ __forceinline__ unsigned long long wave_umax64(unsigned long long v) {
+    const unsigned hi = (unsigned)(v >> 32);
+    const unsigned mh = __ockl_wfred_max_u32(hi);
+    const unsigned ml = __ockl_wfred_max_u32(hi == mh ? (unsigned)v : 0u);
+    return ((unsigned long long)mh << 32) | ml;
+}
+__device__ __forceinline__ unsigned long long wave_umin64(unsigned long long v) {
+    const unsigned hi = (unsigned)(v >> 32);
+    const unsigned mh = __ockl_wfred_min_u32(hi);
+    const unsigned ml = __ockl_wfred_min_u32(hi == mh ? (unsigned)v : 0xFFFFFFFFu);
+    return ((unsigned long long)mh << 32) | ml;
+}
+
 // One wave's contribution.  solved: an agent-QP ran for this lane's ego (>= 1 neighbour);
 // seidel: its QP went to the full solve (queued); fin: its status code is final here (code,
 // viol = violation of the solved rows, vorig = violation of the original rows); d2: smallest
-// neighbour distance^2 of the ego (+inf if none).  Every lane of the wave must call it.
+// neighbour distance^2 of the ego (+inf if none).  Every lane of the wave must call it.  The
+// maxima and the minimum are taken over the bits of the non-negative doubles (only values > 0 enter
+// the maxima), which order like the values.
 __device__ __forceinline__ void wave_stats(unsigned long long* __restrict__ st, long wave, bool solved, bool seidel,
                                            bool fin, int code, bool binding, double viol, double vorig, double d2) {
     const bool opt = fin && code == CBF_STATUS_OPTIMAL, rel = fin && code == CBF_STATUS_RELAXED;
     const bool inf = fin && (code == CBF_STATUS_BOX_INFEASIBLE || code == CBF_STATUS_RELAX_CAP);
     const unsigned long long m_sol = __ballot(solved), m_sei = __ballot(seidel), m_opt = __ballot(opt),
                              m_rel = __ballot(rel), m_inf = __ballot(inf), m_bnd = __ballot(fin && binding);
-    double vo = 0.0, vr = 0.0, dm = INFINITY;
-    if (__ballot(opt && viol > 0.0)) vo = wave_max(opt ? viol : 0.0);
-    if (__ballot(rel && vorig > 0.0)) vr = wave_max(rel ? vorig : 0.0);
-    if (__ballot(d2 < INFINITY)) dm = wave_min(d2);
+    const bool po = opt && viol > 0.0, pr = rel && vorig > 0.0, pd = d2 < INFINITY;
+    unsigned long long vo = 0, vr = 0, dm = 0;
+    if (__ballot(po)) vo = wave_umax64(po ? dbits(viol) : 0ull);
+    if (__ballot(pr)) vr = wave_umax64(pr ? dbits(vorig) : 0ull);
+    if (__ballot(pd)) dm = kDistKeyTop - wave_umin64(pd ? dbits(d2) : kDistKeyTop);
     if ((threadIdx.x & 63) == 0) {
         unsigned long long* s = st + 16 * (wave & 63);
         if (m_sol) atomicAdd(&s[CBF_STAT_SOLVES], (unsigned long long)__popcll(m_sol));
@@ -125,9 +182,9 @@ __device__ __forceinline__ void wave_stats(unsigned long long* __restrict__ st, 
         if (m_inf) atomicAdd(&s[CBF_STAT_INFEASIBLE], (unsigned long long)__popcll(m_inf));
         if (m_sei) atomicAdd(&s[CBF_STAT_SEIDEL], (unsigned long long)__popcll(m_sei));
         if (m_bnd) atomicAdd(&s[CBF_STAT_BINDING], (unsigned long long)__popcll(m_bnd));
-        if (vo > 0.0) atomicMax(&s[CBF_STAT_VIOL_OPTIMAL], dbits(vo));
-        if (vr > 0.0) atomicMax(&s[CBF_STAT_VIOL_ORIGINAL], dbits(vr));
-        if (dm < INFINITY) atomicMax(&s[CBF_STAT_MIN_DIST2], kDistKeyTop - dbits(dm));
+        if (vo) atomicMax(&s[CBF_STAT_VIOL_OPTIMAL], vo);
+        if (vr) atomicMax(&s[CBF_STAT_VIOL_ORIGINAL], vr);
+        if (dm) atomicMax(&s[CBF_STAT_MIN_DIST2], dm);
     }
 }
 
@@ -210,7 +267,7 @@ inline int check_lattice(const cbf_params* p, const cbf_grid* grid, int32_t W, i
     // owned rows plus one neighbour row on each side (where it exists) must be in the window
     if (win_row0 > (row_begin > 0 ? row_begin - 1 : 0)) return CBF_EINVAL;
     if (win_row0 + win_rows < (row_end < H ? row_end + 1 : H)) return CBF_EINVAL;
-    if ((long)W * win_rows >= (1l << 31)) return CBF_EINVAL;
+    if ((long)W * win_rows >= (1l << 28)) return CBF_EINVAL;  // 32-bit byte offsets into the sorted copies (ld_slot)
     if (!pos || !workspace) return CBF_EINVAL;
     if (grid->nx <= 0 || grid->ny <= 0 || !(grid->inv_h > 0) || !(1.0 / grid->inv_h >= sqrt(p->cull_t)))
         return CBF_EINVAL;

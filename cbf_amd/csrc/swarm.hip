@@ -247,23 +247,22 @@ __global__ void __launch_bounds__(kBlock) k_lattice_scatter_ordered(long nwin, c
 // Per-ego outcome of the lattice filter for the statistics.
 struct EgoOut {
     int res;          // 0 not an owned ego, 1 done (outputs written), 2 queued for the full solve
-    int row;          // lattice row
+    int w;            // window index of the agent
     int nbrs;         // neighbours
     int code;         // final status code (res == 1)
     bool binding;     // the minimiser is not the origin (res == 1)
     double viol, vorig, d2, ny;
 };
 
-// Tail of the lattice filter for one owned ego whose QP rows are accumulated in E: solve in place
-// when solve_fast can (origin, or one Seidel event that stays put) or queue to the hard kernel (sub-queue q: header hardq, records qr), clip,
-// Euler, outputs.
+// Tail of the lattice filter for one owned ego (output index k) whose QP rows are accumulated in
+// E: solve in place when solve_fast can (origin, or one Seidel event that stays put) or queue to
+// the hard kernel (sub-queue q: header hardq, records qr), clip, Euler, outputs.
 template <bool FZ>
-__device__ __forceinline__ void ego_finish(const KP& P, Ego& E, int W, int row_begin, int r, int c, double T,
+__device__ __forceinline__ void ego_finish(const KP& P, Ego& E, int w, int k, double T,
                                            double2* __restrict__ pos_out, double2* __restrict__ u,
                                            int32_t* __restrict__ status, int32_t* __restrict__ cnt,
                                            int32_t* __restrict__ hardq, int q, HardRec* __restrict__ qr,
                                            EgoOut& O) {
-    const long k = (long)(r - row_begin) * W + c;
     double ux, uy;
     int32_t st;
     O.code = CBF_STATUS_IDLE;
@@ -287,8 +286,8 @@ __device__ __forceinline__ void ego_finish(const KP& P, Ego& E, int W, int row_b
             h.bq3 = E.bq3;
             h.present = (int)E.present;
             h.count = E.count;
-            h.k = (int)k;
-            h.row = r;
+            h.k = k;
+            h.row = w;
             O.res = 2;
             return;
         }
@@ -311,21 +310,21 @@ __device__ __forceinline__ void ego_finish(const KP& P, Ego& E, int W, int row_b
 // Lattice step K4 for one cell-sorted slot: 3x3-cell cull (the three cell rows scanned as one
 // sequence, hits compacted into the lane's LDS column), row assembly for the hits only (so
 // divergent lanes do not pay assembly for every candidate iteration of the wave), then the tail.
+// Rows are assembled as row_g and the quadrant terms added per quadrant (row_g's note); an ego
+// whose quadrant terms are not all finite, or whose hit list overflowed, is assembled row by row
+// with row_b (scan_range_direct).
 template <bool FZ>
-__device__ __forceinline__ void lattice_ego(const KP& P, const CellGrid& G, int W, int row_begin, int row_end,
-                                            int win_row0, int slot, const double2* __restrict__ spos,
-                                            const double2* __restrict__ svel, const int32_t* __restrict__ sidx,
-                                            const int32_t* __restrict__ start, double T,
-                                            double2* __restrict__ pos_out, double2* __restrict__ u,
+__device__ __forceinline__ void lattice_ego(const KP& P, const CellGrid& G, const WinBounds& B, int slot,
+                                            const double2* __restrict__ spos, const double2* __restrict__ svel,
+                                            const int32_t* __restrict__ sidx, const int32_t* __restrict__ start,
+                                            double T, double2* __restrict__ pos_out, double2* __restrict__ u,
                                             int32_t* __restrict__ status, int32_t* __restrict__ cnt,
                                             int32_t* __restrict__ hardq, int q, HardRec* __restrict__ qr,
                                             int* hit_lds, EgoOut& O) {
     const int w = sidx[slot];
-    const int r = win_row0 + w / W;
-    const int c = w % W;
-    O.row = r;
-    if (!(r >= row_begin && r < row_end)) return;
-    const double2 pe = spos[slot], ve = svel[slot];
+    O.w = w;
+    if (!(w >= B.own_lo && w < B.own_hi)) return;
+    const double2 pe = ld_slot(spos, slot), ve = ld_slot(svel, slot);
     Ego E;
     ego_init(P, E, pe.x, pe.y, ve.x, ve.y, ve.x, ve.y);
     const int cx = cell_coord(pe.x, G.x0, G.inv_h, G.nx);
@@ -343,22 +342,23 @@ __device__ __forceinline__ void lattice_ego(const KP& P, const CellGrid& G, int 
     HitList Hl;
     double d2 = INFINITY;
     scan_rows_joint(rt0, rt1, P, E, Hl, hit_lds, spos, d2);
-    if (!Hl.overflowed()) {
-        double* bq = reinterpret_cast<double*>(hit_lds + kHitCap * kBlock);
+    const double c0 = quad_c(P, E, 0), c1 = quad_c(P, E, 1), c2 = quad_c(P, E, 2), c3 = quad_c(P, E, 3);
+    if (!Hl.overflowed() && isfinite(c0) && isfinite(c1) && isfinite(c2) && isfinite(c3)) {
+        double* gq = reinterpret_cast<double*>(hit_lds + kHitCap * kBlock);
 #pragma unroll
-        for (int q = 0; q < 4; ++q) bq[q * kBlock + threadIdx.x] = INFINITY;
-        Hl.template flush_bq<FZ>(hit_lds, bq, P, E, spos, svel);
-        E.bq0 = bq[threadIdx.x];
-        E.bq1 = bq[kBlock + threadIdx.x];
-        E.bq2 = bq[2 * kBlock + threadIdx.x];
-        E.bq3 = bq[3 * kBlock + threadIdx.x];
+        for (int k = 0; k < 4; ++k) gq[k * kBlock + threadIdx.x] = INFINITY;
+        Hl.template flush_gq<FZ>(hit_lds, gq, P, E, spos, svel);
+        E.bq0 = gq[threadIdx.x] + c0;
+        E.bq1 = gq[kBlock + threadIdx.x] + c1;
+        E.bq2 = gq[2 * kBlock + threadIdx.x] + c2;
+        E.bq3 = gq[3 * kBlock + threadIdx.x] + c3;
     } else {
 #pragma unroll
         for (int k = 0; k < 3; ++k) scan_range_direct<FZ>(rt0[k], rt1[k], P, E, spos, svel);
     }
     O.nbrs = E.count;
     O.d2 = d2;
-    ego_finish<FZ>(P, E, W, row_begin, r, c, T, pos_out, u, status, cnt, hardq, q, qr, O);
+    ego_finish<FZ>(P, E, w, w - B.own_lo, T, pos_out, u, status, cnt, hardq, q, qr, O);
 }
 
 // K4: one lane per cell-sorted slot; QPs that solve_fast settles (the origin, or one Seidel event
@@ -366,8 +366,8 @@ __device__ __forceinline__ void lattice_ego(const KP& P, const CellGrid& G, int 
 // the hard queue: one such lane would otherwise make its whole wave run the full Seidel path (and
 // hold the registers for it, ~180 VGPRs against ~75); K5 solves them.
 template <bool FZ>
-__global__ void __launch_bounds__(kBlock) k_lattice_filter(KP P, CellGrid G, int W, int row_begin, int row_end,
-                                                           int win_row0, long nwin, long ncell,
+__global__ void __launch_bounds__(kBlock) k_lattice_filter(KP P, CellGrid G, WinBounds B, int W, int row_begin,
+                                                           int row_end, int win_row0, long nwin, long ncell,
                                                            const double2* __restrict__ spos,
                                                            const double2* __restrict__ svel,
                                                            const int32_t* __restrict__ sidx,
@@ -375,10 +375,10 @@ __global__ void __launch_bounds__(kBlock) k_lattice_filter(KP P, CellGrid G, int
                                                            const int32_t* __restrict__ sctl, double T,
                                                            double2* __restrict__ pos_out, double2* __restrict__ u,
                                                            int32_t* __restrict__ status, int32_t* __restrict__ cnt,
-                                                           int guard_rows, double* __restrict__ ext_part,
+                                                           double* __restrict__ ext_part,
                                                            unsigned long long* __restrict__ stats,
                                                            int32_t* __restrict__ hardq, HardRec* __restrict__ qrec,
-                                                           long qcap, int cnt_begin, int cnt_end) {
+                                                           long qcap) {
     // hit rows + 4 x fp64 per-quadrant minima, one column per lane
     __shared__ int hit_lds[kHitCap * kBlock + 8 * kBlock];
     const int bx = xcd_block();
@@ -392,19 +392,19 @@ __global__ void __launch_bounds__(kBlock) k_lattice_filter(KP P, CellGrid G, int
     double e0 = INFINITY, e1 = -INFINITY, e2 = -INFINITY, e3 = INFINITY;
     EgoOut O;
     O.res = 0;
-    O.row = -1;
+    O.w = -1;
     O.nbrs = 0;
     O.code = CBF_STATUS_IDLE;
     O.binding = false;
     O.viol = O.vorig = 0.0;
     O.d2 = INFINITY;
     if (slot < total) {
-        lattice_ego<FZ>(P, G, W, row_begin, row_end, win_row0, slot, spos, svel, sidx, start, T, pos_out, u,
-                        status, cnt, hardq, bx % kSubQ, qrec + (long)(bx % kSubQ) * qcap, hit_lds, O);
-        if (O.res == 1) ext_accumulate(O.row, row_begin, row_end, guard_rows, O.ny, e0, e1, e2, e3);
+        lattice_ego<FZ>(P, G, B, slot, spos, svel, sidx, start, T, pos_out, u, status, cnt, hardq, bx % kSubQ,
+                        qrec + (long)(bx % kSubQ) * qcap, hit_lds, O);
+        if (ext_part && O.res == 1) ext_accumulate_w(O.w, B, O.ny, e0, e1, e2, e3);
     }
     if (stats) {
-        const bool counted = O.res != 0 && O.row >= cnt_begin && O.row < cnt_end;
+        const bool counted = O.res != 0 && O.w >= B.cnt_lo && O.w < B.cnt_hi;
         wave_stats(stats, (long)bx * (kBlock / 64) + (threadIdx.x >> 6), counted && O.nbrs > 0,
                    counted && O.res == 2, counted && O.res == 1, O.code, O.binding, O.viol, O.vorig,
                    counted ? O.d2 : INFINITY);
@@ -414,14 +414,13 @@ __global__ void __launch_bounds__(kBlock) k_lattice_filter(KP P, CellGrid G, int
 
 // K5: the queued hard QPs (state assembled by K4): the exact Seidel solve, one per lane, the
 // sub-queues drained in full waves (drain_subq).
-__global__ void __launch_bounds__(64) k_lattice_filter_hard(KP P, int row_begin, int row_end, double T,
+__global__ void __launch_bounds__(64) k_lattice_filter_hard(KP P, WinBounds B, double T,
                                                             double2* __restrict__ pos_out, double2* __restrict__ u,
                                                             int32_t* __restrict__ status, int32_t* __restrict__ cnt,
-                                                            int guard_rows, double* __restrict__ ext_part,
+                                                            double* __restrict__ ext_part,
                                                             unsigned long long* __restrict__ stats,
                                                             int32_t* __restrict__ hardq,
-                                                            const HardRec* __restrict__ qrec, long qcap, int cnt_begin,
-                                                            int cnt_end) {
+                                                            const HardRec* __restrict__ qrec, long qcap) {
     double e0 = INFINITY, e1 = -INFINITY, e2 = -INFINITY, e3 = INFINITY;
     int n_opt = 0, n_rel = 0, n_inf = 0, n_bnd = 0;
     double vo = 0.0, vr = 0.0;
@@ -448,8 +447,8 @@ __global__ void __launch_bounds__(64) k_lattice_filter_hard(KP P, int row_begin,
         u[h.k] = make_double2(ux, uy);
         status[h.k] = pack_status(S);
         if (cnt) cnt[h.k] = E.count;
-        ext_accumulate(h.row, row_begin, row_end, guard_rows, pn.y, e0, e1, e2, e3);
-        if (h.row >= cnt_begin && h.row < cnt_end) {
+        ext_accumulate_w(h.row, B, pn.y, e0, e1, e2, e3);
+        if (h.row >= B.cnt_lo && h.row < B.cnt_hi) {
             n_bnd += (S.x0 != 0.0 || S.x1 != 0.0) ? 1 : 0;
             if (S.status == CBF_STATUS_OPTIMAL) {
                 ++n_opt;
@@ -641,13 +640,12 @@ static int lattice_advance(const cbf_params* p, const cbf_grid* grid, int32_t W,
     double2* po = reinterpret_cast<double2*>(pos_out);
     double2* uo = reinterpret_cast<double2*>(u);
     unsigned long long* st = reinterpret_cast<unsigned long long*>(stats);
+    const WinBounds B = make_win_bounds(W, win_row0, n, row_begin, row_end, cnt_begin, cnt_end, guard_rows);
     hipLaunchKernelGGL(p->f_is_zero ? k_lattice_filter<true> : k_lattice_filter<false>, dim3(nb), dim3(kBlock), 0, s,
-                       kp, G, W, row_begin, row_end, win_row0, n, Wk.ncell, Wk.spos, Wk.svel, Wk.sidx, Wk.start, Wk.sctl,
-                       T, po, uo, status, nbr_count, guard_rows, ext_part, st, Wk.hardq, Wk.qrec, Wk.qcap, cnt_begin,
-                       cnt_end);
-    hipLaunchKernelGGL(k_lattice_filter_hard, dim3(hb), dim3(64), 0, s, kp, row_begin, row_end, T, po, uo, status,
-                       nbr_count, guard_rows, ext_part ? ext_part + 4l * lattice_ext_waves(n) : nullptr, st, Wk.hardq,
-                       Wk.qrec, Wk.qcap, cnt_begin, cnt_end);
+                       kp, G, B, W, row_begin, row_end, win_row0, n, Wk.ncell, Wk.spos, Wk.svel, Wk.sidx, Wk.start,
+                       Wk.sctl, T, po, uo, status, nbr_count, ext_part, st, Wk.hardq, Wk.qrec, Wk.qcap);
+    hipLaunchKernelGGL(k_lattice_filter_hard, dim3(hb), dim3(64), 0, s, kp, B, T, po, uo, status, nbr_count,
+                       ext_part ? ext_part + 4l * lattice_ext_waves(n) : nullptr, st, Wk.hardq, Wk.qrec, Wk.qcap);
     if (extents) launch_extents_finalize((int)lattice_ext_waves(n) + hb, ext_part, extents, s);
     return (int)hipGetLastError();
 }
