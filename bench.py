@@ -117,10 +117,25 @@ def bench_lattice(args, ws, rank, local):
     # the sharded path stays eager: per-sub-step graph replays measured slower than eager
     # launches (110 vs 104 us per step at one rank, 4 sub-steps per exchange)
     use_graph = not args.eager and not (ws > 1 or args.shard)
+    # single GPU, reference barrier: the timesteps run as cbf_lattice_run calls of `chunk`
+    # timesteps (bit-identical to as many cbf_lattice_step calls; each advance bins the next
+    # timestep, so the bin pass runs once per call), each call one hipGraph
+    chunk = args.chunk if (use_graph and args.barrier == "reference" and args.chunk > 1) else 1
+    plan = [chunk] * (args.steps // chunk) + ([args.steps % chunk] if args.steps % chunk else [])
+
+    def advance(n):
+        if chunk > 1:
+            S.run(n)
+        else:
+            for _ in range(n):
+                S.step()
     if use_graph:
-        S.capture()
-    for _ in range(args.warmup):
-        S.step()
+        if chunk > 1:
+            for n in set(plan):
+                S.capture(steps=n)
+        else:
+            S.capture()
+    advance(args.warmup)
     torch.cuda.synchronize()
     S.reset_solves()
     if ws > 1:
@@ -130,8 +145,12 @@ def bench_lattice(args, ws, rank, local):
     ev1 = torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
     ev0.record()
-    for _ in range(args.steps):
-        S.step()
+    if chunk > 1:
+        for n in plan:
+            S.run(n)
+    else:
+        for _ in range(args.steps):
+            S.step()
     ev1.record()
     torch.cuda.synchronize()
     if ws > 1:
@@ -201,7 +220,8 @@ def bench_lattice(args, ws, rank, local):
                    "agents_total": n_total, "agents_per_gpu": n_local,
                    "parallelism": f"row-stripe shards x{ws}, 1 RCCL all-gather of ghost-row slabs per "
                                   f"{args.substeps} steps" if (ws > 1 or args.shard) else "single GPU",
-                   "graph": use_graph},
+                   "graph": use_graph,
+                   "timesteps_per_call": chunk},
         "timesteps_per_s": args.steps / elapsed,
         "solves_per_step": solves / args.steps,
         "feasible_fraction": safety["feasible_fraction"] if safety else None,
@@ -428,6 +448,8 @@ def main():
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--eager", action="store_true", help="no hipGraph capture")
     ap.add_argument("--kernel-iters", type=int, default=20)
+    ap.add_argument("--chunk", type=int, default=10,
+                    help="timesteps per cbf_lattice_run call (single-GPU graph path; 1 = one cbf_lattice_step per step)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--barrier", default="reference", choices=["reference", "euclidean_hocbf"],
                     help="cfg4 single-GPU: the reference's L1 barrier rows or the Euclidean HOCBF mode")

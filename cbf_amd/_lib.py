@@ -15,7 +15,7 @@ PKG = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(PKG, "libcbf_amd.so")
 
 CBF_EINVAL = -1
-ABI_VERSION = 2  # include/cbf_amd.h CBF_ABI_VERSION
+ABI_VERSION = 3  # include/cbf_amd.h CBF_ABI_VERSION
 STATUS_IDLE, STATUS_OPTIMAL, STATUS_RELAXED, STATUS_BOX_INFEASIBLE, STATUS_RELAX_CAP = 0, 1, 2, 3, 4
 STATUS_NBR_OVERFLOW = 5
 STATUS_WORKSPACE_ERROR = 6
@@ -85,6 +85,7 @@ SIGNATURES = {
     "cbf_lattice_workspace_size": (_sz, [_i32, _i32, _G]),
     "cbf_lattice_step": (C.c_int, [_P, _G, _i32, _i32, _i32, _i32, _i32, _i32, _vp, _d, _d, _vp, _vp, _vp, _vp,
                                    _vp, _i32, _vp, _vp, _vp, _sz, _vp]),
+    "cbf_lattice_run": (C.c_int, [_P, _G, _i32, _i32, _vp, _d, _d, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _sz, _vp]),
     "cbf_lattice_build": (C.c_int, [_P, _G, _i32, _i32, _i32, _i32, _i32, _i32, _vp, _d, _vp, _vp, _sz, _vp]),
     "cbf_lattice_advance": (C.c_int, [_P, _G, _i32, _i32, _i32, _i32, _i32, _i32, _vp, _d, _vp, _vp, _vp, _vp,
                                       _i32, _vp, _vp, _vp, _sz, _vp]),

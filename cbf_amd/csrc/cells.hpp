@@ -29,7 +29,7 @@ constexpr int kHardHeader = 32 * (1 + 2 * kSubQ);
 // A QP the filter kernel could not solve at the origin, queued with its assembled state.
 struct HardRec {
     double r0, r1, r2, r3, u0x, u0y, bq0, bq1, bq2, bq3;
-    int present, count, k, row;
+    int present, count, k, row, slot;  // row: window index of the agent; slot: its cell-sorted slot
 };
 
 struct CellGrid {

@@ -91,6 +91,29 @@ __device__ __forceinline__ void ext_accumulate_w(int w, const WinBounds& B, doub
     if (w >= B.g_lo) e3 = pmin(e3, ny);
 }
 
+// Cell of a position (the bin kernels' formula).
+__device__ __forceinline__ int cell_of(const CellGrid& G, double x, double y) {
+    return cell_coord(y, G.y0, G.inv_h, G.ny) * G.nx + cell_coord(x, G.x0, G.inv_h, G.nx);
+}
+
+// Counting-sort binning of one agent per lane (cell < 0: none): the lane's rank in its cell.
+// Consecutive lanes of equal cell form a run served by one atomic (the agents arrive in the
+// previous cell order, so runs are long).  Every lane of the wave must call it.
+__device__ __forceinline__ int run_rank(int cell, int32_t* __restrict__ count) {
+    const int lane = threadIdx.x & 63;
+    const int cprev = __shfl_up(cell, 1, 64);
+    const bool leader = lane == 0 || cell != cprev;
+    const unsigned long long lm = __ballot(leader);
+    const unsigned long long upto = (lane == 63) ? ~0ull : ((2ull << lane) - 1ull);
+    const int my_leader = 63 - __clzll(lm & upto);
+    const unsigned long long above = lm & ~upto;
+    const int next = above ? __ffsll((long long)above) - 1 : 64;
+    int base = 0;
+    if (leader && cell >= 0) base = atomicAdd(&count[cell], next - lane);
+    base = __shfl(base, my_leader, 64);
+    return base + lane - my_leader;
+}
+
 // This lane's entry in sub-queue q (length at hardq[32 (1 + q)]); every active lane of the wave
 // that calls it appends one entry, with one atomic per wave.
 __device__ __forceinline__ int subq_append(int32_t* hardq, int q) {

@@ -120,7 +120,7 @@ __global__ void __launch_bounds__(kBlock) k_lattice_nominal_bin_ordered(
             const int r = win_row0 + (int)(w / W);
             if ((r == 0 || r - 1 >= win_row0) && (r == H - 1 || r + 1 < win_row0 + win_rows)) {
                 p = pos[w];
-                cell = cell_coord(p.y, G.y0, G.inv_h, G.ny) * G.nx + cell_coord(p.x, G.x0, G.inv_h, G.nx);
+                cell = cell_of(G, p.x, p.y);
             }
         }
     }
@@ -186,23 +186,9 @@ __global__ void __launch_bounds__(kBlock) k_lattice_nominal_bin_ordered(
             }
         }
     }
-    // runs of equal cells inside the wave: one atomic per run
-    int cprev = __shfl_up(cell, 1, 64);
-    const bool leader = lane == 0 || cell != cprev;
-    const unsigned long long lm = __ballot(leader);
-    const unsigned long long upto = (lane == 63) ? ~0ull : ((2ull << lane) - 1ull);
-    const int my_leader = 63 - __clzll(lm & upto);
-    const unsigned long long above = lm & ~upto;
-    const int next = above ? __ffsll((long long)above) - 1 : 64;
-    int base = 0;
-    if (leader && cell >= 0) base = atomicAdd(&count[cell], next - lane);
-    base = __shfl(base, my_leader, 64);
+    const int rank = run_rank(cell, count);
     if (t >= nwin) return;
-    if (cell < 0) {
-        bcs[t] = make_int3(-1, 0, (int)w);
-        return;
-    }
-    bcs[t] = make_int3(cell, base + lane - my_leader, (int)w);
+    bcs[t] = cell < 0 ? make_int3(-1, 0, (int)w) : make_int3(cell, rank, (int)w);
 }
 
 // Lattice step K3: counting-sort scatter of the binned window agents into the cell-sorted copies,
@@ -251,14 +237,14 @@ struct EgoOut {
     int nbrs;         // neighbours
     int code;         // final status code (res == 1)
     bool binding;     // the minimiser is not the origin (res == 1)
-    double viol, vorig, d2, ny;
+    double viol, vorig, d2, nx, ny;
 };
 
 // Tail of the lattice filter for one owned ego (output index k) whose QP rows are accumulated in
 // E: solve in place when solve_fast can (origin, or one Seidel event that stays put) or queue to
 // the hard kernel (sub-queue q: header hardq, records qr), clip, Euler, outputs.
 template <bool FZ>
-__device__ __forceinline__ void ego_finish(const KP& P, Ego& E, int w, int k, double T,
+__device__ __forceinline__ void ego_finish(const KP& P, Ego& E, int w, int k, int slot, double T,
                                            double2* __restrict__ pos_out, double2* __restrict__ u,
                                            int32_t* __restrict__ status, int32_t* __restrict__ cnt,
                                            int32_t* __restrict__ hardq, int q, HardRec* __restrict__ qr,
@@ -288,6 +274,7 @@ __device__ __forceinline__ void ego_finish(const KP& P, Ego& E, int w, int k, do
             h.count = E.count;
             h.k = k;
             h.row = w;
+            h.slot = slot;
             O.res = 2;
             return;
         }
@@ -303,6 +290,7 @@ __device__ __forceinline__ void ego_finish(const KP& P, Ego& E, int w, int k, do
     u[k] = make_double2(ux, uy);
     status[k] = st;
     if (cnt) cnt[k] = E.count;
+    O.nx = pn.x;
     O.ny = pn.y;
     O.res = 1;
 }
@@ -358,7 +346,7 @@ __device__ __forceinline__ void lattice_ego(const KP& P, const CellGrid& G, cons
     }
     O.nbrs = E.count;
     O.d2 = d2;
-    ego_finish<FZ>(P, E, w, w - B.own_lo, T, pos_out, u, status, cnt, hardq, q, qr, O);
+    ego_finish<FZ>(P, E, w, w - B.own_lo, slot, T, pos_out, u, status, cnt, hardq, q, qr, O);
 }
 
 // K4: one lane per cell-sorted slot; QPs that solve_fast settles (the origin, or one Seidel event
@@ -378,7 +366,8 @@ __global__ void __launch_bounds__(kBlock) k_lattice_filter(KP P, CellGrid G, Win
                                                            double* __restrict__ ext_part,
                                                            unsigned long long* __restrict__ stats,
                                                            int32_t* __restrict__ hardq, HardRec* __restrict__ qrec,
-                                                           long qcap) {
+                                                           long qcap, int3* __restrict__ nbcs,
+                                                           int32_t* __restrict__ ncount) {
     // hit rows + 4 x fp64 per-quadrant minima, one column per lane
     __shared__ int hit_lds[kHitCap * kBlock + 8 * kBlock];
     const int bx = xcd_block();
@@ -403,6 +392,11 @@ __global__ void __launch_bounds__(kBlock) k_lattice_filter(KP P, CellGrid G, Win
                         qrec + (long)(bx % kSubQ) * qcap, hit_lds, O);
         if (ext_part && O.res == 1) ext_accumulate_w(O.w, B, O.ny, e0, e1, e2, e3);
     }
+    if (nbcs) {  // chained binning: the next build's record of this slot (queued egos: K5)
+        const int cell = O.res == 1 ? cell_of(G, O.nx, O.ny) : -1;
+        const int rank = run_rank(cell, ncount);
+        if (O.res == 1) nbcs[slot] = make_int3(cell, rank, O.w);
+    }
     if (stats) {
         const bool counted = O.res != 0 && O.w >= B.cnt_lo && O.w < B.cnt_hi;
         wave_stats(stats, (long)bx * (kBlock / 64) + (threadIdx.x >> 6), counted && O.nbrs > 0,
@@ -414,13 +408,18 @@ __global__ void __launch_bounds__(kBlock) k_lattice_filter(KP P, CellGrid G, Win
 
 // K5: the queued hard QPs (state assembled by K4): the exact Seidel solve, one per lane, the
 // sub-queues drained in full waves (drain_subq).
-__global__ void __launch_bounds__(64) k_lattice_filter_hard(KP P, WinBounds B, double T,
+__global__ void __launch_bounds__(64) k_lattice_filter_hard(KP P, CellGrid G, WinBounds B, double T,
                                                             double2* __restrict__ pos_out, double2* __restrict__ u,
                                                             int32_t* __restrict__ status, int32_t* __restrict__ cnt,
                                                             double* __restrict__ ext_part,
                                                             unsigned long long* __restrict__ stats,
                                                             int32_t* __restrict__ hardq,
-                                                            const HardRec* __restrict__ qrec, long qcap) {
+                                                            const HardRec* __restrict__ qrec, long qcap,
+                                                            int3* __restrict__ nbcs, int32_t* __restrict__ ncount,
+                                                            int32_t* __restrict__ sctl) {
+    // chained: the next build starts here (its bin kernel is skipped): advance the scan epoch; an
+    // error flag of this build stays set, so the rest of the run reports it
+    if (nbcs && blockIdx.x == 0 && threadIdx.x == 0) sctl[1] = (sctl[1] + 1) & 0x3FFFFFFF;
     double e0 = INFINITY, e1 = -INFINITY, e2 = -INFINITY, e3 = INFINITY;
     int n_opt = 0, n_rel = 0, n_inf = 0, n_bnd = 0;
     double vo = 0.0, vr = 0.0;
@@ -448,6 +447,10 @@ __global__ void __launch_bounds__(64) k_lattice_filter_hard(KP P, WinBounds B, d
         status[h.k] = pack_status(S);
         if (cnt) cnt[h.k] = E.count;
         ext_accumulate_w(h.row, B, pn.y, e0, e1, e2, e3);
+        if (nbcs) {
+            const int cell = cell_of(G, pn.x, pn.y);
+            nbcs[h.slot] = make_int3(cell, atomicAdd(&ncount[cell], 1), h.row);
+        }
         if (h.row >= B.cnt_lo && h.row < B.cnt_hi) {
             n_bnd += (S.x0 != 0.0 || S.x1 != 0.0) ? 1 : 0;
             if (S.status == CBF_STATUS_OPTIMAL) {
@@ -591,6 +594,18 @@ extern "C" size_t cbf_lattice_workspace_size(int32_t W, int32_t win_rows, const 
 }
 
 
+// the bin records, 12 B per agent (the cs area reserves 16)
+static int3* lattice_bcs(const CellWs& Wk) { return reinterpret_cast<int3*>(Wk.cs); }
+
+// scan + scatter (with the nominal control) of a build whose records are in lattice_bcs(Wk)
+static void lattice_scan_scatter(const CellWs& Wk, int W, int H, int row_begin, int row_end, int win_row0, long n,
+                                 const double2* pos, double gain, double* vel_out, hipStream_t s) {
+    launch_scan(Wk, s);
+    hipLaunchKernelGGL(k_lattice_scatter_ordered, dim3(nblk(n)), dim3(kBlock), 0, s, n, lattice_bcs(Wk), Wk.start, pos,
+                       Wk.spos, Wk.svel, Wk.sidx, Wk.hardq + 2, Wk.ncell, win_row0, H, W, row_begin, row_end, gain,
+                       reinterpret_cast<double2*>(vel_out), Wk.sctl);
+}
+
 static int lattice_build(const cbf_params* p, const cbf_grid* grid, int32_t W, int32_t H, int32_t row_begin,
                          int32_t row_end, int32_t win_row0, int32_t win_rows, const double* pos, double gain,
                          double* vel_out, void* workspace, size_t workspace_bytes, unsigned long long* ext_keys,
@@ -603,14 +618,10 @@ static int lattice_build(const cbf_params* p, const cbf_grid* grid, int32_t W, i
     const CellGrid G = make_grid(grid);
     CellWs Wk(workspace, n, (long)G.nx * G.ny);
     const double2* p2 = reinterpret_cast<const double2*>(pos);
-    int3* bcs = reinterpret_cast<int3*>(Wk.cs);  // 12 B per agent (the area reserves 16)
     hipLaunchKernelGGL(k_lattice_nominal_bin_ordered, dim3(nblk(n)), dim3(kBlock), 0, s, G, W, H, row_begin, row_end,
-                       win_row0, win_rows, p2, Wk.count, Wk.sidx, Wk.start, Wk.ncell, bcs, Wk.hardq, ext_keys, X,
-                       Wk.sctl);
-    launch_scan(Wk, s);
-    hipLaunchKernelGGL(k_lattice_scatter_ordered, dim3(nblk(n)), dim3(kBlock), 0, s, n, bcs, Wk.start, p2, Wk.spos,
-                       Wk.svel, Wk.sidx, Wk.hardq + 2, Wk.ncell, win_row0, H, W, row_begin, row_end, gain,
-                       reinterpret_cast<double2*>(vel_out), Wk.sctl);
+                       win_row0, win_rows, p2, Wk.count, Wk.sidx, Wk.start, Wk.ncell, lattice_bcs(Wk), Wk.hardq,
+                       ext_keys, X, Wk.sctl);
+    lattice_scan_scatter(Wk, W, H, row_begin, row_end, win_row0, n, p2, gain, vel_out, s);
     return (int)hipGetLastError();
 }
 
@@ -625,7 +636,7 @@ static int lattice_advance(const cbf_params* p, const cbf_grid* grid, int32_t W,
                            int32_t row_end, int32_t win_row0, int32_t win_rows, const double* pos, double T,
                            double* pos_out, double* u, int32_t* status, int32_t* nbr_count, int32_t guard_rows,
                            double* extents, uint64_t* stats, void* workspace, size_t workspace_bytes,
-                           int32_t cnt_begin, int32_t cnt_end, void* stream) {
+                           int32_t cnt_begin, int32_t cnt_end, void* stream, bool chain = false) {
     int rc = check_lattice(p, grid, W, H, row_begin, row_end, win_row0, win_rows, pos, workspace, workspace_bytes);
     if (rc) return rc;
     if (!pos_out || !u || !status) return CBF_EINVAL;
@@ -643,9 +654,11 @@ static int lattice_advance(const cbf_params* p, const cbf_grid* grid, int32_t W,
     const WinBounds B = make_win_bounds(W, win_row0, n, row_begin, row_end, cnt_begin, cnt_end, guard_rows);
     hipLaunchKernelGGL(p->f_is_zero ? k_lattice_filter<true> : k_lattice_filter<false>, dim3(nb), dim3(kBlock), 0, s,
                        kp, G, B, W, row_begin, row_end, win_row0, n, Wk.ncell, Wk.spos, Wk.svel, Wk.sidx, Wk.start,
-                       Wk.sctl, T, po, uo, status, nbr_count, ext_part, st, Wk.hardq, Wk.qrec, Wk.qcap);
-    hipLaunchKernelGGL(k_lattice_filter_hard, dim3(hb), dim3(64), 0, s, kp, B, T, po, uo, status, nbr_count,
-                       ext_part ? ext_part + 4l * lattice_ext_waves(n) : nullptr, st, Wk.hardq, Wk.qrec, Wk.qcap);
+                       Wk.sctl, T, po, uo, status, nbr_count, ext_part, st, Wk.hardq, Wk.qrec, Wk.qcap,
+                       chain ? lattice_bcs(Wk) : nullptr, Wk.count);
+    hipLaunchKernelGGL(k_lattice_filter_hard, dim3(hb), dim3(64), 0, s, kp, G, B, T, po, uo, status, nbr_count,
+                       ext_part ? ext_part + 4l * lattice_ext_waves(n) : nullptr, st, Wk.hardq, Wk.qrec, Wk.qcap,
+                       chain ? lattice_bcs(Wk) : nullptr, Wk.count, Wk.sctl);
     if (extents) launch_extents_finalize((int)lattice_ext_waves(n) + hb, ext_part, extents, s);
     return (int)hipGetLastError();
 }
@@ -669,6 +682,37 @@ extern "C" int cbf_lattice_step(const cbf_params* p, const cbf_grid* grid, int32
     if (rc) return rc;
     return cbf_lattice_advance(p, grid, W, H, row_begin, row_end, win_row0, win_rows, pos, T, pos_out, u, status,
                                nbr_count, guard_rows, extents, stats, workspace, workspace_bytes, stream);
+}
+
+// `steps` timesteps of the whole lattice in one call, bit-identical to as many cbf_lattice_step
+// calls: every advance but the last bins its new positions for the next build on the fly
+// (chained binning: run_rank in K4, one atomic per queued ego in K5), so only the first build
+// runs the bin kernel.  Positions, workspace and stats as cbf_lattice_step; vel_out, u, status
+// and nbr_count hold the last step's.
+extern "C" int cbf_lattice_run(const cbf_params* p, const cbf_grid* grid, int32_t W, int32_t H, double* pos,
+                               double gain, double T, int32_t steps, double* vel_out, double* u, int32_t* status,
+                               int32_t* nbr_count, uint64_t* stats, void* workspace, size_t workspace_bytes,
+                               void* stream) {
+    int rc = check_lattice(p, grid, W, H, 0, H, 0, H, pos, workspace, workspace_bytes);
+    if (rc) return rc;
+    if (steps < 0 || !vel_out || !u || !status) return CBF_EINVAL;
+    hipStream_t s = (hipStream_t)stream;
+    const long n = (long)W * H;
+    CellWs Wk(workspace, n, (long)grid->nx * grid->ny);
+    for (int k = 0; k < steps; ++k) {
+        if (k == 0) {
+            rc = lattice_build(p, grid, W, H, 0, H, 0, H, pos, gain, vel_out, workspace, workspace_bytes, nullptr,
+                               ExtSpec{0, 0, 0}, stream);
+        } else {
+            lattice_scan_scatter(Wk, W, H, 0, H, 0, n, reinterpret_cast<const double2*>(pos), gain, vel_out, s);
+            rc = (int)hipGetLastError();
+        }
+        if (rc) return rc;
+        rc = lattice_advance(p, grid, W, H, 0, H, 0, H, pos, T, pos, u, status, nbr_count, 0, nullptr, stats,
+                             workspace, workspace_bytes, 0, H, stream, k + 1 < steps);
+        if (rc) return rc;
+    }
+    return 0;
 }
 
 extern "C" int cbf_lattice_step_sharded(const cbf_params* p, const cbf_grid* grid, int32_t W, int32_t H,

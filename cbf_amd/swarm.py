@@ -267,6 +267,7 @@ class LatticeSwarm:
         self.ap_ws = torch.empty((lib.cbf_allpairs_workspace_size(n, n) if method == "allpairs" else 1,),
                                  dtype=torch.uint8, device=self.dev)
         self.graph = None
+        self.run_graphs = {}
 
     def _launch(self):
         if self.method == "allpairs":
@@ -286,6 +287,23 @@ class LatticeSwarm:
                                    ptr(self.pos), self.gain, self.T, ptr(self.pos), ptr(self.vel), ptr(self.u),
                                    ptr(self.status), ptr(self.nbr_count), 0, None, ptr(self.stats), ptr(self.ws),
                                    self.ws_bytes, stream_handle()), "cbf_lattice_step")
+
+    def _launch_run(self, steps):
+        check(lib.cbf_lattice_run(self.cp, _lib.C.byref(self.grid), self.W, self.H, ptr(self.pos), self.gain, self.T,
+                                  steps, ptr(self.vel), ptr(self.u), ptr(self.status), ptr(self.nbr_count),
+                                  ptr(self.stats), ptr(self.ws), self.ws_bytes, stream_handle()), "cbf_lattice_run")
+
+    def run(self, steps):
+        """`steps` timesteps through cbf_lattice_run (bit-identical to `steps` step() calls; the
+        bin pass runs once, later timesteps are binned by the previous advance).  Reference
+        barrier, cell method only."""
+        if self.method != "cells" or self.barrier != "reference":
+            raise ValueError("run() is the fused multi-step path of the reference barrier on the cell list")
+        g = self.run_graphs.get(steps)
+        if g is not None:
+            g.replay()
+        else:
+            self._launch_run(steps)
 
     def build_phase(self):
         """nominal control + cell list only (K1-K3)."""
@@ -321,19 +339,25 @@ class LatticeSwarm:
     def reset_solves(self):
         self.stats.zero_()
 
-    def capture(self):
-        """Capture one step into a hipGraph (replayed by step())."""
+    def capture(self, steps=None):
+        """Capture one step (replayed by step()) or, with `steps`, one run(steps) call (replayed by
+        run(steps); one graph per step count) into a hipGraph.  The warm-up launch outside the
+        capture advances the swarm."""
         import torch
+        launch = self._launch if steps is None else (lambda: self._launch_run(steps))
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):
-            self._launch()  # warm-up outside capture
+            launch()  # warm-up outside capture
         torch.cuda.current_stream().wait_stream(s)
         torch.cuda.synchronize()
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
-            self._launch()
-        self.graph = g
+            launch()
+        if steps is None:
+            self.graph = g
+        else:
+            self.run_graphs[steps] = g
         return g
 
     def step(self):

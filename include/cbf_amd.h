@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define CBF_ABI_VERSION 2
+#define CBF_ABI_VERSION 3
 
 #define CBF_EINVAL (-1)
 
@@ -237,6 +237,19 @@ int cbf_lattice_step(const cbf_params* p, const cbf_grid* grid, int32_t W, int32
                      double* pos_out, double* vel_out, double* u, int32_t* status, int32_t* nbr_count,
                      int32_t guard_rows, double* extents, uint64_t* solves, void* workspace, size_t workspace_bytes,
                      void* stream);
+
+/*
+ * `steps` timesteps of a whole W x H lattice (rows [0, H), no halo) in one call: pos is advanced
+ * in place; vel_out, u, status and nbr_count hold the last timestep's values; solves accumulates
+ * over all of them.  Bit-identical to `steps` calls of cbf_lattice_step(p, grid, W, H, 0, H, 0, H,
+ * pos, gain, T, pos, vel_out, u, status, nbr_count, 0, NULL, solves, ...) on the same workspace
+ * (the reference's timestep loop, cross_and_rescue.py:97-175, run `steps` times).  Each advance
+ * but the last bins the new positions for the next timestep's cell list as it writes them, so
+ * the bin pass over all positions runs once per call instead of once per timestep.
+ */
+int cbf_lattice_run(const cbf_params* p, const cbf_grid* grid, int32_t W, int32_t H, double* pos, double gain,
+                    double T, int32_t steps, double* vel_out, double* u, int32_t* status, int32_t* nbr_count,
+                    uint64_t* solves, void* workspace, size_t workspace_bytes, void* stream);
 
 int cbf_lattice_build(const cbf_params* p, const cbf_grid* grid, int32_t W, int32_t H, int32_t row_begin,
                       int32_t row_end, int32_t win_row0, int32_t win_rows, const double* pos, double gain,

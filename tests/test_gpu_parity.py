@@ -291,6 +291,55 @@ def test_lattice_graph_replay_matches_eager():
     assert torch.equal(A.pos, B.pos) and torch.equal(A.u, B.u)
 
 
+def _lattice_state(L):
+    """Positions, last-step outputs, and the decoded statistics (the raw words are per-slot
+    partial sums whose split over the slots follows queue order)."""
+    torch.cuda.synchronize()
+    st = L.stats_summary()
+    return [t.cpu().numpy().copy() for t in (L.pos, L.vel, L.u, L.status, L.nbr_count)] + \
+        [np.array([st[k] for k in sorted(st)], dtype=object)]
+
+
+@pytest.mark.parametrize("spacing", [scenarios.LATTICE_SPACING, 0.2])
+def test_lattice_run_matches_steps(spacing):
+    """cbf_lattice_run (chained binning: each advance bins the next timestep) == the same number of
+    cbf_lattice_step calls, bit for bit: positions, last-step outputs and every statistics word,
+    in one call, split over calls, and replayed from a hipGraph of run(4).  The first 3 steps of
+    the reference run are also checked against the oracle, so the chain is anchored to it."""
+    W, H = 256, 192
+    pos = scenarios.lattice(W, H, seed=11, spacing=spacing)
+    A = swarm.LatticeSwarm(pos, W, H)
+    ref = pos.copy()
+    states = {}
+    for k in range(1, 17):
+        A.step()
+        if k <= 3:
+            vel = coracle.consensus_lattice(W, H, 0, H, ref, 0.25)
+            ref = coracle.euler(ref, coracle.filter_swarm(po.Params(15), ref, vel, 0)["u"], 1 / 30)
+            assert np.array_equal(A.pos.cpu().numpy(), ref), k
+        if k in (12, 16):
+            states[k] = _lattice_state(A)
+    B = swarm.LatticeSwarm(pos, W, H)
+    B.run(12)
+    for a, b in zip(states[12], _lattice_state(B)):
+        assert np.array_equal(a, b)
+    C = swarm.LatticeSwarm(pos, W, H)
+    for n in (1, 5, 6):
+        C.run(n)
+    for a, b in zip(states[12], _lattice_state(C)):
+        assert np.array_equal(a, b)
+    D = swarm.LatticeSwarm(pos, W, H)
+    D.capture(steps=4)              # the capture's warm-up launch runs steps 1-4
+    for _ in range(3):
+        D.run(4)
+    for a, b in zip(states[16], _lattice_state(D)):
+        assert np.array_equal(a, b)
+    st = B.stats_summary()
+    assert st["errors"] == 0 and st["solves"] > 0
+    if spacing == 0.2:
+        assert st["seidel"] > 0      # the hard-QP kernel's chained binning is exercised
+
+
 def _sample_oracle(pos, vel, idx, threads=16):
     p = po.Params(15)
     chunks = np.array_split(idx, threads)

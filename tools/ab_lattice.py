@@ -36,4 +36,15 @@ for _ in range(10):
     ks.append((a, b))
 torch.cuda.synchronize()
 adv = np.mean([a.elapsed_time(b) for a, b in ks]) * 1e3
-print(f"{root} spacing {spacing}: step {dt * 1e6:.1f} us, advance {adv:.1f} us")
+run = ""
+if hasattr(L, "run"):  # trees with cbf_lattice_run: graphs of 10-timestep calls
+    L.capture(steps=10)
+    for _ in range(2):
+        L.run(10)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps // 10):
+        L.run(10)
+    torch.cuda.synchronize()
+    run = f", run(10) {(time.perf_counter() - t0) / (steps // 10 * 10) * 1e6:.1f} us/step"
+print(f"{root} spacing {spacing}: step {dt * 1e6:.1f} us, advance {adv:.1f} us{run}")
