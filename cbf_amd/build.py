@@ -81,7 +81,8 @@ def build_torch_ops(verbose: bool = False) -> str:
 # Test-only builds of the library with a compile switch flipped in some sources (never loaded by
 # the package): name -> (sources, defines).  CBF_SCAN_TEST_TIMEOUT makes every scan look-back give
 # up, so tests/test_gpu_parity.py can check that the failure is reported, not silent.
-TEST_VARIANTS = {"scantimeout": (["cells.hip"], ["CBF_SCAN_TEST_TIMEOUT=1"])}
+TEST_VARIANTS = {"scantimeout": (["cells.hip"], ["CBF_SCAN_TEST_TIMEOUT=1"]),
+                 "apwpe8": (["filter.hip"], ["CBF_AP_WPE=8"])}
 TEST_LIB_DIR = os.path.join(ROOT, "tests", "_lib")
 
 

@@ -129,6 +129,14 @@ __device__ __forceinline__ void ap_exact(const KP& P, Ego& E, const double2* sp,
 #ifndef CBF_AP_TILE
 #define CBF_AP_TILE 256   // candidates staged per tile (a multiple of kBlock)
 #endif
+// CBF_AP_WPE: test build only (tests/_lib/libcbf_apwpe8.so, tests/test_gpu_parity.py): an
+// occupancy request on the all-pairs kernels that forces register spilling, kept to re-check that
+// the spilled code stays bit-identical (negative results).
+#ifdef CBF_AP_WPE
+#define CBF_AP_OCC __attribute__((amdgpu_waves_per_eu(CBF_AP_WPE, CBF_AP_WPE)))
+#else
+#define CBF_AP_OCC
+#endif
 #ifndef CBF_AP_SCREEN
 #define CBF_AP_SCREEN 8   // candidates per screen step
 #endif
@@ -249,7 +257,7 @@ struct HitRecord {  // exact test only: neighbour indices (first kmax, ascending
     }
 };
 
-__global__ void __launch_bounds__(kBlock) k_filter_allpairs(KP P, int n, int n_obs, const double2* __restrict__ pos,
+__global__ void __launch_bounds__(kBlock) CBF_AP_OCC k_filter_allpairs(KP P, int n, int n_obs, const double2* __restrict__ pos,
                                                             const double2* __restrict__ vel, int ego_begin,
                                                             int ego_end, double* __restrict__ u,
                                                             int32_t* __restrict__ status, int32_t* __restrict__ cnt,
@@ -276,7 +284,7 @@ __global__ void __launch_bounds__(kBlock) k_filter_allpairs(KP P, int n, int n_o
 
 // All-pairs cull only (cross_and_rescue.py:141-150): per ego the first kmax neighbour indices in
 // reference order (obstacles, then agents, ascending) and the full count.
-__global__ void __launch_bounds__(kBlock) k_cull_allpairs(KP P, int n, int n_obs, const double2* __restrict__ pos,
+__global__ void __launch_bounds__(kBlock) CBF_AP_OCC k_cull_allpairs(KP P, int n, int n_obs, const double2* __restrict__ pos,
                                                           int ego_begin, int ego_end, int kmax,
                                                           int32_t* __restrict__ nbr_idx,
                                                           int32_t* __restrict__ nbr_count) {
@@ -312,7 +320,7 @@ inline long ap_chunk_len(long n, int s) {
     return (c + CBF_AP_TILE - 1) / CBF_AP_TILE * CBF_AP_TILE;
 }
 
-__global__ void __launch_bounds__(kBlock) k_allpairs_partial(KP P, int n, int n_obs, const double2* __restrict__ pos,
+__global__ void __launch_bounds__(kBlock) CBF_AP_OCC k_allpairs_partial(KP P, int n, int n_obs, const double2* __restrict__ pos,
                                                              const double2* __restrict__ vel, int ego_begin,
                                                              int ego_end, int chunk, ApPart* __restrict__ part) {
     __shared__ ApLds L;
@@ -341,7 +349,7 @@ __global__ void __launch_bounds__(kBlock) k_allpairs_partial(KP P, int n, int n_
     part[(long)blockIdx.y * (ego_end - ego_begin) + k] = o;
 }
 
-__global__ void __launch_bounds__(kBlock) k_allpairs_finish(KP P, int nchunk, const double2* __restrict__ pos,
+__global__ void __launch_bounds__(kBlock) CBF_AP_OCC k_allpairs_finish(KP P, int nchunk, const double2* __restrict__ pos,
                                                             const double2* __restrict__ vel, int ego_begin,
                                                             int ego_end, const ApPart* __restrict__ part,
                                                             double* __restrict__ u, int32_t* __restrict__ status,

@@ -445,7 +445,7 @@ __global__ void __launch_bounds__(kBlock) k_lattice_filter_hocbf(
     const int slot = bx * kBlock + threadIdx.x;
     if (sctl[2] != 0) {  // unusable cell list (build_begin / scan timeout): touch none of it
         lattice_error_tail(W, row_begin, row_end, win_row0, nwin, slot, u, status, cnt, solves, ext_part,
-                           (long)bx * (kBlock / 64) + (threadIdx.x >> 6));
+                           (long)bx * (kBlock / 64) + (threadIdx.x >> 6), hardq);
         return;
     }
     const int total = start[ncell];

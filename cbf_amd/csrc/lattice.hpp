@@ -213,11 +213,15 @@ __device__ __forceinline__ void wave_stats(unsigned long long* __restrict__ st, 
 
 // The lattice filters' path when the build is flagged unusable: window agent slot (identity order,
 // the cell-sorted copies are not read) reports CBF_STATUS_WORKSPACE_ERROR for an owned agent, with
-// u = 0 and no neighbours; positions are left as they are; the step counts as one error.
+// u = 0 and no neighbours; positions are left as they are; the step counts as one error, and the
+// cell order the build recorded (hardq[2..7]) is dropped.
 __device__ __forceinline__ void lattice_error_tail(int W, int row_begin, int row_end, int win_row0, long nwin,
                                                    long slot, double2* __restrict__ u, int32_t* __restrict__ status,
                                                    int32_t* __restrict__ cnt, unsigned long long* __restrict__ stats,
-                                                   double* __restrict__ ext_part, long wave) {
+                                                   double* __restrict__ ext_part, long wave,
+                                                   int32_t* __restrict__ hardq) {
+    // the sorted copies of this build are not a permutation: the next build walks identity order
+    if (slot == 0) hardq[2] = 0;
     if (slot < nwin) {
         const int r = win_row0 + (int)(slot / W), c = (int)(slot % W);
         if (r >= row_begin && r < row_end) {

@@ -226,7 +226,7 @@ __global__ void __launch_bounds__(kBlock) k_lattice_scatter_ordered(long nwin, c
     const double2 a = lattice_sum(pos, b.z, r, c, W, H);
     const double2 u0 = make_double2(a.x * gain, a.y * gain);
     svel[d] = u0;
-    if (r >= row_begin && r < row_end) vel_out[(long)(r - row_begin) * W + c] = u0;
+    if (vel_out && r >= row_begin && r < row_end) vel_out[(long)(r - row_begin) * W + c] = u0;
     sidx[d] = b.z;
 }
 
@@ -374,7 +374,7 @@ __global__ void __launch_bounds__(kBlock) k_lattice_filter(KP P, CellGrid G, Win
     const int slot = bx * kBlock + threadIdx.x;
     if (sctl[2] != 0) {  // unusable cell list (build_begin / scan timeout): touch none of it
         lattice_error_tail(W, row_begin, row_end, win_row0, nwin, slot, u, status, cnt, stats, ext_part,
-                           (long)bx * (kBlock / 64) + (threadIdx.x >> 6));
+                           (long)bx * (kBlock / 64) + (threadIdx.x >> 6), hardq);
         return;
     }
     const int total = start[ncell];
@@ -699,14 +699,16 @@ extern "C" int cbf_lattice_run(const cbf_params* p, const cbf_grid* grid, int32_
     hipStream_t s = (hipStream_t)stream;
     const long n = (long)W * H;
     CellWs Wk(workspace, n, (long)grid->nx * grid->ny);
+    const CellGrid G = make_grid(grid);
+    const double2* p2 = reinterpret_cast<const double2*>(pos);
     for (int k = 0; k < steps; ++k) {
-        if (k == 0) {
-            rc = lattice_build(p, grid, W, H, 0, H, 0, H, pos, gain, vel_out, workspace, workspace_bytes, nullptr,
-                               ExtSpec{0, 0, 0}, stream);
-        } else {
-            lattice_scan_scatter(Wk, W, H, 0, H, 0, n, reinterpret_cast<const double2*>(pos), gain, vel_out, s);
-            rc = (int)hipGetLastError();
-        }
+        if (k == 0)
+            hipLaunchKernelGGL(k_lattice_nominal_bin_ordered, dim3(nblk(n)), dim3(kBlock), 0, s, G, W, H, 0, H, 0, H,
+                               p2, Wk.count, Wk.sidx, Wk.start, Wk.ncell, lattice_bcs(Wk), Wk.hardq,
+                               (unsigned long long*)nullptr, ExtSpec{0, 0, 0}, Wk.sctl);
+        // vel_out is written by the last timestep only (the earlier ones would be overwritten)
+        lattice_scan_scatter(Wk, W, H, 0, H, 0, n, p2, gain, k + 1 < steps ? nullptr : vel_out, s);
+        rc = (int)hipGetLastError();
         if (rc) return rc;
         rc = lattice_advance(p, grid, W, H, 0, H, 0, H, pos, T, pos, u, status, nbr_count, 0, nullptr, stats,
                              workspace, workspace_bytes, 0, H, stream, k + 1 < steps);

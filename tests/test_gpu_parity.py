@@ -689,3 +689,43 @@ def test_scan_timeout_is_reported():
     with pytest.raises(cbf_amd.CbfError):
         S.stats_summary()
     assert _lib.decode_stats(S.stats.cpu().numpy())["errors"] == 1
+
+
+def test_allpairs_spilled_variant_is_bit_identical():
+    """Round 1 recorded a `waves_per_eu = 8` all-pairs variant with wrong results and blamed the
+    compiler.  The same request on the shipped all-pairs kernels (test build
+    tests/_lib/libcbf_apwpe8.so, CBF_AP_WPE = 8: 64 VGPRs, 84-496 B of scratch per lane) must give
+    the shipped kernels' and the oracle's results bit for bit, on the split (cfg3) and the unsplit
+    path, with obstacles and the diagnostics."""
+    import ctypes as C
+    import os
+    from cbf_amd import _lib
+    V = C.CDLL(os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "libcbf_apwpe8.so"))
+    split, full = V.cbf_filter_allpairs_split, V.cbf_filter_allpairs
+    split.restype, split.argtypes = _lib.SIGNATURES["cbf_filter_allpairs_split"]
+    full.restype, full.argtypes = _lib.SIGNATURES["cbf_filter_allpairs"]
+    W, H, n_obs = 96, 64, 40
+    pos = scenarios.lattice(W, H, seed=21)
+    vel = coracle.consensus_lattice(W, H, 0, H, pos, 0.25)
+    n = pos.shape[0]
+    p = swarm.FilterParams()
+    cp = p.c()
+    tp, tv = _t(pos), _t(vel)
+    ref = swarm.filter_swarm(p, tp, tv, n_obs, method="allpairs")
+    want = coracle.filter_swarm(po.Params(15), pos, vel, n_obs)
+    assert np.array_equal(ref["u"].cpu().numpy(), want["u"])
+    ne = n - n_obs
+    u = torch.empty((ne, 2), dtype=torch.float64, device="cuda")
+    st = torch.empty((ne,), dtype=torch.int32, device="cuda")
+    cnt = torch.empty((ne,), dtype=torch.int32, device="cuda")
+    wsb = _lib.lib.cbf_allpairs_workspace_size(n, ne)
+    ws = torch.empty((wsb,), dtype=torch.uint8, device="cuda")
+    assert split(cp, n, n_obs, _lib.ptr(tp), _lib.ptr(tv), n_obs, n, _lib.ptr(u), _lib.ptr(st), _lib.ptr(cnt),
+                 _lib.ptr(ws), wsb, _lib.stream_handle()) == 0
+    torch.cuda.synchronize()
+    assert torch.equal(u, ref["u"]) and torch.equal(st, ref["status"]) and torch.equal(cnt, ref["nbr_count"])
+    u.zero_()
+    assert full(cp, n, n_obs, _lib.ptr(tp), _lib.ptr(tv), n_obs, n, _lib.ptr(u), _lib.ptr(st), _lib.ptr(cnt),
+                C.byref(_lib.CbfDiag()), _lib.stream_handle()) == 0
+    torch.cuda.synchronize()
+    assert torch.equal(u, ref["u"]) and torch.equal(st, ref["status"]) and torch.equal(cnt, ref["nbr_count"])
