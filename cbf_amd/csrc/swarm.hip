@@ -287,8 +287,8 @@ __device__ __forceinline__ void ego_finish(const KP& P, Ego& E, int w, int k, in
     }
     const double2 pn = make_double2(E.r0 + T * ux, E.r1 + T * uy);
     pos_out[k] = pn;
-    u[k] = make_double2(ux, uy);
-    status[k] = st;
+    if (u) u[k] = make_double2(ux, uy);  // u / status / cnt: null in the inner timesteps of cbf_lattice_run
+    if (status) status[k] = st;
     if (cnt) cnt[k] = E.count;
     O.nx = pn.x;
     O.ny = pn.y;
@@ -423,8 +423,14 @@ __global__ void __launch_bounds__(64) k_lattice_filter_hard(KP P, CellGrid G, Wi
     double e0 = INFINITY, e1 = -INFINITY, e2 = -INFINITY, e3 = INFINITY;
     int n_opt = 0, n_rel = 0, n_inf = 0, n_bnd = 0;
     double vo = 0.0, vr = 0.0;
+    // the first block of each sub-queue (the one that works whenever it is non-empty) loads its
+    // lane's first entry speculatively, beside the queue length (the queue area is allocated;
+    // an entry past the length is never used): one memory round trip less before the solve
+    const bool lead = (int)blockIdx.x < kSubQ;
+    HardRec pre;
+    if (lead) pre = qrec[(long)blockIdx.x * qcap + threadIdx.x];
     drain_subq(hardq, kHardPerQ, [&](int q, int i) {
-        const HardRec& h = qrec[(long)q * qcap + i];
+        const HardRec h = (lead && i == (int)threadIdx.x) ? pre : qrec[(long)q * qcap + i];
         Ego E;
         E.r0 = h.r0;
         E.r1 = h.r1;
@@ -443,8 +449,8 @@ __global__ void __launch_bounds__(64) k_lattice_filter_hard(KP P, CellGrid G, Wi
         clip_u(P, S, E, ux, uy);
         const double2 pn = make_double2(E.r0 + T * ux, E.r1 + T * uy);
         pos_out[h.k] = pn;
-        u[h.k] = make_double2(ux, uy);
-        status[h.k] = pack_status(S);
+        if (u) u[h.k] = make_double2(ux, uy);
+        if (status) status[h.k] = pack_status(S);
         if (cnt) cnt[h.k] = E.count;
         ext_accumulate_w(h.row, B, pn.y, e0, e1, e2, e3);
         if (nbcs) {
@@ -636,10 +642,11 @@ static int lattice_advance(const cbf_params* p, const cbf_grid* grid, int32_t W,
                            int32_t row_end, int32_t win_row0, int32_t win_rows, const double* pos, double T,
                            double* pos_out, double* u, int32_t* status, int32_t* nbr_count, int32_t guard_rows,
                            double* extents, uint64_t* stats, void* workspace, size_t workspace_bytes,
-                           int32_t cnt_begin, int32_t cnt_end, void* stream, bool chain = false) {
+                           int32_t cnt_begin, int32_t cnt_end, void* stream, bool chain = false,
+                           bool inner = false) {
     int rc = check_lattice(p, grid, W, H, row_begin, row_end, win_row0, win_rows, pos, workspace, workspace_bytes);
     if (rc) return rc;
-    if (!pos_out || !u || !status) return CBF_EINVAL;
+    if (!pos_out || (!inner && (!u || !status))) return CBF_EINVAL;  // inner: a cbf_lattice_run timestep
     hipStream_t s = (hipStream_t)stream;
     const long n = (long)W * win_rows;
     const CellGrid G = make_grid(grid);
@@ -706,12 +713,15 @@ extern "C" int cbf_lattice_run(const cbf_params* p, const cbf_grid* grid, int32_
             hipLaunchKernelGGL(k_lattice_nominal_bin_ordered, dim3(nblk(n)), dim3(kBlock), 0, s, G, W, H, 0, H, 0, H,
                                p2, Wk.count, Wk.sidx, Wk.start, Wk.ncell, lattice_bcs(Wk), Wk.hardq,
                                (unsigned long long*)nullptr, ExtSpec{0, 0, 0}, Wk.sctl);
-        // vel_out is written by the last timestep only (the earlier ones would be overwritten)
+        // vel_out is written by the last timestep only (the inner ones' would be overwritten)
         lattice_scan_scatter(Wk, W, H, 0, H, 0, n, p2, gain, k + 1 < steps ? nullptr : vel_out, s);
         rc = (int)hipGetLastError();
         if (rc) return rc;
-        rc = lattice_advance(p, grid, W, H, 0, H, 0, H, pos, T, pos, u, status, nbr_count, 0, nullptr, stats,
-                             workspace, workspace_bytes, 0, H, stream, k + 1 < steps);
+        // u, status and nbr_count are written by the last timestep only, like vel_out
+        const bool last = k + 1 == steps;
+        rc = lattice_advance(p, grid, W, H, 0, H, 0, H, pos, T, pos, last ? u : nullptr, last ? status : nullptr,
+                             last ? nbr_count : nullptr, 0, nullptr, stats, workspace, workspace_bytes, 0, H, stream,
+                             !last, !last);
         if (rc) return rc;
     }
     return 0;
