@@ -477,7 +477,7 @@ __global__ void __launch_bounds__(kBlock) k_lattice_filter_hocbf(
     if (solves) {
         const unsigned long long mk = __ballot(solved);
         if ((threadIdx.x & 63) == 0 && mk)
-            atomicAdd(&solves[16 * ((bx * (kBlock / 64) + (threadIdx.x >> 6)) & 63)],
+            atomicAdd(&solves[16 * stat_slot(bx * (kBlock / 64) + (threadIdx.x >> 6))],
                       (unsigned long long)__popcll(mk));
     }
     if (ext_part) wave_extents(e0, e1, e2, e3, ext_part, (long)bx * (kBlock / 64) + (threadIdx.x >> 6));
@@ -512,7 +512,7 @@ __global__ void __launch_bounds__(64) k_lattice_filter_hocbf_wide(
     if (solves) {
         int t = (int)ns;
         for (int o = 32; o > 0; o >>= 1) t += __shfl_xor(t, o, 64);
-        if (threadIdx.x == 0 && t) atomicAdd(&solves[16 * (blockIdx.x & 63)], (unsigned long long)t);
+        if (threadIdx.x == 0 && t) atomicAdd(&solves[16 * stat_slot(blockIdx.x)], (unsigned long long)t);
     }
     if (ext_part) wave_extents(e0, e1, e2, e3, ext_part, blockIdx.x);
 }

@@ -156,6 +156,11 @@ __device__ __forceinline__ void drain_subq(int32_t* __restrict__ hardq, int per_
 // neighbour distance^2 is kept as kDistKeyTop - bits(s) under atomicMax, so a zero-filled array
 // reads as "no neighbour pair".  Word layout: cbf_amd.h (CBF_STAT_*).
 constexpr unsigned long long kDistKeyTop = 0x7FF0000000000000ull;
+// Slots 0..62 take the atomics; slot 63 only ever holds a copy of the three maxima taken at the
+// end of an earlier step (stat_snapshot), read by the filter waves to skip lanes that cannot
+// raise them.  Zeroing the array zeroes the copy too, so the skip stays exact across resets.
+constexpr int kStatSlots = 63, kStatSnap = 63;
+__device__ __forceinline__ long stat_slot(long i) { return i % kStatSlots; }
 
 __device__ __forceinline__ unsigned long long dbits(double v) { return (unsigned long long)__double_as_longlong(v); }
 
@@ -192,13 +197,17 @@ __device__ __forceinline__ void wave_stats(unsigned long long* __restrict__ st, 
     const bool inf = fin && (code == CBF_STATUS_BOX_INFEASIBLE || code == CBF_STATUS_RELAX_CAP);
     const unsigned long long m_sol = __ballot(solved), m_sei = __ballot(seidel), m_opt = __ballot(opt),
                              m_rel = __ballot(rel), m_inf = __ballot(inf), m_bnd = __ballot(fin && binding);
-    const bool po = opt && viol > 0.0, pr = rel && vorig > 0.0, pd = d2 < INFINITY;
+    // only values beyond the snapshot (a maximum already recorded) can change the result
+    const unsigned long long* snap = st + 16 * kStatSnap;
+    const bool po = opt && viol > 0.0 && dbits(viol) > snap[CBF_STAT_VIOL_OPTIMAL];
+    const bool pr = rel && vorig > 0.0 && dbits(vorig) > snap[CBF_STAT_VIOL_ORIGINAL];
+    const bool pd = d2 < INFINITY && kDistKeyTop - dbits(d2) > snap[CBF_STAT_MIN_DIST2];
     unsigned long long vo = 0, vr = 0, dm = 0;
     if (__ballot(po)) vo = wave_umax64(po ? dbits(viol) : 0ull);
     if (__ballot(pr)) vr = wave_umax64(pr ? dbits(vorig) : 0ull);
     if (__ballot(pd)) dm = kDistKeyTop - wave_umin64(pd ? dbits(d2) : kDistKeyTop);
     if ((threadIdx.x & 63) == 0) {
-        unsigned long long* s = st + 16 * (wave & 63);
+        unsigned long long* s = st + 16 * stat_slot(wave);
         if (m_sol) atomicAdd(&s[CBF_STAT_SOLVES], (unsigned long long)__popcll(m_sol));
         if (m_opt) atomicAdd(&s[CBF_STAT_OPTIMAL], (unsigned long long)__popcll(m_opt));
         if (m_rel) atomicAdd(&s[CBF_STAT_RELAXED], (unsigned long long)__popcll(m_rel));
@@ -254,13 +263,34 @@ __device__ __forceinline__ void wave_stats_counts(unsigned long long* __restrict
     vo = wave_max(vo);
     vr = wave_max(vr);
     if ((threadIdx.x & 63) == 0) {
-        unsigned long long* s = st + 16 * (wave & 63);
+        unsigned long long* s = st + 16 * stat_slot(wave);
         if (n_opt) atomicAdd(&s[CBF_STAT_OPTIMAL], (unsigned long long)n_opt);
         if (n_rel) atomicAdd(&s[CBF_STAT_RELAXED], (unsigned long long)n_rel);
         if (n_inf) atomicAdd(&s[CBF_STAT_INFEASIBLE], (unsigned long long)n_inf);
         if (n_bnd) atomicAdd(&s[CBF_STAT_BINDING], (unsigned long long)n_bnd);
         if (vo > 0.0) atomicMax(&s[CBF_STAT_VIOL_OPTIMAL], dbits(vo));
         if (vr > 0.0) atomicMax(&s[CBF_STAT_VIOL_ORIGINAL], dbits(vr));
+    }
+}
+
+// Refresh the snapshot slot: the maxima over slots 0..62 (and the old copy) into slot 63, by one
+// 64-lane block.  Values read mid-update are earlier ones, which are still valid lower bounds.
+__device__ __forceinline__ void stat_snapshot(unsigned long long* __restrict__ st) {
+    const int l = threadIdx.x;
+    unsigned long long a = 0, b = 0, c = 0;
+    if (l <= kStatSlots) {  // lane 63 reads the old copy
+        a = st[16 * l + CBF_STAT_VIOL_OPTIMAL];
+        b = st[16 * l + CBF_STAT_VIOL_ORIGINAL];
+        c = st[16 * l + CBF_STAT_MIN_DIST2];
+    }
+    a = wave_umax64(a);
+    b = wave_umax64(b);
+    c = wave_umax64(c);
+    if (l == 0) {
+        unsigned long long* s = st + 16 * kStatSnap;
+        s[CBF_STAT_VIOL_OPTIMAL] = a;
+        s[CBF_STAT_VIOL_ORIGINAL] = b;
+        s[CBF_STAT_MIN_DIST2] = c;
     }
 }
 

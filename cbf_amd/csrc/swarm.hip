@@ -420,6 +420,8 @@ __global__ void __launch_bounds__(64) k_lattice_filter_hard(KP P, CellGrid G, Wi
     // chained: the next build starts here (its bin kernel is skipped): advance the scan epoch; an
     // error flag of this build stays set, so the rest of the run reports it
     if (nbcs && blockIdx.x == 0 && threadIdx.x == 0) sctl[1] = (sctl[1] + 1) & 0x3FFFFFFF;
+    // the last block (idle unless its sub-queue is long) refreshes the statistics snapshot
+    if (stats && blockIdx.x == gridDim.x - 1) stat_snapshot(stats);
     double e0 = INFINITY, e1 = -INFINITY, e2 = -INFINITY, e3 = INFINITY;
     int n_opt = 0, n_rel = 0, n_inf = 0, n_bnd = 0;
     double vo = 0.0, vr = 0.0;
