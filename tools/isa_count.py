@@ -22,7 +22,7 @@ def counts(src="swarm.hip", kernel="k_lattice_filterILb1", defines=()):
         subprocess.run(cmd, check=True, stderr=subprocess.DEVNULL)
         lines = open(out).read().split("\n")
     start = next(i for i, l in enumerate(lines) if re.match(r"^_Z\S*" + kernel + r"\S*:", l))
-    end = next(i for i in range(start, len(lines)) if "s_endpgm" in lines[i])
+    end = next(i for i in range(start, len(lines)) if lines[i].startswith(".Lfunc_end"))  # (several s_endpgm)
     body = lines[start:end]
     res = {"valu": sum(1 for l in body if re.match(r"\s+v_", l)),
            "salu": sum(1 for l in body if re.match(r"\s+s_", l)),
