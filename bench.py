@@ -263,7 +263,7 @@ def bench_allpairs(args, ws, rank, local):
     if ws > 1:
         torch.distributed.barrier()
     elapsed = time.perf_counter() - t0
-    solves = int(L.solves[0].item())
+    solves = L.solves_total()
     elapsed, solves = _reduce(elapsed, solves, ws)
     n = W * H
     pairs = float(n) * n * args.steps * ws / elapsed
