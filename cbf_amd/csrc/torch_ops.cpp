@@ -132,6 +132,40 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> lattice_step(
     return {vel, u, status, cnt};
 }
 
+// `steps` timesteps of the whole lattice in one call (cbf_lattice_run): positions advanced in place,
+// bit-identical to `steps` lattice_step calls; returns the last timestep's (nominal control,
+// filtered control, status, neighbour count).
+std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> lattice_run(
+    at::Tensor pos, int64_t W, int64_t H, double gain, double T, int64_t steps, double x0, double y0, double cell,
+    int64_t nx, int64_t ny, at::Tensor workspace, at::Tensor stats, double max_speed, double dmin, double k,
+    double safety_distance) {
+    check_f64(pos, "pos", 2);
+    TORCH_CHECK(pos.size(0) == W * H, "pos must hold W x H agents");
+    TORCH_CHECK(steps >= 0, "steps must be >= 0");
+    TORCH_CHECK(workspace.is_cuda() && workspace.scalar_type() == at::kByte && workspace.is_contiguous(),
+                "workspace must be a contiguous uint8 GPU tensor");
+    TORCH_CHECK(stats.is_cuda() && stats.scalar_type() == at::kLong && stats.is_contiguous() && stats.numel() == 1024,
+                "stats must be an int64[1024] GPU tensor");
+    const cbf_params p = make_params(max_speed, dmin, k, c10::nullopt, c10::nullopt, safety_distance);
+    cbf_grid g;
+    g.x0 = x0;
+    g.y0 = y0;
+    g.inv_h = 1.0 / cell;
+    g.nx = (int32_t)nx;
+    g.ny = (int32_t)ny;
+    const int64_t n = W * H;
+    at::Tensor vel = at::empty({n, 2}, pos.options());
+    at::Tensor u = at::empty({n, 2}, pos.options());
+    at::Tensor status = at::empty({n}, pos.options().dtype(at::kInt));
+    at::Tensor cnt = at::empty({n}, pos.options().dtype(at::kInt));
+    check_rc(cbf_lattice_run(&p, &g, (int32_t)W, (int32_t)H, pos.data_ptr<double>(), gain, T, (int32_t)steps,
+                             vel.data_ptr<double>(), u.data_ptr<double>(), status.data_ptr<int32_t>(),
+                             cnt.data_ptr<int32_t>(), reinterpret_cast<uint64_t*>(stats.data_ptr<int64_t>()),
+                             workspace.data_ptr(), (size_t)workspace.numel(), stream()),
+             "cbf_lattice_run");
+    return {vel, u, status, cnt};
+}
+
 int64_t lattice_workspace_size(int64_t W, int64_t H, double x0, double y0, double cell, int64_t nx, int64_t ny) {
     cbf_grid g;
     g.x0 = x0;
@@ -152,6 +186,9 @@ TORCH_LIBRARY(cbf_amd, m) {
     m.def("lattice_step(Tensor(a!) pos, int W, int H, float gain, float T, float x0, float y0, float cell, int nx, "
           "int ny, Tensor(b!) workspace, Tensor(c!) stats, float max_speed=15., float dmin=0.2, float k=1., "
           "float safety_distance=0.2) -> (Tensor, Tensor, Tensor, Tensor)");
+    m.def("lattice_run(Tensor(a!) pos, int W, int H, float gain, float T, int steps, float x0, float y0, float cell, "
+          "int nx, int ny, Tensor(b!) workspace, Tensor(c!) stats, float max_speed=15., float dmin=0.2, float k=1., "
+          "float safety_distance=0.2) -> (Tensor, Tensor, Tensor, Tensor)");
     m.def("lattice_workspace_size(int W, int H, float x0, float y0, float cell, int nx, int ny) -> int",
           &lattice_workspace_size);
     m.def("abi_version() -> int", []() -> int64_t { return cbf_abi_version(); });
@@ -161,4 +198,5 @@ TORCH_LIBRARY_IMPL(cbf_amd, CUDA, m) {
     m.impl("get_safe_control_batch", get_safe_control_batch);
     m.impl("filter_swarm", filter_swarm);
     m.impl("lattice_step", lattice_step);
+    m.impl("lattice_run", lattice_run);
 }

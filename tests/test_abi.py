@@ -72,6 +72,11 @@ def test_argument_validation_without_launch():
     g.inv_h = 4.0
     assert L.cbf_lattice_step(cp, C.byref(g), 8, 8, 2, 4, 2, 2, 1, 0.25, 0.1, 1, 1, 1, 1, null, 0, null, null, 1,
                               1 << 24, null) == _lib.CBF_EINVAL
+    # multi-timestep run: negative step count; window too large for 32-bit slot offsets
+    assert L.cbf_lattice_run(cp, C.byref(g), 8, 8, 1, 0.25, 0.1, -1, 1, 1, 1, null, null, 1, 1 << 24,
+                             null) == _lib.CBF_EINVAL
+    assert L.cbf_lattice_run(cp, C.byref(g), 1 << 14, 1 << 14, 1, 0.25, 0.1, 1, 1, 1, 1, null, null, 1, 1 << 62,
+                             null) == _lib.CBF_EINVAL
     # mc: too many entities per scenario
     assert L.cbf_mc_rollout(cp, 4, 200, 100, 1, 0.1, 1.0, 0.0, 1.0, 1.0, 1, 1, 1, null, null) == _lib.CBF_EINVAL
     # sharded halo exchange: bad geometry is refused before any launch
@@ -150,7 +155,8 @@ def test_torch_extension_registers_ops():
     import torch
     from cbf_amd import _lib, swarm, torch_ops
     o = torch_ops.ops()
-    for name in ("get_safe_control_batch", "filter_swarm", "lattice_step", "lattice_workspace_size", "abi_version"):
+    for name in ("get_safe_control_batch", "filter_swarm", "lattice_step", "lattice_run", "lattice_workspace_size",
+                 "abi_version"):
         assert hasattr(o, name), name
     assert o.abi_version() == _lib.ABI_VERSION
     g = swarm.make_grid(-1.0, -1.0, 20.0, 30.0, 0.204)
