@@ -123,8 +123,10 @@ def bench_lattice(args, ws, rank, local):
     chunk = args.chunk if (use_graph and args.barrier == "reference" and args.chunk > 1) else 1
     plan = [chunk] * (args.steps // chunk) + ([args.steps % chunk] if args.steps % chunk else [])
 
+    sharded = ws > 1 or args.shard
+
     def advance(n):
-        if chunk > 1:
+        if chunk > 1 or sharded:  # sharded: whole exchange cycles as one cbf_lattice_cycle_sharded call
             S.run(n)
         else:
             for _ in range(n):
@@ -149,8 +151,7 @@ def bench_lattice(args, ws, rank, local):
         for n in plan:
             S.run(n)
     else:
-        for _ in range(args.steps):
-            S.step()
+        advance(args.steps)
     ev1.record()
     torch.cuda.synchronize()
     if ws > 1:

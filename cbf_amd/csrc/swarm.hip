@@ -21,6 +21,75 @@ struct ExtSpec {
     int own_begin, own_end, guard;
 };
 
+// Halo-guard y-extents of one block's agents into slot (slot & 511) of an extents set (e[] per
+// lane: {min, max} over the computed rows, {max below the guard, min above it, min, max} over the
+// owned rows; y = the lane's y where any).  Each wave reduces its own; the LAST wave of the block
+// to arrive (an LDS counter, `arrive`, zeroed by the caller before a block barrier at kernel start)
+// combines the NW partials and issues one atomic per non-identity value.  No barrier at the end
+// (it would hold every wave until the block's slowest is done), and a quarter of the per-wave
+// atomics.  ONE: each lane holds at most one agent (its e[] are
+// y or infinite, which allows a two-reduction fast path).  Every lane of the wave must call it.
+template <int NW, bool ONE = true>
+__device__ __forceinline__ void ext_keys_flush(double (&e)[6], int any, double y,
+                                               unsigned long long* __restrict__ ext_keys, long slot,
+                                               double (*red)[NW], int* arrive) {
+    const unsigned long long act = __ballot(any);
+    const unsigned code = any ? ((e[0] != INFINITY ? 1u : 0u) | (e[2] != -INFINITY ? 2u : 0u) |
+                                 (e[3] != INFINITY ? 4u : 0u) | (e[4] != INFINITY ? 8u : 0u))
+                              : 0u;
+    const unsigned c0 = (unsigned)__shfl((int)code, act ? __ffsll((long long)act) - 1 : 0, 64);
+    if (!act) {
+#pragma unroll
+        for (int q = 0; q < 6; ++q) e[q] = ext_is_min(q) ? INFINITY : -INFINITY;
+    } else if (ONE && __ballot(any && code != c0) == 0) {
+        // the common wave: one membership pattern for all its agents, two reductions instead of six
+        const double mn = wave_min(any ? y : INFINITY), mx = wave_max(any ? y : -INFINITY);
+        e[0] = (c0 & 1u) ? mn : INFINITY;
+        e[1] = (c0 & 1u) ? mx : -INFINITY;
+        e[2] = (c0 & 2u) ? mx : -INFINITY;
+        e[3] = (c0 & 4u) ? mn : INFINITY;
+        e[4] = (c0 & 8u) ? mn : INFINITY;
+        e[5] = (c0 & 8u) ? mx : -INFINITY;
+    } else {
+#pragma unroll
+        for (int q = 0; q < 6; ++q) e[q] = ext_is_min(q) ? wave_min(e[q]) : wave_max(e[q]);
+    }
+    if ((threadIdx.x & 63) != 0) return;
+    const int wid = threadIdx.x >> 6;
+#pragma unroll
+    for (int q = 0; q < 6; ++q) red[q][wid] = e[q];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    if (atomicAdd(arrive, 1) != NW - 1) return;  // not the last wave of the block
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    for (int v = 0; v < NW; ++v)
+#pragma unroll
+        for (int q = 0; q < 6; ++q) e[q] = ext_is_min(q) ? pmin(e[q], red[q][v]) : pmax(e[q], red[q][v]);
+    unsigned long long* k = ext_keys + kExtSlotWords * (slot & (kExtSlots - 1));
+#pragma unroll
+    for (int q = 0; q < 6; ++q) {
+        if (ext_is_min(q)) {
+            if (e[q] != INFINITY) atomicMin(&k[q], dkey(e[q]));
+        } else if (e[q] != -INFINITY) {
+            atomicMax(&k[q], dkey(e[q]));
+        }
+    }
+}
+
+// Chained binning: the build an advance bins its new positions for (the same window in
+// cbf_lattice_run; the next sub-step's window, its own workspace, in cbf_lattice_cycle_sharded).
+// Records are indexed by this advance's slots and name the agent by its index in the next window
+// (= this window's index - shift), which holds exactly this advance's owned agents; an agent is
+// binned (computable: its lattice neighbours are in the window) iff that index is in
+// [comp_lo, comp_hi) (bounds, no division).  The next build's scatter computes its halo-guard
+// extents (sharded), as the bin kernel does for an unchained build.
+struct ChainSpec {
+    int3* bcs;            // next build's records (null: no chaining)
+    int32_t* count;       // next build's cell counts
+    int32_t* sctl;        // next build's control words
+    int shift, comp_lo, comp_hi;
+};
+
+
 __global__ void __launch_bounds__(kBlock) k_consensus_csr(int n_dst, int self_offset, int n_group,
                                                           const double2* __restrict__ src,
                                                           const double2* __restrict__ anchors,
@@ -104,6 +173,12 @@ __global__ void __launch_bounds__(kBlock) k_lattice_nominal_bin_ordered(
     const long t = (long)xcd_block() * kBlock + threadIdx.x;
     const long nwin = (long)win_rows * W;
     if (t == 0) build_begin(sctl, nwin, ncell);
+    __shared__ double red[6][kBlock / 64];
+    __shared__ int arrive;
+    if (ext_keys) {
+        if (threadIdx.x == 0) arrive = 0;
+        __syncthreads();
+    }
     // hardq[2..7]: the previous build left a cell order for exactly this window and grid (else
     // identity).  The order only permutes the work; it must list every window agent once, which
     // holds when window size, width, first row, lattice height and cell count all match.
@@ -124,14 +199,12 @@ __global__ void __launch_bounds__(kBlock) k_lattice_nominal_bin_ordered(
             }
         }
     }
-    const int lane = threadIdx.x & 63;
     if (ext_keys) {
         // y-extents of the INPUT positions for the halo guard of the sharded step (checked at the
         // next exchange): {min, max} over the computed rows [row_begin, row_end), and over the
         // owned rows {max y of rows < own_end - guard, min y of rows >= own_begin + guard, min,
         // max}.  Reduced per block, then one atomic per value into one of 64 slots on separate
         // 128-B lines (cross-XCD atomics on a shared line serialise at the memory side).
-        __shared__ double red[6][kBlock / 64];
         double e[6] = {INFINITY, -INFINITY, -INFINITY, INFINITY, INFINITY, -INFINITY};
         int any = 0;
         if (cell >= 0) {
@@ -149,42 +222,7 @@ __global__ void __launch_bounds__(kBlock) k_lattice_nominal_bin_ordered(
                 any = 1;
             }
         }
-        // the common wave has one membership pattern for all its agents: two reductions (min and
-        // max of y) instead of six
-        const unsigned code = any ? ((e[0] != INFINITY ? 1u : 0u) | (e[2] != -INFINITY ? 2u : 0u) |
-                                     (e[3] != INFINITY ? 4u : 0u) | (e[4] != INFINITY ? 8u : 0u))
-                                  : 0u;
-        const unsigned long long act = __ballot(any);
-        const unsigned c0 = (unsigned)__shfl((int)code, act ? __ffsll((long long)act) - 1 : 0, 64);
-        if (__ballot(any && code != c0) == 0) {
-            const double mn = wave_min(any ? p.y : INFINITY), mx = wave_max(any ? p.y : -INFINITY);
-            const bool has = act != 0;
-            e[0] = (has && (c0 & 1u)) ? mn : INFINITY;
-            e[1] = (has && (c0 & 1u)) ? mx : -INFINITY;
-            e[2] = (has && (c0 & 2u)) ? mx : -INFINITY;
-            e[3] = (has && (c0 & 4u)) ? mn : INFINITY;
-            e[4] = (has && (c0 & 8u)) ? mn : INFINITY;
-            e[5] = (has && (c0 & 8u)) ? mx : -INFINITY;
-        } else {
-#pragma unroll
-            for (int q = 0; q < 6; ++q) e[q] = ext_is_min(q) ? wave_min(e[q]) : wave_max(e[q]);
-        }
-        const int wid = threadIdx.x >> 6;
-        if (lane == 0)
-#pragma unroll
-            for (int q = 0; q < 6; ++q) red[q][wid] = e[q];
-        if (__syncthreads_or(any) && threadIdx.x == 0) {
-            for (int v = 1; v < kBlock / 64; ++v)
-#pragma unroll
-                for (int q = 0; q < 6; ++q)
-                    e[q] = ext_is_min(q) ? pmin(e[q], red[q][v]) : pmax(e[q], red[q][v]);
-            unsigned long long* k = ext_keys + kExtSlotWords * (blockIdx.x & (kExtSlots - 1));
-#pragma unroll
-            for (int q = 0; q < 6; ++q) {
-                if (ext_is_min(q)) atomicMin(&k[q], dkey(e[q]));
-                else atomicMax(&k[q], dkey(e[q]));
-            }
-        }
+        ext_keys_flush<kBlock / 64>(e, any, p.y, ext_keys, blockIdx.x, red, &arrive);
     }
     const int rank = run_rank(cell, count);
     if (t >= nwin) return;
@@ -195,7 +233,7 @@ __global__ void __launch_bounds__(kBlock) k_lattice_nominal_bin_ordered(
 // with each agent's lattice-Laplacian nominal control (cross_and_rescue.py:121-125 shape) computed
 // here: the agent's position is loaded anyway and its 4 lattice neighbours are mostly L2 hits
 // (cell order ~ lattice order), so the control never makes an HBM round trip.
-__global__ void __launch_bounds__(kBlock) k_lattice_scatter_ordered(long nwin, const int3* __restrict__ bcs,
+__global__ void __launch_bounds__(kBlock) k_lattice_scatter_ordered(long nwin, long nrec, const int3* __restrict__ bcs,
                                                                     const int32_t* __restrict__ start,
                                                                     const double2* __restrict__ pos,
                                                                     double2* __restrict__ spos,
@@ -205,7 +243,16 @@ __global__ void __launch_bounds__(kBlock) k_lattice_scatter_ordered(long nwin, c
                                                                     int win_row0, int H, int W, int row_begin,
                                                                     int row_end, double gain,
                                                                     double2* __restrict__ vel_out,
-                                                                    const int32_t* __restrict__ sctl) {
+                                                                    const int32_t* __restrict__ sctl,
+                                                                    unsigned long long* __restrict__ ext_keys, ExtSpec X) {
+    // ext_keys (a chained build of the sharded cycle, whose bin pass ran in the previous advance):
+    // the halo-guard extents of this build's input positions, as the bin kernel computes them
+    __shared__ double red[6][kBlock / 64];
+    __shared__ int arrive;
+    if (ext_keys) {
+        if (threadIdx.x == 0) arrive = 0;
+        __syncthreads();
+    }
     const long t = (long)xcd_block() * kBlock + threadIdx.x;
     if (t == 0 && sctl[2] == 0) {  // the cell order now exists for this window and grid: the next build walks it
         order_state[0] = 1;
@@ -215,19 +262,34 @@ __global__ void __launch_bounds__(kBlock) k_lattice_scatter_ordered(long nwin, c
         order_state[4] = H;
         order_state[5] = W;
     }
-    if (t >= nwin || sctl[2] != 0) return;  // an unusable build (build_begin / scan timeout): no scatter
-    const int3 b = bcs[t];
-    if (b.x < 0) return;
-    const int d = start[b.x] + b.y;
-    if (d < 0 || d >= nwin) return;
-    const double2 p = pos[b.z];
-    spos[d] = p;
-    const int r = win_row0 + b.z / W, c = b.z % W;
-    const double2 a = lattice_sum(pos, b.z, r, c, W, H);
-    const double2 u0 = make_double2(a.x * gain, a.y * gain);
-    svel[d] = u0;
-    if (vel_out && r >= row_begin && r < row_end) vel_out[(long)(r - row_begin) * W + c] = u0;
-    sidx[d] = b.z;
+    double e[6] = {INFINITY, -INFINITY, -INFINITY, INFINITY, INFINITY, -INFINITY};
+    int any = 0;
+    double py = 0.0;
+    // an unusable build (build_begin / scan timeout): no scatter
+    const int3 b = (t < nrec && sctl[2] == 0) ? bcs[t] : make_int3(-1, 0, 0);
+    const int d = b.x >= 0 ? start[b.x] + b.y : -1;
+    if (d >= 0 && d < nwin) {
+        const double2 p = pos[b.z];
+        spos[d] = p;
+        const int r = win_row0 + b.z / W, c = b.z % W;
+        const double2 a = lattice_sum(pos, b.z, r, c, W, H);
+        const double2 u0 = make_double2(a.x * gain, a.y * gain);
+        svel[d] = u0;
+        if (vel_out && r >= row_begin && r < row_end) vel_out[(long)(r - row_begin) * W + c] = u0;
+        sidx[d] = b.z;
+        py = p.y;
+        if (r >= row_begin && r < row_end) {
+            e[0] = e[1] = p.y;
+            any = 1;
+        }
+        if (r >= X.own_begin && r < X.own_end) {
+            if (r < X.own_end - X.guard) e[2] = p.y;
+            if (r >= X.own_begin + X.guard) e[3] = p.y;
+            e[4] = e[5] = p.y;
+            any = 1;
+        }
+    }
+    if (ext_keys) ext_keys_flush<kBlock / 64>(e, any, py, ext_keys, blockIdx.x, red, &arrive);
 }
 
 // Per-ego outcome of the lattice filter for the statistics.
@@ -366,8 +428,7 @@ __global__ void __launch_bounds__(kBlock) k_lattice_filter(KP P, CellGrid G, Win
                                                            double* __restrict__ ext_part,
                                                            unsigned long long* __restrict__ stats,
                                                            int32_t* __restrict__ hardq, HardRec* __restrict__ qrec,
-                                                           long qcap, int3* __restrict__ nbcs,
-                                                           int32_t* __restrict__ ncount) {
+                                                           long qcap, ChainSpec C) {
     // hit rows + 4 x fp64 per-quadrant minima, one column per lane
     __shared__ int hit_lds[kHitCap * kBlock + 8 * kBlock];
     const int bx = xcd_block();
@@ -392,10 +453,15 @@ __global__ void __launch_bounds__(kBlock) k_lattice_filter(KP P, CellGrid G, Win
                         qrec + (long)(bx % kSubQ) * qcap, hit_lds, O);
         if (ext_part && O.res == 1) ext_accumulate_w(O.w, B, O.ny, e0, e1, e2, e3);
     }
-    if (nbcs) {  // chained binning: the next build's record of this slot (queued egos: K5)
-        const int cell = O.res == 1 ? cell_of(G, O.nx, O.ny) : -1;
-        const int rank = run_rank(cell, ncount);
-        if (O.res == 1) nbcs[slot] = make_int3(cell, rank, O.w);
+    if (C.bcs) {  // chained binning: the next build's record of this agent (queued egos: K5)
+        // indexed by this advance's slot (the next scatter then reads its records in cell order and
+        // writes nearly sequential slots); slots of agents outside the next window hold none
+        const int wn = O.w - C.shift;
+        const bool comp = O.res == 1 && wn >= C.comp_lo && wn < C.comp_hi;
+        const int cell = comp ? cell_of(G, O.nx, O.ny) : -1;
+        const int rank = run_rank(cell, C.count);
+        if (slot < nwin && O.res != 2)
+            C.bcs[slot] = comp ? make_int3(cell, rank, wn) : make_int3(-1, 0, O.res == 1 ? wn : -1);
     }
     if (stats) {
         const bool counted = O.res != 0 && O.w >= B.cnt_lo && O.w < B.cnt_hi;
@@ -415,11 +481,14 @@ __global__ void __launch_bounds__(64) k_lattice_filter_hard(KP P, CellGrid G, Wi
                                                             unsigned long long* __restrict__ stats,
                                                             int32_t* __restrict__ hardq,
                                                             const HardRec* __restrict__ qrec, long qcap,
-                                                            int3* __restrict__ nbcs, int32_t* __restrict__ ncount,
-                                                            int32_t* __restrict__ sctl) {
+                                                            ChainSpec C, const int32_t* __restrict__ sctl) {
     // chained: the next build starts here (its bin kernel is skipped): advance the scan epoch; an
     // error flag of this build stays set, so the rest of the run reports it
-    if (nbcs && blockIdx.x == 0 && threadIdx.x == 0) sctl[1] = (sctl[1] + 1) & 0x3FFFFFFF;
+    if (C.bcs && blockIdx.x == 0 && threadIdx.x == 0) {
+        C.sctl[1] = (C.sctl[1] + 1) & 0x3FFFFFFF;
+        if (C.sctl != sctl) C.sctl[2] = sctl[2];  // a failed build leaves the chained one unusable too
+    }
+
     // the last block (idle unless its sub-queue is long) refreshes the statistics snapshot
     if (stats && blockIdx.x == gridDim.x - 1) stat_snapshot(stats);
     double e0 = INFINITY, e1 = -INFINITY, e2 = -INFINITY, e3 = INFINITY;
@@ -455,9 +524,11 @@ __global__ void __launch_bounds__(64) k_lattice_filter_hard(KP P, CellGrid G, Wi
         if (status) status[h.k] = pack_status(S);
         if (cnt) cnt[h.k] = E.count;
         ext_accumulate_w(h.row, B, pn.y, e0, e1, e2, e3);
-        if (nbcs) {
-            const int cell = cell_of(G, pn.x, pn.y);
-            nbcs[h.slot] = make_int3(cell, atomicAdd(&ncount[cell], 1), h.row);
+        if (C.bcs) {
+            const int wn = h.row - C.shift;
+            const bool comp = wn >= C.comp_lo && wn < C.comp_hi;
+            const int cell = comp ? cell_of(G, pn.x, pn.y) : -1;
+            C.bcs[h.slot] = comp ? make_int3(cell, atomicAdd(&C.count[cell], 1), wn) : make_int3(-1, 0, wn);
         }
         if (h.row >= B.cnt_lo && h.row < B.cnt_hi) {
             n_bnd += (S.x0 != 0.0 || S.x1 != 0.0) ? 1 : 0;
@@ -606,12 +677,17 @@ extern "C" size_t cbf_lattice_workspace_size(int32_t W, int32_t win_rows, const 
 static int3* lattice_bcs(const CellWs& Wk) { return reinterpret_cast<int3*>(Wk.cs); }
 
 // scan + scatter (with the nominal control) of a build whose records are in lattice_bcs(Wk)
+// nrec: records to read (the window of the binning pass: this build's own for the bin kernel, the
+// previous sub-step's for a chained build, whose records are indexed by that advance's slots)
 static void lattice_scan_scatter(const CellWs& Wk, int W, int H, int row_begin, int row_end, int win_row0, long n,
-                                 const double2* pos, double gain, double* vel_out, hipStream_t s) {
+                                 const double2* pos, double gain, double* vel_out, hipStream_t s, long nrec = -1,
+                                 unsigned long long* ext_keys = nullptr, ExtSpec X = ExtSpec{0, 0, 0}) {
+    if (nrec < 0) nrec = n;
     launch_scan(Wk, s);
-    hipLaunchKernelGGL(k_lattice_scatter_ordered, dim3(nblk(n)), dim3(kBlock), 0, s, n, lattice_bcs(Wk), Wk.start, pos,
+    hipLaunchKernelGGL(k_lattice_scatter_ordered, dim3(nblk(nrec)), dim3(kBlock), 0, s, n, nrec, lattice_bcs(Wk),
+                       Wk.start, pos,
                        Wk.spos, Wk.svel, Wk.sidx, Wk.hardq + 2, Wk.ncell, win_row0, H, W, row_begin, row_end, gain,
-                       reinterpret_cast<double2*>(vel_out), Wk.sctl);
+                       reinterpret_cast<double2*>(vel_out), Wk.sctl, ext_keys, X);
 }
 
 static int lattice_build(const cbf_params* p, const cbf_grid* grid, int32_t W, int32_t H, int32_t row_begin,
@@ -640,11 +716,26 @@ extern "C" int cbf_lattice_build(const cbf_params* p, const cbf_grid* grid, int3
                          workspace_bytes, nullptr, ExtSpec{0, 0, 0}, stream);
 }
 
+// The ChainSpec of the build of window rows [nw0, nw0 + nrows) in workspace nws, for an advance
+// whose window starts at row w0.
+static ChainSpec make_chain(const cbf_grid* grid, int W, int H, int w0, int nw0, int nrows, void* nws) {
+    const long nn = (long)W * nrows;
+    CellWs Nk(nws, nn, (long)grid->nx * grid->ny);
+    ChainSpec C;
+    C.bcs = lattice_bcs(Nk);
+    C.count = Nk.count;
+    C.sctl = Nk.sctl;
+    C.shift = (nw0 - w0) * W;
+    C.comp_lo = nw0 != 0 ? W : 0;                       // K1: the first window row only at the lattice edge
+    C.comp_hi = nw0 + nrows != H ? (int)(nn - W) : (int)nn;  // ... the last likewise
+    return C;
+}
+
 static int lattice_advance(const cbf_params* p, const cbf_grid* grid, int32_t W, int32_t H, int32_t row_begin,
                            int32_t row_end, int32_t win_row0, int32_t win_rows, const double* pos, double T,
                            double* pos_out, double* u, int32_t* status, int32_t* nbr_count, int32_t guard_rows,
                            double* extents, uint64_t* stats, void* workspace, size_t workspace_bytes,
-                           int32_t cnt_begin, int32_t cnt_end, void* stream, bool chain = false,
+                           int32_t cnt_begin, int32_t cnt_end, void* stream, const ChainSpec* chain = nullptr,
                            bool inner = false) {
     int rc = check_lattice(p, grid, W, H, row_begin, row_end, win_row0, win_rows, pos, workspace, workspace_bytes);
     if (rc) return rc;
@@ -664,10 +755,10 @@ static int lattice_advance(const cbf_params* p, const cbf_grid* grid, int32_t W,
     hipLaunchKernelGGL(p->f_is_zero ? k_lattice_filter<true> : k_lattice_filter<false>, dim3(nb), dim3(kBlock), 0, s,
                        kp, G, B, W, row_begin, row_end, win_row0, n, Wk.ncell, Wk.spos, Wk.svel, Wk.sidx, Wk.start,
                        Wk.sctl, T, po, uo, status, nbr_count, ext_part, st, Wk.hardq, Wk.qrec, Wk.qcap,
-                       chain ? lattice_bcs(Wk) : nullptr, Wk.count);
+                       chain ? *chain : ChainSpec{});
     hipLaunchKernelGGL(k_lattice_filter_hard, dim3(hb), dim3(64), 0, s, kp, G, B, T, po, uo, status, nbr_count,
                        ext_part ? ext_part + 4l * lattice_ext_waves(n) : nullptr, st, Wk.hardq, Wk.qrec, Wk.qcap,
-                       chain ? lattice_bcs(Wk) : nullptr, Wk.count, Wk.sctl);
+                       chain ? *chain : ChainSpec{}, Wk.sctl);
     if (extents) launch_extents_finalize((int)lattice_ext_waves(n) + hb, ext_part, extents, s);
     return (int)hipGetLastError();
 }
@@ -721,9 +812,92 @@ extern "C" int cbf_lattice_run(const cbf_params* p, const cbf_grid* grid, int32_
         if (rc) return rc;
         // u, status and nbr_count are written by the last timestep only, like vel_out
         const bool last = k + 1 == steps;
+        const ChainSpec C = make_chain(grid, W, H, 0, 0, H, workspace);
         rc = lattice_advance(p, grid, W, H, 0, H, 0, H, pos, T, pos, last ? u : nullptr, last ? status : nullptr,
                              last ? nbr_count : nullptr, 0, nullptr, stats, workspace, workspace_bytes, 0, H, stream,
-                             !last, !last);
+                             last ? nullptr : &C, !last);
+        if (rc) return rc;
+    }
+    return 0;
+}
+
+// One exchange cycle of the row-sharded step (cbf_amd/shard.py): nsub sub-steps after the caller's
+// halo unpack, sub-step s with workspace s of `workspaces` (nsub x ws_bytes).  Sub-step 0 builds
+// its cell list from the window positions (bin kernel, guard extents of set 0); every advance but
+// the last bins the rows it computed straight into the next sub-step's build (whose window is
+// exactly those rows) and accumulates that build's guard extents.  Bit-identical to nsub
+// cbf_lattice_step_sharded calls with the same geometry.
+extern "C" int cbf_lattice_cycle_sharded(const cbf_params* p, const cbf_grid* grid, int32_t W, int32_t H,
+                                         int32_t own_begin, int32_t own_end, int32_t halo, int32_t nsub,
+                                         int32_t win_row0, int32_t win_rows, double* wpos, double gain, double T,
+                                         double* wvel, double* wu, int32_t* wstatus, int32_t* wcnt,
+                                         uint64_t* ext_keys, uint64_t* stats, void* workspaces, size_t ws_bytes,
+                                         void* stream) {
+    if (!p || !grid || W <= 0 || H <= 0 || halo < 2 || nsub < 1 || own_begin < 0 || own_end > H ||
+        own_begin >= own_end)
+        return CBF_EINVAL;
+    const long G = (long)halo * nsub;
+    if (G > own_end - own_begin) return CBF_EINVAL;
+    const int w0 = (int)(own_begin - G > 0 ? own_begin - G : 0), w1 = (int)(own_end + G < H ? own_end + G : H);
+    if (win_row0 != w0 || win_rows != w1 - w0) return CBF_EINVAL;
+    if (!wpos || !wvel || !wu || !wstatus || !ext_keys || !workspaces) return CBF_EINVAL;
+    if (ws_bytes < cbf_lattice_workspace_size(W, win_rows, grid)) return CBF_EINVAL;
+    hipStream_t st = (hipStream_t)stream;
+    const size_t set_words = cbf_halo_ext_bytes(1) / 8;
+    auto sub = [&](int k, int& a, int& b, int& sw0, int& sw1, int& guard) {
+        const int d = (int)G - halo * (k + 1);
+        a = own_begin - d > 0 ? own_begin - d : 0;
+        b = own_end + d < H ? own_end + d : H;
+        sw0 = a - halo > 0 ? a - halo : 0;
+        sw1 = b + halo < H ? b + halo : H;
+        guard = d + halo - 1;
+    };
+    // a chained build's records are indexed by the previous sub-step's slots (12 B each; that
+    // window has up to 2 halo rows more): they must fit its record area (16 B per agent of its
+    // own window), which holds for stripes of >= 4 halo rows; checked before anything is launched
+    for (int k = 1; k < nsub; ++k) {
+        int a, b, w0k, w1k, g, pa, pb, pw0, pw1, pg;
+        sub(k, a, b, w0k, w1k, g);
+        sub(k - 1, pa, pb, pw0, pw1, pg);
+        if (12l * (pw1 - pw0) > 16l * (w1k - w0k)) return CBF_EINVAL;
+    }
+    for (int k = 0; k < nsub; ++k) {
+        int a, b, sw0, sw1, guard;
+        sub(k, a, b, sw0, sw1, guard);
+        void* ws = (char*)workspaces + (size_t)k * ws_bytes;
+        // the per-sub-step outputs (nominal / filtered control, status, count) are written by the
+        // last sub-step only: its rows are the owned rows, the earlier ones' would be overwritten
+        // there (and the ghost rows' are not outputs)
+        const bool last = k + 1 == nsub;
+        double* spos = wpos + 2l * (sw0 - win_row0) * W;
+        const long o = (long)(a - win_row0) * W;
+        unsigned long long* ek = reinterpret_cast<unsigned long long*>(ext_keys) + (size_t)k * set_words;
+        int rc;
+        if (k == 0) {
+            rc = lattice_build(p, grid, W, H, a, b, sw0, sw1 - sw0, spos, gain, wvel + 2 * o, ws, ws_bytes, ek,
+                               ExtSpec{own_begin, own_end, guard}, stream);  // (vel_out: sub-step 0 must)
+        } else {
+            rc = check_lattice(p, grid, W, H, a, b, sw0, sw1 - sw0, spos, ws, ws_bytes);
+            if (!rc) {
+                int pa, pb, pw0, pw1, pg;
+                sub(k - 1, pa, pb, pw0, pw1, pg);
+                const long n = (long)W * (sw1 - sw0), nprev = (long)W * (pw1 - pw0);
+                CellWs Wk(ws, n, (long)grid->nx * grid->ny);
+                lattice_scan_scatter(Wk, W, H, a, b, sw0, n, reinterpret_cast<const double2*>(spos), gain,
+                                     last ? wvel + 2 * o : nullptr, st, nprev, ek, ExtSpec{own_begin, own_end, guard});
+                rc = (int)hipGetLastError();
+            }
+        }
+        if (rc) return rc;
+        ChainSpec C;
+        if (k + 1 < nsub) {
+            int na, nb, nw0, nw1, ng;
+            sub(k + 1, na, nb, nw0, nw1, ng);
+            C = make_chain(grid, W, H, sw0, nw0, nw1 - nw0, (char*)workspaces + (size_t)(k + 1) * ws_bytes);
+        }
+        rc = lattice_advance(p, grid, W, H, a, b, sw0, sw1 - sw0, spos, T, wpos + 2 * o, last ? wu + 2 * o : nullptr,
+                             last ? wstatus + o : nullptr, last && wcnt ? wcnt + o : nullptr, guard, nullptr, stats, ws,
+                             ws_bytes, own_begin, own_end, stream, last ? nullptr : &C, !last);
         if (rc) return rc;
     }
     return 0;

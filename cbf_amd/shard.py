@@ -87,9 +87,11 @@ class HipBackend:
         self.radius = params.safety_distance
         self.grid = grid
         self.nsub = nsub
-        self.ws_bytes = _lib.lib.cbf_lattice_workspace_size(W, win_rows, _lib.C.byref(grid))
-        # one workspace per sub-step: each keeps the cell order of its own window across cycles
-        self.wss = [torch.zeros((self.ws_bytes,), dtype=torch.uint8, device=self.dev) for _ in range(nsub)]
+        self.ws_bytes = (_lib.lib.cbf_lattice_workspace_size(W, win_rows, _lib.C.byref(grid)) + 255) // 256 * 256
+        # one workspace per sub-step (each keeps the cell order of its own window across cycles),
+        # contiguous so that a whole cycle can run in one cbf_lattice_cycle_sharded call
+        self.ws_all = torch.zeros((nsub * self.ws_bytes,), dtype=torch.uint8, device=self.dev)
+        self.wss = [self.ws_all[s * self.ws_bytes:(s + 1) * self.ws_bytes] for s in range(nsub)]
         self.flag = torch.zeros((1,), dtype=torch.int32, device=self.dev)
         # the guard flag is read back asynchronously after every exchange: a pinned host copy per
         # exchange in flight, polled (never waited on) at the next exchanges
@@ -121,6 +123,15 @@ class HipBackend:
             P(S.wpos[(sub.w0 - S.w0) * W:]), self.gain, self.T, P(S.wpos[o:]), P(S.wvel[o:]), P(S.wu[o:]),
             P(S.wstatus[o:]), P(S.wcnt[o:]), sub.guard, P(self.ext_keys[s * self.set_words:]), P(S.stats),
             P(self.wss[s]), self.ws_bytes, L.stream_handle()), "cbf_lattice_step_sharded")
+
+    def lattice_cycle(self, S):
+        """All nsub sub-steps of one exchange cycle (cbf_lattice_cycle_sharded: the sub-steps after
+        the first are binned by the previous sub-step's advance)."""
+        L, P = self._lib, self._lib.ptr
+        L.check(L.lib.cbf_lattice_cycle_sharded(
+            self.cp, L.C.byref(self.grid), self.W, self.H, S.rb, S.re, S.halo, self.nsub, S.w0, S.win_rows,
+            P(S.wpos), self.gain, self.T, P(S.wvel), P(S.wu), P(S.wstatus), P(S.wcnt), P(self.ext_keys),
+            P(S.stats), P(self.ws_all), self.ws_bytes, L.stream_handle()), "cbf_lattice_cycle_sharded")
 
     def lattice_build(self, S):
         L, P = self._lib, self._lib.ptr
@@ -254,6 +265,19 @@ class ShardedLattice:
         else:
             self.be.lattice_step(self, self.sub, self.subs[self.sub])
         self.sub = (self.sub + 1) % self.k
+
+    def run(self, steps):
+        """`steps` timesteps; whole exchange cycles run as one device call each (the same results
+        as `steps` step() calls), the rest one sub-step at a time."""
+        done = 0
+        while done < steps:
+            if self.sub == 0 and steps - done >= self.k and hasattr(self.be, "lattice_cycle"):
+                self.exchange()
+                self.be.lattice_cycle(self)
+                done += self.k
+            else:
+                self.step()
+                done += 1
 
     def build_phase(self):
         self.be.lattice_build(self)

@@ -316,6 +316,21 @@ int cbf_lattice_step_sharded(const cbf_params* p, const cbf_grid* grid, int32_t 
                              int32_t* status, int32_t* nbr_count, int32_t guard_rows, uint64_t* ext_keys,
                              uint64_t* solves, void* workspace, size_t workspace_bytes, void* stream);
 
+/* One exchange cycle of the row-sharded step: the nsub sub-steps that follow the caller's
+ * cbf_halo_unpack, bit-identical to nsub cbf_lattice_step_sharded calls with the geometry of
+ * cbf_amd/shard.py (sub-step s computes rows [own_begin - d, own_end + d), d = halo (nsub - s - 1),
+ * clamped to the lattice, over that band +- halo rows; guard rows d + halo - 1).  wpos and the
+ * window-indexed outputs (wvel, wu, wstatus, wcnt nullable) cover rows [win_row0, win_row0 +
+ * win_rows) = own +- halo nsub, clamped; ext_keys holds nsub extents sets (cbf_halo_ext_bytes);
+ * workspaces holds nsub workspaces of ws_bytes >= cbf_lattice_workspace_size(W, win_rows, grid),
+ * workspace s for sub-step s (kept across cycles).  Sub-step 0 bins the window; every later
+ * sub-step's cell list is binned by the previous sub-step's advance as it writes the rows. */
+int cbf_lattice_cycle_sharded(const cbf_params* p, const cbf_grid* grid, int32_t W, int32_t H, int32_t own_begin,
+                              int32_t own_end, int32_t halo, int32_t nsub, int32_t win_row0, int32_t win_rows,
+                              double* wpos, double gain, double T, double* wvel, double* wu, int32_t* wstatus,
+                              int32_t* wcnt, uint64_t* ext_keys, uint64_t* stats, void* workspaces, size_t ws_bytes,
+                              void* stream);
+
 /*
  * Batched Monte-Carlo rendezvous (SURVEY cfg5): n_scen independent scenarios, each with
  * n_o pursuit obstacles (ring i -> i+1, rotation (rc, rs), scale so) then n_a free agents

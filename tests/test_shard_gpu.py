@@ -25,7 +25,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, ws, port, W, R, steps, q, k=4, graph=False):
+def _worker(rank, ws, port, W, R, steps, q, k=4, graph=False, run=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     torch.cuda.set_device(0)
     dist.init_process_group("gloo", rank=rank, world_size=ws)
@@ -34,8 +34,11 @@ def _worker(rank, ws, port, W, R, steps, q, k=4, graph=False):
     if graph:
         S.capture()
     S.reset_solves()
-    for _ in range(steps):
-        S.step()
+    if run:      # whole cycles through cbf_lattice_cycle_sharded (chained sub-steps), the rest by step()
+        S.run(steps)
+    else:
+        for _ in range(steps):
+            S.step()
     torch.cuda.synchronize()
     S.check_guard()
     q.put((rank, S.own.cpu().numpy(), S.status.cpu().numpy(), S.u.cpu().numpy(), S.stats_summary()))
@@ -43,14 +46,15 @@ def _worker(rank, ws, port, W, R, steps, q, k=4, graph=False):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("ws,k,graph", [(2, 1, False), (3, 4, False), (2, 4, True)])
-def test_sharded_equals_single_gpu(ws, k, graph):
+@pytest.mark.parametrize("ws,k,graph,run", [(2, 1, False, False), (3, 4, False, False), (2, 4, True, False),
+                                            (3, 4, False, True), (2, 2, False, True)])
+def test_sharded_equals_single_gpu(ws, k, graph, run):
     from cbf_amd import scenarios, swarm
     W, R, steps = 96, 40, 6
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, ws, port, W, R, steps, q, k, graph)) for r in range(ws)]
+    procs = [ctx.Process(target=_worker, args=(r, ws, port, W, R, steps, q, k, graph, run)) for r in range(ws)]
     for p in procs:
         p.start()
     res = sorted([q.get(timeout=300) for _ in range(ws)], key=lambda t: t[0])
