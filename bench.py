@@ -459,7 +459,7 @@ def main():
                     help="CPU-baseline processes (default: this job's host cores, oracle/cpu_baseline.py)")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="torch.distributed backend for N > 1 (nccl = RCCL; gloo = host-staged rehearsal)")
-    ap.add_argument("--substeps", type=int, default=4,
+    ap.add_argument("--substeps", type=int, default=8,
                     help="sharded cfg4: timesteps per halo exchange (ghost rows = 4 x substeps)")
     ap.add_argument("--shard", action="store_true",
                     help="cfg4: run the sharded step (halo pack + collective + unpack) even on one rank")
