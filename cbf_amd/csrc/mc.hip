@@ -11,8 +11,12 @@ using namespace cbf;
 
 namespace {
 
+// 3 waves per SIMD: the unrolled Seidel solve wants ~197 VGPRs (2 waves/SIMD); capped at 168 the
+// compiler spills ~116 B per lane, and the third wave hides more than the spills cost: 1.62 ->
+// 1.32 ms per 10 timesteps at 100 k scenarios (4 waves, 128 VGPRs and 272 B spilled: 1.93 ms;
+// the rolled LDS solve at 101 VGPRs: 2.21 ms).  Bit-identical (tests/test_gpu_parity.py).
 template <bool FZ>
-__global__ void __launch_bounds__(kBlock) k_mc_rollout(KP P, int n_scen, int n_o, int n_a, int steps, double T,
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3, 3))) k_mc_rollout(KP P, int n_scen, int n_o, int n_a, int steps, double T,
                                                        double rc, double rs, double so, double ga,
                                                        double2* __restrict__ pos, long long* __restrict__ counters,
                                                        double* __restrict__ maxviol, double* __restrict__ safety) {
