@@ -71,7 +71,8 @@ def full_size_check(S, args):
     pos0 = S.pos.clone()
     S.step()
     torch.cuda.synchronize()
-    vel = swarm.consensus_lattice(pos0, S.W, S.H, S.gain)
+    # the nominal control of that step: recomputed for the consensus, the step's own for cfg4r
+    vel = swarm.consensus_lattice(pos0, S.W, S.H, S.gain) if S.nominal is None else S.vel.clone()
     out = swarm.filter_swarm(S.params, pos0, vel, 0, method="cells", grid=S.grid, diag=True)
     st = out["status"]
     opt = (st & 0xFF) == 1
@@ -110,12 +111,14 @@ def bench_lattice(args, ws, rank, local):
     rows = args.rows
     if ws > 1 or args.shard:
         from cbf_amd.shard import ShardedLattice
-        S = ShardedLattice(W, rows, seed=args.seed, substeps=args.substeps, spacing=args.spacing, gain=args.gain)
+        S = ShardedLattice(W, rows, seed=args.seed, substeps=args.substeps, spacing=args.spacing, gain=args.gain,
+                           nominal=args.nominal)
     else:
         pos = scenarios.lattice(W, rows, seed=args.seed, spacing=args.spacing)
-        S = swarm.LatticeSwarm(pos, W, rows, gain=args.gain, barrier=args.barrier)
-    # the sharded path stays eager: per-sub-step graph replays measured slower than eager
-    # launches (110 vs 104 us per step at one rank, 4 sub-steps per exchange)
+        S = swarm.LatticeSwarm(pos, W, rows, gain=args.gain, barrier=args.barrier, nominal=args.nominal)
+    # the sharded path stays eager: one cbf_lattice_cycle_sharded call per exchange cycle; a
+    # hipGraph of the cycle (ShardedLattice.capture_cycle) measured the same (93.9 vs 93.1 us/step
+    # at one rank), and capturing beside an RCCL communicator is avoided
     use_graph = not args.eager and not (ws > 1 or args.shard)
     # single GPU, reference barrier: the timesteps run as cbf_lattice_run calls of `chunk`
     # timesteps (bit-identical to as many cbf_lattice_step calls; each advance bins the next
@@ -216,8 +219,10 @@ def bench_lattice(args, ws, rank, local):
         "dtype": "f64",
         "data": "synthetic",
         "config": {"workload": f"{args.config}: {W}x{rows * ws} jittered lattice swarm (spacing {args.spacing}), "
-                               f"lattice-Laplacian consensus (gain {args.gain}) + radius-0.2 cell-list cull + CBF QP "
-                               "+ clip + Euler, one fused timestep per step", "barrier": args.barrier,
+                               + (f"lattice-Laplacian consensus (gain {args.gain})" if args.nominal is None else
+                                  f"random-walk nominal control (amplitude {args.nominal[1]}, CBF_NOMINAL_RANDOM)")
+                               + " + radius-0.2 cell-list cull + CBF QP + clip + Euler, one fused timestep per step",
+                   "barrier": args.barrier,
                    "agents_total": n_total, "agents_per_gpu": n_local,
                    "parallelism": f"row-stripe shards x{ws}, 1 RCCL all-gather of ghost-row slabs per "
                                   f"{args.substeps} steps" if (ws > 1 or args.shard) else "single GPU",
@@ -432,9 +437,10 @@ def _reduce(elapsed, solves, ws):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--config", default="cfg4", choices=["cfg4", "cfg4f", "cfg3", "cfg5", "cert"],
-                    help="cfg4f: the cfg4 swarm at spacing 0.2 (= dmin), where most QPs are feasible and "
-                         "barrier rows bind (the exact QP path at scale)")
+    ap.add_argument("--config", default="cfg4", choices=["cfg4", "cfg4f", "cfg4r", "cfg3", "cfg5", "cert"],
+                    help="cfg4f: the cfg4 swarm at spacing 0.2 (= dmin), where most QPs are feasible; cfg4r: "
+                         "spacing 0.22 with random-walk nominal controls (amplitude 1), where most QPs are "
+                         "feasible AND a barrier row binds (the exact QP path at scale)")
     ap.add_argument("--spacing", type=float, default=None, help="lattice spacing (cfg4 0.145, cfg4f 0.2)")
     ap.add_argument("--gain", type=float, default=None, help="lattice consensus gain (default 0.25)")
     ap.add_argument("--cert-scenarios", type=int, default=100000)
@@ -466,7 +472,8 @@ def main():
     args = ap.parse_args()
     from cbf_amd import scenarios as _sc
     if args.spacing is None:
-        args.spacing = 0.2 if args.config == "cfg4f" else _sc.LATTICE_SPACING
+        args.spacing = {"cfg4f": 0.2, "cfg4r": 0.22}.get(args.config, _sc.LATTICE_SPACING)
+    args.nominal = ("random", 1.0, args.seed) if args.config == "cfg4r" else None
     if args.gain is None:
         args.gain = _sc.LATTICE_GAIN
     # stdout carries exactly one JSON line: everything else that writes to fd 1 (RCCL prints a

@@ -83,6 +83,7 @@ SIGNATURES = {
     "cbf_consensus_lattice": (C.c_int, [_i32, _i32, _i32, _i32, _i32, _vp, _d, _vp, _vp]),
     "cbf_euler": (C.c_int, [_i32, _vp, _vp, _d, _vp]),
     "cbf_lattice_workspace_size": (_sz, [_i32, _i32, _G]),
+    "cbf_lattice_set_nominal": (C.c_int, [_vp, _sz, _i32, _d, C.c_uint64, _vp]),
     "cbf_lattice_step": (C.c_int, [_P, _G, _i32, _i32, _i32, _i32, _i32, _i32, _vp, _d, _d, _vp, _vp, _vp, _vp,
                                    _vp, _i32, _vp, _vp, _vp, _sz, _vp]),
     "cbf_lattice_cycle_sharded": (C.c_int, [_P, _G, _i32, _i32, _i32, _i32, _i32, _i32, _i32, _i32, _vp, _d, _d,

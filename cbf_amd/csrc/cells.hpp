@@ -54,7 +54,8 @@ inline size_t align256(size_t b) { return (b + 255) & ~size_t(255); }
 struct CellWs {
     int32_t* sctl;    // [64] control: [1] scan epoch, [2] error flag of this build (scan look-back
                       // gave up, or workspace shape mismatch), [4] n, [5] ncell: the shape the
-                      // workspace is bound to (0 = fresh)
+                      // workspace is bound to (0 = fresh); [8] lattice nominal-control mode, bytes
+                      // 40..55 its amplitude (double) and seed (uint64) (cbf_lattice_set_nominal)
     int32_t* count;   // [ncell]
     int32_t* start;   // [ncell + 1]
     unsigned long long* tstate;  // [ntiles] scan tile status {epoch:30 | flag:2 | value:32}
@@ -120,6 +121,21 @@ void launch_scan(const CellWs& W, hipStream_t s);
 // would corrupt the cell list, so a mismatch sets the error flag (every ego of the step reports
 // CBF_STATUS_WORKSPACE_ERROR) and stays bound to the old shape, so later calls fail the same way
 // until the caller zero-fills the workspace.
+// The lattice nominal-control spec in a workspace's control words (cbf_lattice_set_nominal):
+// mode 0 (the zero-filled default) = lattice-Laplacian consensus with the call's gain.
+struct NominalSpec {
+    int mode;
+    double amp;
+    unsigned long long seed;
+};
+__device__ __forceinline__ NominalSpec nominal_spec(const int32_t* sctl) {
+    NominalSpec N;
+    N.mode = sctl[8];
+    N.amp = reinterpret_cast<const double*>(sctl)[5];
+    N.seed = reinterpret_cast<const unsigned long long*>(sctl)[6];
+    return N;
+}
+
 __device__ __forceinline__ void build_begin(int32_t* sctl, long n, long ncell) {
     sctl[1] = (sctl[1] + 1) & 0x3FFFFFFF;
     const bool fresh = sctl[4] == 0 && sctl[5] == 0;

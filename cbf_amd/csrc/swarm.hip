@@ -141,6 +141,27 @@ __device__ __forceinline__ double2 lattice_sum(const double2* __restrict__ pos, 
     return make_double2(a0, a1);
 }
 
+// CBF_NOMINAL_RANDOM: a random-walk nominal control, a pure function of (seed, global agent
+// index, the bits of the agent's current position): splitmix64 finalisers chained over the three
+// words; each component amp (2 U - 1) with U = (h >> 11) 2^-53 (2 U - 1 is exact, so the only
+// rounding is the product).  The position changes every step, so each step draws afresh, with no
+// step counter; any sharding of the lattice draws the same values.  Restated in
+// oracle/pyoracle.py:random_nominal.
+__device__ __forceinline__ unsigned long long mix64(unsigned long long z) {
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+__device__ __forceinline__ double2 random_nominal(const NominalSpec& N, long g, double2 p) {
+    unsigned long long h = mix64(N.seed + 0x9E3779B97F4A7C15ull * (unsigned long long)(g + 1));
+    h = mix64(h ^ (unsigned long long)__double_as_longlong(p.x));
+    h = mix64(h ^ (unsigned long long)__double_as_longlong(p.y));
+    const unsigned long long h2 = mix64(h + 0x9E3779B97F4A7C15ull);
+    const double v0 = 2.0 * ((double)(h >> 11) * 0x1p-53) - 1.0;
+    const double v1 = 2.0 * ((double)(h2 >> 11) * 0x1p-53) - 1.0;
+    return make_double2(N.amp * v0, N.amp * v1);
+}
+
 __global__ void __launch_bounds__(kBlock) k_consensus_lattice(int W, int H, int row_begin, int row_end, int pos_row0,
                                                               const double2* __restrict__ pos, double scale,
                                                               double2* __restrict__ out) {
@@ -268,12 +289,18 @@ __global__ void __launch_bounds__(kBlock) k_lattice_scatter_ordered(long nwin, l
     // an unusable build (build_begin / scan timeout): no scatter
     const int3 b = (t < nrec && sctl[2] == 0) ? bcs[t] : make_int3(-1, 0, 0);
     const int d = b.x >= 0 ? start[b.x] + b.y : -1;
+    const NominalSpec N = nominal_spec(sctl);
     if (d >= 0 && d < nwin) {
         const double2 p = pos[b.z];
         spos[d] = p;
         const int r = win_row0 + b.z / W, c = b.z % W;
-        const double2 a = lattice_sum(pos, b.z, r, c, W, H);
-        const double2 u0 = make_double2(a.x * gain, a.y * gain);
+        double2 u0;
+        if (N.mode == CBF_NOMINAL_RANDOM) {
+            u0 = random_nominal(N, (long)win_row0 * W + b.z, p);
+        } else {
+            const double2 a = lattice_sum(pos, b.z, r, c, W, H);
+            u0 = make_double2(a.x * gain, a.y * gain);
+        }
         svel[d] = u0;
         if (vel_out && r >= row_begin && r < row_end) vel_out[(long)(r - row_begin) * W + c] = u0;
         sidx[d] = b.z;
@@ -665,6 +692,22 @@ extern "C" int cbf_euler(int32_t n, double* pos, const double* vel, double T, vo
     return (int)hipGetLastError();
 }
 
+
+__global__ void k_set_nominal(int32_t* sctl, int mode, double amp, unsigned long long seed) {
+    sctl[8] = mode;
+    reinterpret_cast<double*>(sctl)[5] = amp;
+    reinterpret_cast<unsigned long long*>(sctl)[6] = seed;
+}
+
+extern "C" int cbf_lattice_set_nominal(void* workspace, size_t workspace_bytes, int32_t mode, double amp,
+                                       uint64_t seed, void* stream) {
+    if (!workspace || workspace_bytes < 256) return CBF_EINVAL;
+    if (mode != CBF_NOMINAL_CONSENSUS && mode != CBF_NOMINAL_RANDOM) return CBF_EINVAL;
+    if (mode == CBF_NOMINAL_RANDOM && !(amp >= 0.0 && amp <= 1e300)) return CBF_EINVAL;
+    hipLaunchKernelGGL(k_set_nominal, dim3(1), dim3(1), 0, (hipStream_t)stream, (int32_t*)workspace, (int)mode, amp,
+                       (unsigned long long)seed);
+    return (int)hipGetLastError();
+}
 
 extern "C" size_t cbf_lattice_workspace_size(int32_t W, int32_t win_rows, const cbf_grid* grid) {
     if (!grid || W <= 0 || win_rows <= 0 || grid->nx <= 0 || grid->ny <= 0) return 0;

@@ -77,7 +77,7 @@ class Sub:
 class HipBackend:
     """Device work of one rank through libcbf_amd.so."""
 
-    def __init__(self, W, H, gain, T, params, grid, win_rows, nsub=1):
+    def __init__(self, W, H, gain, T, params, grid, win_rows, nsub=1, nominal=None):
         import torch
         from . import _lib, swarm
         self.torch, self._lib, self.swarm = torch, _lib, swarm
@@ -92,6 +92,8 @@ class HipBackend:
         # contiguous so that a whole cycle can run in one cbf_lattice_cycle_sharded call
         self.ws_all = torch.zeros((nsub * self.ws_bytes,), dtype=torch.uint8, device=self.dev)
         self.wss = [self.ws_all[s * self.ws_bytes:(s + 1) * self.ws_bytes] for s in range(nsub)]
+        for w in self.wss:
+            swarm.set_nominal(w, nominal)
         self.flag = torch.zeros((1,), dtype=torch.int32, device=self.dev)
         # the guard flag is read back asynchronously after every exchange: a pinned host copy per
         # exchange in flight, polled (never waited on) at the next exchanges
@@ -173,7 +175,8 @@ class ShardedLattice:
     """One rank's stripe of a W x (rows_per_rank * world) lattice swarm (see module docstring)."""
 
     def __init__(self, W, rows_per_rank, seed=0, halo=4, substeps=4, gain=scenarios.LATTICE_GAIN, T=scenarios.T,
-                 params=None, backend=None, group=None, pos_global=None, spacing=scenarios.LATTICE_SPACING):
+                 params=None, backend=None, group=None, pos_global=None, spacing=scenarios.LATTICE_SPACING,
+                 nominal=None):
         import torch
         import torch.distributed as dist
         from .swarm import FilterParams, make_grid
@@ -202,7 +205,7 @@ class ShardedLattice:
         grid = make_grid(-1.0 - a, self.w0 * a - 1.0 - a, W * a + 1.0, self.w1 * a + 1.0,
                          self.params.safety_distance * 1.02)
         if backend is None:
-            backend = HipBackend(W, self.H, gain, T, self.params, grid, self.win_rows, substeps)
+            backend = HipBackend(W, self.H, gain, T, self.params, grid, self.win_rows, substeps, nominal)
         self.be = backend
         t = backend.tensor
         self.wpos = t(win)
@@ -227,7 +230,8 @@ class ShardedLattice:
         self.recv = t(np.zeros(self.stride * self.ws))
         self.use_list_gather = dist.get_backend(group) == "gloo"
         self.graph = None
-        self.sub = 0   # next sub-step of the current exchange cycle
+        self.cycle_graph = None
+        self.sub = 0  # next sub-step of the current exchange cycle
 
     # ---- one timestep -------------------------------------------------------------------------
     def _gather(self):
@@ -268,12 +272,16 @@ class ShardedLattice:
 
     def run(self, steps):
         """`steps` timesteps; whole exchange cycles run as one device call each (the same results
-        as `steps` step() calls), the rest one sub-step at a time."""
+        as `steps` step() calls; one hipGraph replay after capture_cycle()), the rest one sub-step
+        at a time."""
         done = 0
         while done < steps:
             if self.sub == 0 and steps - done >= self.k and hasattr(self.be, "lattice_cycle"):
                 self.exchange()
-                self.be.lattice_cycle(self)
+                if self.cycle_graph is not None:
+                    self.cycle_graph.replay()
+                else:
+                    self.be.lattice_cycle(self)
                 done += self.k
             else:
                 self.step()
@@ -300,6 +308,21 @@ class ShardedLattice:
             graphs.append(g)
         self.graph = graphs
         return graphs
+
+    def capture_cycle(self):
+        """Capture one whole exchange cycle's device work (the cbf_lattice_cycle_sharded call: k
+        sub-steps, ~5 launches each) into one hipGraph that run() replays after each exchange; the
+        exchange itself (pack, collective, unpack) stays eager.  Capture launches nothing, so the
+        swarm does not advance."""
+        torch = self.torch
+        if not self.own.is_cuda or not hasattr(self.be, "lattice_cycle"):
+            return None
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            self.be.lattice_cycle(self)
+        self.cycle_graph = g
+        return g
 
     def reset_solves(self):
         self.stats.zero_()

@@ -231,13 +231,26 @@ class GroupSwarm:
         return out
 
 
+def set_nominal(ws, nominal):
+    """Bind a lattice workspace's nominal control (cbf_lattice_set_nominal): None or "consensus",
+    or ("random", amp, seed).  Returns the normalised spec."""
+    if nominal is None or nominal == "consensus":
+        return None
+    kind, amp, seed = nominal
+    if kind != "random":
+        raise ValueError(f"nominal must be 'consensus' or ('random', amp, seed), got {nominal!r}")
+    check(lib.cbf_lattice_set_nominal(ptr(ws), ws.numel(), 1, float(amp), int(seed) & (2 ** 64 - 1),
+                                      stream_handle()), "cbf_lattice_set_nominal")
+    return ("random", float(amp), int(seed))
+
+
 class LatticeSwarm:
     """SURVEY cfg3/cfg4: a W x H lattice swarm, one fused timestep per `step()` through
     cbf_lattice_step (nominal + cell list + filter + clip + Euler); optionally captured in a
     hipGraph.  Single-GPU: the window is the whole lattice."""
 
     def __init__(self, pos, W, H, gain=0.25, params: FilterParams = None, T=1 / 30, grid=None, margin=1.0,
-                 method="cells", barrier="reference", alpha=(1.0, 1.0)):
+                 method="cells", barrier="reference", alpha=(1.0, 1.0), nominal=None):
         torch = _lib.require_gpu()
         self.dev = torch.device("cuda")
         pos = np.asarray(pos, dtype=np.float64).reshape(W * H, 2)
@@ -261,6 +274,9 @@ class LatticeSwarm:
         self.nbr_count = torch.empty((n,), dtype=torch.int32, device=self.dev)
         self.ws_bytes = lib.cbf_lattice_workspace_size(W, H, _lib.C.byref(self.grid))
         self.ws = torch.zeros((self.ws_bytes,), dtype=torch.uint8, device=self.dev)
+        # nominal control: None / "consensus" = the lattice Laplacian (gain); ("random", amp, seed)
+        # = the synthetic random walk of include/cbf_amd.h CBF_NOMINAL_RANDOM (cell method only)
+        self.nominal = set_nominal(self.ws, nominal)
         # rollout statistics of the fused step (include/cbf_amd.h CBF_STAT_*: solves, status counts,
         # violations, minimum neighbour distance), accumulated on device by every step
         self.stats = torch.zeros((1024,), dtype=torch.int64, device=self.dev)

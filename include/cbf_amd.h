@@ -232,6 +232,19 @@ int cbf_euler(int32_t n, double* pos, const double* vel, double T, void* stream)
  */
 size_t cbf_lattice_workspace_size(int32_t W, int32_t win_rows, const cbf_grid* grid);
 
+/* The nominal control the lattice builds form (a workspace setting, stream-ordered; a zero-filled
+ * workspace holds CBF_NOMINAL_CONSENSUS).  CBF_NOMINAL_CONSENSUS: the lattice Laplacian scaled by
+ * the call's gain (cross_and_rescue.py:121-125 shape).  CBF_NOMINAL_RANDOM: a synthetic random
+ * walk, each component amp * (2 U - 1) with U in [0, 1) a hash of (seed, global agent index
+ * win_row0 W + w, the bits of the agent's current position) -- fresh every step, identical under
+ * any sharding (restated in oracle/pyoracle.py:random_nominal).  It keeps most QPs feasible with
+ * a binding barrier row (the exact-QP regime); gain is then unused.  No reference counterpart:
+ * cfg4 names a synthetic swarm, not its nominal controller. */
+#define CBF_NOMINAL_CONSENSUS 0
+#define CBF_NOMINAL_RANDOM 1
+int cbf_lattice_set_nominal(void* workspace, size_t workspace_bytes, int32_t mode, double amp, uint64_t seed,
+                            void* stream);
+
 int cbf_lattice_step(const cbf_params* p, const cbf_grid* grid, int32_t W, int32_t H, int32_t row_begin,
                      int32_t row_end, int32_t win_row0, int32_t win_rows, const double* pos, double gain, double T,
                      double* pos_out, double* vel_out, double* u, int32_t* status, int32_t* nbr_count,

@@ -359,6 +359,33 @@ def euler(pos, vel, T):
     return np.asarray(pos) + T * np.asarray(vel)
 
 
+_M1, _M2, _GOLD = np.uint64(0xBF58476D1CE4E5B9), np.uint64(0x94D049BB133111EB), np.uint64(0x9E3779B97F4A7C15)
+
+
+def _mix64(z):
+    z = (z ^ (z >> np.uint64(30))) * _M1
+    z = (z ^ (z >> np.uint64(27))) * _M2
+    return z ^ (z >> np.uint64(31))
+
+
+def random_nominal(pos, g0, amp, seed):
+    """The synthetic random-walk nominal control of the lattice builds (include/cbf_amd.h
+    CBF_NOMINAL_RANDOM; no reference counterpart -- cfg4 names a synthetic swarm, not its nominal
+    controller): for agent g0 + i at pos[i], h = splitmix64 finalisers chained over (seed + gold
+    (g + 1), bits(x), bits(y)); u0 = amp (2 U - 1) per component, U = (h >> 11) 2^-53 for x and
+    the same of mix(h + gold) for y.  Integer arithmetic mod 2^64, then one rounding (amp * v)."""
+    pos = np.ascontiguousarray(pos, dtype=np.float64).reshape(-1, 2)
+    g = np.arange(pos.shape[0], dtype=np.uint64) + np.uint64(g0 + 1)
+    with np.errstate(over="ignore"):
+        h = _mix64(np.uint64(seed) + _GOLD * g)
+        h = _mix64(h ^ pos[:, 0].copy().view(np.uint64))
+        h = _mix64(h ^ pos[:, 1].copy().view(np.uint64))
+        h2 = _mix64(h + _GOLD)
+    v0 = 2.0 * ((h >> np.uint64(11)).astype(np.float64) * 2.0 ** -53) - 1.0
+    v1 = 2.0 * ((h2 >> np.uint64(11)).astype(np.float64) * 2.0 ** -53) - 1.0
+    return np.stack([amp * v0, amp * v1], axis=1)
+
+
 # --------------------------------------------------------------------------------------
 # Euclidean HOCBF barrier mode (BASELINE.json north star (2); SURVEY 8f rank 4).
 # The reference has no such mode, so there is no reference oracle: this restatement

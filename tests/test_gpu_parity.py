@@ -276,6 +276,41 @@ def test_lattice_step_vs_oracle(spacing):
         assert want["optimal"] > 0.5 * want["solves"] and want["binding"] > 0.1 * want["solves"]
 
 
+def test_lattice_random_nominal_vs_oracle():
+    """The random-walk nominal control (CBF_NOMINAL_RANDOM, the exact-QP regime cfg4r): fused
+    steps == oracle steps bit for bit (nominal controls, controls, statuses, positions, rollout
+    statistics); most QPs are feasible with a binding row; cbf_lattice_run (chained binning) and
+    a hipGraph of run(4) give the same rollout."""
+    W, H, amp, seed = 48, 40, 1.0, 3
+    pos = scenarios.lattice(W, H, seed=5, spacing=0.22)
+    L = swarm.LatticeSwarm(pos, W, H, nominal=("random", amp, seed))
+    ref = pos.copy()
+    outs = []
+    for step in range(8):
+        L.step()
+        vel = po.random_nominal(ref, 0, amp, seed)
+        out = coracle.filter_swarm(po.Params(15), ref, vel, 0, diag=True, stats=True)
+        ref = coracle.euler(ref, out["u"], 1 / 30)
+        outs.append(out)
+        assert np.array_equal(L.vel.cpu().numpy(), vel), step
+        assert np.array_equal(L.u.cpu().numpy(), out["u"]), step
+        assert np.array_equal(L.status.cpu().numpy(), out["status"]), step
+        assert np.array_equal(L.pos.cpu().numpy(), ref), step
+    want = _oracle_stats(outs)
+    _check_stats(L.stats_summary(), want)
+    assert want["optimal"] > 0.6 * want["solves"] and want["binding"] > 0.4 * want["solves"]
+    B = swarm.LatticeSwarm(pos, W, H, nominal=("random", amp, seed))
+    B.run(3)
+    B.run(5)
+    for a, b in zip(_lattice_state(L), _lattice_state(B)):
+        assert np.array_equal(a, b)
+    D = swarm.LatticeSwarm(pos, W, H, nominal=("random", amp, seed))
+    D.capture(steps=4)              # the capture's warm-up launch runs steps 1-4
+    D.run(4)
+    for a, b in zip(_lattice_state(L), _lattice_state(D)):
+        assert np.array_equal(a, b)
+
+
 def test_lattice_graph_replay_matches_eager():
     W, H = 64, 64
     pos = scenarios.lattice(W, H, seed=9)

@@ -178,3 +178,35 @@ def test_rollout_steps_vs_golden(golden, name):
         assert np.array_equal(np.where(out["cnt"] > 0, its, 0), R["relax_iters"][t]), (name, t)
         nxt = coracle.euler(pos, ref_u, T)
         assert np.array_equal(nxt, R["pos_next"][t]), (name, t)
+
+
+def test_random_nominal_restatement():
+    """oracle random_nominal (numpy uint64) == a pure-Python integer restatement of the hash of
+    include/cbf_amd.h CBF_NOMINAL_RANDOM; values lie in [-amp, amp) and change with the position."""
+    import struct
+    from oracle import pyoracle as po
+    M = (1 << 64) - 1
+
+    def mix(z):
+        z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & M
+        z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & M
+        return z ^ (z >> 31)
+
+    def bits(v):
+        return struct.unpack("<Q", struct.pack("<d", v))[0]
+
+    rng = np.random.default_rng(3)
+    pos = rng.normal(size=(200, 2))
+    pos[0] = [0.0, -0.0]
+    amp, seed, g0 = 1.25, 0xDEADBEEFCAFEF00D, 12345
+    got = po.random_nominal(pos, g0, amp, seed)
+    for i, (x, y) in enumerate(pos):
+        h = mix((seed + 0x9E3779B97F4A7C15 * (g0 + i + 1)) & M)
+        h = mix(h ^ bits(x))
+        h = mix(h ^ bits(y))
+        h2 = mix((h + 0x9E3779B97F4A7C15) & M)
+        want = (amp * (2.0 * ((h >> 11) * 2.0 ** -53) - 1.0), amp * (2.0 * ((h2 >> 11) * 2.0 ** -53) - 1.0))
+        assert got[i, 0] == want[0] and got[i, 1] == want[1], i
+    assert np.all(np.abs(got) <= amp)
+    moved = po.random_nominal(pos + 1e-12, g0, amp, seed)
+    assert np.all(moved != got)

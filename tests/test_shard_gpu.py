@@ -25,13 +25,32 @@ def _free_port():
     return p
 
 
-def _worker(rank, ws, port, W, R, steps, q, k=4, graph=False, run=False):
+def _worker(rank, ws, port, W, R, steps, q, k=4, graph=False, run=False, nominal=None):
+    try:
+        _work(rank, ws, port, W, R, steps, q, k, graph, run, nominal)
+    except BaseException as e:   # report instead of leaving the test waiting on the queue
+        q.put((rank, "error", repr(e)))
+        raise
+
+
+def _spacing(nominal):
+    from cbf_amd import scenarios
+    return scenarios.LATTICE_SPACING if nominal is None else 0.22   # random walk: the cfg4r spacing
+
+
+def _work(rank, ws, port, W, R, steps, q, k, graph, run, nominal):
+    import datetime
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     torch.cuda.set_device(0)
-    dist.init_process_group("gloo", rank=rank, world_size=ws)
+    dist.init_process_group("gloo", rank=rank, world_size=ws, timeout=datetime.timedelta(seconds=60))
     from cbf_amd.shard import ShardedLattice
-    S = ShardedLattice(W, R, seed=7, substeps=k)
-    if graph:
+    # the random walk's RELAXED QPs can move an agent up to T * max_speed = 0.5 per step (the
+    # guard catches it with the default 4-row halo): 10 rows per sub-step cover it
+    S = ShardedLattice(W, R, seed=7, substeps=k, nominal=nominal, spacing=_spacing(nominal),
+                       halo=4 if nominal is None else 10)
+    if graph == "cycle":   # whole exchange cycles replayed as one hipGraph each
+        S.capture_cycle()
+    elif graph:
         S.capture()
     S.reset_solves()
     if run:      # whole cycles through cbf_lattice_cycle_sharded (chained sub-steps), the rest by step()
@@ -46,28 +65,36 @@ def _worker(rank, ws, port, W, R, steps, q, k=4, graph=False, run=False):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("ws,k,graph,run", [(2, 1, False, False), (3, 4, False, False), (2, 4, True, False),
-                                            (3, 4, False, True), (2, 2, False, True)])
-def test_sharded_equals_single_gpu(ws, k, graph, run):
+RANDOM = ("random", 1.0, 3)   # the random-walk nominal control (CBF_NOMINAL_RANDOM)
+
+
+@pytest.mark.parametrize("ws,k,graph,run,nominal", [(2, 1, False, False, None), (3, 4, False, False, None),
+                                                    (2, 4, True, False, None), (3, 4, False, True, None),
+                                                    (2, 2, False, True, None), (2, 4, "cycle", True, None),
+                                                    (2, 2, False, True, RANDOM)])
+def test_sharded_equals_single_gpu(ws, k, graph, run, nominal):
     from cbf_amd import scenarios, swarm
     W, R, steps = 96, 40, 6
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, ws, port, W, R, steps, q, k, graph, run)) for r in range(ws)]
+    procs = [ctx.Process(target=_worker, args=(r, ws, port, W, R, steps, q, k, graph, run, nominal))
+             for r in range(ws)]
     for p in procs:
         p.start()
-    res = sorted([q.get(timeout=300) for _ in range(ws)], key=lambda t: t[0])
+    res = sorted([q.get(timeout=120) for _ in range(ws)], key=lambda t: t[0])
+    assert not any(isinstance(r[1], str) for r in res), res
     for p in procs:
         p.join(timeout=120)
         assert p.exitcode == 0
     H = R * ws
     # the oracle's rollout of the whole lattice (test infrastructure, oracle/)
     from oracle import coracle, pyoracle as po
-    pos = scenarios.lattice(W, H, seed=7)
+    pos = scenarios.lattice(W, H, seed=7, spacing=_spacing(nominal))
     solves = optimal = relaxed = 0
     for _ in range(steps):
-        vel = coracle.consensus_lattice(W, H, 0, H, pos, scenarios.LATTICE_GAIN)
+        vel = coracle.consensus_lattice(W, H, 0, H, pos, scenarios.LATTICE_GAIN) if nominal is None else \
+            po.random_nominal(pos, 0, nominal[1], nominal[2])
         out = coracle.filter_swarm(po.Params(15), pos, vel, 0)
         pos = coracle.euler(pos, out["u"], scenarios.T)
         solves += int((out["cnt"] > 0).sum())
@@ -79,7 +106,7 @@ def test_sharded_equals_single_gpu(ws, k, graph, run):
     assert sum(r[4]["solves"] for r in res) == solves
     assert sum(r[4]["optimal"] for r in res) == optimal and sum(r[4]["relaxed"] for r in res) == relaxed
     # and the single-GPU fused step of the whole lattice
-    L = swarm.LatticeSwarm(scenarios.lattice(W, H, seed=7), W, H)
+    L = swarm.LatticeSwarm(scenarios.lattice(W, H, seed=7, spacing=_spacing(nominal)), W, H, nominal=nominal)
     for _ in range(steps):
         L.step()
     torch.cuda.synchronize()

@@ -81,10 +81,18 @@ def main(prof, rnd):
         if not os.path.exists(os.path.join(prof, cfg, "trace", "run_kernel_stats.csv")):
             continue
         allk[cfg] = summarize(prof, cfg, rnd)
-    with open(os.path.join(ROOT, "profiles", f"{rnd}_pmc.json"), "w") as f:
-        json.dump(allk, f, indent=1, sort_keys=True)
-    with open(os.path.join(ROOT, "profiles", "pmc_summary.json"), "w") as f:
-        json.dump({"round": rnd, **allk}, f, indent=1, sort_keys=True)
+    # merged per config into what is already there (a run may profile a subset of the configs)
+    for name, extra in ((f"{rnd}_pmc.json", {}), ("pmc_summary.json", {"round": rnd})):
+        path = os.path.join(ROOT, "profiles", name)
+        try:
+            with open(path) as f:
+                old = json.load(f)
+        except (OSError, ValueError):
+            old = {}
+        old.update(allk)
+        old.update(extra)
+        with open(path, "w") as f:
+            json.dump(old, f, indent=1, sort_keys=True)
     for cfg, ks in allk.items():
         print(cfg)
         for k, e in sorted(ks.items(), key=lambda kv: -(kv[1].get("avg_duration_ns") or 0)):
