@@ -3,7 +3,7 @@ set -o pipefail
 export TMPDIR=/tmp
 OUT=gpurun_out/prof_shard
 mkdir -p $OUT
-timeout -k 10 200 rocprofv3 --kernel-trace --stats -f csv -d $OUT -o run -- python3 bench.py --shard --substeps 4 --steps 100 --warmup 10 --no-cpu-baseline --kernel-iters 5 > $OUT/log 2>&1 || { tail $OUT/log; exit 1; }
+timeout -k 10 200 rocprofv3 --kernel-trace --stats -f csv -d $OUT -o run -- python3 bench.py --shard --steps 96 --warmup 10 --no-cpu-baseline --kernel-iters 5 > $OUT/log 2>&1 || { tail $OUT/log; exit 1; }
 python3 - <<'PY'
 import csv
 for r in csv.DictReader(open("gpurun_out/prof_shard/run_kernel_stats.csv")):
