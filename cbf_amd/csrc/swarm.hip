@@ -21,56 +21,65 @@ struct ExtSpec {
     int own_begin, own_end, guard;
 };
 
-// Halo-guard y-extents of one block's agents into slot (slot & 511) of an extents set (e[] per
-// lane: {min, max} over the computed rows, {max below the guard, min above it, min, max} over the
-// owned rows; y = the lane's y where any).  Each wave reduces its own; the LAST wave of the block
-// to arrive (an LDS counter, `arrive`, zeroed by the caller before a block barrier at kernel start)
-// combines the NW partials and issues one atomic per non-identity value.  No barrier at the end
-// (it would hold every wave until the block's slowest is done), and a quarter of the per-wave
-// atomics.  ONE: each lane holds at most one agent (its e[] are
-// y or infinite, which allows a two-reduction fast path).  Every lane of the wave must call it.
+// Halo-guard y-extents of one block's agents into slot (slot & (kExtSlots - 1)) of an extents
+// set (e[] per lane: {min, max} over the computed rows, {max below the guard, min above it, min,
+// max} over the owned rows; y = the lane's y where any).  The values travel as dkey()s (order-
+// preserving uint64 keys, the form the slots hold), so each wave reduces them with 32-bit DPP
+// reductions (wave_umin64 / wave_umax64) instead of 64-bit shuffle trees through LDS; a NaN y
+// keys above +inf, so it wins a maximum and fails the guard (conservative).  The LAST wave of the
+// block to arrive (an LDS counter, `arrive`, zeroed by the caller before a block barrier at
+// kernel start) combines the NW partials and issues one atomic per non-identity value.  No
+// barrier at the end (it would hold every wave until the block's slowest is done), and a quarter
+// of the per-wave atomics.  ONE: each lane holds at most one agent (its e[] are y or infinite,
+// which allows a two-reduction fast path).  Every lane of the wave must call it.
 template <int NW, bool ONE = true>
 __device__ __forceinline__ void ext_keys_flush(double (&e)[6], int any, double y,
                                                unsigned long long* __restrict__ ext_keys, long slot,
-                                               double (*red)[NW], int* arrive) {
+                                               unsigned long long (*red)[NW], int* arrive) {
+    const unsigned long long kmin_id = dkey(INFINITY), kmax_id = dkey(-INFINITY);
     const unsigned long long act = __ballot(any);
     const unsigned code = any ? ((e[0] != INFINITY ? 1u : 0u) | (e[2] != -INFINITY ? 2u : 0u) |
                                  (e[3] != INFINITY ? 4u : 0u) | (e[4] != INFINITY ? 8u : 0u))
                               : 0u;
     const unsigned c0 = (unsigned)__shfl((int)code, act ? __ffsll((long long)act) - 1 : 0, 64);
+    unsigned long long k[6];
     if (!act) {
 #pragma unroll
-        for (int q = 0; q < 6; ++q) e[q] = ext_is_min(q) ? INFINITY : -INFINITY;
+        for (int q = 0; q < 6; ++q) k[q] = ext_is_min(q) ? kmin_id : kmax_id;
     } else if (ONE && __ballot(any && code != c0) == 0) {
         // the common wave: one membership pattern for all its agents, two reductions instead of six
-        const double mn = wave_min(any ? y : INFINITY), mx = wave_max(any ? y : -INFINITY);
-        e[0] = (c0 & 1u) ? mn : INFINITY;
-        e[1] = (c0 & 1u) ? mx : -INFINITY;
-        e[2] = (c0 & 2u) ? mx : -INFINITY;
-        e[3] = (c0 & 4u) ? mn : INFINITY;
-        e[4] = (c0 & 8u) ? mn : INFINITY;
-        e[5] = (c0 & 8u) ? mx : -INFINITY;
+        const unsigned long long ky = dkey(y);
+        const unsigned long long mn = wave_umin64(any ? ky : kmin_id), mx = wave_umax64(any ? ky : kmax_id);
+        k[0] = (c0 & 1u) ? mn : kmin_id;
+        k[1] = (c0 & 1u) ? mx : kmax_id;
+        k[2] = (c0 & 2u) ? mx : kmax_id;
+        k[3] = (c0 & 4u) ? mn : kmin_id;
+        k[4] = (c0 & 8u) ? mn : kmin_id;
+        k[5] = (c0 & 8u) ? mx : kmax_id;
     } else {
 #pragma unroll
-        for (int q = 0; q < 6; ++q) e[q] = ext_is_min(q) ? wave_min(e[q]) : wave_max(e[q]);
+        for (int q = 0; q < 6; ++q) k[q] = ext_is_min(q) ? wave_umin64(dkey(e[q])) : wave_umax64(dkey(e[q]));
     }
     if ((threadIdx.x & 63) != 0) return;
     const int wid = threadIdx.x >> 6;
 #pragma unroll
-    for (int q = 0; q < 6; ++q) red[q][wid] = e[q];
+    for (int q = 0; q < 6; ++q) red[q][wid] = k[q];
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     if (atomicAdd(arrive, 1) != NW - 1) return;  // not the last wave of the block
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
     for (int v = 0; v < NW; ++v)
 #pragma unroll
-        for (int q = 0; q < 6; ++q) e[q] = ext_is_min(q) ? pmin(e[q], red[q][v]) : pmax(e[q], red[q][v]);
-    unsigned long long* k = ext_keys + kExtSlotWords * (slot & (kExtSlots - 1));
+        for (int q = 0; q < 6; ++q) {
+            const unsigned long long x = red[q][v];
+            k[q] = ext_is_min(q) ? (x < k[q] ? x : k[q]) : (x > k[q] ? x : k[q]);
+        }
+    unsigned long long* ks = ext_keys + kExtSlotWords * (slot & (kExtSlots - 1));
 #pragma unroll
     for (int q = 0; q < 6; ++q) {
         if (ext_is_min(q)) {
-            if (e[q] != INFINITY) atomicMin(&k[q], dkey(e[q]));
-        } else if (e[q] != -INFINITY) {
-            atomicMax(&k[q], dkey(e[q]));
+            if (k[q] != kmin_id) atomicMin(&ks[q], k[q]);
+        } else if (k[q] != kmax_id) {
+            atomicMax(&ks[q], k[q]);
         }
     }
 }
@@ -194,7 +203,7 @@ __global__ void __launch_bounds__(kBlock) k_lattice_nominal_bin_ordered(
     const long t = (long)xcd_block() * kBlock + threadIdx.x;
     const long nwin = (long)win_rows * W;
     if (t == 0) build_begin(sctl, nwin, ncell);
-    __shared__ double red[6][kBlock / 64];
+    __shared__ unsigned long long red[6][kBlock / 64];
     __shared__ int arrive;
     if (ext_keys) {
         if (threadIdx.x == 0) arrive = 0;
@@ -268,7 +277,7 @@ __global__ void __launch_bounds__(kBlock) k_lattice_scatter_ordered(long nwin, l
                                                                     unsigned long long* __restrict__ ext_keys, ExtSpec X) {
     // ext_keys (a chained build of the sharded cycle, whose bin pass ran in the previous advance):
     // the halo-guard extents of this build's input positions, as the bin kernel computes them
-    __shared__ double red[6][kBlock / 64];
+    __shared__ unsigned long long red[6][kBlock / 64];
     __shared__ int arrive;
     if (ext_keys) {
         if (threadIdx.x == 0) arrive = 0;
