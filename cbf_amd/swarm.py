@@ -276,6 +276,8 @@ class LatticeSwarm:
         self.ws = torch.zeros((self.ws_bytes,), dtype=torch.uint8, device=self.dev)
         # nominal control: None / "consensus" = the lattice Laplacian (gain); ("random", amp, seed)
         # = the synthetic random walk of include/cbf_amd.h CBF_NOMINAL_RANDOM (cell method only)
+        if nominal not in (None, "consensus") and method != "cells":
+            raise ValueError("a random-walk nominal control needs the cell method (the lattice builds form it)")
         self.nominal = set_nominal(self.ws, nominal)
         # rollout statistics of the fused step (include/cbf_amd.h CBF_STAT_*: solves, status counts,
         # violations, minimum neighbour distance), accumulated on device by every step
