@@ -86,7 +86,8 @@ SIGNATURES = {
     "cbf_lattice_set_nominal": (C.c_int, [_vp, _sz, _i32, _d, C.c_uint64, _vp]),
     "cbf_lattice_step": (C.c_int, [_P, _G, _i32, _i32, _i32, _i32, _i32, _i32, _vp, _d, _d, _vp, _vp, _vp, _vp,
                                    _vp, _i32, _vp, _vp, _vp, _sz, _vp]),
-    "cbf_lattice_cycle_sharded": (C.c_int, [_P, _G, _i32, _i32, _i32, _i32, _i32, _i32, _i32, _i32, _vp, _d, _d,
+    "cbf_lattice_cycle_sharded": (C.c_int, [_P, _G, _i32, _i32, _i32, _i32, _i32, _i32, _i32, _i32, _i32, _i32,
+                                            _vp, _d, _d,
                                             _vp, _vp, _vp, _vp, _vp, _vp, _vp, _sz, _vp]),
     "cbf_lattice_run": (C.c_int, [_P, _G, _i32, _i32, _vp, _d, _d, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _sz, _vp]),
     "cbf_lattice_build": (C.c_int, [_P, _G, _i32, _i32, _i32, _i32, _i32, _i32, _vp, _d, _vp, _vp, _sz, _vp]),

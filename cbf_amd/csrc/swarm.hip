@@ -881,12 +881,13 @@ extern "C" int cbf_lattice_run(const cbf_params* p, const cbf_grid* grid, int32_
 // cbf_lattice_step_sharded calls with the same geometry.
 extern "C" int cbf_lattice_cycle_sharded(const cbf_params* p, const cbf_grid* grid, int32_t W, int32_t H,
                                          int32_t own_begin, int32_t own_end, int32_t halo, int32_t nsub,
+                                         int32_t sub_begin, int32_t sub_end,
                                          int32_t win_row0, int32_t win_rows, double* wpos, double gain, double T,
                                          double* wvel, double* wu, int32_t* wstatus, int32_t* wcnt,
                                          uint64_t* ext_keys, uint64_t* stats, void* workspaces, size_t ws_bytes,
                                          void* stream) {
     if (!p || !grid || W <= 0 || H <= 0 || halo < 2 || nsub < 1 || own_begin < 0 || own_end > H ||
-        own_begin >= own_end)
+        own_begin >= own_end || sub_begin < 0 || sub_end > nsub || sub_begin >= sub_end)
         return CBF_EINVAL;
     const long G = (long)halo * nsub;
     if (G > own_end - own_begin) return CBF_EINVAL;
@@ -913,21 +914,21 @@ extern "C" int cbf_lattice_cycle_sharded(const cbf_params* p, const cbf_grid* gr
         sub(k - 1, pa, pb, pw0, pw1, pg);
         if (12l * (pw1 - pw0) > 16l * (w1k - w0k)) return CBF_EINVAL;
     }
-    for (int k = 0; k < nsub; ++k) {
+    for (int k = sub_begin; k < sub_end; ++k) {
         int a, b, sw0, sw1, guard;
         sub(k, a, b, sw0, sw1, guard);
         void* ws = (char*)workspaces + (size_t)k * ws_bytes;
         // the per-sub-step outputs (nominal / filtered control, status, count) are written by the
-        // last sub-step only: its rows are the owned rows, the earlier ones' would be overwritten
-        // there (and the ghost rows' are not outputs)
-        const bool last = k + 1 == nsub;
+        // call's last sub-step only: the earlier ones' would be overwritten there (its computed rows
+        // contain the owned rows; the ghost rows' are not outputs)
+        const bool last = k + 1 == sub_end;
         double* spos = wpos + 2l * (sw0 - win_row0) * W;
         const long o = (long)(a - win_row0) * W;
         unsigned long long* ek = reinterpret_cast<unsigned long long*>(ext_keys) + (size_t)k * set_words;
         int rc;
-        if (k == 0) {
+        if (k == sub_begin) {
             rc = lattice_build(p, grid, W, H, a, b, sw0, sw1 - sw0, spos, gain, wvel + 2 * o, ws, ws_bytes, ek,
-                               ExtSpec{own_begin, own_end, guard}, stream);  // (vel_out: sub-step 0 must)
+                               ExtSpec{own_begin, own_end, guard}, stream);  // (vel_out: the bin build must)
         } else {
             rc = check_lattice(p, grid, W, H, a, b, sw0, sw1 - sw0, spos, ws, ws_bytes);
             if (!rc) {
@@ -942,7 +943,7 @@ extern "C" int cbf_lattice_cycle_sharded(const cbf_params* p, const cbf_grid* gr
         }
         if (rc) return rc;
         ChainSpec C;
-        if (k + 1 < nsub) {
+        if (!last) {
             int na, nb, nw0, nw1, ng;
             sub(k + 1, na, nb, nw0, nw1, ng);
             C = make_chain(grid, W, H, sw0, nw0, nw1 - nw0, (char*)workspaces + (size_t)(k + 1) * ws_bytes);

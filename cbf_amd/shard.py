@@ -126,12 +126,13 @@ class HipBackend:
             P(S.wstatus[o:]), P(S.wcnt[o:]), sub.guard, P(self.ext_keys[s * self.set_words:]), P(S.stats),
             P(self.wss[s]), self.ws_bytes, L.stream_handle()), "cbf_lattice_step_sharded")
 
-    def lattice_cycle(self, S):
-        """All nsub sub-steps of one exchange cycle (cbf_lattice_cycle_sharded: the sub-steps after
-        the first are binned by the previous sub-step's advance)."""
+    def lattice_cycle(self, S, s0=0, s1=None):
+        """Sub-steps [s0, s1) of an exchange cycle, by default all nsub (cbf_lattice_cycle_sharded:
+        the sub-steps after the first are binned by the previous sub-step's advance)."""
         L, P = self._lib, self._lib.ptr
+        s1 = self.nsub if s1 is None else s1
         L.check(L.lib.cbf_lattice_cycle_sharded(
-            self.cp, L.C.byref(self.grid), self.W, self.H, S.rb, S.re, S.halo, self.nsub, S.w0, S.win_rows,
+            self.cp, L.C.byref(self.grid), self.W, self.H, S.rb, S.re, S.halo, self.nsub, s0, s1, S.w0, S.win_rows,
             P(S.wpos), self.gain, self.T, P(S.wvel), P(S.wu), P(S.wstatus), P(S.wcnt), P(self.ext_keys),
             P(S.stats), P(self.ws_all), self.ws_bytes, L.stream_handle()), "cbf_lattice_cycle_sharded")
 
@@ -271,21 +272,25 @@ class ShardedLattice:
         self.sub = (self.sub + 1) % self.k
 
     def run(self, steps):
-        """`steps` timesteps; whole exchange cycles run as one device call each (the same results
-        as `steps` step() calls; one hipGraph replay after capture_cycle()), the rest one sub-step
-        at a time."""
+        """`steps` timesteps: the sub-steps of each exchange cycle run as one device call (a whole
+        cycle, or the part of one that is left; one hipGraph replay per whole cycle after
+        capture_cycle()), each after the cycle's exchange -- the same results as `steps` step()
+        calls."""
         done = 0
         while done < steps:
-            if self.sub == 0 and steps - done >= self.k and hasattr(self.be, "lattice_cycle"):
-                self.exchange()
-                if self.cycle_graph is not None:
-                    self.cycle_graph.replay()
-                else:
-                    self.be.lattice_cycle(self)
-                done += self.k
-            else:
+            if not hasattr(self.be, "lattice_cycle"):
                 self.step()
                 done += 1
+                continue
+            if self.sub == 0:
+                self.exchange()
+            n = min(self.k - self.sub, steps - done)
+            if n == self.k and self.cycle_graph is not None:
+                self.cycle_graph.replay()
+            else:   # a whole cycle, or the sub-steps left of one: one call (its first sub-step bins)
+                self.be.lattice_cycle(self, self.sub, self.sub + n)
+            self.sub = (self.sub + n) % self.k
+            done += n
 
     def build_phase(self):
         self.be.lattice_build(self)

@@ -336,13 +336,16 @@ int cbf_lattice_step_sharded(const cbf_params* p, const cbf_grid* grid, int32_t 
  * window-indexed outputs (wvel, wu, wstatus, wcnt nullable) cover rows [win_row0, win_row0 +
  * win_rows) = own +- halo nsub, clamped; ext_keys holds nsub extents sets (cbf_halo_ext_bytes);
  * workspaces holds nsub workspaces of ws_bytes >= cbf_lattice_workspace_size(W, win_rows, grid),
- * workspace s for sub-step s (kept across cycles).  Sub-step 0 bins the window; every later
- * sub-step's cell list is binned by the previous sub-step's advance as it writes the rows. */
+ * workspace s for sub-step s (kept across cycles).  Runs sub-steps [sub_begin, sub_end) of the
+ * cycle (0 <= sub_begin < sub_end <= nsub; a whole cycle is [0, nsub)): the first of them bins
+ * its window; every later sub-step's cell list is binned by the previous sub-step's advance as it
+ * writes the rows.  The outputs of the call's last sub-step are written (its computed rows, which
+ * contain the owned rows), as its cbf_lattice_step_sharded call would. */
 int cbf_lattice_cycle_sharded(const cbf_params* p, const cbf_grid* grid, int32_t W, int32_t H, int32_t own_begin,
-                              int32_t own_end, int32_t halo, int32_t nsub, int32_t win_row0, int32_t win_rows,
-                              double* wpos, double gain, double T, double* wvel, double* wu, int32_t* wstatus,
-                              int32_t* wcnt, uint64_t* ext_keys, uint64_t* stats, void* workspaces, size_t ws_bytes,
-                              void* stream);
+                              int32_t own_end, int32_t halo, int32_t nsub, int32_t sub_begin, int32_t sub_end,
+                              int32_t win_row0, int32_t win_rows, double* wpos, double gain, double T, double* wvel,
+                              double* wu, int32_t* wstatus, int32_t* wcnt, uint64_t* ext_keys, uint64_t* stats,
+                              void* workspaces, size_t ws_bytes, void* stream);
 
 /*
  * Batched Monte-Carlo rendezvous (SURVEY cfg5): n_scen independent scenarios, each with

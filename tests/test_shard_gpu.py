@@ -53,7 +53,11 @@ def _work(rank, ws, port, W, R, steps, q, k, graph, run, nominal):
     elif graph:
         S.capture()
     S.reset_solves()
-    if run:      # whole cycles through cbf_lattice_cycle_sharded (chained sub-steps), the rest by step()
+    if run == "mixed":   # two single sub-steps, then the rest of that cycle as one partial call
+        S.step()
+        S.step()
+        S.run(steps - 2)
+    elif run:    # cycles (whole, or the part left) through cbf_lattice_cycle_sharded (chained sub-steps)
         S.run(steps)
     else:
         for _ in range(steps):
@@ -71,7 +75,7 @@ RANDOM = ("random", 1.0, 3)   # the random-walk nominal control (CBF_NOMINAL_RAN
 @pytest.mark.parametrize("ws,k,graph,run,nominal", [(2, 1, False, False, None), (3, 4, False, False, None),
                                                     (2, 4, True, False, None), (3, 4, False, True, None),
                                                     (2, 2, False, True, None), (2, 4, "cycle", True, None),
-                                                    (2, 2, False, True, RANDOM)])
+                                                    (2, 2, False, True, RANDOM), (3, 4, False, "mixed", None)])
 def test_sharded_equals_single_gpu(ws, k, graph, run, nominal):
     from cbf_amd import scenarios, swarm
     W, R, steps = 96, 40, 6
