@@ -58,6 +58,8 @@ def cpu_baseline_lattice(W, H, seed, budget_s, spacing, gain, procs=None):
     from oracle import cpu_baseline
     res = cpu_baseline.run("cfg4", budget_s, procs=procs, shape=(W, H, seed, spacing, gain))
     res["qp_dominated_cfg2"] = cpu_baseline.run("qp", budget_s, procs=procs)
+    res["c_restatement"] = cpu_baseline.run("cfg4_c", min(budget_s, 5.0), procs=procs,
+                                            shape=(W, H, seed, spacing, gain))
     return res
 
 

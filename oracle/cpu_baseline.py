@@ -9,7 +9,8 @@ independent within a step (the loop is a Jacobi update over the packed nominal s
 cross_and_rescue.py:133), so the egos are split over one single-threaded process per host core
 (OMP / OPENBLAS / MKL threads pinned to 1) and the rates add.
 
-Two shapes, both on the same inputs the GPU runs:
+Two shapes, both on the same inputs the GPU runs (plus ``cfg4_c``: the cfg4 egos through the C
+restatement, oracle/cbf_oracle.c, SURVEY 8(d)'s second baseline):
   * ``qp``   -- cfg2 (meet_at_center.py:76-153 at N = 100: 50 pursuit obstacles, 50 agents), where
                 the interior-point QP dominates each agent-QP;
   * ``cfg4`` -- random egos of the 1M-agent lattice, where the reference's O(N) Python cull per
@@ -84,12 +85,32 @@ def _cfg4_state(W, H, seed, spacing, gain):
     return pos, coracle.consensus_lattice(W, H, 0, H, pos, gain), 0
 
 
+def _c_loop(pos, vel, egos, budget_s):
+    """The same loop in the C restatement (oracle/cbf_oracle.c: the reference's O(N) cull per ego,
+    rows, the exact 2-D QP with the +1 rule, clip): SURVEY 8(d)'s second CPU baseline."""
+    from oracle import coracle, pyoracle as po
+    p = po.Params(15)
+    t0 = time.perf_counter()
+    done = solves = 0
+    for e in egos:
+        if time.perf_counter() - t0 >= budget_s:
+            break
+        out = coracle.filter_swarm(p, pos, vel, 0, e, e + 1)
+        solves += int(out["cnt"][0] > 0)
+        done += 1
+    return done, solves, time.perf_counter() - t0
+
+
 def _worker(arg):
     kind, shape, rank, procs, budget_s = arg
     _pin_blas()
     if ROOT not in sys.path:
         sys.path.insert(0, ROOT)
     from oracle import pyoracle as po, refloop
+    if kind == "cfg4_c":
+        pos, vel, _ = _cfg4_state(*shape)
+        order = np.random.default_rng(321).permutation(pos.shape[0])
+        return _c_loop(pos, vel, (int(e) for e in order[rank::procs]), budget_s)
     if kind == "qp":
         pos, vel, n_obs = _cfg2_state()
         n_ego = pos.shape[0] - n_obs
@@ -115,6 +136,13 @@ def run(kind, budget_s, procs=None, shape=None):
     done = sum(r[0] for r in res)
     solves = sum(r[1] for r in res)
     dt = max(r[2] for r in res)
+    if kind == "cfg4_c":
+        return {"value": solves / dt, "unit": "agent-QP solves/s", "cores": procs, "kind": "port",
+                "per_core": solves / dt / procs,
+                "sample": f"{done} random egos of the {shape[0]}x{shape[1]} lattice (spacing {shape[3]}) through the "
+                          f"C restatement oracle/cbf_oracle.c (the reference's O(N) cull per ego, cbf.py rows, the "
+                          f"exact 2-D QP with the +1 rule, clip), {procs} single-threaded processes x {dt:.1f} s",
+                "cores_source": how}
     what = ("cfg2 (meet_at_center.py at N=100: 50 obstacles + 50 agents, step-0 states), every agent-QP "
             "one cvxopt-coneqp solve" if kind == "qp" else
             f"random egos of the {shape[0]}x{shape[1]} lattice (spacing {shape[3]}), each an O(N) Python cull "
