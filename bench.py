@@ -136,42 +136,73 @@ def bench_lattice(args, ws, rank, local):
         else:
             for _ in range(n):
                 S.step()
+    # The timed rollout runs the filter path alone (stats=NULL: the reference computes no such
+    # record); the safety record then comes from a replay of the same steps from the same device
+    # state with the statistics on, checked bit-identical to the timed one and timed as well
+    # (ms_per_step_with_stats).  --timed-stats keeps the statistics inside the timed region.
+    modes = (True,) if args.timed_stats else (False, True)
     if use_graph:
-        if chunk > 1:
-            for n in set(plan):
-                S.capture(steps=n)
-        else:
-            S.capture()
+        for cs in modes:
+            S.collect_stats = cs
+            if chunk > 1:
+                for n in set(plan):
+                    S.capture(steps=n)
+            else:
+                S.capture()
+    S.collect_stats = modes[0]
     advance(args.warmup)
     torch.cuda.synchronize()
+    snap = S.snapshot() if len(modes) > 1 else None
     S.reset_solves()
+
+    def timed():
+        if ws > 1:
+            torch.distributed.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        if chunk > 1:
+            for n in plan:
+                S.run(n)
+        else:
+            advance(args.steps)
+        torch.cuda.synchronize()
+        if ws > 1:
+            torch.distributed.barrier()
+        return time.perf_counter() - t0
+
+    def max_over_ranks(x):
+        if ws == 1:
+            return x
+        t = torch.tensor([x], dtype=torch.float64, device="cuda")
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        return float(t[0])
+
+    elapsed = max_over_ranks(timed())
+    own = S.own if sharded else S.pos
+    end_state = (own.clone(), S.u.clone(), S.status.clone())
     if ws > 1:
-        torch.distributed.barrier()
-    torch.cuda.synchronize()
-    ev0 = torch.cuda.Event(enable_timing=True)
-    ev1 = torch.cuda.Event(enable_timing=True)
-    t0 = time.perf_counter()
-    ev0.record()
-    if chunk > 1:
-        for n in plan:
-            S.run(n)
-    else:
-        advance(args.steps)
-    ev1.record()
-    torch.cuda.synchronize()
-    if ws > 1:
-        torch.distributed.barrier()
-    t1 = time.perf_counter()
-    elapsed = t1 - t0
-    solves = S.solves_total()
-    n_local = S.n_owned if (ws > 1 or args.shard) else S.n
-    if ws > 1:
-        t = torch.tensor([elapsed, float(solves), float(n_local)], dtype=torch.float64, device="cuda")
-        mx = t.clone()
-        torch.distributed.all_reduce(mx[:1], op=torch.distributed.ReduceOp.MAX)
-        torch.distributed.all_reduce(t[1:], op=torch.distributed.ReduceOp.SUM)
-        elapsed = float(mx[0]); solves = int(t[1]); n_total = int(t[2])
         S.check_guard()
+    elapsed_stats = None
+    if snap is not None:  # the statistics replay of the timed steps
+        S.restore(snap)
+        S.collect_stats = True
+        S.reset_solves()
+        elapsed_stats = max_over_ranks(timed())
+        same = all(bool(torch.equal(a, b)) for a, b in zip(end_state, (own, S.u, S.status)))
+        if ws > 1:
+            f = torch.tensor([0 if same else 1], dtype=torch.int32, device="cuda")
+            torch.distributed.all_reduce(f)
+            same = int(f[0]) == 0
+            S.check_guard()
+        if not same:
+            raise RuntimeError("the statistics replay did not repeat the timed rollout bit for bit")
+        del snap
+    solves = S.solves_total()
+    n_local = S.n_owned if sharded else S.n
+    if ws > 1:
+        t = torch.tensor([float(solves), float(n_local)], dtype=torch.float64, device="cuda")
+        torch.distributed.all_reduce(t)
+        solves = int(t[0]); n_total = int(t[1])
     else:
         n_total = n_local
     # the timed rollout's safety record, before the kernel-timing launches below add to it
@@ -190,6 +221,7 @@ def bench_lattice(args, ws, rank, local):
                     min_dist2=None if not np.isfinite(m[2].item()) else -float(m[2]))
     safety = safety_report(stat, args.steps) if args.barrier == "reference" else None
     # dominant kernel (filter + clip + Euler) timed alone with HIP events on the launch stream
+    S.collect_stats = modes[0]  # as in the timed region
     kt = []
     for _ in range(args.kernel_iters):
         S.build_phase()
@@ -215,6 +247,9 @@ def bench_lattice(args, ws, rank, local):
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": elapsed / args.steps * 1e3,
+        "ms_per_step_with_stats": None if elapsed_stats is None else elapsed_stats / args.steps * 1e3,
+        "timed_region": "filter path only (stats=NULL); safety from a bit-identical statistics replay of the same "
+                        "steps" if elapsed_stats is not None else "filter path with the statistics bookkeeping",
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
@@ -456,6 +491,9 @@ def main():
     ap.add_argument("--rows", type=int, default=1024, help="lattice rows per GPU")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--eager", action="store_true", help="no hipGraph capture")
+    ap.add_argument("--timed-stats", action="store_true",
+                    help="cfg4: keep the rollout statistics inside the timed region (default: a bit-identical "
+                         "statistics replay after it)")
     ap.add_argument("--kernel-iters", type=int, default=20)
     ap.add_argument("--chunk", type=int, default=10,
                     help="timesteps per cbf_lattice_run call (single-GPU graph path; 1 = one cbf_lattice_step per step)")

@@ -123,7 +123,7 @@ class HipBackend:
         L.check(L.lib.cbf_lattice_step_sharded(
             self.cp, L.C.byref(self.grid), W, self.H, sub.a, sub.b, S.rb, S.re, sub.w0, sub.w1 - sub.w0,
             P(S.wpos[(sub.w0 - S.w0) * W:]), self.gain, self.T, P(S.wpos[o:]), P(S.wvel[o:]), P(S.wu[o:]),
-            P(S.wstatus[o:]), P(S.wcnt[o:]), sub.guard, P(self.ext_keys[s * self.set_words:]), P(S.stats),
+            P(S.wstatus[o:]), P(S.wcnt[o:]), sub.guard, P(self.ext_keys[s * self.set_words:]), P(S.stats_ptr()),
             P(self.wss[s]), self.ws_bytes, L.stream_handle()), "cbf_lattice_step_sharded")
 
     def lattice_cycle(self, S, s0=0, s1=None):
@@ -134,7 +134,7 @@ class HipBackend:
         L.check(L.lib.cbf_lattice_cycle_sharded(
             self.cp, L.C.byref(self.grid), self.W, self.H, S.rb, S.re, S.halo, self.nsub, s0, s1, S.w0, S.win_rows,
             P(S.wpos), self.gain, self.T, P(S.wvel), P(S.wu), P(S.wstatus), P(S.wcnt), P(self.ext_keys),
-            P(S.stats), P(self.ws_all), self.ws_bytes, L.stream_handle()), "cbf_lattice_cycle_sharded")
+            P(S.stats_ptr()), P(self.ws_all), self.ws_bytes, L.stream_handle()), "cbf_lattice_cycle_sharded")
 
     def lattice_build(self, S):
         L, P = self._lib, self._lib.ptr
@@ -148,7 +148,7 @@ class HipBackend:
         sub = S.subs[-1]
         L.check(L.lib.cbf_lattice_advance(self.cp, L.C.byref(self.grid), self.W, self.H, S.rb, S.re, sub.w0,
                                           sub.w1 - sub.w0, P(S.wpos[(sub.w0 - S.w0) * self.W:]), self.T, P(S.own),
-                                          P(S.u), P(S.status), P(S.nbr_count), sub.guard, None, P(S.stats),
+                                          P(S.u), P(S.status), P(S.nbr_count), sub.guard, None, P(S.stats_ptr()),
                                           P(self.wss[-1]), self.ws_bytes, L.stream_handle()), "cbf_lattice_advance")
 
     def arm_guard_readback(self):
@@ -224,6 +224,8 @@ class ShardedLattice:
         self.status = self.wstatus[o0:o0 + self.n_owned]
         self.nbr_count = self.wcnt[o0:o0 + self.n_owned]
         self.stats = t(np.zeros(1024, np.int64))  # rollout statistics, include/cbf_amd.h CBF_STAT_*
+        # collect_stats=False passes stats=NULL (no statistics bookkeeping; results bit-identical)
+        self.collect_stats = True
         # send slab: [first G rows | last G rows | k guard records of 8 doubles] doubles
         self.slab = 2 * self.G * W * 2
         self.stride = self.slab + 8 * substeps
@@ -328,6 +330,32 @@ class ShardedLattice:
             self.be.lattice_cycle(self)
         self.cycle_graph = g
         return g
+
+    def stats_ptr(self):
+        return self.stats if self.collect_stats else None
+
+    def snapshot(self):
+        """Copies of this rank's whole device state (window positions and outputs, exchange slabs,
+        statistics, the backend's workspaces, guard keys and flag) and the cycle position, for
+        restore().  Call after a synchronize; pending guard read-backs are settled first."""
+        self.torch.cuda.synchronize()
+        if self.be.poll_guard():
+            raise RuntimeError(self._guard_msg())
+        return (self.sub, [t.clone() for t in self._state()])
+
+    def restore(self, snap):
+        """Back to a snapshot(): the following steps repeat its trajectory bit for bit."""
+        self.torch.cuda.synchronize()
+        if self.be.poll_guard():
+            raise RuntimeError(self._guard_msg())
+        self.be._pending.clear()
+        self.sub = snap[0]
+        for t, c in zip(self._state(), snap[1]):
+            t.copy_(c)
+
+    def _state(self):
+        ts = [self.wpos, self.wvel, self.wu, self.wstatus, self.wcnt, self.stats, self.send, self.recv]
+        return ts + [self.be.ws_all, self.be.flag, self.be.ext_keys]
 
     def reset_solves(self):
         self.stats.zero_()

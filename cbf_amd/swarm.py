@@ -282,10 +282,16 @@ class LatticeSwarm:
         # rollout statistics of the fused step (include/cbf_amd.h CBF_STAT_*: solves, status counts,
         # violations, minimum neighbour distance), accumulated on device by every step
         self.stats = torch.zeros((1024,), dtype=torch.int64, device=self.dev)
+        # collect_stats=False passes stats=NULL: the kernels skip the statistics bookkeeping (the
+        # reference computes none of it); results are bit-identical either way
+        self.collect_stats = True
         self.ap_ws = torch.empty((lib.cbf_allpairs_workspace_size(n, n) if method == "allpairs" else 1,),
                                  dtype=torch.uint8, device=self.dev)
-        self.graph = None
-        self.run_graphs = {}
+        self.graphs = {}      # captured step() graphs, keyed by collect_stats
+        self.run_graphs = {}  # captured run(steps) graphs, keyed by (steps, collect_stats)
+
+    def _st(self):
+        return ptr(self.stats) if self.collect_stats else None
 
     def _launch(self):
         if self.method == "allpairs":
@@ -295,7 +301,8 @@ class LatticeSwarm:
                                                 ptr(self.ap_ws), self.ap_ws.numel(), stream_handle()),
                   "cbf_filter_allpairs_split")
             euler(self.pos, self.u, self.T)
-            self.stats[_lib.STAT_SOLVES] += (self.nbr_count > 0).sum()
+            if self.collect_stats:
+                self.stats[_lib.STAT_SOLVES] += (self.nbr_count > 0).sum()
             return
         if self.barrier == "euclidean_hocbf":
             self.build_phase()
@@ -303,13 +310,13 @@ class LatticeSwarm:
             return
         check(lib.cbf_lattice_step(self.cp, _lib.C.byref(self.grid), self.W, self.H, 0, self.H, 0, self.H,
                                    ptr(self.pos), self.gain, self.T, ptr(self.pos), ptr(self.vel), ptr(self.u),
-                                   ptr(self.status), ptr(self.nbr_count), 0, None, ptr(self.stats), ptr(self.ws),
+                                   ptr(self.status), ptr(self.nbr_count), 0, None, self._st(), ptr(self.ws),
                                    self.ws_bytes, stream_handle()), "cbf_lattice_step")
 
     def _launch_run(self, steps):
         check(lib.cbf_lattice_run(self.cp, _lib.C.byref(self.grid), self.W, self.H, ptr(self.pos), self.gain, self.T,
                                   steps, ptr(self.vel), ptr(self.u), ptr(self.status), ptr(self.nbr_count),
-                                  ptr(self.stats), ptr(self.ws), self.ws_bytes, stream_handle()), "cbf_lattice_run")
+                                  self._st(), ptr(self.ws), self.ws_bytes, stream_handle()), "cbf_lattice_run")
 
     def run(self, steps):
         """`steps` timesteps through cbf_lattice_run (bit-identical to `steps` step() calls; the
@@ -317,7 +324,7 @@ class LatticeSwarm:
         barrier, cell method only."""
         if self.method != "cells" or self.barrier != "reference":
             raise ValueError("run() is the fused multi-step path of the reference barrier on the cell list")
-        g = self.run_graphs.get(steps)
+        g = self.run_graphs.get((steps, self.collect_stats))
         if g is not None:
             g.replay()
         else:
@@ -335,12 +342,12 @@ class LatticeSwarm:
             check(lib.cbf_lattice_advance_hocbf(self.cp, _lib.C.byref(self.hp), _lib.C.byref(self.grid), self.W,
                                                 self.H, 0, self.H, 0, self.H, ptr(self.pos), self.T, ptr(self.pos),
                                                 ptr(self.u), ptr(self.status), ptr(self.nbr_count), 0, None,
-                                                ptr(self.stats), ptr(self.ws), self.ws_bytes, stream_handle()),
+                                                self._st(), ptr(self.ws), self.ws_bytes, stream_handle()),
                   "cbf_lattice_advance_hocbf")
             return
         check(lib.cbf_lattice_advance(self.cp, _lib.C.byref(self.grid), self.W, self.H, 0, self.H, 0, self.H,
                                       ptr(self.pos), self.T, ptr(self.pos), ptr(self.u), ptr(self.status),
-                                      ptr(self.nbr_count), 0, None, ptr(self.stats), ptr(self.ws), self.ws_bytes,
+                                      ptr(self.nbr_count), 0, None, self._st(), ptr(self.ws), self.ws_bytes,
                                       stream_handle()), "cbf_lattice_advance")
 
     def stats_summary(self) -> dict:
@@ -373,14 +380,28 @@ class LatticeSwarm:
         with torch.cuda.graph(g):
             launch()
         if steps is None:
-            self.graph = g
+            self.graphs[self.collect_stats] = g
         else:
-            self.run_graphs[steps] = g
+            self.run_graphs[(steps, self.collect_stats)] = g
         return g
 
+    def snapshot(self) -> list:
+        """Device copies of the swarm's whole state (positions, workspace incl. the cell order and
+        the nominal-control state, outputs, statistics), for restore()."""
+        return [t.clone() for t in self._state()]
+
+    def restore(self, snap: list) -> None:
+        """Back to a snapshot(): the following steps repeat the snapshot's trajectory bit for bit."""
+        for t, c in zip(self._state(), snap):
+            t.copy_(c)
+
+    def _state(self):
+        return [self.pos, self.vel, self.u, self.status, self.nbr_count, self.ws, self.stats, self.ap_ws]
+
     def step(self):
-        if self.graph is not None:
-            self.graph.replay()
+        g = self.graphs.get(self.collect_stats)
+        if g is not None:
+            g.replay()
         else:
             self._launch()
 

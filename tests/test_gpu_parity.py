@@ -375,6 +375,49 @@ def test_lattice_run_matches_steps(spacing):
         assert st["seidel"] > 0      # the hard-QP kernel's chained binning is exercised
 
 
+@pytest.mark.parametrize("nominal", [None, ("random", 0.05, 3)])
+def test_lattice_stats_off_and_replay(nominal):
+    """The bench's timed path: run() with stats=NULL (graphs of both modes captured) gives the same
+    trajectory bit for bit as with the statistics on, and snapshot()/restore() makes the statistics
+    replay repeat a stats-off rollout exactly (positions, outputs), with the replay's statistics
+    equal to those of a stats-on rollout from the start (incl. the random-walk nominal state)."""
+    W, H = 128, 96
+    pos = scenarios.lattice(W, H, seed=5, spacing=0.2)
+    A = swarm.LatticeSwarm(pos, W, H, nominal=nominal)
+    A.run(6)
+    B = swarm.LatticeSwarm(pos, W, H, nominal=nominal)
+    B.collect_stats = False
+    B.capture(steps=3)              # runs steps 1-3 (stats off)
+    B.collect_stats = True
+    B.capture(steps=3)              # runs steps 4-6 (stats on)
+    B.reset_solves()
+    torch.cuda.synchronize()
+    assert torch.equal(A.pos, B.pos) and torch.equal(A.u, B.u) and torch.equal(A.status, B.status)
+    snap = B.snapshot()
+    ref = swarm.LatticeSwarm(pos, W, H, nominal=nominal)
+    ref.run(6)
+    ref.reset_solves()
+    ref.run(8)                      # the statistics of steps 7-14 alone
+    B.collect_stats = False
+    for _ in range(2):
+        B.run(3)
+    B.run(2)
+    torch.cuda.synchronize()
+    end = [t.clone() for t in (B.pos, B.u, B.status)]
+    assert int(B.stats.abs().sum()) == 0   # nothing recorded with stats=NULL
+    B.restore(snap)
+    B.collect_stats = True
+    B.reset_solves()
+    for _ in range(2):
+        B.run(3)
+    B.run(2)
+    torch.cuda.synchronize()
+    assert all(torch.equal(a, b) for a, b in zip(end, (B.pos, B.u, B.status)))
+    assert torch.equal(B.pos, ref.pos)
+    sa, sb = ref.stats_summary(), B.stats_summary()
+    assert sa == sb and sb["solves"] > 0 and sb["errors"] == 0
+
+
 def _sample_oracle(pos, vel, idx, threads=16):
     p = po.Params(15)
     chunks = np.array_split(idx, threads)

@@ -57,6 +57,19 @@ def _work(rank, ws, port, W, R, steps, q, k, graph, run, nominal):
         S.step()
         S.step()
         S.run(steps - 2)
+    elif run == "replay":   # the bench's timed path: stats off, then restore() and a stats-on replay
+        snap = S.snapshot()
+        S.collect_stats = False
+        S.run(steps)
+        torch.cuda.synchronize()
+        S.check_guard()
+        first = S.own.clone()
+        assert int(S.stats.abs().sum()) == 0
+        S.restore(snap)
+        S.collect_stats = True
+        S.run(steps)
+        torch.cuda.synchronize()
+        assert torch.equal(first, S.own)
     elif run:    # cycles (whole, or the part left) through cbf_lattice_cycle_sharded (chained sub-steps)
         S.run(steps)
     else:
@@ -75,7 +88,8 @@ RANDOM = ("random", 1.0, 3)   # the random-walk nominal control (CBF_NOMINAL_RAN
 @pytest.mark.parametrize("ws,k,graph,run,nominal", [(2, 1, False, False, None), (3, 4, False, False, None),
                                                     (2, 4, True, False, None), (3, 4, False, True, None),
                                                     (2, 2, False, True, None), (2, 4, "cycle", True, None),
-                                                    (2, 2, False, True, RANDOM), (3, 4, False, "mixed", None)])
+                                                    (2, 2, False, True, RANDOM), (3, 4, False, "mixed", None),
+                                                    (2, 4, False, "replay", None)])
 def test_sharded_equals_single_gpu(ws, k, graph, run, nominal):
     from cbf_amd import scenarios, swarm
     W, R, steps = 96, 40, 6
