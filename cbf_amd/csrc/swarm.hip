@@ -341,7 +341,7 @@ struct EgoOut {
 // Tail of the lattice filter for one owned ego (output index k) whose QP rows are accumulated in
 // E: solve in place when solve_fast can (origin, or one Seidel event that stays put) or queue to
 // the hard kernel (sub-queue q: header hardq, records qr), clip, Euler, outputs.
-template <bool FZ>
+template <bool FZ, bool ST>
 __device__ __forceinline__ void ego_finish(const KP& P, Ego& E, int w, int k, int slot, double T,
                                            double2* __restrict__ pos_out, double2* __restrict__ u,
                                            int32_t* __restrict__ status, int32_t* __restrict__ cnt,
@@ -379,9 +379,11 @@ __device__ __forceinline__ void ego_finish(const KP& P, Ego& E, int w, int k, in
         clip_u(P, S, E, ux, uy);
         st = pack_status(S);
         O.code = S.status;
-        O.binding = S.x0 != 0.0 || S.x1 != 0.0;
-        O.viol = S.viol;
-        O.vorig = S.viol_orig;
+        if (ST) {  // statistics only (a kernel without them compiles the violations away)
+            O.binding = S.x0 != 0.0 || S.x1 != 0.0;
+            O.viol = S.viol;
+            O.vorig = S.viol_orig;
+        }
     }
     const double2 pn = make_double2(E.r0 + T * ux, E.r1 + T * uy);
     pos_out[k] = pn;
@@ -399,7 +401,7 @@ __device__ __forceinline__ void ego_finish(const KP& P, Ego& E, int w, int k, in
 // Rows are assembled as row_g and the quadrant terms added per quadrant (row_g's note); an ego
 // whose quadrant terms are not all finite, or whose hit list overflowed, is assembled row by row
 // with row_b (scan_range_direct).
-template <bool FZ>
+template <bool FZ, bool ST>
 __device__ __forceinline__ void lattice_ego(const KP& P, const CellGrid& G, const WinBounds& B, int slot,
                                             const double2* __restrict__ spos, const double2* __restrict__ svel,
                                             const int32_t* __restrict__ sidx, const int32_t* __restrict__ start,
@@ -443,15 +445,15 @@ __device__ __forceinline__ void lattice_ego(const KP& P, const CellGrid& G, cons
         for (int k = 0; k < 3; ++k) scan_range_direct<FZ>(rt0[k], rt1[k], P, E, spos, svel);
     }
     O.nbrs = E.count;
-    O.d2 = d2;
-    ego_finish<FZ>(P, E, w, w - B.own_lo, slot, T, pos_out, u, status, cnt, hardq, q, qr, O);
+    if (ST) O.d2 = d2;
+    ego_finish<FZ, ST>(P, E, w, w - B.own_lo, slot, T, pos_out, u, status, cnt, hardq, q, qr, O);
 }
 
 // K4: one lane per cell-sorted slot; QPs that solve_fast settles (the origin, or one Seidel event
 // that stays put) are finished in place, the others are appended with their assembled state to
 // the hard queue: one such lane would otherwise make its whole wave run the full Seidel path (and
 // hold the registers for it, ~180 VGPRs against ~75); K5 solves them.
-template <bool FZ>
+template <bool FZ, bool ST>
 __global__ void __launch_bounds__(kBlock) k_lattice_filter(KP P, CellGrid G, WinBounds B, int W, int row_begin,
                                                            int row_end, int win_row0, long nwin, long ncell,
                                                            const double2* __restrict__ spos,
@@ -485,7 +487,7 @@ __global__ void __launch_bounds__(kBlock) k_lattice_filter(KP P, CellGrid G, Win
     O.viol = O.vorig = 0.0;
     O.d2 = INFINITY;
     if (slot < total) {
-        lattice_ego<FZ>(P, G, B, slot, spos, svel, sidx, start, T, pos_out, u, status, cnt, hardq, bx % kSubQ,
+        lattice_ego<FZ, ST>(P, G, B, slot, spos, svel, sidx, start, T, pos_out, u, status, cnt, hardq, bx % kSubQ,
                         qrec + (long)(bx % kSubQ) * qcap, hit_lds, O);
         if (ext_part && O.res == 1) ext_accumulate_w(O.w, B, O.ny, e0, e1, e2, e3);
     }
@@ -499,7 +501,7 @@ __global__ void __launch_bounds__(kBlock) k_lattice_filter(KP P, CellGrid G, Win
         if (slot < nwin && O.res != 2)
             C.bcs[slot] = comp ? make_int3(cell, rank, wn) : make_int3(-1, 0, O.res == 1 ? wn : -1);
     }
-    if (stats) {
+    if (ST && stats) {
         const bool counted = O.res != 0 && O.w >= B.cnt_lo && O.w < B.cnt_hi;
         wave_stats(stats, (long)bx * (kBlock / 64) + (threadIdx.x >> 6), counted && O.nbrs > 0,
                    counted && O.res == 2, counted && O.res == 1, O.code, O.binding, O.viol, O.vorig,
@@ -804,7 +806,10 @@ static int lattice_advance(const cbf_params* p, const cbf_grid* grid, int32_t W,
     double2* uo = reinterpret_cast<double2*>(u);
     unsigned long long* st = reinterpret_cast<unsigned long long*>(stats);
     const WinBounds B = make_win_bounds(W, win_row0, n, row_begin, row_end, cnt_begin, cnt_end, guard_rows);
-    hipLaunchKernelGGL(p->f_is_zero ? k_lattice_filter<true> : k_lattice_filter<false>, dim3(nb), dim3(kBlock), 0, s,
+    // without a statistics array the filter is the instantiation that computes none of them
+    const auto filter = st ? (p->f_is_zero ? k_lattice_filter<true, true> : k_lattice_filter<false, true>)
+                           : (p->f_is_zero ? k_lattice_filter<true, false> : k_lattice_filter<false, false>);
+    hipLaunchKernelGGL(filter, dim3(nb), dim3(kBlock), 0, s,
                        kp, G, B, W, row_begin, row_end, win_row0, n, Wk.ncell, Wk.spos, Wk.svel, Wk.sidx, Wk.start,
                        Wk.sctl, T, po, uo, status, nbr_count, ext_part, st, Wk.hardq, Wk.qrec, Wk.qcap,
                        chain ? *chain : ChainSpec{});
