@@ -43,7 +43,11 @@ def load_pmc(config):
         return {}
 
 
-def load_pmc_traffic(config, kernels=("k_lattice_filter", "k_lattice_filter_hard")):
+# the timed advance phase: the filter instantiation without statistics (f = 0) and the queue kernel
+ADVANCE_KERNELS = ("k_lattice_filter<true, false>", "k_lattice_filter_hard")
+
+
+def load_pmc_traffic(config, kernels=ADVANCE_KERNELS):
     """HBM bytes per launch of the advance phase (sum over its kernels) for this config, if profiled."""
     d = load_pmc(config)
     vals = [d.get(k, {}).get("hbm_bytes_per_launch") for k in kernels]
@@ -276,7 +280,7 @@ def bench_lattice(args, ws, rank, local):
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS,
                      "traffic": traffic,
-                     "kernel": "advance phase: k_lattice_filter + k_lattice_filter_hard" if args.barrier == "reference"
+                     "kernel": "advance phase: k_lattice_filter<f=0, no statistics> + k_lattice_filter_hard" if args.barrier == "reference"
                      else "advance phase: k_lattice_filter_hocbf + k_lattice_filter_hocbf_wide",
                      "kernel_ms": k_ms,
                      "algorithmic_bytes_per_launch": FILTER_BYTES_PER_AGENT * n_local,

@@ -31,7 +31,9 @@ XCDS = 8
 
 
 def short(name: str) -> str:
-    m = re.search(r"(k_[A-Za-z0-9_]+)", name)
+    """Kernel name with its template arguments (the lattice filter has one instantiation per
+    statistics mode: k_lattice_filter<FZ, ST>)."""
+    m = re.search(r"(k_[A-Za-z0-9_]+(<[^<>()]*>)?)", name)
     return m.group(1) if m else name[:40]
 
 
