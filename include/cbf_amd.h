@@ -55,7 +55,9 @@ extern "C" {
 
 /* Rollout statistics of the lattice step (`stats`, device uint64[1024] zero-filled by the caller:
  * 64 slots of 16 words, slot i at stats + 16 i; sum the counts and take the maximum of the other
- * words over the slots).  Counted over the egos of the counted rows. */
+ * words over the slots).  Counted over the egos of the counted rows.  `stats` may be NULL in every
+ * lattice entry point: nothing is recorded and the filter runs the instantiation that computes no
+ * statistics (results are bit-identical either way; the reference computes none of them). */
 #define CBF_STAT_SOLVES 0        /* agent-QP solves (egos with >= 1 neighbour) */
 #define CBF_STAT_OPTIMAL 1       /* ... with status OPTIMAL (the reference's QP is feasible) */
 #define CBF_STAT_RELAXED 2       /* ... RELAXED (infeasible as posed; the cbf.py:84-87 rule applied) */
