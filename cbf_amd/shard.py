@@ -22,6 +22,11 @@ the computed rows per rank (k = 4, R = 1024: 3 % and 1.6 %), for a k-fold cut in
 
 The backend object does the device work (HipBackend here; the CPU gloo tests plug in the
 oracle as a backend to check the exchange logic).
+
+Swarms that are not a lattice (GroupSwarm: cfg1/cfg2 groups, or any entity set with Laplacian
+nominal controls) shard by contiguous entity ranges instead (ShardedGroupSwarm, at the end of
+this module): every rank holds all positions, filters its own egos, and the new positions are
+all-gathered once per timestep.
 """
 from __future__ import annotations
 
@@ -380,3 +385,125 @@ class ShardedLattice:
 
     def owned_positions(self):
         return self.own
+
+
+# ---- any swarm: contiguous entity ranges, one all-gather of the positions per timestep ----------
+
+class HipGroupBackend:
+    """Device work of ShardedGroupSwarm through the C ABI (cbf_amd.swarm)."""
+
+    def __init__(self, groups, params, method, pos0):
+        import torch
+        from . import swarm
+        self.torch, self.swarm = torch, swarm
+        self.dev = torch.device("cuda", torch.cuda.current_device())
+        self.cp = params.c()
+        self.method = "allpairs" if method == "auto" and len(pos0) <= 8192 else ("cells" if method == "auto" else method)
+        # the cell grid of the whole swarm, fixed at the start (with a margin; agents that drift
+        # outside it fall into the edge cells, which only lengthens their candidate lists)
+        self.grid = swarm.grid_for_points(pos0, params.safety_distance) if self.method == "cells" else None
+        self.groups = []
+        for (b, e, rows, anchors, rot, scale) in groups:
+            rp, col = swarm.csr_from_rows(rows, self.dev)
+            anc = None if anchors is None else torch.as_tensor(np.asarray(anchors, np.float64).reshape(-1, 2),
+                                                               device=self.dev).contiguous()
+            self.groups.append((b, e, rp, col, anc, rot, scale))
+
+    def tensor(self, a):
+        return self.torch.as_tensor(np.ascontiguousarray(a), device=self.dev).clone()
+
+    def nominal(self, pos, vel):
+        for (b, e, rp, col, anc, rot, scale) in self.groups:
+            self.swarm.consensus_csr(pos[b:e], rp, col, 0, anc, rot, scale, out=vel[b:e])
+
+    def filter(self, pos, vel, n_obs, eb, ee):
+        out = self.swarm.filter_swarm(self.cp, pos, vel, n_obs, eb, ee, method=self.method, grid=self.grid)
+        return out["u"], out["status"], out["nbr_count"]
+
+    def euler(self, pos, u, T):
+        self.swarm.euler(pos, u, T)
+
+
+class ShardedGroupSwarm:
+    """A swarm that is not a lattice (GroupSwarm: entity groups with graph-Laplacian nominal
+    controls, cfg1/cfg2 or any random swarm), sharded the way the north star plans it: rank r owns
+    the contiguous entity range [b_r, e_r) (ceil(n / world) entities each), every rank holds all
+    positions, and each timestep is
+      1. the nominal controls of all entities (replicated: a Laplacian row reads its neighbours'
+         positions, which every rank holds; cross_and_rescue.py:108-125),
+      2. the filter of this rank's egos [max(n_obs, b_r), e_r) against the whole swarm
+         (filter_swarm with an ego range; cross_and_rescue.py:135-160),
+      3. Euler for the rank's entities (obstacles with their nominal velocity, :173),
+      4. one all-gather of every rank's new positions (RCCL all_gather_into_tensor over xGMI; gloo
+         for the CPU tests).
+    Each entity's step reads only the gathered state, so the rollout is bit-identical to the
+    single-GPU GroupSwarm.step of the whole swarm at any world size.  The work that is replicated
+    (nominal controls, and the cell list or candidate set the filter scans) is O(n); the filter
+    itself, the dominant part, is split.  The lattice swarm's stripes (ShardedLattice) exchange
+    only ghost rows instead."""
+
+    def __init__(self, pos, n_obs, groups, params=None, T=1 / 30, method="auto", group=None, backend=None):
+        import torch
+        import torch.distributed as dist
+        from .swarm import FilterParams
+        self.torch, self.dist, self.group = torch, dist, group
+        self.ws = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
+        pos = np.asarray(pos, dtype=np.float64).reshape(-1, 2)
+        self.n, self.n_obs, self.T = pos.shape[0], n_obs, T
+        self.chunk = -(-self.n // self.ws)
+        self.b = min(self.n, self.rank * self.chunk)
+        self.e = min(self.n, self.b + self.chunk)
+        self.params = params or FilterParams()
+        self.be = backend if backend is not None else HipGroupBackend(groups, self.params, method, pos)
+        t = self.be.tensor
+        self.buf = t(np.zeros((self.ws * self.chunk, 2)))   # the gathered positions (padded ranks)
+        self.buf[:self.n].copy_(torch.as_tensor(pos))
+        self.pos = self.buf[:self.n]
+        self.vel = t(np.zeros((self.n, 2)))
+        self.send = t(np.zeros((self.chunk, 2)))
+        self.u = t(np.zeros((self.e - self.b, 2)))           # this rank's applied controls
+        self.status = t(np.zeros(self.e - self.b, np.int32))
+        self.nbr_count = t(np.zeros(self.e - self.b, np.int32))
+        self.solves = 0 if not self.buf.is_cuda else torch.zeros((), dtype=torch.int64, device=self.buf.device)
+        self.use_list_gather = dist.get_backend(group) == "gloo"
+
+    def _gather(self):
+        if self.use_list_gather:
+            if self.send.is_cuda:   # gloo beside a GPU (1-GPU rehearsals): staged through the host
+                rc = self.buf.cpu()
+                self.dist.all_gather(list(rc.view(self.ws, self.chunk, 2).unbind(0)), self.send.cpu(),
+                                     group=self.group)
+                self.buf.copy_(rc)
+            else:
+                self.dist.all_gather(list(self.buf.view(self.ws, self.chunk, 2).unbind(0)), self.send,
+                                     group=self.group)
+        else:
+            self.dist.all_gather_into_tensor(self.buf, self.send, group=self.group)
+
+    def step(self):
+        be, b, e = self.be, self.b, self.e
+        be.nominal(self.pos, self.vel)
+        self.u.copy_(self.vel[b:e])              # obstacles (and idle entities) keep their nominal velocity
+        eb = max(self.n_obs, b)
+        ee = max(eb, e)
+        if ee > eb:
+            u, st, cnt = be.filter(self.pos, self.vel, self.n_obs, eb, ee)
+            self.u[eb - b:].copy_(u)
+            self.status[eb - b:].copy_(st)
+            self.nbr_count[eb - b:].copy_(cnt)
+            self.solves += (cnt > 0).sum()
+        self.send[:e - b].copy_(self.pos[b:e])
+        be.euler(self.send[:e - b], self.u, self.T)
+        self._gather()
+
+    def run(self, steps):
+        for _ in range(steps):
+            self.step()
+
+    def solves_total(self) -> int:
+        """This rank's agent-QP solves (egos with >= 1 neighbour) since construction."""
+        return int(self.solves)
+
+    def owned_positions(self):
+        return self.pos[self.b:self.e]

@@ -192,3 +192,84 @@ def test_too_small_halo_is_caught_after_the_step(k):
         p.join(timeout=60)
         assert p.exitcode == 0
     assert any(r[1] == "raised" for r in res)
+
+
+# ---- ShardedGroupSwarm: any swarm, contiguous entity ranges, one all-gather per timestep ------
+
+class OracleGroupBackend:
+    """ShardedGroupSwarm's device work restated on the CPU (oracle)."""
+
+    def __init__(self, groups):
+        self.p = po.Params(15)
+        self.groups = []
+        for (b, e, rows, anc, rot, scale) in groups:
+            rp = np.concatenate([[0], np.cumsum([len(r) for r in rows])]).astype(np.int32)
+            col = np.array([j for r in rows for j in r], np.int32)
+            self.groups.append((b, e, rp, col, anc, rot, scale))
+
+    def tensor(self, a):
+        return torch.as_tensor(np.ascontiguousarray(a)).clone()
+
+    def nominal(self, pos, vel):
+        p = pos.numpy()
+        for (b, e, rp, col, anc, rot, scale) in self.groups:
+            vel[b:e].copy_(torch.as_tensor(coracle.consensus_csr(p[b:e], rp, col, 0, e - b, anchors=anc, rot=rot,
+                                                                 scale=scale)))
+
+    def filter(self, pos, vel, n_obs, eb, ee):
+        out = coracle.filter_swarm(self.p, pos.numpy(), vel.numpy(), n_obs, eb, ee)
+        return torch.as_tensor(out["u"]), torch.as_tensor(out["status"]), torch.as_tensor(out["cnt"])
+
+    def euler(self, pos, u, T):
+        pos.copy_(torch.as_tensor(coracle.euler(pos.numpy(), u.numpy(), T)))
+
+
+def _group_case(name):
+    if name == "car":
+        return scenarios.cross_and_rescue()
+    return scenarios.meet_at_center(int(name[3:]))
+
+
+def _group_worker(rank, ws, port, name, steps, q):
+    from cbf_amd.shard import ShardedGroupSwarm
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=ws)
+    pos0, n_obs, groups = _group_case(name)
+    S = ShardedGroupSwarm(pos0, n_obs, groups, backend=OracleGroupBackend(groups))
+    S.run(steps)
+    q.put((rank, S.pos.numpy().copy(), S.u.numpy().copy(), S.solves_total()))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("name,ws", [("car", 2), ("mac10", 3), ("mac100", 2), ("mac100", 3)])
+def test_sharded_group_swarm_equals_single_domain(name, ws):
+    """Any-swarm sharding (entity ranges + one position all-gather per step) == the single-domain
+    oracle rollout of the caller loop bit for bit, on every rank; solves summed over ranks."""
+    steps = 6
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_group_worker, args=(r, ws, port, name, steps, q)) for r in range(ws)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=300) for _ in range(ws)], key=lambda t: t[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    pos, n_obs, groups = _group_case(name)
+    be = OracleGroupBackend(groups)
+    solves = 0
+    for _ in range(steps):
+        vel = torch.zeros((len(pos), 2), dtype=torch.float64)
+        be.nominal(torch.as_tensor(pos), vel)
+        vel = vel.numpy()
+        out = coracle.filter_swarm(be.p, pos, vel, n_obs)
+        solves += int((out["cnt"] > 0).sum())
+        u = vel.copy()
+        u[n_obs:] = out["u"]
+        pos = coracle.euler(pos, u, scenarios.T)
+    for r in res:
+        assert np.array_equal(r[1], pos)
+    assert np.array_equal(np.concatenate([r[2] for r in res]), u)
+    assert sum(r[3] for r in res) == solves

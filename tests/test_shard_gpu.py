@@ -163,3 +163,88 @@ def test_halo_breach_stops_the_rollout_early():
     for p in procs:
         p.join(timeout=120)
     assert any(r[1] == "raised" and r[2] < 5 for r in res), res
+
+
+# ---- ShardedGroupSwarm (any swarm): entity ranges + one position all-gather per step ----------
+
+def _grid_swarm(W=120, H=100):
+    """A 12,000-agent jittered lattice driven by a 4-neighbour Laplacian given as a generic group
+    (so the filter takes the cell-list path of filter_swarm, n > 8192)."""
+    from cbf_amd import scenarios
+    pos = scenarios.lattice(W, H, seed=4)
+    rows = []
+    for i in range(W * H):
+        r, c = divmod(i, W)
+        rows.append([j for j in (i - W if r > 0 else -1, i - 1 if c > 0 else -1, i + 1 if c < W - 1 else -1,
+                                 i + W if r < H - 1 else -1) if j >= 0])
+    return pos, 0, [(0, W * H, rows, None, None, scenarios.LATTICE_GAIN)]
+
+
+def _group_case(name):
+    from cbf_amd import scenarios
+    return scenarios.meet_at_center(100) if name == "mac100" else _grid_swarm()
+
+
+def _group_worker(rank, ws, port, name, steps, q):
+    try:
+        import datetime
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        torch.cuda.set_device(0)
+        dist.init_process_group("gloo", rank=rank, world_size=ws, timeout=datetime.timedelta(seconds=60))
+        from cbf_amd.shard import ShardedGroupSwarm
+        pos0, n_obs, groups = _group_case(name)
+        S = ShardedGroupSwarm(pos0, n_obs, groups)
+        S.run(steps)
+        torch.cuda.synchronize()
+        q.put((rank, S.pos.cpu().numpy(), S.u.cpu().numpy(), S.status.cpu().numpy(), S.solves_total()))
+        dist.barrier()
+        dist.destroy_process_group()
+    except BaseException as e:
+        q.put((rank, "error", repr(e)))
+        raise
+
+
+@pytest.mark.parametrize("name,ws,steps", [("mac100", 2, 20), ("grid12k", 2, 4), ("grid12k", 3, 3)])
+def test_sharded_group_swarm_equals_single_gpu(name, ws, steps):
+    """The any-swarm sharded path on the HIP backend (2 / 3 ranks on one GPU, gloo) == the
+    single-GPU GroupSwarm rollout bit for bit on every rank (all-pairs for mac100, the cell list for
+    the 12 k swarm), and == the oracle's rollout for mac100."""
+    from cbf_amd import swarm
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_group_worker, args=(r, ws, port, name, steps, q)) for r in range(ws)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=120) for _ in range(ws)], key=lambda t: t[0])
+    assert not any(isinstance(r[1], str) for r in res), res
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    pos0, n_obs, groups = _group_case(name)
+    G = swarm.GroupSwarm(pos0, n_obs, groups)
+    solves = 0
+    for _ in range(steps):
+        out = G.step()
+        solves += int((out["nbr_count"] > 0).sum())
+    torch.cuda.synchronize()
+    ref = G.pos.cpu().numpy()
+    for r in res:
+        assert np.array_equal(r[1], ref)
+    assert np.array_equal(np.concatenate([r[2] for r in res]), out["u_all"].cpu().numpy())
+    assert np.array_equal(np.concatenate([r[3] for r in res])[n_obs:], out["status"].cpu().numpy())
+    assert sum(r[4] for r in res) == solves
+    if name == "mac100":
+        from oracle import coracle, pyoracle as po
+        pos = pos0.copy()
+        for _ in range(steps):
+            vel = np.zeros_like(pos)
+            for (b, e, rows, anc, rot, scale) in groups:
+                rp = np.concatenate([[0], np.cumsum([len(r) for r in rows])]).astype(np.int32)
+                col = np.array([j for r in rows for j in r], np.int32)
+                vel[b:e] = coracle.consensus_csr(pos[b:e], rp, col, 0, e - b, anchors=anc, rot=rot, scale=scale)
+            o = coracle.filter_swarm(po.Params(15), pos, vel, n_obs)
+            u = vel.copy()
+            u[n_obs:] = o["u"]
+            pos = coracle.euler(pos, u, 1 / 30)
+        assert np.array_equal(ref, pos)
