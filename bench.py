@@ -146,6 +146,9 @@ def bench_lattice(args, ws, rank, local):
     # (ms_per_step_with_stats).  --timed-stats keeps the statistics inside the timed region.
     modes = (True,) if args.timed_stats else (False, True)
     if use_graph:
+        # a capture's eager warm-up launch advances the swarm: restore it afterwards, so that the
+        # timed steps are timesteps W+1 .. W+K of the rollout whatever the graphs' sizes
+        snap0 = S.snapshot()
         for cs in modes:
             S.collect_stats = cs
             if chunk > 1:
@@ -153,6 +156,8 @@ def bench_lattice(args, ws, rank, local):
                     S.capture(steps=n)
             else:
                 S.capture()
+        S.restore(snap0)
+        del snap0
     S.collect_stats = modes[0]
     advance(args.warmup)
     torch.cuda.synchronize()
@@ -268,7 +273,7 @@ def bench_lattice(args, ws, rank, local):
                    "parallelism": f"row-stripe shards x{ws}, 1 RCCL all-gather of ghost-row slabs per "
                                   f"{args.substeps} steps" if (ws > 1 or args.shard) else "single GPU",
                    "graph": use_graph,
-                   "timesteps_per_call": chunk},
+                   "timesteps_per_call": max(plan) if chunk > 1 else 1},
         "timesteps_per_s": args.steps / elapsed,
         "solves_per_step": solves / args.steps,
         "feasible_fraction": safety["feasible_fraction"] if safety else None,
@@ -499,7 +504,7 @@ def main():
                     help="cfg4: keep the rollout statistics inside the timed region (default: a bit-identical "
                          "statistics replay after it)")
     ap.add_argument("--kernel-iters", type=int, default=20)
-    ap.add_argument("--chunk", type=int, default=10,
+    ap.add_argument("--chunk", type=int, default=50,
                     help="timesteps per cbf_lattice_run call (single-GPU graph path; 1 = one cbf_lattice_step per step)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--barrier", default="reference", choices=["reference", "euclidean_hocbf"],
