@@ -341,29 +341,53 @@ def bench_mc(args, ws, rank, local):
     import torch
     from cbf_amd.montecarlo import MonteCarlo
     mc = MonteCarlo(args.mc_scenarios, 16, 16, seed=args.seed)
+    # as cfg4: the timed rollouts compute no statistics (counters only); the safety record comes
+    # from a replay of the same steps from a snapshot, checked bit-identical (--timed-stats: off)
+    mc.collect_stats = args.timed_stats
     for _ in range(max(1, args.warmup)):  # the same launches as a timed step
         mc.run(args.mc_inner)
     torch.cuda.synchronize()
+    snap = None if args.timed_stats else mc.snapshot()
     mc.reset_totals()
-    if ws > 1:
-        torch.distributed.barrier()
-    torch.cuda.synchronize()
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    t0 = time.perf_counter()
-    ev0.record()
-    for _ in range(args.steps):
-        mc.run(args.mc_inner)
-    ev1.record()
-    torch.cuda.synchronize()
-    if ws > 1:
-        torch.distributed.barrier()
-    elapsed = time.perf_counter() - t0
-    kernel_ms = ev0.elapsed_time(ev1) / args.steps
+
+    def timed():
+        if ws > 1:
+            torch.distributed.barrier()
+        torch.cuda.synchronize()
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        t0 = time.perf_counter()
+        ev0.record()
+        for _ in range(args.steps):
+            mc.run(args.mc_inner)
+        ev1.record()
+        torch.cuda.synchronize()
+        if ws > 1:
+            torch.distributed.barrier()
+        return time.perf_counter() - t0, ev0.elapsed_time(ev1) / args.steps
+
+    elapsed, kernel_ms = timed()
     elapsed, _ = _reduce(elapsed, 0, ws)
+    elapsed_stats = None
+    if snap is not None:
+        counts_timed = mc.totals()["calls"]
+        end = mc.pos.clone()
+        mc.restore(snap)
+        mc.collect_stats = True
+        mc.reset_totals()
+        elapsed_stats, _ = timed()
+        elapsed_stats, _ = _reduce(elapsed_stats, 0, ws)
+        same = bool(torch.equal(end, mc.pos))
+        if ws > 1:
+            f = torch.tensor([0 if same else 1], dtype=torch.int32, device="cuda")
+            torch.distributed.all_reduce(f)
+            same = int(f[0]) == 0
+        if not same or mc.totals()["calls"] != counts_timed:
+            raise RuntimeError("cfg5: the statistics replay did not repeat the timed rollouts bit for bit")
     tot = mc.totals()
     scen_steps = args.mc_scenarios * args.mc_inner * args.steps
     return {"metric": METRIC, "value": tot["calls"] / elapsed, "unit": "agent-QP solves/s", "n_gpus": ws,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
+            "ms_per_step_with_stats": None if elapsed_stats is None else elapsed_stats / args.steps * 1e3,
             "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f64",
             "data": "synthetic",
             "config": {"workload": f"cfg5: {args.mc_scenarios} independent 16+16 rendezvous scenarios, "
@@ -385,8 +409,10 @@ def mc_roofline(kernel_ms, n_scen, inner):
     its bound is the VALU: the VALU busy fraction of k_mc_rollout from the committed rocprof
     counters (profiles/pmc_summary.json "cfg5", tools/summarize_profile.py: SQ_ACTIVE_INST_VALU x 4 /
     (SIMDs x GRBM_GUI_ACTIVE)), measured on the same launch shape."""
-    e = load_pmc("cfg5").get("k_mc_rollout", {})
-    out = {"bound": "valu", "unit": "fraction of VALU issue cycles", "peak": 1.0, "kernel": "k_mc_rollout",
+    d = load_pmc("cfg5")   # the timed instantiation: f = 0, no statistics
+    e = d.get("k_mc_rollout<true, false>", d.get("k_mc_rollout<true>", {}))
+    out = {"bound": "valu", "unit": "fraction of VALU issue cycles", "peak": 1.0,
+           "kernel": "k_mc_rollout<f=0, no statistics>",
            "kernel_ms": kernel_ms, "traffic": None}
     busy = e.get("valu_busy")
     out.update(achieved=busy, frac=busy,

@@ -15,7 +15,9 @@ namespace {
 // compiler spills ~116 B per lane, and the third wave hides more than the spills cost: 1.62 ->
 // 1.32 ms per 10 timesteps at 100 k scenarios (4 waves, 128 VGPRs and 272 B spilled: 1.93 ms;
 // the rolled LDS solve at 101 VGPRs: 2.21 ms).  Bit-identical (tests/test_gpu_parity.py).
-template <bool FZ>
+// ST: the statistics (violations, neighbour distances); without them (maxviol = NULL) the kernel
+// computes none of them and writes the counters only.
+template <bool FZ, bool ST>
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3, 3))) k_mc_rollout(KP P, int n_scen, int n_o, int n_a, int steps, double T,
                                                        double rc, double rs, double so, double ga,
                                                        double2* __restrict__ pos, long long* __restrict__ counters,
@@ -73,7 +75,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3, 
                 if (cull_keep(P, E.r0, E.r1, pj.x, pj.y, j < n_o, s)) {
                     if (nh < kHitCap) hit_lds[nh * kBlock + threadIdx.x] = j;
                     ++nh;
-                    d2min = pmin(d2min, s);
+                    if (ST) d2min = pmin(d2min, s);
                 }
             }
             if (nh <= kHitCap) {
@@ -103,8 +105,8 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3, 
                 if (Sl.status == CBF_STATUS_RELAXED) c_relax++;
                 if (Sl.status == CBF_STATUS_BOX_INFEASIBLE) c_box++;
                 if (Sl.status == CBF_STATUS_RELAX_CAP) c_cap++;
-                if (Sl.status == CBF_STATUS_OPTIMAL) mv = Sl.viol > mv ? Sl.viol : mv;
-                if (Sl.status == CBF_STATUS_RELAXED) mvo = Sl.viol_orig > mvo ? Sl.viol_orig : mvo;
+                if (ST && Sl.status == CBF_STATUS_OPTIMAL) mv = Sl.viol > mv ? Sl.viol : mv;
+                if (ST && Sl.status == CBF_STATUS_RELAXED) mvo = Sl.viol_orig > mvo ? Sl.viol_orig : mvo;
             }
         }
         __syncthreads();
@@ -148,7 +150,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3, 
             mo = ml[3 * th + 1] > mo ? ml[3 * th + 1] : mo;
             dm = pmin(dm, ml[3 * th + 2]);
         }
-        if (safety) {
+        if (ST && safety) {
             safety[2l * scen] = mo;
             safety[2l * scen + 1] = dm;
         }
@@ -156,7 +158,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3, 
         counters[4l * scen + 1] = b;
         counters[4l * scen + 2] = c;
         counters[4l * scen + 3] = d;
-        maxviol[scen] = m;
+        if (ST) maxviol[scen] = m;
     }
 }
 
@@ -167,14 +169,16 @@ extern "C" int cbf_mc_rollout(const cbf_params* p, int32_t n_scen, int32_t n_o, 
                               double* maxviol, double* safety, void* stream) {
     if (!p || n_scen < 0 || n_o < 1 || n_a < 1 || n_o + n_a > kBlock || steps < 0) return CBF_EINVAL;
     if (n_scen == 0) return 0;
-    if (!pos || !counters || !maxviol) return CBF_EINVAL;
+    if (!pos || !counters || (safety && !maxviol)) return CBF_EINVAL;
     const int tps = n_o > n_a ? n_o : n_a;
     const int S = kBlock / tps;
     const int stride = n_o + n_a + 1;
     // [positions | velocities | counter reduction (4 int64 + 3 double per thread)]
     const size_t lds = sizeof(double2) * (2 * S * stride) + (4 * sizeof(long long) + 3 * sizeof(double)) * kBlock;
     const int blocks = (n_scen + S - 1) / S;
-    hipLaunchKernelGGL(p->f_is_zero ? k_mc_rollout<true> : k_mc_rollout<false>, dim3(blocks), dim3(kBlock), lds, (hipStream_t)stream, make_kp(p), n_scen, n_o,
+    const auto kern = maxviol ? (p->f_is_zero ? k_mc_rollout<true, true> : k_mc_rollout<false, true>)
+                              : (p->f_is_zero ? k_mc_rollout<true, false> : k_mc_rollout<false, false>);
+    hipLaunchKernelGGL(kern, dim3(blocks), dim3(kBlock), lds, (hipStream_t)stream, make_kp(p), n_scen, n_o,
                        n_a, steps, T, rc, rs, so, ga, reinterpret_cast<double2*>(pos),
                        reinterpret_cast<long long*>(counters), maxviol, safety);
     return (int)hipGetLastError();

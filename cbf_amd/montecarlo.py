@@ -34,9 +34,10 @@ class HipBackend:
     def tensor(self, a):
         return self.torch.as_tensor(np.ascontiguousarray(a), device="cuda")
 
-    def rollout(self, pos, n_o, n_a, steps, ga):
-        """Advances pos in place; returns (counters (B,4) int64, maxviol (B,), safety (B,2))."""
-        return self.swarm.mc_rollout(self.params, pos, n_o, n_a, steps, ga=ga, safety=True)
+    def rollout(self, pos, n_o, n_a, steps, ga, stats=True):
+        """Advances pos in place; returns (counters (B,4) int64, maxviol (B,), safety (B,2)); with
+        stats=False the last two are None (the kernel without statistics)."""
+        return self.swarm.mc_rollout(self.params, pos, n_o, n_a, steps, ga=ga, safety=True, stats=stats)
 
 
 class MonteCarlo:
@@ -53,6 +54,8 @@ class MonteCarlo:
         self.be = backend or HipBackend()
         # scenario s's initial condition depends only on (seed, s), whatever the sharding
         self.pos = self.be.tensor(scenarios.mc_scenarios(n_scen, n_o, n_a, seed=seed)[self.lo:self.hi])
+        # False: the rollouts compute no violations or distances (counters only), bit-identical
+        self.collect_stats = True
         self.reset_totals()
 
     def reset_totals(self):
@@ -65,14 +68,25 @@ class MonteCarlo:
     def run(self, steps):
         """Advance this rank's scenarios by `steps` timesteps (device work only; no host sync)."""
         if self.hi > self.lo:
-            self._pending.append(self.be.rollout(self.pos, self.n_o, self.n_a, steps, self.ga))
+            self._pending.append(self.be.rollout(self.pos, self.n_o, self.n_a, steps, self.ga) if self.collect_stats
+                                 else self.be.rollout(self.pos, self.n_o, self.n_a, steps, self.ga, stats=False))
+
+    def snapshot(self):
+        """A copy of this rank's scenario states, for restore()."""
+        return self.pos.clone()
+
+    def restore(self, snap):
+        """Back to a snapshot(): the following runs repeat its rollouts bit for bit."""
+        self.pos.copy_(snap)
 
     def _local(self):
         for cnt, mv, sf in self._pending:
             self.counts += np.asarray(cnt.sum(0).tolist(), dtype=np.int64)
-            self.viol_opt = max(self.viol_opt, float(mv.max()))
-            self.viol_orig = max(self.viol_orig, float(sf[:, 0].max()))
-            self.min_d2 = min(self.min_d2, float(sf[:, 1].min()))
+            if mv is not None:
+                self.viol_opt = max(self.viol_opt, float(mv.max()))
+            if sf is not None:
+                self.viol_orig = max(self.viol_orig, float(sf[:, 0].max()))
+                self.min_d2 = min(self.min_d2, float(sf[:, 1].min()))
         self._pending = []
 
     def totals(self) -> dict:

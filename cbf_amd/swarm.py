@@ -406,19 +406,21 @@ class LatticeSwarm:
             self._launch()
 
 
-def mc_rollout(params, pos, n_o, n_a, steps, T=1 / 30, theta=None, so=1.0, ga=1.0, safety=False):
+def mc_rollout(params, pos, n_o, n_a, steps, T=1 / 30, theta=None, so=1.0, ga=1.0, safety=False, stats=True):
     """SURVEY cfg5: pos (n_scen, n_o+n_a, 2) CUDA float64, advanced in place by `steps` steps.
     Returns (counters int64 (n_scen,4) = {filter calls, relaxed, box-infeasible, relax-cap},
     maxviol (n_scen,) = max row violation over OPTIMAL solves[, safety (n_scen, 2) = {max violation
-    of the original barrier rows over RELAXED solves, min neighbour distance^2}])."""
+    of the original barrier rows over RELAXED solves, min neighbour distance^2}]).  stats=False:
+    the kernel instantiation without statistics (maxviol / safety are None; same positions and
+    counters)."""
     torch = _lib.require_gpu()
     theta = -math.pi / n_o if theta is None else theta
     rc, rs = float(np.cos(theta)), float(np.sin(theta))
     n_scen = pos.shape[0]
     assert pos.is_contiguous() and pos.dtype == torch.float64 and pos.shape[1] == n_o + n_a
     cnt = torch.empty((n_scen, 4), dtype=torch.int64, device=pos.device)
-    mv = torch.empty((n_scen,), dtype=torch.float64, device=pos.device)
-    sf = torch.empty((n_scen, 2), dtype=torch.float64, device=pos.device) if safety else None
+    mv = torch.empty((n_scen,), dtype=torch.float64, device=pos.device) if stats else None
+    sf = torch.empty((n_scen, 2), dtype=torch.float64, device=pos.device) if safety and stats else None
     cp = params.c() if isinstance(params, FilterParams) else params
     check(lib.cbf_mc_rollout(cp, n_scen, n_o, n_a, steps, float(T), rc, rs, float(so), float(ga), ptr(pos), ptr(cnt),
                              ptr(mv), ptr(sf), stream_handle()), "cbf_mc_rollout")
