@@ -356,8 +356,9 @@ int cbf_lattice_cycle_sharded(const cbf_params* p, const cbf_grid* grid, int32_t
  * pos [n_scen][n_o + n_a][2] is updated in place.  counters [n_scen][4] int64 = {filter calls,
  * relaxed, box-infeasible, relax-cap}; maxviol [n_scen] = max row violation over the OPTIMAL
  * (feasible) solves; safety [n_scen][2] (nullable) = {max violation of the ORIGINAL barrier rows over
- * the RELAXED solves, min distance^2 from an agent to a culled neighbour (+inf if none)}.  One
- * workgroup runs several scenarios for all steps with the state in LDS.
+ * the RELAXED solves, min distance^2 from an agent to a culled neighbour (+inf if none)}.
+ * maxviol may be NULL when safety is NULL: the kernel then computes no statistics (same positions
+ * and counters).  One workgroup runs several scenarios for all steps with the state in LDS.
  * Requires 1 <= n_o, n_a and n_o + n_a <= 256.
  */
 int cbf_mc_rollout(const cbf_params* p, int32_t n_scen, int32_t n_o, int32_t n_a, int32_t steps, double T, double rc,
