@@ -159,6 +159,16 @@ def bench_lattice(args, ws, rank, local):
         S.restore(snap0)
         del snap0
     S.collect_stats = modes[0]
+    if sharded:
+        # first-use costs (the collective's buffers and connections, allocations) are paid by two
+        # throwaway exchange cycles, undone by restoring the state: the timed steps stay W+1 .. W+K
+        snap0 = S.snapshot()
+        S.run(2 * args.substeps)
+        torch.cuda.synchronize()
+        if ws > 1:
+            S.check_guard()
+        S.restore(snap0)
+        del snap0
     advance(args.warmup)
     torch.cuda.synchronize()
     snap = S.snapshot() if len(modes) > 1 else None

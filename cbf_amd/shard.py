@@ -101,8 +101,11 @@ class HipBackend:
             swarm.set_nominal(w, nominal)
         self.flag = torch.zeros((1,), dtype=torch.int32, device=self.dev)
         # the guard flag is read back asynchronously after every exchange: a pinned host copy per
-        # exchange in flight, polled (never waited on) at the next exchanges
+        # exchange in flight, polled (never waited on) at the next exchanges.  The pinned words are
+        # a ring allocated here, so no exchange pays a pinned allocation
         self._pending = []
+        self._ring = [torch.empty((1,), dtype=torch.int32, pin_memory=True) for _ in range(8)]
+        self._next = 0
         self.set_words = _lib.lib.cbf_halo_ext_bytes(1) // 8
         self.ext_keys = torch.empty((nsub * self.set_words,), dtype=torch.int64, device=self.dev)
         _lib.check(_lib.lib.cbf_halo_ext_reset(_lib.ptr(self.ext_keys), nsub, _lib.stream_handle()),
@@ -159,7 +162,13 @@ class HipBackend:
     def arm_guard_readback(self):
         """Queue a copy of the guard flag to pinned host memory behind this exchange's unpack."""
         torch = self.torch
-        host = torch.empty((1,), dtype=torch.int32, pin_memory=True)
+        while len(self._pending) >= len(self._ring) - 1:  # the oldest read-back is still in flight
+            ev, host = self._pending.pop(0)
+            ev.synchronize()
+            if int(host[0]):
+                self._failed_late = True
+        host = self._ring[self._next % len(self._ring)]
+        self._next += 1
         host.copy_(self.flag, non_blocking=True)
         ev = torch.cuda.Event()
         ev.record()
@@ -167,6 +176,8 @@ class HipBackend:
 
     def poll_guard(self) -> bool:
         """True once a completed exchange's guard has failed (does not wait for the GPU)."""
+        if getattr(self, "_failed_late", False):
+            return True
         while self._pending and self._pending[0][0].query():
             _, host = self._pending.pop(0)
             if int(host[0]):
