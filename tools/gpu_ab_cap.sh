@@ -1,3 +1,4 @@
+# RECORD ONLY: the hit-list cap variants this measured were not kept (profiles/r02_hitcap_ab.txt).
 # GPU box: hit-list cap A/B (tools/_ab/c14, c12 vs the working tree's 16), tools/ab_stats.py, cfg4 and cfg4f
 set -u
 cd /root/repo

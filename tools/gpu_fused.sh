@@ -1,3 +1,4 @@
+# RECORD ONLY: the fused queue + scan kernel this measured was reverted (profiles/r02_hard_scan_fused_ab.txt).
 # GPU box: the fused queue + next-scan kernel (CBF_HARD_SCAN_FUSED): lattice run / shard / full-size
 # GPU tests, then tools/ab_stats.py A/B against tools/_ab/head (separate launches), cfg4 and cfg4f
 set -u

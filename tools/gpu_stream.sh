@@ -1,3 +1,4 @@
+# RECORD ONLY: the streaming queue kernel this measured was reverted (profiles/r02_hard_stream_ab.txt); the variant trees no longer exist.
 # GPU box: the streaming hard-QP kernel (CBF_HARD_STREAM): lattice GPU tests, then A/B against the
 # post-filter queue kernel (tools/_ab/s0) and 1 / 2 blocks per sub-queue (q1, q2), cfg4 and cfg4f.
 set -u
