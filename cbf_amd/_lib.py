@@ -93,6 +93,8 @@ SIGNATURES = {
     "cbf_lattice_build": (C.c_int, [_P, _G, _i32, _i32, _i32, _i32, _i32, _i32, _vp, _d, _vp, _vp, _sz, _vp]),
     "cbf_lattice_advance": (C.c_int, [_P, _G, _i32, _i32, _i32, _i32, _i32, _i32, _vp, _d, _vp, _vp, _vp, _vp,
                                       _i32, _vp, _vp, _vp, _sz, _vp]),
+    "cbf_lattice_advance_marked": (C.c_int, [_P, _G, _i32, _i32, _i32, _i32, _i32, _i32, _vp, _d, _vp, _vp, _vp, _vp,
+                                      _i32, _vp, _vp, _vp, _sz, _vp, _vp]),
     "cbf_lattice_advance_hocbf": (C.c_int, [_P, _HP, _G, _i32, _i32, _i32, _i32, _i32, _i32, _vp, _d, _vp, _vp, _vp,
                                             _vp, _i32, _vp, _vp, _vp, _sz, _vp]),
     "cbf_mc_rollout": (C.c_int, [_P, _i32, _i32, _i32, _i32, _d, _d, _d, _d, _d, _vp, _vp, _vp, _vp, _vp]),

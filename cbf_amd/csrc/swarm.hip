@@ -790,7 +790,7 @@ static int lattice_advance(const cbf_params* p, const cbf_grid* grid, int32_t W,
                            double* pos_out, double* u, int32_t* status, int32_t* nbr_count, int32_t guard_rows,
                            double* extents, uint64_t* stats, void* workspace, size_t workspace_bytes,
                            int32_t cnt_begin, int32_t cnt_end, void* stream, const ChainSpec* chain = nullptr,
-                           bool inner = false) {
+                           bool inner = false, hipEvent_t filter_done = nullptr) {
     int rc = check_lattice(p, grid, W, H, row_begin, row_end, win_row0, win_rows, pos, workspace, workspace_bytes);
     if (rc) return rc;
     if (!pos_out || (!inner && (!u || !status))) return CBF_EINVAL;  // inner: a cbf_lattice_run timestep
@@ -813,6 +813,8 @@ static int lattice_advance(const cbf_params* p, const cbf_grid* grid, int32_t W,
                        kp, G, B, W, row_begin, row_end, win_row0, n, Wk.ncell, Wk.spos, Wk.svel, Wk.sidx, Wk.start,
                        Wk.sctl, T, po, uo, status, nbr_count, ext_part, st, Wk.hardq, Wk.qrec, Wk.qcap,
                        chain ? *chain : ChainSpec{});
+    if (filter_done)
+        if (hipError_t e = hipEventRecord(filter_done, s)) return (int)e;
     hipLaunchKernelGGL(k_lattice_filter_hard, dim3(hb), dim3(64), 0, s, kp, G, B, T, po, uo, status, nbr_count,
                        ext_part ? ext_part + 4l * lattice_ext_waves(n) : nullptr, st, Wk.hardq, Wk.qrec, Wk.qcap,
                        chain ? *chain : ChainSpec{}, Wk.sctl);
@@ -827,6 +829,16 @@ extern "C" int cbf_lattice_advance(const cbf_params* p, const cbf_grid* grid, in
                                    void* workspace, size_t workspace_bytes, void* stream) {
     return lattice_advance(p, grid, W, H, row_begin, row_end, win_row0, win_rows, pos, T, pos_out, u, status, nbr_count,
                            guard_rows, extents, stats, workspace, workspace_bytes, row_begin, row_end, stream);
+}
+
+extern "C" int cbf_lattice_advance_marked(const cbf_params* p, const cbf_grid* grid, int32_t W, int32_t H,
+                                          int32_t row_begin, int32_t row_end, int32_t win_row0, int32_t win_rows,
+                                          const double* pos, double T, double* pos_out, double* u, int32_t* status,
+                                          int32_t* nbr_count, int32_t guard_rows, double* extents, uint64_t* stats,
+                                          void* workspace, size_t workspace_bytes, void* filter_done, void* stream) {
+    return lattice_advance(p, grid, W, H, row_begin, row_end, win_row0, win_rows, pos, T, pos_out, u, status, nbr_count,
+                           guard_rows, extents, stats, workspace, workspace_bytes, row_begin, row_end, stream, nullptr,
+                           false, (hipEvent_t)filter_done);
 }
 
 extern "C" int cbf_lattice_step(const cbf_params* p, const cbf_grid* grid, int32_t W, int32_t H, int32_t row_begin,

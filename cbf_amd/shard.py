@@ -151,13 +151,14 @@ class HipBackend:
                                         sub.w1 - sub.w0, P(S.wpos[(sub.w0 - S.w0) * self.W:]), self.gain, P(S.vel),
                                         P(self.wss[-1]), self.ws_bytes, L.stream_handle()), "cbf_lattice_build")
 
-    def lattice_advance(self, S):
+    def lattice_advance(self, S, mark=None):
         L, P = self._lib, self._lib.ptr
         sub = S.subs[-1]
-        L.check(L.lib.cbf_lattice_advance(self.cp, L.C.byref(self.grid), self.W, self.H, S.rb, S.re, sub.w0,
-                                          sub.w1 - sub.w0, P(S.wpos[(sub.w0 - S.w0) * self.W:]), self.T, P(S.own),
-                                          P(S.u), P(S.status), P(S.nbr_count), sub.guard, None, P(S.stats_ptr()),
-                                          P(self.wss[-1]), self.ws_bytes, L.stream_handle()), "cbf_lattice_advance")
+        L.check(L.lib.cbf_lattice_advance_marked(
+            self.cp, L.C.byref(self.grid), self.W, self.H, S.rb, S.re, sub.w0, sub.w1 - sub.w0,
+            P(S.wpos[(sub.w0 - S.w0) * self.W:]), self.T, P(S.own), P(S.u), P(S.status), P(S.nbr_count), sub.guard,
+            None, P(S.stats_ptr()), P(self.wss[-1]), self.ws_bytes,
+            L.C.c_void_p(mark.cuda_event if mark is not None else 0), L.stream_handle()), "cbf_lattice_advance_marked")
 
     def arm_guard_readback(self):
         """Queue a copy of the guard flag to pinned host memory behind this exchange's unpack."""
@@ -313,8 +314,8 @@ class ShardedLattice:
     def build_phase(self):
         self.be.lattice_build(self)
 
-    def advance_phase(self):
-        self.be.lattice_advance(self)
+    def advance_phase(self, mark=None):
+        self.be.lattice_advance(self, mark)
 
     def capture(self):
         """Capture each sub-step's device work (cbf_lattice_step_sharded) into its own hipGraph;

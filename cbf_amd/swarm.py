@@ -336,14 +336,22 @@ class LatticeSwarm:
                                     ptr(self.pos), self.gain, ptr(self.vel), ptr(self.ws), self.ws_bytes,
                                     stream_handle()), "cbf_lattice_build")
 
-    def advance_phase(self):
-        """filter + clip + Euler only (the dominant kernel, K4)."""
+    def advance_phase(self, mark=None):
+        """filter + clip + Euler only (the dominant kernel, K4, then the queued-QP kernel K5).
+        mark: a torch.cuda.Event (already recorded once) that is recorded between K4 and K5."""
         if self.barrier == "euclidean_hocbf":
             check(lib.cbf_lattice_advance_hocbf(self.cp, _lib.C.byref(self.hp), _lib.C.byref(self.grid), self.W,
                                                 self.H, 0, self.H, 0, self.H, ptr(self.pos), self.T, ptr(self.pos),
                                                 ptr(self.u), ptr(self.status), ptr(self.nbr_count), 0, None,
                                                 self._st(), ptr(self.ws), self.ws_bytes, stream_handle()),
                   "cbf_lattice_advance_hocbf")
+            return
+        if mark is not None:
+            check(lib.cbf_lattice_advance_marked(self.cp, _lib.C.byref(self.grid), self.W, self.H, 0, self.H, 0, self.H,
+                                                 ptr(self.pos), self.T, ptr(self.pos), ptr(self.u), ptr(self.status),
+                                                 ptr(self.nbr_count), 0, None, self._st(), ptr(self.ws), self.ws_bytes,
+                                                 _lib.C.c_void_p(mark.cuda_event), stream_handle()),
+                  "cbf_lattice_advance_marked")
             return
         check(lib.cbf_lattice_advance(self.cp, _lib.C.byref(self.grid), self.W, self.H, 0, self.H, 0, self.H,
                                       ptr(self.pos), self.T, ptr(self.pos), ptr(self.u), ptr(self.status),

@@ -274,6 +274,13 @@ int cbf_lattice_advance(const cbf_params* p, const cbf_grid* grid, int32_t W, in
                         int32_t row_end, int32_t win_row0, int32_t win_rows, const double* pos, double T,
                         double* pos_out, double* u, int32_t* status, int32_t* nbr_count, int32_t guard_rows,
                         double* extents, uint64_t* solves, void* workspace, size_t workspace_bytes, void* stream);
+/* cbf_lattice_advance, recording `filter_done` (a hipEvent_t, nullable) on `stream` between the
+ * filter kernel and the queued-QP kernel: the measurement hook for the dominant kernel alone. */
+int cbf_lattice_advance_marked(const cbf_params* p, const cbf_grid* grid, int32_t W, int32_t H, int32_t row_begin,
+                               int32_t row_end, int32_t win_row0, int32_t win_rows, const double* pos, double T,
+                               double* pos_out, double* u, int32_t* status, int32_t* nbr_count, int32_t guard_rows,
+                               double* extents, uint64_t* solves, void* workspace, size_t workspace_bytes,
+                               void* filter_done, void* stream);
 
 /* cbf_lattice_advance with Euclidean HOCBF rows (cbf_hocbf above): after cbf_lattice_build, the
  * filter of every owned agent over its 3x3-cell neighbours in ascending entity order, the HOCBF
