@@ -418,6 +418,26 @@ def test_lattice_stats_off_and_replay(nominal):
     assert sa == sb and sb["solves"] > 0 and sb["errors"] == 0
 
 
+def test_lattice_advance_marked_equals_advance():
+    """cbf_lattice_advance_marked (the bench's measurement hook) == cbf_lattice_advance bit for bit,
+    and its event lands between the start and the end of the advance call."""
+    W, H = 96, 64
+    pos = scenarios.lattice(W, H, seed=8, spacing=0.2)
+    A = swarm.LatticeSwarm(pos, W, H)
+    B = swarm.LatticeSwarm(pos, W, H)
+    A.build_phase()
+    A.advance_phase()
+    B.build_phase()
+    a, m, b = (torch.cuda.Event(enable_timing=True) for _ in range(3))
+    m.record()
+    a.record()
+    B.advance_phase(mark=m)
+    b.record()
+    torch.cuda.synchronize()
+    assert torch.equal(A.pos, B.pos) and torch.equal(A.u, B.u) and torch.equal(A.status, B.status)
+    assert 0 <= a.elapsed_time(m) <= a.elapsed_time(b)
+
+
 def _sample_oracle(pos, vel, idx, threads=16):
     p = po.Params(15)
     chunks = np.array_split(idx, threads)
