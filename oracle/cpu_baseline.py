@@ -147,10 +147,11 @@ def run(kind, budget_s, procs=None, shape=None):
             "one cvxopt-coneqp solve" if kind == "qp" else
             f"random egos of the {shape[0]}x{shape[1]} lattice (spacing {shape[3]}), each an O(N) Python cull "
             "+ cvxopt-coneqp solve")
+    from oracle import refloop
     return {"value": solves / dt, "unit": "agent-QP solves/s", "cores": procs, "kind": "port",
             "per_core": solves / dt / procs,
+            "qp_solver": refloop.QP_SOLVER,
             "sample": f"{done} egos of {what}, through oracle/refloop.py (cross_and_rescue.py:135-160 restated "
-                      f"line by line; cbf.py's cvxopt coneqp restated in numpy, maxiters 600; cvxopt itself is "
-                      f"absent from the image), {procs} single-threaded processes x {dt:.1f} s "
-                      f"({wall:.1f} s wall incl. start-up)",
+                      f"line by line; QP: {refloop.QP_SOLVER}, maxiters 600), {procs} single-threaded processes "
+                      f"x {dt:.1f} s ({wall:.1f} s wall incl. start-up)",
             "cores_source": how}

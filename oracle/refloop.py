@@ -19,9 +19,38 @@ import numpy as np
 from . import cvxqp
 from . import pyoracle as po
 
+# the real cvxopt binary is used when the box has it (it is absent from this
+# image); otherwise the numpy restatement of its coneqp (oracle/cvxqp.py).
+try:
+    import cvxopt as _cvxopt
+    QP_SOLVER = f"cvxopt {getattr(_cvxopt, '__version__', '?')} (solvers.qp)"
+except ImportError:
+    _cvxopt = None
+    QP_SOLVER = "cvxopt coneqp restated in numpy (oracle/cvxqp.py; the cvxopt binary is absent)"
+
+
+def _cvxopt_safe_control(A, b, m, u0, max_speed):
+    """cbf.py:64-92 through the cvxopt binary: min 1/2 |x|^2 s.t. A x <= b, every barrier rhs +1
+    while the solver raises ValueError, then de-bias and clip."""
+    M = _cvxopt.matrix
+    _cvxopt.solvers.options["show_progress"] = False                  # cbf.py:75-76
+    _cvxopt.solvers.options["maxiters"] = 600
+    P, q = M(np.eye(2)), M(np.zeros((2, 1)))
+    b = np.array(b, dtype=np.float64).reshape(-1, 1)
+    while True:
+        try:
+            x = np.array(_cvxopt.solvers.qp(P, q, M(np.asarray(A, dtype=np.float64)), M(b))["x"]).reshape(2)
+            break
+        except ValueError:                                             # cbf.py:84-87
+            b[:m] += 1
+    u = x + np.asarray(u0, dtype=np.float64).reshape(2)
+    return np.array([max(min(u[0], max_speed), -max_speed), max(min(u[1], max_speed), -max_speed)])
+
 
 def get_safe_control(p: po.Params, robot_state, danger, u0):
     A, b = po.assemble(p, robot_state, danger, u0)                    # cbf.py:38-80
+    if _cvxopt is not None:
+        return _cvxopt_safe_control(A, b, len(danger), u0, p.max_speed)
     with warnings.catch_warnings():
         warnings.simplefilter("ignore", RuntimeWarning)
         u, _ = cvxqp.get_safe_control(A, b, len(danger), u0, p.max_speed)  # cbf.py:75-92
