@@ -1,17 +1,25 @@
 """Benchmark of the CBF safety-filter hot path on MI355X (BASELINE.json metric).
 
-Default workload (cfg4): a 1024 x 1024 jittered lattice swarm per GPU, one fused timestep
-(lattice-Laplacian nominal control + cell-list cull + barrier assembly + exact QP + clip + Euler)
-per step, captured in a hipGraph.  value = agent-QP solves/s over the whole job (agents whose
-filter ran, counted on device).  With --gpus N (torchrun, one rank per GPU) the lattice is
-1024 x 1024 N rows, sharded in row stripes, with one RCCL all-gather of halo slabs per step
-(weak scaling).  Prints ONE JSON line on rank 0.
+Default workload (cfg4): a 1024 x 1024 jittered lattice swarm (N = 1,048,576 agents), one fused
+timestep (lattice-Laplacian nominal control + cell-list cull + barrier assembly + exact QP + clip
++ Euler) per step, captured in hipGraphs.  value = agent-QP solves/s over the whole job (agents
+whose filter ran, counted on device).
+
+--gpus N: one rank per GPU.  Under a launcher (torchrun: RANK / WORLD_SIZE set) this process is
+one rank; without one, bench.py starts the N ranks itself as child processes and relays rank 0's
+line.  The lattice is split into N row stripes: by default the SAME 1M-agent
+lattice at any N (strong scaling, 1024 / N rows per GPU, as BASELINE.json's metric is quoted at
+N = 1M); --weak keeps --rows rows per GPU instead.  Ranks exchange ghost rows every few steps
+through ONE RCCL all-to-all (neighbour rows + guard records).  Prints ONE JSON line on rank 0.
 """
 from __future__ import annotations
 
 import argparse
+import hashlib
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -31,6 +39,59 @@ def _dist_env():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     return ws, rank, local
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(n, argv, timeout_s=None):
+    """--gpus N without a launcher: start N copies of this script as child processes, one rank
+    each (RANK = LOCAL_RANK = r, WORLD_SIZE = N, rendezvous on 127.0.0.1), and relay rank 0's
+    one JSON line.  This parent never touches the GPU.  If a rank fails, the others are given a
+    grace period (they may be blocked in a collective) and then terminated; the exit status is
+    non-zero whenever any rank failed."""
+    import threading
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY="0")
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv, env=env,
+                                      stdout=subprocess.PIPE if r == 0 else subprocess.DEVNULL))
+    out = []
+    reader = threading.Thread(target=lambda: out.append(procs[0].stdout.read()), daemon=True)
+    reader.start()
+    t0 = time.time()
+    failed_at = None
+    while any(p.poll() is None for p in procs):
+        if failed_at is None and any(p.poll() not in (None, 0) for p in procs):
+            failed_at = time.time()
+        if (failed_at is not None and time.time() - failed_at > 60) or \
+                (timeout_s is not None and time.time() - t0 > timeout_s):
+            for p in procs:
+                if p.poll() is None:
+                    p.terminate()
+            for p in procs:
+                try:
+                    p.wait(timeout=20)
+                except subprocess.TimeoutExpired:
+                    p.kill()
+                    p.wait()
+            break
+        time.sleep(0.2)
+    reader.join(timeout=30)
+    codes = [p.returncode for p in procs]
+    if all(c == 0 for c in codes):
+        sys.stdout.write(b"".join(out).decode())
+        sys.stdout.flush()
+        return 0
+    sys.stderr.write(f"bench.py: rank exit codes {codes}\n")
+    return next(c for c in codes if c != 0)
 
 
 def load_pmc(config):
@@ -54,17 +115,44 @@ def load_pmc_traffic(config, kernels=ADVANCE_KERNELS):
     return None if any(v is None for v in vals) else float(sum(vals))
 
 
-def cpu_baseline_lattice(W, H, seed, budget_s, spacing, gain, procs=None):
+def cpu_baseline_lattice(W, H, seed, budget_s, spacing, gain, procs=None, nominal=None, cfg2=True):
     """The reference's CPU loop (oracle/refloop.py: cross_and_rescue.py:135-160 restated, with
     cvxopt's coneqp restated) on every core of this job's host share (oracle/cpu_baseline.py):
     random egos of this workload (O(N) Python cull per ego, as the reference does at this N), and
-    beside it the QP-dominated cfg2 shape (N = 100)."""
+    beside it the QP-dominated cfg2 shape (N = 100) and the C restatement on the same egos."""
     from oracle import cpu_baseline
-    res = cpu_baseline.run("cfg4", budget_s, procs=procs, shape=(W, H, seed, spacing, gain))
-    res["qp_dominated_cfg2"] = cpu_baseline.run("qp", budget_s, procs=procs)
-    res["c_restatement"] = cpu_baseline.run("cfg4_c", min(budget_s, 5.0), procs=procs,
-                                            shape=(W, H, seed, spacing, gain))
+    shape = (W, H, seed, spacing, gain, nominal)
+    res = cpu_baseline.run("cfg4", budget_s, procs=procs, shape=shape)
+    if cfg2:
+        res["qp_dominated_cfg2"] = cpu_baseline.run("qp", budget_s, procs=procs)
+    res["c_restatement"] = cpu_baseline.run("cfg4_c", min(budget_s, 5.0), procs=procs, shape=shape)
     return res
+
+
+def cpu_baseline_for(args, cert_sample=None):
+    """The reference's CPU path on the same inputs as this config's GPU run: a
+    bounded sample on rank 0's host cores, N = 1 only (oracle/ is test infrastructure, reached
+    only here, after the timed region)."""
+    from oracle import cpu_baseline
+    b = args.cpu_budget
+    if args.config in ("cfg4", "cfg4f", "cfg4r"):
+        return cpu_baseline_lattice(args.width, args.rows, args.seed, b, args.spacing, args.gain, args.cpu_procs,
+                                    nominal=args.nominal, cfg2=args.config != "cfg4r")
+    if args.config == "cfg3":   # every pair tested on the GPU; the reference's loop culls O(N) per ego too
+        return cpu_baseline_lattice(args.width, args.rows, args.seed, b, args.spacing, args.gain, args.cpu_procs,
+                                    cfg2=False)
+    if args.config == "cfg5":   # meet_at_center.py:118-143 per scenario (its 16 agents vs its 32 entities)
+        mid = (max(1, args.warmup) + args.steps // 2) * args.mc_inner   # the middle of the timed rollout
+        return cpu_baseline.run("mc", b, procs=args.cpu_procs,
+                                shape=(args.mc_scenarios, args.seed, scenarios_mc_gain(), mid))
+    if args.config == "cert" and cert_sample is not None:
+        return cpu_baseline_cert(*cert_sample, budget_s=min(b, 8.0))
+    return None
+
+
+def scenarios_mc_gain():
+    from cbf_amd import scenarios
+    return scenarios.MC_GAIN
 
 
 def full_size_check(S, args):
@@ -110,29 +198,65 @@ def safety_report(st, steps):
                                           "cross_and_rescue.py:147-150); None = no pair closer than 0.2"}
 
 
+def lattice_geometry(args, ws):
+    """(rows per rank, whole-lattice rows, ghost-row halo, sub-steps per exchange).  Strong
+    scaling (default): the --rows-row lattice split into ws stripes; --weak: --rows rows per rank.
+    The halo is the rows one timestep can reach (4 for the consensus lattice; 10 for cfg4r's
+    random walk, whose RELAXED QPs move an agent up to T max_speed = 0.5 per step); the sub-steps
+    default to as many as fit twice into a stripe, at most 8."""
+    if args.weak or ws == 1:
+        R = args.rows
+    else:
+        if args.rows % ws:
+            raise SystemExit(f"bench.py: --rows {args.rows} is not divisible into {ws} stripes (or use --weak)")
+        R = args.rows // ws
+    halo = 10 if args.nominal is not None else 4
+    k = args.substeps if args.substeps else max(1, min(8, R // (2 * halo)))
+    if halo * k > R:
+        raise SystemExit(f"bench.py: {k} sub-steps x {halo} halo rows do not fit a stripe of {R} rows")
+    return R, R * ws, halo, k
+
+
+def gather_state_sha(own, ws):
+    """sha256 of the whole lattice's positions (the ranks' owned rows in rank order, float64 bytes):
+    the same digest for the same rollout at any rank count."""
+    import torch
+    x = own.contiguous()
+    if ws > 1:
+        import torch.distributed as dist
+        if dist.get_backend() == "gloo":
+            x = x.cpu()
+            parts = [torch.empty_like(x) for _ in range(ws)]
+            dist.all_gather(parts, x)
+            x = torch.cat(parts)
+        else:
+            full = torch.empty((ws * x.shape[0],) + tuple(x.shape[1:]), dtype=x.dtype, device=x.device)
+            dist.all_gather_into_tensor(full, x)
+            x = full
+    return hashlib.sha256(x.cpu().numpy().tobytes()).hexdigest()
+
+
 def bench_lattice(args, ws, rank, local):
     import torch
     from cbf_amd import scenarios, swarm
     W = args.width
-    rows = args.rows
-    if ws > 1 or args.shard:
+    sharded = ws > 1 or args.shard
+    rows, rows_total, halo, k = lattice_geometry(args, ws)
+    if sharded:
         from cbf_amd.shard import ShardedLattice
-        S = ShardedLattice(W, rows, seed=args.seed, substeps=args.substeps, spacing=args.spacing, gain=args.gain,
-                           nominal=args.nominal)
+        S = ShardedLattice(W, rows, seed=args.seed, halo=halo, substeps=k, spacing=args.spacing, gain=args.gain,
+                           nominal=args.nominal, exchange=args.exchange)
     else:
         pos = scenarios.lattice(W, rows, seed=args.seed, spacing=args.spacing)
         S = swarm.LatticeSwarm(pos, W, rows, gain=args.gain, barrier=args.barrier, nominal=args.nominal)
-    # the sharded path stays eager: one cbf_lattice_cycle_sharded call per exchange cycle; a
-    # hipGraph of the cycle (ShardedLattice.capture_cycle) measured the same (93.9 vs 93.1 us/step
-    # at one rank), and capturing beside an RCCL communicator is avoided
-    use_graph = not args.eager and not (ws > 1 or args.shard)
+    use_graph = not args.eager
     # single GPU, reference barrier: the timesteps run as cbf_lattice_run calls of `chunk`
     # timesteps (bit-identical to as many cbf_lattice_step calls; each advance bins the next
-    # timestep, so the bin pass runs once per call), each call one hipGraph
-    chunk = args.chunk if (use_graph and args.barrier == "reference" and args.chunk > 1) else 1
+    # timestep, so the bin pass runs once per call), each call one hipGraph.  Sharded: one
+    # hipGraph per exchange cycle (cbf_lattice_cycle_sharded) replayed after each exchange, whose
+    # pack / collective / unpack stay eager.
+    chunk = args.chunk if (use_graph and not sharded and args.barrier == "reference" and args.chunk > 1) else 1
     plan = [chunk] * (args.steps // chunk) + ([args.steps % chunk] if args.steps % chunk else [])
-
-    sharded = ws > 1 or args.shard
 
     def advance(n):
         if chunk > 1 or sharded:  # sharded: whole exchange cycles as one cbf_lattice_cycle_sharded call
@@ -145,7 +269,11 @@ def bench_lattice(args, ws, rank, local):
     # state with the statistics on, checked bit-identical to the timed one and timed as well
     # (ms_per_step_with_stats).  --timed-stats keeps the statistics inside the timed region.
     modes = (True,) if args.timed_stats else (False, True)
-    if use_graph:
+    if use_graph and sharded:
+        for cs in modes:   # (capture_cycle launches nothing)
+            S.collect_stats = cs
+            S.capture_cycle()
+    elif use_graph:
         # a capture's eager warm-up launch advances the swarm: restore it afterwards, so that the
         # timed steps are timesteps W+1 .. W+K of the rollout whatever the graphs' sizes
         snap0 = S.snapshot()
@@ -156,6 +284,10 @@ def bench_lattice(args, ws, rank, local):
                     S.capture(steps=n)
             else:
                 S.capture()
+        if chunk > 1 and not args.timed_stats:   # the per-step-outputs variant (history), statistics off
+            S.collect_stats = False
+            for n in set(plan):
+                S.capture(steps=n, history=True)
         S.restore(snap0)
         del snap0
     S.collect_stats = modes[0]
@@ -163,7 +295,7 @@ def bench_lattice(args, ws, rank, local):
         # first-use costs (the collective's buffers and connections, allocations) are paid by two
         # throwaway exchange cycles, undone by restoring the state: the timed steps stay W+1 .. W+K
         snap0 = S.snapshot()
-        S.run(2 * args.substeps)
+        S.run(2 * k)
         torch.cuda.synchronize()
         if ws > 1:
             S.check_guard()
@@ -174,14 +306,14 @@ def bench_lattice(args, ws, rank, local):
     snap = S.snapshot() if len(modes) > 1 else None
     S.reset_solves()
 
-    def timed():
+    def timed(history=False):
         if ws > 1:
             torch.distributed.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         if chunk > 1:
             for n in plan:
-                S.run(n)
+                S.run(n, history=True) if history else S.run(n)
         else:
             advance(args.steps)
         torch.cuda.synchronize()
@@ -215,6 +347,21 @@ def bench_lattice(args, ws, rank, local):
             S.check_guard()
         if not same:
             raise RuntimeError("the statistics replay did not repeat the timed rollout bit for bit")
+    state_sha = gather_state_sha(own, ws)
+    elapsed_hist = None
+    if snap is not None and chunk > 1:
+        # the same timed steps again with every timestep's outputs stored (u, status, nominal
+        # control, neighbour count: the reference's per-step si_velocities), statistics off
+        stats_keep = S.stats.clone()
+        S.restore(snap)
+        S.collect_stats = False
+        elapsed_hist = timed(history=True)
+        if not all(bool(torch.equal(a, b)) for a, b in zip(end_state, (own, S.history(plan[-1])[1][-1],
+                                                                       S.history(plan[-1])[2][-1]))):
+            raise RuntimeError("the per-step-outputs run did not repeat the timed rollout bit for bit")
+        S.stats.copy_(stats_keep)
+        S.collect_stats = True
+    if snap is not None:
         del snap
     solves = S.solves_total()
     n_local = S.n_owned if sharded else S.n
@@ -239,6 +386,7 @@ def bench_lattice(args, ws, rank, local):
         stat.update(viol_optimal=float(m[0]), viol_original_relaxed=float(m[1]),
                     min_dist2=None if not np.isfinite(m[2].item()) else -float(m[2]))
     safety = safety_report(stat, args.steps) if args.barrier == "reference" else None
+    comm = ("RCCL" if args.backend == "nccl" else "gloo (host-staged rehearsal)") if ws > 1 else "single-rank"
     # dominant kernel (filter + clip + Euler) timed alone with HIP events on the launch stream
     S.collect_stats = modes[0]  # as in the timed region
     # the dominant kernel (k_lattice_filter) alone: an event recorded by the advance call between
@@ -279,21 +427,30 @@ def bench_lattice(args, ws, rank, local):
         "warmup": args.warmup,
         "ms_per_step": elapsed / args.steps * 1e3,
         "ms_per_step_with_stats": None if elapsed_stats is None else elapsed_stats / args.steps * 1e3,
+        "ms_per_step_outputs_every_step": None if elapsed_hist is None else elapsed_hist / args.steps * 1e3,
+        "outputs_every_step_note": "the timed steps replayed with every timestep's filtered control, status, nominal "
+                                   "control and neighbour count stored (cbf_lattice_run_ex CBF_RUN_OUTPUT_HISTORY: "
+                                   "the reference's per-step si_velocities); the headline run stores positions every "
+                                   "timestep and the other outputs on each call's last timestep",
         "timed_region": "filter path only (stats=NULL); safety from a bit-identical statistics replay of the same "
                         "steps" if elapsed_stats is not None else "filter path with the statistics bookkeeping",
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "weak" if args.weak and ws > 1 else "strong",
         "vs_baseline": None,
         "dtype": "f64",
         "data": "synthetic",
-        "config": {"workload": f"{args.config}: {W}x{rows * ws} jittered lattice swarm (spacing {args.spacing}), "
+        "end_state_sha256": state_sha,
+        "config": {"workload": f"{args.config}: {W}x{rows_total} jittered lattice swarm (spacing {args.spacing}), "
                                + (f"lattice-Laplacian consensus (gain {args.gain})" if args.nominal is None else
                                   f"random-walk nominal control (amplitude {args.nominal[1]}, CBF_NOMINAL_RANDOM)")
                                + " + radius-0.2 cell-list cull + CBF QP + clip + Euler, one fused timestep per step",
                    "barrier": args.barrier,
                    "agents_total": n_total, "agents_per_gpu": n_local,
-                   "parallelism": f"row-stripe shards x{ws}, 1 RCCL all-gather of ghost-row slabs per "
-                                  f"{args.substeps} steps" if (ws > 1 or args.shard) else "single GPU",
+                   "parallelism": (f"row-stripe shards x{ws} ({rows} rows each), one {comm} "
+                                   + ("all-to-all (ghost rows to the 2 neighbours + guard records to all)"
+                                      if args.exchange == "neighbour" else "all-gather of ghost-row slabs")
+                                   + f" per {k} steps ({halo * k} ghost rows per side)") if sharded else "single GPU",
+                   "exchange_bytes_per_rank": S.exchange_bytes() if sharded else 0,
                    "graph": use_graph,
                    "timesteps_per_call": max(plan) if chunk > 1 else 1},
         "timesteps_per_s": args.steps / elapsed,
@@ -414,6 +571,11 @@ def bench_mc(args, ws, rank, local):
     return {"metric": METRIC, "value": tot["calls"] / elapsed, "unit": "agent-QP solves/s", "n_gpus": ws,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
             "ms_per_step_with_stats": None if elapsed_stats is None else elapsed_stats / args.steps * 1e3,
+        "ms_per_step_outputs_every_step": None if elapsed_hist is None else elapsed_hist / args.steps * 1e3,
+        "outputs_every_step_note": "the timed steps replayed with every timestep's filtered control, status, nominal "
+                                   "control and neighbour count stored (cbf_lattice_run_ex CBF_RUN_OUTPUT_HISTORY: "
+                                   "the reference's per-step si_velocities); the headline run stores positions every "
+                                   "timestep and the other outputs on each call's last timestep",
             "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f64",
             "data": "synthetic",
             "config": {"workload": f"cfg5: {args.mc_scenarios} independent 16+16 rendezvous scenarios, "
@@ -545,11 +707,15 @@ def main():
     ap.add_argument("--cert-agents", type=int, default=16)
     ap.add_argument("--mc-scenarios", type=int, default=100000)
     ap.add_argument("--mc-inner", type=int, default=10, help="cfg5: timesteps per bench step")
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=1,
+                    help="ranks, one per GPU (without torchrun, bench.py starts them itself)")
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--width", type=int, default=1024)
-    ap.add_argument("--rows", type=int, default=1024, help="lattice rows per GPU")
+    ap.add_argument("--rows", type=int, default=1024,
+                    help="lattice rows: of the whole lattice, split over the ranks (strong scaling, default), "
+                         "or per rank with --weak")
+    ap.add_argument("--weak", action="store_true", help="weak scaling: --rows rows per rank")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--eager", action="store_true", help="no hipGraph capture")
     ap.add_argument("--timed-stats", action="store_true",
@@ -565,12 +731,24 @@ def main():
     ap.add_argument("--cpu-procs", type=int, default=None,
                     help="CPU-baseline processes (default: this job's host cores, oracle/cpu_baseline.py)")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
-                    help="torch.distributed backend for N > 1 (nccl = RCCL; gloo = host-staged rehearsal)")
-    ap.add_argument("--substeps", type=int, default=8,
-                    help="sharded cfg4: timesteps per halo exchange (ghost rows = 4 x substeps)")
+                    help="torch.distributed backend for N > 1 (nccl = RCCL; gloo = host-staged rehearsal, which "
+                         "may put several ranks on one GPU)")
+    ap.add_argument("--exchange", default="neighbour", choices=["neighbour", "allgather"],
+                    help="sharded cfg4: ghost rows by one all-to-all to the two neighbours (default) or by one "
+                         "all-gather to every rank")
+    ap.add_argument("--substeps", type=int, default=None,
+                    help="sharded cfg4: timesteps per halo exchange (default: min(8, rows per rank / (2 halo)))")
     ap.add_argument("--shard", action="store_true",
                     help="cfg4: run the sharded step (halo pack + collective + unpack) even on one rank")
     args = ap.parse_args()
+    if args.gpus < 1:
+        raise SystemExit("bench.py: --gpus must be >= 1")
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # no launcher: this process starts the ranks and relays rank 0's line (it never touches the GPU)
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
+    ws, rank, local = _dist_env()
+    if ws != args.gpus:
+        raise SystemExit(f"bench.py: WORLD_SIZE={ws} from the launcher but --gpus {args.gpus}")
     from cbf_amd import scenarios as _sc
     if args.spacing is None:
         args.spacing = {"cfg4f": 0.2, "cfg4r": 0.22}.get(args.config, _sc.LATTICE_SPACING)
@@ -582,7 +760,6 @@ def main():
     sys.stdout.flush()
     json_out = os.fdopen(os.dup(1), "w")
     os.dup2(2, 1)
-    ws, rank, local = _dist_env()
     import torch
     if ws > 1 or args.shard:
         # (gloo: a rehearsal of several ranks on fewer GPUs, exchanges staged through the host)
@@ -590,7 +767,7 @@ def main():
         torch.cuda.set_device(dev)
         os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        os.environ.setdefault("MASTER_PORT", "29533")
+        os.environ.setdefault("MASTER_PORT", str(_free_port()) if ws == 1 else "29533")
         if args.backend == "gloo":
             torch.distributed.init_process_group("gloo", rank=rank, world_size=ws)
         else:
@@ -610,13 +787,9 @@ def main():
         res = bench_lattice(args, ws, rank, local)
     if rank == 0:
         sample = res.pop("_cert_sample", None)
-        if ws == 1 and not args.no_cpu_baseline and args.config in ("cfg4", "cfg4f"):
-            res["cpu_baseline"] = cpu_baseline_lattice(args.width, args.rows, args.seed, args.cpu_budget,
-                                                       args.spacing, args.gain, args.cpu_procs)
-        elif ws == 1 and not args.no_cpu_baseline and args.config == "cert":
-            res["cpu_baseline"] = cpu_baseline_cert(*sample, budget_s=min(args.cpu_budget, 8.0))
-        else:
-            res["cpu_baseline"] = None
+        res["cpu_baseline"] = None
+        if ws == 1 and not args.no_cpu_baseline:
+            res["cpu_baseline"] = cpu_baseline_for(args, sample)
         json_out.write(json.dumps(res) + "\n")
         json_out.flush()
     if torch.distributed.is_initialized():

@@ -19,6 +19,7 @@ ABI_VERSION = 3  # include/cbf_amd.h CBF_ABI_VERSION
 STATUS_IDLE, STATUS_OPTIMAL, STATUS_RELAXED, STATUS_BOX_INFEASIBLE, STATUS_RELAX_CAP = 0, 1, 2, 3, 4
 STATUS_NBR_OVERFLOW = 5
 STATUS_WORKSPACE_ERROR = 6
+RUN_OUTPUT_HISTORY = 1  # cbf_lattice_run_ex flags (include/cbf_amd.h CBF_RUN_*)
 # words of a lattice-step statistics slot (include/cbf_amd.h CBF_STAT_*)
 (STAT_SOLVES, STAT_OPTIMAL, STAT_RELAXED, STAT_INFEASIBLE, STAT_SEIDEL, STAT_VIOL_OPTIMAL, STAT_VIOL_ORIGINAL,
  STAT_MIN_DIST2, STAT_ERRORS, STAT_BINDING) = range(10)
@@ -90,6 +91,8 @@ SIGNATURES = {
                                             _vp, _d, _d,
                                             _vp, _vp, _vp, _vp, _vp, _vp, _vp, _sz, _vp]),
     "cbf_lattice_run": (C.c_int, [_P, _G, _i32, _i32, _vp, _d, _d, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _sz, _vp]),
+    "cbf_lattice_run_ex": (C.c_int, [_P, _G, _i32, _i32, _vp, _d, _d, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _sz,
+                                     C.c_uint32, _vp]),
     "cbf_lattice_build": (C.c_int, [_P, _G, _i32, _i32, _i32, _i32, _i32, _i32, _vp, _d, _vp, _vp, _sz, _vp]),
     "cbf_lattice_advance": (C.c_int, [_P, _G, _i32, _i32, _i32, _i32, _i32, _i32, _vp, _d, _vp, _vp, _vp, _vp,
                                       _i32, _vp, _vp, _vp, _sz, _vp]),
@@ -104,6 +107,10 @@ SIGNATURES = {
     "cbf_halo_pack": (C.c_int, [_i32, _i32, C.c_int64, _vp, _vp, _i32, _vp, _vp]),
     "cbf_halo_unpack": (C.c_int, [_i32, _i32, _i32, _i32, C.c_int64, _vp, C.c_int64, _i32, _i32, _d, _i32, _vp, _vp,
                                   _vp]),
+    "cbf_halo_nbr_elems": (C.c_int64, [_i32, _i32, _i32, _i32, _i32]),
+    "cbf_halo_pack_nbr": (C.c_int, [_i32, _i32, C.c_int64, _vp, _vp, _i32, _i32, _i32, _vp, _vp]),
+    "cbf_halo_unpack_nbr": (C.c_int, [_i32, _i32, _i32, _i32, C.c_int64, _vp, _i32, _i32, _d, _i32, _vp, _vp,
+                                      _vp]),
     "cbf_lattice_step_sharded": (C.c_int, [_P, _G, _i32, _i32, _i32, _i32, _i32, _i32, _i32, _i32, _vp, _d, _d, _vp,
                                            _vp, _vp, _vp, _vp, _i32, _vp, _vp, _vp, _sz, _vp]),
     "cbf_cert_params_init": (C.c_int, [_CP, _d, _d, _d, _vp]),

@@ -7,6 +7,7 @@ The product boundary is a plain C ABI (include/cbf_amd.h): non-torch callers bin
 from __future__ import annotations
 
 import concurrent.futures as cf
+import hashlib
 import os
 import subprocess
 import sys
@@ -30,13 +31,24 @@ def _compile(src: str, variant: str = "", defines=()) -> str:
     os.makedirs(bdir, exist_ok=True)
     out = os.path.join(bdir, os.path.splitext(src)[0] + ".o")
     path = os.path.join(CSRC, src)
+    lang = ["-x", "hip"] if src.endswith(".hip") else []
+    cmd = [HIPCC] + FLAGS + [f"-D{d}" for d in defines] + lang + ["-c", path, "-o", out]
+    # the object is reused only if it is newer than its sources AND was built with this exact
+    # command line (a stamp beside it): an A/B build with CBF_EXTRA_DEFS never leaks into a plain one
+    stamp = out + ".cmd"
+    key = hashlib.sha256("\0".join(cmd).encode()).hexdigest()
     deps = [path] + [os.path.join(CSRC, h) for h in os.listdir(CSRC) if h.endswith(".hpp")] + \
         [os.path.join(ROOT, "include", "cbf_amd.h")]
     if os.path.exists(out) and os.path.getmtime(out) >= max(os.path.getmtime(d) for d in deps):
-        return out
-    lang = ["-x", "hip"] if src.endswith(".hip") else []
-    cmd = [HIPCC] + FLAGS + [f"-D{d}" for d in defines] + lang + ["-c", path, "-o", out]
+        try:
+            with open(stamp) as f:
+                if f.read() == key:
+                    return out
+        except OSError:
+            pass
     subprocess.run(cmd, check=True)
+    with open(stamp, "w") as f:
+        f.write(key)
     return out
 
 

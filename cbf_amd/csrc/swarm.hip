@@ -858,13 +858,14 @@ extern "C" int cbf_lattice_step(const cbf_params* p, const cbf_grid* grid, int32
 // (chained binning: run_rank in K4, one atomic per queued ego in K5), so only the first build
 // runs the bin kernel.  Positions, workspace and stats as cbf_lattice_step; vel_out, u, status
 // and nbr_count hold the last step's.
-extern "C" int cbf_lattice_run(const cbf_params* p, const cbf_grid* grid, int32_t W, int32_t H, double* pos,
-                               double gain, double T, int32_t steps, double* vel_out, double* u, int32_t* status,
-                               int32_t* nbr_count, uint64_t* stats, void* workspace, size_t workspace_bytes,
-                               void* stream) {
+extern "C" int cbf_lattice_run_ex(const cbf_params* p, const cbf_grid* grid, int32_t W, int32_t H, double* pos,
+                                  double gain, double T, int32_t steps, double* vel_out, double* u, int32_t* status,
+                                  int32_t* nbr_count, uint64_t* stats, void* workspace, size_t workspace_bytes,
+                                  uint32_t flags, void* stream) {
     int rc = check_lattice(p, grid, W, H, 0, H, 0, H, pos, workspace, workspace_bytes);
     if (rc) return rc;
-    if (steps < 0 || !vel_out || !u || !status) return CBF_EINVAL;
+    if (steps < 0 || !vel_out || !u || !status || (flags & ~CBF_RUN_OUTPUT_HISTORY)) return CBF_EINVAL;
+    const bool hist = (flags & CBF_RUN_OUTPUT_HISTORY) != 0;
     hipStream_t s = (hipStream_t)stream;
     const long n = (long)W * H;
     CellWs Wk(workspace, n, (long)grid->nx * grid->ny);
@@ -875,19 +876,28 @@ extern "C" int cbf_lattice_run(const cbf_params* p, const cbf_grid* grid, int32_
             hipLaunchKernelGGL(k_lattice_nominal_bin_ordered, dim3(nblk(n)), dim3(kBlock), 0, s, G, W, H, 0, H, 0, H,
                                p2, Wk.count, Wk.sidx, Wk.start, Wk.ncell, lattice_bcs(Wk), Wk.hardq,
                                (unsigned long long*)nullptr, ExtSpec{0, 0, 0}, Wk.sctl);
-        // vel_out is written by the last timestep only (the inner ones' would be overwritten)
-        lattice_scan_scatter(Wk, W, H, 0, H, 0, n, p2, gain, k + 1 < steps ? nullptr : vel_out, s);
+        // vel_out, u, status and nbr_count are written by the last timestep only (the inner ones'
+        // would be overwritten), or by every timestep into its slice of the history arrays
+        const bool last = k + 1 == steps, out = last || hist;
+        const long o = hist ? (long)k * n : 0;
+        lattice_scan_scatter(Wk, W, H, 0, H, 0, n, p2, gain, out ? vel_out + 2 * o : nullptr, s);
         rc = (int)hipGetLastError();
         if (rc) return rc;
-        // u, status and nbr_count are written by the last timestep only, like vel_out
-        const bool last = k + 1 == steps;
         const ChainSpec C = make_chain(grid, W, H, 0, 0, H, workspace);
-        rc = lattice_advance(p, grid, W, H, 0, H, 0, H, pos, T, pos, last ? u : nullptr, last ? status : nullptr,
-                             last ? nbr_count : nullptr, 0, nullptr, stats, workspace, workspace_bytes, 0, H, stream,
-                             last ? nullptr : &C, !last);
+        rc = lattice_advance(p, grid, W, H, 0, H, 0, H, pos, T, pos, out ? u + 2 * o : nullptr,
+                             out ? status + o : nullptr, out && nbr_count ? nbr_count + o : nullptr, 0, nullptr,
+                             stats, workspace, workspace_bytes, 0, H, stream, last ? nullptr : &C, !out);
         if (rc) return rc;
     }
     return 0;
+}
+
+extern "C" int cbf_lattice_run(const cbf_params* p, const cbf_grid* grid, int32_t W, int32_t H, double* pos,
+                               double gain, double T, int32_t steps, double* vel_out, double* u, int32_t* status,
+                               int32_t* nbr_count, uint64_t* stats, void* workspace, size_t workspace_bytes,
+                               void* stream) {
+    return cbf_lattice_run_ex(p, grid, W, H, pos, gain, T, steps, vel_out, u, status, nbr_count, stats, workspace,
+                              workspace_bytes, 0u, stream);
 }
 
 // One exchange cycle of the row-sharded step (cbf_amd/shard.py): nsub sub-steps after the caller's
@@ -1088,7 +1098,137 @@ __global__ void __launch_bounds__(kBlock) k_halo_unpack(int W, int halo, int row
         atomicOr(flag, 1);
 }
 
+// ---- neighbour exchange (one all_to_all_single): rank r sends its first G rows to r-1 and its
+// last G rows to r+1 only, and its nsub guard records (8 doubles each) to every rank, which the
+// guard needs from all of them.  Chunk q of the send buffer (to rank q) and of the receive buffer
+// (from rank q) are [records (8 nsub) | rows (G W double2s) if q = r +- 1]: the two layouts have the
+// same sizes, so one offset formula serves both (cbf_amd/shard.py: ShardedLattice.nbr_splits).
+__device__ __forceinline__ long nbr_chunk_off(int q, int rank, int ws, long r8, long rs2) {
+    long o = (long)q * r8;
+    if (rank > 0 && q > rank - 1) o += rs2;
+    if (rank + 1 < ws && q > rank + 1) o += rs2;
+    return o;
+}
+
+// rows: thread t < n_lo copies the first G rows (to rank - 1), the next n_hi the last G rows (to
+// rank + 1); block 0 reduces the guard records as k_halo_pack does and writes them into every chunk
+__global__ void __launch_bounds__(kBlock) k_halo_pack_nbr(int W, int halo, long n_own, const double2* __restrict__ own,
+                                                          unsigned long long* __restrict__ keys, int nsub, int ws,
+                                                          int rank, double* __restrict__ send) {
+    const long t = (long)blockIdx.x * kBlock + threadIdx.x;
+    const long rs = (long)halo * W, r8 = 8l * nsub;
+    const long n_lo = rank > 0 ? rs : 0, n_hi = rank + 1 < ws ? rs : 0;
+    if (t < n_lo) {
+        reinterpret_cast<double2*>(send + nbr_chunk_off(rank - 1, rank, ws, r8, 2 * rs) + r8)[t] = own[t];
+    } else if (t < n_lo + n_hi) {
+        const long i = t - n_lo;
+        reinterpret_cast<double2*>(send + nbr_chunk_off(rank + 1, rank, ws, r8, 2 * rs) + r8)[i] = own[n_own - rs + i];
+    }
+    if (blockIdx.x == 0) {
+        const int l = threadIdx.x & 63;
+        for (int q = threadIdx.x >> 6; q < nsub; q += kBlock / 64) {
+            unsigned long long k[kExtVals];
+#pragma unroll
+            for (int v = 0; v < kExtVals; ++v) k[v] = dkey(ext_is_min(v) ? INFINITY : -INFINITY);
+            for (int j = l; j < kExtSlots; j += 64) {
+                unsigned long long* kl = keys + (long)kExtSlotWords * (kExtSlots * q + j);
+#pragma unroll
+                for (int v = 0; v < kExtVals; ++v) {
+                    const unsigned long long x = kl[v];
+                    k[v] = ext_is_min(v) ? (x < k[v] ? x : k[v]) : (x > k[v] ? x : k[v]);
+                    kl[v] = dkey(ext_is_min(v) ? INFINITY : -INFINITY);
+                }
+            }
+            for (int o = 32; o > 0; o >>= 1)
+#pragma unroll
+                for (int v = 0; v < kExtVals; ++v) {
+                    const unsigned long long x = __shfl_xor(k[v], o, 64);
+                    k[v] = ext_is_min(v) ? (x < k[v] ? x : k[v]) : (x > k[v] ? x : k[v]);
+                }
+            // lane d writes the record into the chunks of destinations d, d + 64, ...
+            for (int d = l; d < ws; d += 64) {
+                double* e = send + nbr_chunk_off(d, rank, ws, r8, 2 * rs) + 8 * q;
+#pragma unroll
+                for (int v = 0; v < kExtVals; ++v) e[v] = dkey_inv(k[v]);
+            }
+        }
+    }
+}
+
+// the guard of one sub-step over records at recv + off(q) + 8 s (halo_guard_ok's rule)
+__device__ __forceinline__ bool halo_guard_ok_nbr(const double* recv, int s, int ws, int rank, long r8, long rs2,
+                                                  double radius) {
+    const double rm = radius * (1.0 + 1e-9) + 1e-12;
+    const double* me = recv + nbr_chunk_off(rank, rank, ws, r8, rs2) + 8 * s;
+    const double ymin = me[0], ymax = me[1];
+    if (!(ymin <= ymax)) return true;
+    bool ok = true;
+    for (int q = 0; q < ws; ++q) {
+        const double* o = recv + nbr_chunk_off(q, rank, ws, r8, rs2) + 8 * s;
+        if (q < rank) {
+            const double lim = (q == rank - 1) ? o[2] : o[5];
+            if (!(ymin - lim > rm)) ok = false;
+        } else if (q > rank) {
+            const double lim = (q == rank + 1) ? o[3] : o[4];
+            if (!(lim - ymax > rm)) ok = false;
+        }
+    }
+    return ok;
+}
+
+// Window ghost rows from the neighbours' chunks (rank-1's last rows_lo rows below, rank+1's first
+// rows_hi rows above); block 0 lanes s < nsub run the guard of sub-step s.
+__global__ void __launch_bounds__(kBlock) k_halo_unpack_nbr(int W, int halo, int rows_lo, int rows_hi, long hi_off,
+                                                            const double* __restrict__ recv, int ws, int rank,
+                                                            double radius, int nsub, double2* __restrict__ wpos,
+                                                            int32_t* __restrict__ flag) {
+    const long t = (long)blockIdx.x * kBlock + threadIdx.x;
+    const long nlo = (long)rows_lo * W, nhi = (long)rows_hi * W, rs = (long)halo * W, r8 = 8l * nsub;
+    if (t < nlo) {
+        const double2* src = reinterpret_cast<const double2*>(recv + nbr_chunk_off(rank - 1, rank, ws, r8, 2 * rs) + r8);
+        wpos[t] = src[rs - nlo + t];
+    } else if (t < nlo + nhi) {
+        const double2* src = reinterpret_cast<const double2*>(recv + nbr_chunk_off(rank + 1, rank, ws, r8, 2 * rs) + r8);
+        wpos[hi_off + (t - nlo)] = src[t - nlo];
+    }
+    if (blockIdx.x == 0 && threadIdx.x < nsub && !halo_guard_ok_nbr(recv, threadIdx.x, ws, rank, r8, 2 * rs, radius))
+        atomicOr(flag, 1);
+}
+
 }  // namespace
+
+extern "C" int64_t cbf_halo_nbr_elems(int32_t W, int32_t halo, int32_t nsub, int32_t world_size, int32_t rank) {
+    if (W <= 0 || halo <= 0 || nsub < 1 || world_size < 1 || rank < 0 || rank >= world_size) return -1;
+    const long r8 = 8l * nsub, rs2 = 2l * halo * W;
+    return (int64_t)(world_size * r8 + (rank > 0 ? rs2 : 0) + (rank + 1 < world_size ? rs2 : 0));
+}
+
+extern "C" int cbf_halo_pack_nbr(int32_t W, int32_t halo, int64_t n_own, const double* own, uint64_t* ext_keys,
+                                 int32_t nsub, int32_t world_size, int32_t rank, double* send, void* stream) {
+    if (W <= 0 || halo <= 0 || n_own < 2l * halo * W || !own || !ext_keys || !send || nsub < 1 || nsub > 64 ||
+        world_size < 1 || rank < 0 || rank >= world_size)
+        return CBF_EINVAL;
+    const long rs = (long)halo * W;
+    const long n = (rank > 0 ? rs : 0) + (rank + 1 < world_size ? rs : 0);
+    hipLaunchKernelGGL(k_halo_pack_nbr, dim3(nblk(n > 0 ? n : 1)), dim3(kBlock), 0, (hipStream_t)stream, W, halo,
+                       (long)n_own, reinterpret_cast<const double2*>(own),
+                       reinterpret_cast<unsigned long long*>(ext_keys), nsub, world_size, rank, send);
+    return (int)hipGetLastError();
+}
+
+extern "C" int cbf_halo_unpack_nbr(int32_t W, int32_t halo, int32_t rows_lo, int32_t rows_hi, int64_t hi_row_offset,
+                                   const double* recv, int32_t world_size, int32_t rank, double radius, int32_t nsub,
+                                   double* wpos, int32_t* flag, void* stream) {
+    if (W <= 0 || halo <= 0 || rows_lo < 0 || rows_hi < 0 || rows_lo > halo || rows_hi > halo || !recv || !wpos ||
+        !flag || world_size < 1 || rank < 0 || rank >= world_size || nsub < 1 || nsub > 64 ||
+        (rows_lo > 0 && rank == 0) || (rows_hi > 0 && rank == world_size - 1) || hi_row_offset < 0)
+        return CBF_EINVAL;
+    const long n = (long)(rows_lo + rows_hi) * W;
+    hipLaunchKernelGGL(k_halo_unpack_nbr, dim3(nblk(n > 0 ? n : 1)), dim3(kBlock), 0, (hipStream_t)stream, W, halo,
+                       rows_lo, rows_hi, (long)hi_row_offset * W, recv, world_size, rank, radius, nsub,
+                       reinterpret_cast<double2*>(wpos), flag);
+    return (int)hipGetLastError();
+}
 
 extern "C" size_t cbf_halo_ext_bytes(int32_t nsub) {
     return nsub < 1 ? 0 : (size_t)nsub * kExtSlots * kExtSlotWords * sizeof(unsigned long long);

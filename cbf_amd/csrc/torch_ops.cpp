@@ -23,6 +23,26 @@ void check_rc(int rc, const char* what) {
     TORCH_CHECK(rc == 0, what, ": HIP error ", rc);
 }
 
+// every tensor of a call on the device of its first (the op's stream is that device's)
+void check_device(const at::Tensor& ref, const at::Tensor& t, const char* name) {
+    TORCH_CHECK(t.device() == ref.device(), name, " must be on ", ref.device(), " (got ", t.device(), ")");
+}
+
+// the lattice ops' persistent state: a zero-filled-before-first-use uint8 workspace, and optional
+// int64[1024] statistics (None: the statistics-free kernel instantiation the bench times)
+uint64_t* check_lattice_state(const at::Tensor& pos, const at::Tensor& workspace,
+                              const c10::optional<at::Tensor>& stats) {
+    TORCH_CHECK(workspace.is_cuda() && workspace.scalar_type() == at::kByte && workspace.is_contiguous(),
+                "workspace must be a contiguous uint8 GPU tensor");
+    check_device(pos, workspace, "workspace");
+    if (!stats) return nullptr;
+    TORCH_CHECK(stats->is_cuda() && stats->scalar_type() == at::kLong && stats->is_contiguous() &&
+                    stats->numel() == 1024,
+                "stats must be an int64[1024] GPU tensor (or None)");
+    check_device(pos, *stats, "stats");
+    return reinterpret_cast<uint64_t*>(stats->data_ptr<int64_t>());
+}
+
 void check_f64(const at::Tensor& t, const char* name, int64_t cols) {
     TORCH_CHECK(t.is_cuda(), name, " must be a GPU tensor");
     TORCH_CHECK(t.scalar_type() == at::kDouble, name, " must be float64");
@@ -60,6 +80,9 @@ std::tuple<at::Tensor, at::Tensor> get_safe_control_batch(const at::Tensor& robo
     check_f64(obs_states, "obs_states", 4);
     const int64_t n = robot_state.size(0);
     TORCH_CHECK(u0.size(0) == n, "u0 must have one row per ego");
+    check_device(robot_state, u0, "u0");
+    check_device(robot_state, nbr_off, "nbr_off");
+    check_device(robot_state, obs_states, "obs_states");
     TORCH_CHECK(nbr_off.is_cuda() && nbr_off.scalar_type() == at::kInt && nbr_off.is_contiguous() &&
                     nbr_off.dim() == 1 && nbr_off.size(0) == n + 1,
                 "nbr_off must be an int32 GPU tensor of n + 1 offsets");
@@ -82,6 +105,7 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> filter_swarm(const at::Tensor& po
     check_f64(vel, "vel", 2);
     const int64_t n = pos.size(0);
     TORCH_CHECK(vel.size(0) == n && n_obs >= 0 && n_obs <= n, "pos / vel / n_obs do not match");
+    check_device(pos, vel, "vel");
     const cbf_params p = make_params(max_speed, dmin, k, c10::nullopt, c10::nullopt, safety_distance);
     const int64_t ne = n - n_obs;
     at::Tensor u = at::empty({ne, 2}, pos.options());
@@ -99,18 +123,15 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> filter_swarm(const at::Tensor& po
 
 // One fused lattice timestep (cbf_lattice_step) of a W x H lattice swarm, positions advanced in
 // place.  The cell grid is (x0, y0, cell edge, nx, ny); `workspace` (uint8, zero-filled before its
-// first use, cbf_lattice_workspace_size bytes) and `stats` (int64[1024], CBF_STAT_* words) persist
-// across steps.  Returns (nominal control, filtered control, status, neighbour count).
+// first use, cbf_lattice_workspace_size bytes) and `stats` (int64[1024], CBF_STAT_* words, or None
+// for the statistics-free kernels) persist across steps; all tensors on pos's device.  Returns (nominal control, filtered control, status, neighbour count).
 std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> lattice_step(
     at::Tensor pos, int64_t W, int64_t H, double gain, double T, double x0, double y0, double cell, int64_t nx,
-    int64_t ny, at::Tensor workspace, at::Tensor stats, double max_speed, double dmin, double k,
+    int64_t ny, at::Tensor workspace, c10::optional<at::Tensor> stats, double max_speed, double dmin, double k,
     double safety_distance) {
     check_f64(pos, "pos", 2);
     TORCH_CHECK(pos.size(0) == W * H, "pos must hold W x H agents");
-    TORCH_CHECK(workspace.is_cuda() && workspace.scalar_type() == at::kByte && workspace.is_contiguous(),
-                "workspace must be a contiguous uint8 GPU tensor");
-    TORCH_CHECK(stats.is_cuda() && stats.scalar_type() == at::kLong && stats.is_contiguous() && stats.numel() == 1024,
-                "stats must be an int64[1024] GPU tensor");
+    uint64_t* st = check_lattice_state(pos, workspace, stats);
     const cbf_params p = make_params(max_speed, dmin, k, c10::nullopt, c10::nullopt, safety_distance);
     cbf_grid g;
     g.x0 = x0;
@@ -126,7 +147,7 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> lattice_step(
     check_rc(cbf_lattice_step(&p, &g, (int32_t)W, (int32_t)H, 0, (int32_t)H, 0, (int32_t)H, pos.data_ptr<double>(),
                               gain, T, pos.data_ptr<double>(), vel.data_ptr<double>(), u.data_ptr<double>(),
                               status.data_ptr<int32_t>(), cnt.data_ptr<int32_t>(), 0, nullptr,
-                              reinterpret_cast<uint64_t*>(stats.data_ptr<int64_t>()), workspace.data_ptr(),
+                              st, workspace.data_ptr(),
                               (size_t)workspace.numel(), stream()),
              "cbf_lattice_step");
     return {vel, u, status, cnt};
@@ -137,15 +158,12 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> lattice_step(
 // filtered control, status, neighbour count).
 std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> lattice_run(
     at::Tensor pos, int64_t W, int64_t H, double gain, double T, int64_t steps, double x0, double y0, double cell,
-    int64_t nx, int64_t ny, at::Tensor workspace, at::Tensor stats, double max_speed, double dmin, double k,
+    int64_t nx, int64_t ny, at::Tensor workspace, c10::optional<at::Tensor> stats, double max_speed, double dmin, double k,
     double safety_distance) {
     check_f64(pos, "pos", 2);
     TORCH_CHECK(pos.size(0) == W * H, "pos must hold W x H agents");
-    TORCH_CHECK(steps >= 0, "steps must be >= 0");
-    TORCH_CHECK(workspace.is_cuda() && workspace.scalar_type() == at::kByte && workspace.is_contiguous(),
-                "workspace must be a contiguous uint8 GPU tensor");
-    TORCH_CHECK(stats.is_cuda() && stats.scalar_type() == at::kLong && stats.is_contiguous() && stats.numel() == 1024,
-                "stats must be an int64[1024] GPU tensor");
+    TORCH_CHECK(steps >= 1, "steps must be >= 1 (the outputs are the last timestep's)");
+    uint64_t* st = check_lattice_state(pos, workspace, stats);
     const cbf_params p = make_params(max_speed, dmin, k, c10::nullopt, c10::nullopt, safety_distance);
     cbf_grid g;
     g.x0 = x0;
@@ -160,7 +178,7 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> lattice_run(
     at::Tensor cnt = at::empty({n}, pos.options().dtype(at::kInt));
     check_rc(cbf_lattice_run(&p, &g, (int32_t)W, (int32_t)H, pos.data_ptr<double>(), gain, T, (int32_t)steps,
                              vel.data_ptr<double>(), u.data_ptr<double>(), status.data_ptr<int32_t>(),
-                             cnt.data_ptr<int32_t>(), reinterpret_cast<uint64_t*>(stats.data_ptr<int64_t>()),
+                             cnt.data_ptr<int32_t>(), st,
                              workspace.data_ptr(), (size_t)workspace.numel(), stream()),
              "cbf_lattice_run");
     return {vel, u, status, cnt};
@@ -184,11 +202,11 @@ TORCH_LIBRARY(cbf_amd, m) {
     m.def("filter_swarm(Tensor pos, Tensor vel, int n_obs, float max_speed, float dmin=0.2, float k=1., "
           "float safety_distance=0.2) -> (Tensor, Tensor, Tensor)");
     m.def("lattice_step(Tensor(a!) pos, int W, int H, float gain, float T, float x0, float y0, float cell, int nx, "
-          "int ny, Tensor(b!) workspace, Tensor(c!) stats, float max_speed=15., float dmin=0.2, float k=1., "
-          "float safety_distance=0.2) -> (Tensor, Tensor, Tensor, Tensor)");
+          "int ny, Tensor(b!) workspace, Tensor(c!)? stats=None, float max_speed=15., float dmin=0.2, "
+          "float k=1., float safety_distance=0.2) -> (Tensor, Tensor, Tensor, Tensor)");
     m.def("lattice_run(Tensor(a!) pos, int W, int H, float gain, float T, int steps, float x0, float y0, float cell, "
-          "int nx, int ny, Tensor(b!) workspace, Tensor(c!) stats, float max_speed=15., float dmin=0.2, float k=1., "
-          "float safety_distance=0.2) -> (Tensor, Tensor, Tensor, Tensor)");
+          "int nx, int ny, Tensor(b!) workspace, Tensor(c!)? stats=None, float max_speed=15., float dmin=0.2, "
+          "float k=1., float safety_distance=0.2) -> (Tensor, Tensor, Tensor, Tensor)");
     m.def("lattice_workspace_size(int W, int H, float x0, float y0, float cell, int nx, int ny) -> int",
           &lattice_workspace_size);
     m.def("abi_version() -> int", []() -> int64_t { return cbf_abi_version(); });

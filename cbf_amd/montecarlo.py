@@ -63,13 +63,32 @@ class MonteCarlo:
         self.viol_opt = 0.0                          # max row violation over OPTIMAL solves
         self.viol_orig = 0.0                         # max original-row violation over RELAXED solves
         self.min_d2 = math.inf                       # min neighbour distance^2
-        self._pending = []
+        # running accumulators of the rollouts since the last fold, in the backend's array type
+        # (device tensors for the HIP backend): each rollout's per-scenario results are reduced
+        # into them right away (no host sync), so a long run holds O(1) result memory
+        self._acc = None
+
+    def _fold(self, cnt, mv, sf):
+        """Reduce one rollout's per-scenario results into the running accumulators: counts summed,
+        {max violation (OPTIMAL), max original-row violation (RELAXED), -min distance^2} maxed."""
+        xp = np
+        if hasattr(cnt, "is_cuda"):
+            import torch as xp
+        c = cnt.sum(0)
+        # (the backends return both statistics arrays or neither)
+        m = None if mv is None or sf is None else xp.stack([mv.max(), sf[:, 0].max(), -sf[:, 1].min()])
+        if self._acc is None:
+            self._acc = [c, m]
+            return
+        self._acc[0] = self._acc[0] + c
+        if m is not None:
+            self._acc[1] = m if self._acc[1] is None else xp.maximum(self._acc[1], m)
 
     def run(self, steps):
         """Advance this rank's scenarios by `steps` timesteps (device work only; no host sync)."""
         if self.hi > self.lo:
-            self._pending.append(self.be.rollout(self.pos, self.n_o, self.n_a, steps, self.ga) if self.collect_stats
-                                 else self.be.rollout(self.pos, self.n_o, self.n_a, steps, self.ga, stats=False))
+            self._fold(*(self.be.rollout(self.pos, self.n_o, self.n_a, steps, self.ga) if self.collect_stats
+                         else self.be.rollout(self.pos, self.n_o, self.n_a, steps, self.ga, stats=False)))
 
     def snapshot(self):
         """A copy of this rank's scenario states, for restore()."""
@@ -80,14 +99,15 @@ class MonteCarlo:
         self.pos.copy_(snap)
 
     def _local(self):
-        for cnt, mv, sf in self._pending:
-            self.counts += np.asarray(cnt.sum(0).tolist(), dtype=np.int64)
-            if mv is not None:
-                self.viol_opt = max(self.viol_opt, float(mv.max()))
-            if sf is not None:
-                self.viol_orig = max(self.viol_orig, float(sf[:, 0].max()))
-                self.min_d2 = min(self.min_d2, float(sf[:, 1].min()))
-        self._pending = []
+        if self._acc is not None:
+            c, m = self._acc
+            self.counts += np.asarray(c.tolist(), dtype=np.int64)
+            if m is not None:
+                m = [float(v) for v in m.tolist()]
+                self.viol_opt = max(self.viol_opt, m[0])
+                self.viol_orig = max(self.viol_orig, m[1])
+                self.min_d2 = min(self.min_d2, -m[2])
+        self._acc = None
 
     def totals(self) -> dict:
         """The whole batch's counters and safety record (one all-reduce per kind across ranks)."""

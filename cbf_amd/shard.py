@@ -5,11 +5,16 @@ GPU).  One timestep depends on lattice rows up to `halo` = 4 away (cull candidat
 away, plus the row that forms their nominal control), so a rank that holds G = halo * k ghost rows
 on each side can advance k timesteps ("sub-steps") between exchanges, recomputing the ghost rows
 that are still exact.  Each exchange (every k sub-steps) is ONE collective:
-  1. pack    (cbf_halo_pack)   the first and last G owned rows + the guard records of the last k
-             sub-steps into one send slab;
-  2. gather  ONE all_gather_into_tensor of the slabs (RCCL over xGMI) -- 2 G W 16 B per rank;
-  3. unpack  (cbf_halo_unpack) rank r-1's last rows and rank r+1's first rows into the ghost rows
-             of the window, and the halo guard of the k recorded sub-steps;
+  1. pack    (cbf_halo_pack_nbr)   the first G owned rows into the chunk for rank r-1, the last G
+             rows into the chunk for rank r+1, and the guard records of the last k sub-steps into
+             every rank's chunk;
+  2. a2a     ONE all_to_all_single (RCCL over xGMI): G W 16 B of rows to each neighbour and 64 k B
+             of records to every rank -- the neighbour exchange of SURVEY 8(f)1.  (exchange=
+             "allgather": one all_gather_into_tensor of [first G rows | last G rows | records]
+             slabs, cbf_halo_pack / cbf_halo_unpack, which delivers every rank's rows to everyone:
+             (world - 1) x 2 G W 16 B per rank instead of 2 x G W 16 B.)
+  3. unpack  (cbf_halo_unpack_nbr) rank r-1's last rows and rank r+1's first rows into the ghost
+             rows of the window, and the halo guard of the k recorded sub-steps;
 then sub-step s (cbf_lattice_step_sharded) computes rows [rb - D_s, re + D_s), D_s = G - halo (s+1)
 (the owned rows at the last sub-step), over the window of those rows +- halo, with its own
 workspace (so each sub-step keeps its cell order from cycle to cycle).
@@ -116,11 +121,20 @@ class HipBackend:
 
     def pack(self, S):
         L, P = self._lib, self._lib.ptr
+        if S.exchange_mode == "neighbour":
+            L.check(L.lib.cbf_halo_pack_nbr(self.W, S.G, S.n_owned, P(S.own), P(self.ext_keys), self.nsub, S.ws,
+                                            S.rank, P(S.send), L.stream_handle()), "cbf_halo_pack_nbr")
+            return
         L.check(L.lib.cbf_halo_pack(self.W, S.G, S.n_owned, P(S.own), P(self.ext_keys), self.nsub, P(S.send),
                                     L.stream_handle()), "cbf_halo_pack")
 
     def unpack_guard(self, S):
         L, P = self._lib, self._lib.ptr
+        if S.exchange_mode == "neighbour":
+            L.check(L.lib.cbf_halo_unpack_nbr(self.W, S.G, S.rb - S.w0, S.w1 - S.re, S.re - S.w0, P(S.recv), S.ws,
+                                              S.rank, self.radius, self.nsub, P(S.wpos), P(self.flag),
+                                              L.stream_handle()), "cbf_halo_unpack_nbr")
+            return
         L.check(L.lib.cbf_halo_unpack(self.W, S.G, S.rb - S.w0, S.w1 - S.re, S.re - S.w0, P(S.recv), S.stride,
                                       S.ws, S.rank, self.radius, self.nsub, P(S.wpos), P(self.flag),
                                       L.stream_handle()), "cbf_halo_unpack")
@@ -194,7 +208,7 @@ class ShardedLattice:
 
     def __init__(self, W, rows_per_rank, seed=0, halo=4, substeps=4, gain=scenarios.LATTICE_GAIN, T=scenarios.T,
                  params=None, backend=None, group=None, pos_global=None, spacing=scenarios.LATTICE_SPACING,
-                 nominal=None):
+                 nominal=None, exchange="neighbour"):
         import torch
         import torch.distributed as dist
         from .swarm import FilterParams, make_grid
@@ -243,29 +257,55 @@ class ShardedLattice:
         self.stats = t(np.zeros(1024, np.int64))  # rollout statistics, include/cbf_amd.h CBF_STAT_*
         # collect_stats=False passes stats=NULL (no statistics bookkeeping; results bit-identical)
         self.collect_stats = True
-        # send slab: [first G rows | last G rows | k guard records of 8 doubles] doubles
-        self.slab = 2 * self.G * W * 2
+        if exchange not in ("neighbour", "allgather"):
+            raise ValueError(f"exchange must be 'neighbour' or 'allgather', got {exchange!r}")
+        self.exchange_mode = exchange
+        self.slab = 2 * self.G * W * 2      # doubles of the first + last G owned rows
         self.stride = self.slab + 8 * substeps
-        self.send = t(np.zeros(self.stride))
-        self.recv = t(np.zeros(self.stride * self.ws))
-        self.use_list_gather = dist.get_backend(group) == "gloo"
-        self.graph = None
-        self.cycle_graph = None
+        if exchange == "neighbour":
+            # chunk q (to / from rank q) = [k records of 8 doubles | G rows if q = rank +- 1]
+            self.splits = self.nbr_splits(self.ws, self.rank, self.G * W * 2, substeps)
+            self.send = t(np.zeros(sum(self.splits)))
+            self.recv = t(np.zeros(sum(self.splits)))
+        else:
+            # all-gather: send slab [first G rows | last G rows | k records], world slabs received
+            self.send = t(np.zeros(self.stride))
+            self.recv = t(np.zeros(self.stride * self.ws))
+        self.use_gloo = dist.get_backend(group) == "gloo"
+        # captured device work, keyed by collect_stats (the statistics pointer is baked into a graph)
+        self.graphs = {}         # per-sub-step graphs (capture())
+        self.cycle_graphs = {}   # whole-cycle graphs (capture_cycle())
         self.sub = 0  # next sub-step of the current exchange cycle
 
+    @staticmethod
+    def nbr_splits(ws, rank, rows_elems, nsub):
+        """Chunk sizes (doubles) of the neighbour exchange's send and receive buffers, in rank
+        order: every rank gets this rank's 8 nsub doubles of guard records, ranks rank - 1 and
+        rank + 1 also its first / last G rows (rows_elems doubles); receiving mirrors it
+        (cbf_halo_nbr_elems, nbr_chunk_off in swarm.hip)."""
+        return [8 * nsub + (rows_elems if abs(q - rank) == 1 else 0) for q in range(ws)]
+
+    def chunk_offset(self, q):
+        """Offset (doubles) of chunk q in the neighbour exchange's send / receive buffer."""
+        return sum(self.splits[:q])
+
     # ---- one timestep -------------------------------------------------------------------------
-    def _gather(self):
-        if self.use_list_gather:   # gloo (CPU tests, or a 1-GPU rehearsal of several ranks via host staging)
-            if self.send.is_cuda:
-                rc = self.recv.cpu()
-                self.dist.all_gather(list(rc.view(self.ws, self.stride).unbind(0)), self.send.cpu(),
-                                     group=self.group)
-                self.recv.copy_(rc)
-            else:
-                self.dist.all_gather(list(self.recv.view(self.ws, self.stride).unbind(0)), self.send,
-                                     group=self.group)
-        else:                      # RCCL: one all-gather into the contiguous receive slab
-            self.dist.all_gather_into_tensor(self.recv, self.send, group=self.group)
+    def _collective(self):
+        """The exchange's one collective: all_to_all_single of the neighbour chunks (default) or
+        all_gather of the slabs.  RCCL works on the device buffers; gloo (the CPU tests, or a 1-GPU
+        rehearsal of several ranks) on host copies."""
+        dist = self.dist
+        staged = self.use_gloo and self.send.is_cuda
+        send = self.send.cpu() if staged else self.send
+        recv = self.recv.cpu() if staged else self.recv
+        if self.exchange_mode == "neighbour":
+            dist.all_to_all_single(recv, send, self.splits, self.splits, group=self.group)
+        elif self.use_gloo:
+            dist.all_gather(list(recv.view(self.ws, self.stride).unbind(0)), send, group=self.group)
+        else:
+            dist.all_gather_into_tensor(recv, send, group=self.group)
+        if staged:
+            self.recv.copy_(recv)
 
     def exchange(self):
         # the guard of the sub-steps certified at earlier exchanges, read back without waiting:
@@ -273,9 +313,15 @@ class ShardedLattice:
         if self.be.poll_guard():
             raise RuntimeError(self._guard_msg())
         self.be.pack(self)
-        self._gather()
+        self._collective()
         self.be.unpack_guard(self)
         self.be.arm_guard_readback()
+
+    def exchange_bytes(self):
+        """Bytes this rank sends per exchange (rows + guard records, self excluded)."""
+        if self.exchange_mode == "neighbour":
+            return 8 * (sum(self.splits) - self.splits[self.rank])
+        return 8 * self.stride * (self.ws - 1)
 
     def _guard_msg(self):
         return (f"rank {self.rank}: halo guard failed -- an agent moved within the cull radius of a stripe from "
@@ -284,8 +330,9 @@ class ShardedLattice:
     def step(self):
         if self.sub == 0:
             self.exchange()
-        if self.graph is not None:
-            self.graph[self.sub].replay()
+        graph = self.graphs.get(self.collect_stats)
+        if graph is not None:
+            graph[self.sub].replay()
         else:
             self.be.lattice_step(self, self.sub, self.subs[self.sub])
         self.sub = (self.sub + 1) % self.k
@@ -304,8 +351,9 @@ class ShardedLattice:
             if self.sub == 0:
                 self.exchange()
             n = min(self.k - self.sub, steps - done)
-            if n == self.k and self.cycle_graph is not None:
-                self.cycle_graph.replay()
+            cycle_graph = self.cycle_graphs.get(self.collect_stats)
+            if n == self.k and cycle_graph is not None:
+                cycle_graph.replay()
             else:   # a whole cycle, or the sub-steps left of one: one call (its first sub-step bins)
                 self.be.lattice_cycle(self, self.sub, self.sub + n)
             self.sub = (self.sub + n) % self.k
@@ -318,8 +366,10 @@ class ShardedLattice:
         self.be.lattice_advance(self, mark)
 
     def capture(self):
-        """Capture each sub-step's device work (cbf_lattice_step_sharded) into its own hipGraph;
-        the exchange (pack, collective, unpack) stays eager at the start of a cycle."""
+        """Capture each sub-step's device work (cbf_lattice_step_sharded) into its own hipGraph,
+        for the current collect_stats (graphs are kept per setting: the statistics pointer is part
+        of the captured launches); the exchange (pack, collective, unpack) stays eager at the start
+        of a cycle.  Capture is thread-local, so a communicator's watchdog thread is unaffected."""
         torch = self.torch
         if not self.own.is_cuda:
             return None
@@ -327,25 +377,25 @@ class ShardedLattice:
         graphs = []
         for s in range(self.k):
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
+            with torch.cuda.graph(g, capture_error_mode="thread_local"):
                 self.be.lattice_step(self, s, self.subs[s])
             graphs.append(g)
-        self.graph = graphs
+        self.graphs[self.collect_stats] = graphs
         return graphs
 
     def capture_cycle(self):
         """Capture one whole exchange cycle's device work (the cbf_lattice_cycle_sharded call: k
-        sub-steps, ~5 launches each) into one hipGraph that run() replays after each exchange; the
-        exchange itself (pack, collective, unpack) stays eager.  Capture launches nothing, so the
-        swarm does not advance."""
+        sub-steps, ~5 launches each) into one hipGraph, for the current collect_stats, that run()
+        replays after each exchange; the exchange itself (pack, collective, unpack) stays eager.
+        Capture launches nothing, so the swarm does not advance."""
         torch = self.torch
         if not self.own.is_cuda or not hasattr(self.be, "lattice_cycle"):
             return None
         torch.cuda.synchronize()
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
+        with torch.cuda.graph(g, capture_error_mode="thread_local"):
             self.be.lattice_cycle(self)
-        self.cycle_graph = g
+        self.cycle_graphs[self.collect_stats] = g
         return g
 
     def stats_ptr(self):

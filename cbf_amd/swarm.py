@@ -288,7 +288,8 @@ class LatticeSwarm:
         self.ap_ws = torch.empty((lib.cbf_allpairs_workspace_size(n, n) if method == "allpairs" else 1,),
                                  dtype=torch.uint8, device=self.dev)
         self.graphs = {}      # captured step() graphs, keyed by collect_stats
-        self.run_graphs = {}  # captured run(steps) graphs, keyed by (steps, collect_stats)
+        self.run_graphs = {}  # captured run(steps) graphs, keyed by (steps, collect_stats, history)
+        self._hist = {}       # per-timestep output arrays of run(steps, history=True), keyed by steps
 
     def _st(self):
         return ptr(self.stats) if self.collect_stats else None
@@ -313,22 +314,48 @@ class LatticeSwarm:
                                    ptr(self.status), ptr(self.nbr_count), 0, None, self._st(), ptr(self.ws),
                                    self.ws_bytes, stream_handle()), "cbf_lattice_step")
 
-    def _launch_run(self, steps):
-        check(lib.cbf_lattice_run(self.cp, _lib.C.byref(self.grid), self.W, self.H, ptr(self.pos), self.gain, self.T,
-                                  steps, ptr(self.vel), ptr(self.u), ptr(self.status), ptr(self.nbr_count),
-                                  self._st(), ptr(self.ws), self.ws_bytes, stream_handle()), "cbf_lattice_run")
+    def _history(self, steps):
+        """Per-timestep output arrays for run(steps, history=True): (vel, u, status, nbr_count) of
+        `steps` timesteps, grown as needed (the graphs of a size keep their buffers)."""
+        import torch
+        h = self._hist.get(steps)
+        if h is None:
+            n, dev = self.n, self.dev
+            h = (torch.empty((steps, n, 2), dtype=torch.float64, device=dev),
+                 torch.empty((steps, n, 2), dtype=torch.float64, device=dev),
+                 torch.empty((steps, n), dtype=torch.int32, device=dev),
+                 torch.empty((steps, n), dtype=torch.int32, device=dev))
+            self._hist[steps] = h
+        return h
 
-    def run(self, steps):
+    def _launch_run(self, steps, history=False):
+        if history:
+            vel, u, st, cnt = self._history(steps)
+            flags = _lib.RUN_OUTPUT_HISTORY
+        else:
+            vel, u, st, cnt, flags = self.vel, self.u, self.status, self.nbr_count, 0
+        check(lib.cbf_lattice_run_ex(self.cp, _lib.C.byref(self.grid), self.W, self.H, ptr(self.pos), self.gain,
+                                     self.T, steps, ptr(vel), ptr(u), ptr(st), ptr(cnt), self._st(), ptr(self.ws),
+                                     self.ws_bytes, flags, stream_handle()), "cbf_lattice_run_ex")
+
+    def run(self, steps, history=False):
         """`steps` timesteps through cbf_lattice_run (bit-identical to `steps` step() calls; the
         bin pass runs once, later timesteps are binned by the previous advance).  Reference
-        barrier, cell method only."""
+        barrier, cell method only.  history=True stores every timestep's nominal control, filtered
+        control, status and neighbour count (the reference's per-step si_velocities,
+        cross_and_rescue.py:159-160) in the arrays of history(steps) instead of the last one only."""
         if self.method != "cells" or self.barrier != "reference":
             raise ValueError("run() is the fused multi-step path of the reference barrier on the cell list")
-        g = self.run_graphs.get((steps, self.collect_stats))
+        g = self.run_graphs.get((steps, self.collect_stats, history))
         if g is not None:
             g.replay()
         else:
-            self._launch_run(steps)
+            self._launch_run(steps, history)
+
+    def history(self, steps):
+        """The per-timestep outputs of the last run(steps, history=True): (vel, u, status,
+        nbr_count), leading dimension = timestep."""
+        return self._history(steps)
 
     def build_phase(self):
         """nominal control + cell list only (K1-K3)."""
@@ -372,12 +399,12 @@ class LatticeSwarm:
     def reset_solves(self):
         self.stats.zero_()
 
-    def capture(self, steps=None):
-        """Capture one step (replayed by step()) or, with `steps`, one run(steps) call (replayed by
-        run(steps); one graph per step count) into a hipGraph.  The warm-up launch outside the
-        capture advances the swarm."""
+    def capture(self, steps=None, history=False):
+        """Capture one step (replayed by step()) or, with `steps`, one run(steps, history) call
+        (replayed by run(steps, history); one graph per step count) into a hipGraph.  The warm-up
+        launch outside the capture advances the swarm."""
         import torch
-        launch = self._launch if steps is None else (lambda: self._launch_run(steps))
+        launch = self._launch if steps is None else (lambda: self._launch_run(steps, history))
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):
@@ -390,7 +417,7 @@ class LatticeSwarm:
         if steps is None:
             self.graphs[self.collect_stats] = g
         else:
-            self.run_graphs[(steps, self.collect_stats)] = g
+            self.run_graphs[(steps, self.collect_stats, history)] = g
         return g
 
     def snapshot(self) -> list:

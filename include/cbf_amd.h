@@ -266,6 +266,17 @@ int cbf_lattice_run(const cbf_params* p, const cbf_grid* grid, int32_t W, int32_
                     double T, int32_t steps, double* vel_out, double* u, int32_t* status, int32_t* nbr_count,
                     uint64_t* solves, void* workspace, size_t workspace_bytes, void* stream);
 
+/*
+ * cbf_lattice_run with flags.  CBF_RUN_OUTPUT_HISTORY: vel_out, u, status and nbr_count are
+ * arrays of `steps` timesteps (timestep t at element offset t W H of each) and every timestep's
+ * values are stored -- the reference's per-step si_velocities (cross_and_rescue.py:159-160) for a
+ * controller that consumes each step's filtered control.  flags = 0 is cbf_lattice_run.
+ */
+#define CBF_RUN_OUTPUT_HISTORY 1u
+int cbf_lattice_run_ex(const cbf_params* p, const cbf_grid* grid, int32_t W, int32_t H, double* pos, double gain,
+                       double T, int32_t steps, double* vel_out, double* u, int32_t* status, int32_t* nbr_count,
+                       uint64_t* solves, void* workspace, size_t workspace_bytes, uint32_t flags, void* stream);
+
 int cbf_lattice_build(const cbf_params* p, const cbf_grid* grid, int32_t W, int32_t H, int32_t row_begin,
                       int32_t row_end, int32_t win_row0, int32_t win_rows, const double* pos, double gain,
                       double* vel_out, void* workspace, size_t workspace_bytes, void* stream);
@@ -332,6 +343,22 @@ int cbf_halo_pack(int32_t W, int32_t halo, int64_t n_own, const double* own, uin
 int cbf_halo_unpack(int32_t W, int32_t halo, int32_t rows_lo, int32_t rows_hi, int64_t hi_row_offset,
                     const double* recv, int64_t stride, int32_t world_size, int32_t rank, double radius, int32_t nsub,
                     double* wpos, int32_t* flag, void* stream);
+
+/*
+ * The neighbour form of the exchange (the default of cbf_amd/shard.py): ONE
+ * all-to-all (RCCL all_to_all_single over xGMI) in which rank r sends its first `halo` owned rows to
+ * r-1 only, its last `halo` rows to r+1 only, and its nsub guard records (8 doubles each) to every
+ * rank.  Chunk q of send (to q) and of recv (from q), in rank order, is [nsub records | halo W
+ * positions if q = r +- 1]; cbf_halo_nbr_elems gives the total doubles of either buffer (-1 on a
+ * bad argument).  Per rank that is 2 halo W 16 B of rows instead of the all-gather's
+ * world_size x that.  pack / unpack + guard as cbf_halo_pack / cbf_halo_unpack, same semantics.
+ */
+int64_t cbf_halo_nbr_elems(int32_t W, int32_t halo, int32_t nsub, int32_t world_size, int32_t rank);
+int cbf_halo_pack_nbr(int32_t W, int32_t halo, int64_t n_own, const double* own, uint64_t* ext_keys, int32_t nsub,
+                      int32_t world_size, int32_t rank, double* send, void* stream);
+int cbf_halo_unpack_nbr(int32_t W, int32_t halo, int32_t rows_lo, int32_t rows_hi, int64_t hi_row_offset,
+                        const double* recv, int32_t world_size, int32_t rank, double radius, int32_t nsub,
+                        double* wpos, int32_t* flag, void* stream);
 int cbf_lattice_step_sharded(const cbf_params* p, const cbf_grid* grid, int32_t W, int32_t H, int32_t row_begin,
                              int32_t row_end, int32_t own_begin, int32_t own_end, int32_t win_row0, int32_t win_rows,
                              const double* pos, double gain, double T, double* pos_out, double* vel_out, double* u,

@@ -9,12 +9,14 @@ independent within a step (the loop is a Jacobi update over the packed nominal s
 cross_and_rescue.py:133), so the egos are split over one single-threaded process per host core
 (OMP / OPENBLAS / MKL threads pinned to 1) and the rates add.
 
-Two shapes, both on the same inputs the GPU runs (plus ``cfg4_c``: the cfg4 egos through the C
+Shapes, each on the same inputs the GPU runs (plus ``cfg4_c``: the lattice egos through the C
 restatement, oracle/cbf_oracle.c, SURVEY 8(d)'s second baseline):
   * ``qp``   -- cfg2 (meet_at_center.py:76-153 at N = 100: 50 pursuit obstacles, 50 agents), where
                 the interior-point QP dominates each agent-QP;
-  * ``cfg4`` -- random egos of the 1M-agent lattice, where the reference's O(N) Python cull per
-                ego dominates (that is what its loop does at that N).
+  * ``cfg4`` -- random egos of a lattice (cfg4 / cfg4f / cfg4r at 1M agents, cfg3 at 65,536), where
+                the reference's O(N) Python cull per ego dominates (that is what its loop does at
+                that N);
+  * ``mc``   -- cfg5: whole scenarios (16 agents against 32 entities each), QP-dominated.
 """
 from __future__ import annotations
 
@@ -79,10 +81,32 @@ def _cfg2_state():
     return pos, vel, n_obs
 
 
-def _cfg4_state(W, H, seed, spacing, gain):
-    from oracle import coracle
+def _cfg4_state(W, H, seed, spacing, gain, nominal=None):
+    """The lattice at step 0 with its nominal controls: the lattice Laplacian (cfg4 / cfg4f /
+    cfg3) or cfg4r's random walk (pyoracle.random_nominal)."""
+    from oracle import coracle, pyoracle as po
     pos = _scenarios().lattice(W, H, seed=seed, spacing=spacing)
+    if nominal is not None:
+        _, amp, nseed = nominal
+        return pos, po.random_nominal(pos, 0, amp, nseed), 0
     return pos, coracle.consensus_lattice(W, H, 0, H, pos, gain), 0
+
+
+def _mc_state(all_pos, gain, s):
+    """cfg5 scenario s at step 0 (scenarios.mc_scenarios: 16 pursuit obstacles + 16 free agents)
+    with its nominal controls: cyclic pursuit of the obstacles (rotation -pi/16, meet_at_center.py:
+    86-96) and the complete-graph consensus of the agents with the cfg5 gain (:99-103)."""
+    from oracle import coracle
+    pos = np.ascontiguousarray(all_pos[s])
+    ring = [[(i + 1) % 16] for i in range(16)]
+    full = [[j for j in range(16) if j != i] for i in range(16)]
+    th = -np.pi / 16
+    vel = np.zeros_like(pos)
+    for (b, e, rows, rot, scale) in ((0, 16, ring, (np.cos(th), np.sin(th)), 1.0), (16, 32, full, None, gain)):
+        rp = np.concatenate([[0], np.cumsum([len(r) for r in rows])]).astype(np.int32)
+        col = np.array([j for r in rows for j in r], np.int32)
+        vel[b:e] = coracle.consensus_csr(pos[b:e], rp, col, 0, e - b, rot=rot, scale=scale)
+    return pos, vel, 16
 
 
 def _c_loop(pos, vel, egos, budget_s):
@@ -107,6 +131,27 @@ def _worker(arg):
     if ROOT not in sys.path:
         sys.path.insert(0, ROOT)
     from oracle import pyoracle as po, refloop
+    if kind == "mc":   # scenarios rank, rank + procs, ...: each one loop over its 16 agents
+        # scenario states at timestep t_state of the GPU rollout (step 0 has no neighbour within
+        # the cull radius), rolled forward by the C restatement (not timed)
+        n_scen, seed, gain, t_state = shape
+        from oracle import coracle
+        all_pos = _scenarios().mc_scenarios(n_scen, 16, 16, seed=seed)   # the GPU run's batch
+        th = -np.pi / 16
+        done = solves = 0
+        spent = 0.0   # seconds in the reference loop only
+        for sc in range(rank, n_scen, procs):
+            left = budget_s - spent
+            if left <= 0:
+                break
+            rolled = coracle.mc_rollout(po.Params(15), all_pos[sc:sc + 1], 16, 16, t_state, 1 / 30,
+                                        (np.cos(th), np.sin(th)), 1.0, gain)[0]
+            pos, vel, n_obs = _mc_state(rolled, gain, 0)
+            d, s, dt = refloop.loop_sample(po.Params(15), pos, vel, n_obs, range(16), left)
+            done += d
+            solves += s
+            spent += dt
+        return done, solves, spent
     if kind == "cfg4_c":
         pos, vel, _ = _cfg4_state(*shape)
         order = np.random.default_rng(321).permutation(pos.shape[0])
@@ -143,10 +188,18 @@ def run(kind, budget_s, procs=None, shape=None):
                           f"C restatement oracle/cbf_oracle.c (the reference's O(N) cull per ego, cbf.py rows, the "
                           f"exact 2-D QP with the +1 rule, clip), {procs} single-threaded processes x {dt:.1f} s",
                 "cores_source": how}
-    what = ("cfg2 (meet_at_center.py at N=100: 50 obstacles + 50 agents, step-0 states), every agent-QP "
-            "one cvxopt-coneqp solve" if kind == "qp" else
-            f"random egos of the {shape[0]}x{shape[1]} lattice (spacing {shape[3]}), each an O(N) Python cull "
-            "+ cvxopt-coneqp solve")
+    if kind == "qp":
+        what = ("cfg2 (meet_at_center.py at N=100: 50 obstacles + 50 agents, step-0 states), every agent-QP "
+                "one cvxopt-coneqp solve")
+    elif kind == "mc":
+        what = (f"cfg5 scenarios (of {shape[0]}; 16 pursuit obstacles + 16 agents each, states at timestep "
+                f"{shape[3]} of the rollout, meet_at_center.py:118-143 per scenario), each agent a 32-entity Python "
+                "cull + cvxopt-coneqp solve (the rollout to that timestep by the C restatement, untimed, is "
+                "excluded from the rate)")
+    else:
+        nom = "" if len(shape) < 6 or shape[5] is None else ", random-walk nominal control"
+        what = (f"random egos of the {shape[0]}x{shape[1]} lattice (spacing {shape[3]}{nom}), each an O(N) "
+                "Python cull + cvxopt-coneqp solve")
     from oracle import refloop
     return {"value": solves / dt, "unit": "agent-QP solves/s", "cores": procs, "kind": "port",
             "per_core": solves / dt / procs,

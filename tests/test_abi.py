@@ -16,7 +16,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 def _declared():
     src = open(os.path.join(ROOT, "include", "cbf_amd.h")).read()
     src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
-    return sorted(set(re.findall(r"^\s*(?:int|size_t)\s+(cbf_\w+)\s*\(", src, flags=re.M)))
+    return sorted(set(re.findall(r"^\s*(?:int|int64_t|size_t)\s+(cbf_\w+)\s*\(", src, flags=re.M)))
 
 
 def test_library_loads_and_exports_every_declared_symbol():
@@ -85,6 +85,15 @@ def test_argument_validation_without_launch():
     assert L.cbf_halo_pack(8, 2, 64, 1, 1, 0, 1, null) == _lib.CBF_EINVAL          # no sub-step records
     assert L.cbf_halo_unpack(8, 2, 2, 0, 0, 1, 4 * 2 * 8 + 8, 2, 0, 0.2, 1, 1, 1, null) == _lib.CBF_EINVAL  # rank 0 below
     assert L.cbf_halo_unpack(8, 2, 0, 2, 2, 1, 4 * 2 * 8, 2, 0, 0.2, 1, 1, 1, null) == _lib.CBF_EINVAL      # stride short
+    # neighbour exchange: buffer sizes (records to every rank, rows to the two neighbours only)
+    assert L.cbf_halo_nbr_elems(8, 2, 3, 1, 0) == 24                          # one rank: its own records
+    assert L.cbf_halo_nbr_elems(8, 2, 3, 4, 0) == 4 * 24 + 2 * 2 * 8          # an edge rank: one neighbour
+    assert L.cbf_halo_nbr_elems(8, 2, 3, 4, 2) == 4 * 24 + 2 * 2 * 2 * 8      # a middle rank: two
+    assert L.cbf_halo_nbr_elems(8, 2, 3, 4, 4) == -1
+    assert L.cbf_halo_pack_nbr(8, 2, 64, 1, 1, 1, 2, 2, 1, null) == _lib.CBF_EINVAL      # rank outside the world
+    assert L.cbf_halo_pack_nbr(8, 4, 16, 1, 1, 1, 2, 0, 1, null) == _lib.CBF_EINVAL      # fewer owned rows than 2 halos
+    assert L.cbf_halo_unpack_nbr(8, 2, 2, 0, 0, 1, 2, 0, 0.2, 1, 1, 1, null) == _lib.CBF_EINVAL  # rank 0 has no rows below
+    assert L.cbf_halo_unpack_nbr(8, 2, 0, 2, 2, 1, 2, 1, 0.2, 1, 1, 1, null) == _lib.CBF_EINVAL  # last rank none above
     assert L.cbf_lattice_step_sharded(cp, C.byref(g), 8, 8, 0, 8, 2, 9, 0, 8, 1, 0.25, 0.1, 1, 1, 1, 1, null, 3, 1,
                                       null, 1, 1 << 24, null) == _lib.CBF_EINVAL   # owned rows outside the computed rows
     # certificate / unicycle

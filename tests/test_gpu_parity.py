@@ -375,6 +375,36 @@ def test_lattice_run_matches_steps(spacing):
         assert st["seidel"] > 0      # the hard-QP kernel's chained binning is exercised
 
 
+def test_lattice_run_output_history():
+    """cbf_lattice_run_ex(CBF_RUN_OUTPUT_HISTORY): every timestep's nominal control, filtered
+    control, status and neighbour count (the reference's per-step si_velocities) equal those of
+    the corresponding step() call, and the trajectory is the plain run's, bit for bit; also from a
+    hipGraph of run(5, history=True)."""
+    W, H = 160, 128
+    pos = scenarios.lattice(W, H, seed=12, spacing=0.2)
+    A = swarm.LatticeSwarm(pos, W, H)
+    per_step = []
+    for _ in range(10):
+        A.step()
+        per_step.append((A.vel.clone(), A.u.clone(), A.status.clone(), A.nbr_count.clone()))
+    B = swarm.LatticeSwarm(pos, W, H)
+    B.run(5, history=True)
+    hist = [t.clone() for t in B.history(5)]
+    B.capture(steps=5, history=True)   # the capture's warm-up launch runs timesteps 6-10
+    torch.cuda.synchronize()
+    hist2 = B.history(5)
+    for t in range(10):
+        got = [h[t] for h in hist] if t < 5 else [h[t - 5] for h in hist2]
+        for a, b in zip(per_step[t], got):
+            assert torch.equal(a, b), t
+    assert torch.equal(A.pos, B.pos)
+    B.run(5, history=True)            # graph replay: timesteps 11-15
+    C = swarm.LatticeSwarm(pos, W, H)
+    C.run(15)
+    torch.cuda.synchronize()
+    assert torch.equal(C.pos, B.pos) and torch.equal(C.u, B.history(5)[1][4])
+
+
 @pytest.mark.parametrize("nominal", [None, ("random", 0.05, 3)])
 def test_lattice_stats_off_and_replay(nominal):
     """The bench's timed path: run() with stats=NULL (graphs of both modes captured) gives the same

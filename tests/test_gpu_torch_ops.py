@@ -112,3 +112,30 @@ def test_lattice_run_op_equals_step_ops():
     (pa, oa, sa), (pb, ob, sb) = outs
     assert torch.equal(pa, pb) and all(torch.equal(x, y) for x, y in zip(oa, ob)) and sa == sb
     assert sa["solves"] > 0 and sa["errors"] == 0
+
+
+def test_lattice_ops_without_stats_and_argument_checks():
+    """stats=None reaches the statistics-free kernels (the bench's timed instantiation): the same
+    positions and outputs as with statistics; steps=0 and tensors on another device are rejected."""
+    W, H = 96, 64
+    pos = scenarios.lattice(W, H, seed=9)
+    L = swarm.LatticeSwarm(pos, W, H)
+    g = L.grid
+    geo = (g.x0, g.y0, 1 / g.inv_h, g.nx, g.ny)
+    nb = OPS.lattice_workspace_size(W, H, *geo)
+    outs = []
+    for stats in (torch.zeros(1024, dtype=torch.int64, device=DEV), None):
+        ws = torch.zeros(nb, dtype=torch.uint8, device=DEV)
+        P = _t(pos)
+        out = OPS.lattice_run(P, W, H, L.gain, L.T, 5, *geo, ws, stats)
+        out2 = OPS.lattice_step(P, W, H, L.gain, L.T, *geo, ws, stats)
+        torch.cuda.synchronize()
+        outs.append((P, out, out2))
+    (pa, oa, qa), (pb, ob, qb) = outs
+    assert torch.equal(pa, pb)
+    assert all(torch.equal(x, y) for x, y in zip(oa + qa, ob + qb))
+    ws = torch.zeros(nb, dtype=torch.uint8, device=DEV)
+    with pytest.raises(RuntimeError, match="steps"):
+        OPS.lattice_run(_t(pos), W, H, L.gain, L.T, 0, *geo, ws, None)
+    with pytest.raises(RuntimeError, match="workspace"):
+        OPS.lattice_step(_t(pos), W, H, L.gain, L.T, *geo, torch.zeros(nb, dtype=torch.uint8), None)

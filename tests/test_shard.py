@@ -35,27 +35,40 @@ class OracleBackend:
     def pack(self, S):
         rs = S.G * S.W * 2
         own = S.own.reshape(-1)
-        S.send[:rs].copy_(own[:rs])
-        S.send[rs:2 * rs].copy_(own[own.numel() - rs:])
-        for s in range(self.nsub):
-            S.send[S.slab + 8 * s:S.slab + 8 * s + 6].copy_(torch.as_tensor(self.recs[s]))
+        if S.exchange_mode == "neighbour":    # chunk q: [records | first rows to q = r-1, last rows to r+1]
+            for q in range(S.ws):
+                o = S.chunk_offset(q)
+                for s in range(self.nsub):
+                    S.send[o + 8 * s:o + 8 * s + 6].copy_(torch.as_tensor(self.recs[s]))
+                r8 = o + 8 * self.nsub
+                if q == S.rank - 1:
+                    S.send[r8:r8 + rs].copy_(own[:rs])
+                elif q == S.rank + 1:
+                    S.send[r8:r8 + rs].copy_(own[own.numel() - rs:])
+        else:
+            S.send[:rs].copy_(own[:rs])
+            S.send[rs:2 * rs].copy_(own[own.numel() - rs:])
+            for s in range(self.nsub):
+                S.send[S.slab + 8 * s:S.slab + 8 * s + 6].copy_(torch.as_tensor(self.recs[s]))
         self.recs = np.tile(IDENT, (self.nsub, 1))
 
     def unpack_guard(self, S):
         W, rs = S.W, S.G * S.W * 2
+        nbr = S.exchange_mode == "neighbour"
+        r8 = 8 * self.nsub
         wv = S.wpos.view(-1)
         if S.rank > 0:
-            lo = (S.rank - 1) * S.stride
+            lo = S.chunk_offset(S.rank - 1) + r8 if nbr else (S.rank - 1) * S.stride + rs
             n = (S.rb - S.w0) * W * 2
-            wv[:n].copy_(S.recv[lo + 2 * rs - n:lo + 2 * rs])
+            wv[:n].copy_(S.recv[lo + rs - n:lo + rs])
         if S.rank < S.ws - 1:
-            hi = (S.rank + 1) * S.stride
+            hi = S.chunk_offset(S.rank + 1) + r8 if nbr else (S.rank + 1) * S.stride
             a = (S.re - S.w0) * W * 2
             n = (S.w1 - S.re) * W * 2
             wv[a:a + n].copy_(S.recv[hi:hi + n])
         for s in range(self.nsub):
-            recs = np.stack([S.recv[q * S.stride + S.slab + 8 * s:q * S.stride + S.slab + 8 * s + 6].numpy()
-                             for q in range(S.ws)])
+            base = [S.chunk_offset(q) if nbr else q * S.stride + S.slab for q in range(S.ws)]
+            recs = np.stack([S.recv[b + 8 * s:b + 8 * s + 6].numpy() for b in base])
             if not guard_ok(recs, S.rank, self.radius):
                 self.flag = 1
 
@@ -98,12 +111,12 @@ def _free_port():
     return port
 
 
-def _worker(rank, ws, port, W, R, steps, halo, q, k=1):
+def _worker(rank, ws, port, W, R, steps, halo, q, k=1, exchange="neighbour"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=ws)
     H = R * ws
     be = OracleBackend(W, H, scenarios.LATTICE_GAIN, scenarios.T, 0.2, k)
-    S = ShardedLattice(W, R, seed=2, halo=halo, substeps=k, backend=be)
+    S = ShardedLattice(W, R, seed=2, halo=halo, substeps=k, backend=be, exchange=exchange)
     for _ in range(steps):
         S.step()
     S.check_guard()
@@ -112,13 +125,14 @@ def _worker(rank, ws, port, W, R, steps, halo, q, k=1):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("ws,k", [(2, 1), (3, 1), (2, 2), (3, 3)])
-def test_sharded_rollout_equals_single_lattice(ws, k):
+@pytest.mark.parametrize("ws,k,exchange", [(2, 1, "neighbour"), (3, 1, "neighbour"), (2, 2, "neighbour"),
+                                           (3, 3, "neighbour"), (4, 2, "neighbour"), (3, 2, "allgather")])
+def test_sharded_rollout_equals_single_lattice(ws, k, exchange):
     W, R, steps, halo = 20, 12, 5, 4
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, ws, port, W, R, steps, halo, q, k)) for r in range(ws)]
+    procs = [ctx.Process(target=_worker, args=(r, ws, port, W, R, steps, halo, q, k, exchange)) for r in range(ws)]
     for p in procs:
         p.start()
     res = sorted([q.get(timeout=300) for _ in range(ws)], key=lambda t: t[0])
@@ -141,6 +155,17 @@ def test_sharded_rollout_equals_single_lattice(ws, k):
     assert sum(r[4] for r in res) == solves
 
 
+def test_neighbour_splits_send_rows_to_neighbours_only():
+    """Chunk sizes of the neighbour exchange (cbf_halo_nbr_elems / nbr_chunk_off in swarm.hip):
+    records to every rank, rows only to rank +- 1, and a symmetric send / receive pattern."""
+    ws, rows, k = 5, 100, 3
+    for r in range(ws):
+        sp = ShardedLattice.nbr_splits(ws, r, rows, k)
+        assert [q for q in range(ws) if sp[q] > 8 * k] == [q for q in (r - 1, r + 1) if 0 <= q < ws]
+        # what rank r receives from q is what q sends to r
+        assert sp == [ShardedLattice.nbr_splits(ws, q, rows, k)[r] for q in range(ws)]
+
+
 def test_guard_logic():
     W, halo = 10, 4
     a = scenarios.LATTICE_SPACING
@@ -160,12 +185,12 @@ def test_guard_logic():
     assert a * (halo - 2) > 0.2            # default halo leaves slack for the jittered lattice
 
 
-def _worker_small_halo(rank, ws, port, q, k):
+def _worker_small_halo(rank, ws, port, q, k, exchange):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=ws)
     W, R = 12, 6
     be = OracleBackend(W, R * ws, scenarios.LATTICE_GAIN, scenarios.T, 0.2, k)
-    S = ShardedLattice(W, R, seed=3, halo=2, substeps=k, backend=be)
+    S = ShardedLattice(W, R, seed=3, halo=2, substeps=k, backend=be, exchange=exchange)
     for _ in range(k):
         S.step()
     try:
@@ -177,14 +202,14 @@ def _worker_small_halo(rank, ws, port, q, k):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("k", [1, 2])
-def test_too_small_halo_is_caught_after_the_step(k):
+@pytest.mark.parametrize("k,exchange", [(1, "neighbour"), (2, "neighbour"), (2, "allgather")])
+def test_too_small_halo_is_caught_after_the_step(k, exchange):
     """halo 2 lets rows two apart (0.29 - jitter < 0.2) reach past the candidate rows: the
     guard, run at the exchange after the step, must flag it and check_guard() must raise."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker_small_halo, args=(r, 2, port, q, k)) for r in range(2)]
+    procs = [ctx.Process(target=_worker_small_halo, args=(r, 2, port, q, k, exchange)) for r in range(2)]
     for p in procs:
         p.start()
     res = sorted([q.get(timeout=300) for _ in range(2)])

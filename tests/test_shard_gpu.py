@@ -25,9 +25,9 @@ def _free_port():
     return p
 
 
-def _worker(rank, ws, port, W, R, steps, q, k=4, graph=False, run=False, nominal=None):
+def _worker(rank, ws, port, W, R, steps, q, k=4, graph=False, run=False, nominal=None, exchange="neighbour"):
     try:
-        _work(rank, ws, port, W, R, steps, q, k, graph, run, nominal)
+        _work(rank, ws, port, W, R, steps, q, k, graph, run, nominal, exchange)
     except BaseException as e:   # report instead of leaving the test waiting on the queue
         q.put((rank, "error", repr(e)))
         raise
@@ -38,7 +38,7 @@ def _spacing(nominal):
     return scenarios.LATTICE_SPACING if nominal is None else 0.22   # random walk: the cfg4r spacing
 
 
-def _work(rank, ws, port, W, R, steps, q, k, graph, run, nominal):
+def _work(rank, ws, port, W, R, steps, q, k, graph, run, nominal, exchange):
     import datetime
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     torch.cuda.set_device(0)
@@ -47,7 +47,7 @@ def _work(rank, ws, port, W, R, steps, q, k, graph, run, nominal):
     # the random walk's RELAXED QPs can move an agent up to T * max_speed = 0.5 per step (the
     # guard catches it with the default 4-row halo): 10 rows per sub-step cover it
     S = ShardedLattice(W, R, seed=7, substeps=k, nominal=nominal, spacing=_spacing(nominal),
-                       halo=4 if nominal is None else 10)
+                       halo=4 if nominal is None else 10, exchange=exchange)
     if graph == "cycle":   # whole exchange cycles replayed as one hipGraph each
         S.capture_cycle()
     elif graph:
@@ -58,6 +58,10 @@ def _work(rank, ws, port, W, R, steps, q, k, graph, run, nominal):
         S.step()
         S.run(steps - 2)
     elif run == "replay":   # the bench's timed path: stats off, then restore() and a stats-on replay
+        if graph == "cycle":    # cycle graphs of both statistics settings, as the bench captures them
+            S.collect_stats = False
+            S.capture_cycle()
+            S.collect_stats = True
         snap = S.snapshot()
         S.collect_stats = False
         S.run(steps)
@@ -85,18 +89,20 @@ def _work(rank, ws, port, W, R, steps, q, k, graph, run, nominal):
 RANDOM = ("random", 1.0, 3)   # the random-walk nominal control (CBF_NOMINAL_RANDOM)
 
 
-@pytest.mark.parametrize("ws,k,graph,run,nominal", [(2, 1, False, False, None), (3, 4, False, False, None),
-                                                    (2, 4, True, False, None), (3, 4, False, True, None),
-                                                    (2, 2, False, True, None), (2, 4, "cycle", True, None),
-                                                    (2, 2, False, True, RANDOM), (3, 4, False, "mixed", None),
-                                                    (2, 4, False, "replay", None)])
-def test_sharded_equals_single_gpu(ws, k, graph, run, nominal):
+@pytest.mark.parametrize("ws,k,graph,run,nominal,exchange", [
+    (2, 1, False, False, None, "neighbour"), (3, 4, False, False, None, "neighbour"),
+    (2, 4, True, False, None, "neighbour"), (3, 4, False, True, None, "neighbour"),
+    (2, 2, False, True, None, "neighbour"), (2, 4, "cycle", True, None, "neighbour"),
+    (2, 2, False, True, RANDOM, "neighbour"), (3, 4, False, "mixed", None, "neighbour"),
+    (2, 4, False, "replay", None, "neighbour"), (3, 4, "cycle", "replay", None, "neighbour"),
+    (4, 2, False, True, None, "neighbour"), (3, 4, False, True, None, "allgather")])
+def test_sharded_equals_single_gpu(ws, k, graph, run, nominal, exchange):
     from cbf_amd import scenarios, swarm
     W, R, steps = 96, 40, 6
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, ws, port, W, R, steps, q, k, graph, run, nominal))
+    procs = [ctx.Process(target=_worker, args=(r, ws, port, W, R, steps, q, k, graph, run, nominal, exchange))
              for r in range(ws)]
     for p in procs:
         p.start()
