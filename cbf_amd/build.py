@@ -94,7 +94,11 @@ def build_torch_ops(verbose: bool = False) -> str:
 # the package): name -> (sources, defines).  CBF_SCAN_TEST_TIMEOUT makes every scan look-back give
 # up, so tests/test_gpu_parity.py can check that the failure is reported, not silent.
 TEST_VARIANTS = {"scantimeout": (["cells.hip"], ["CBF_SCAN_TEST_TIMEOUT=1"]),
-                 "apwpe8": (["filter.hip"], ["CBF_AP_WPE=8"])}
+                 "apwpe8": (["filter.hip"], ["CBF_AP_WPE=8"]),
+                 # the wave-cooperative exact solve of the queued QPs, in the filter (1) and in the
+                 # queue kernel (2): kept bit-identical to the shipped one-lane solve by a GPU test
+                 "hardcoop1": (["swarm.hip"], ["CBF_HARD_MODE=1"]),
+                 "hardcoop2": (["swarm.hip"], ["CBF_HARD_MODE=2"])}
 TEST_LIB_DIR = os.path.join(ROOT, "tests", "_lib")
 
 

@@ -129,12 +129,15 @@ __device__ __forceinline__ int subq_append(int32_t* hardq, int q) {
 // The queue kernels: 64-lane blocks, block g serving sub-queue g % kSubQ as its (g / kSubQ)-th of
 // per_q blocks.  Of a sub-queue of length nq, nwork = min(per_q, ceil(nq / 64)) blocks work, lane
 // i of the k-th taking entries k 64 + i, then + nwork 64, ...; visit(entry) per entry.  The working
-// blocks of a sub-queue then count themselves done; the last empties the sub-queue (length and
-// done counter), so the next advance starts from empty queues with no extra launch.  A chain of
-// <= per_q returning atomics per sub-queue line, the 64 lines in parallel.  No fence: a block is
-// one wave whose load of the length has returned before lane 0's atomic, and nothing the reset
-// races with is written by the queue kernels.  A block k >= nwork that reads the length after the
-// reset sees 0 and is still idle (any smaller length gives it no work either).
+// blocks of a sub-queue count themselves done as soon as they have read the length (a block needs
+// only the length: the records stay untouched until the next advance), so the counter's return
+// trip overlaps the solves instead of ending the kernel; the last one to count empties the
+// sub-queue (length and done counter) at its end, so the next advance starts from empty queues
+// with no extra launch.  No fence: a block is one wave whose load of the length has returned
+// before lane 0's atomic, and nothing the reset races with is written by the queue kernels.  A
+// block k >= nwork that reads the length after the reset sees 0 and is still idle (any smaller
+// length gives it no work either); a working block cannot read it after the reset, which needs
+// its own count first.
 template <class Visit>
 __device__ __forceinline__ void drain_subq(int32_t* __restrict__ hardq, int per_q, Visit&& visit) {
     const int q = blockIdx.x % kSubQ, k = blockIdx.x / kSubQ;
@@ -142,8 +145,34 @@ __device__ __forceinline__ void drain_subq(int32_t* __restrict__ hardq, int per_
     const int need = (nq + 63) / 64;
     const int nwork = need < per_q ? need : per_q;
     if (k >= nwork) return;
+    int done = 0;
+    if (threadIdx.x == 0) done = atomicAdd(&hardq[32 * (1 + kSubQ + q)], 1);
     for (int i = k * 64 + threadIdx.x; i < nq; i += nwork * 64) visit(q, i);
-    if (threadIdx.x == 0 && atomicAdd(&hardq[32 * (1 + kSubQ + q)], 1) == nwork - 1) {
+    if (threadIdx.x == 0 && done == nwork - 1) {
+        hardq[32 * (1 + q)] = 0;
+        hardq[32 * (1 + kSubQ + q)] = 0;
+    }
+}
+
+// drain_subq for the cooperative queue kernel: lane group g (8 lanes) of the k-th working block
+// of sub-queue q takes entries 8 k + g, then + 8 nwork, ...; visit(q, i, act) is called by EVERY
+// lane of the wave in each pass (the solve's shuffles and ballots need the whole wave), act =
+// the group has an entry.  The done counter is taken as soon as the length is read (a block
+// needs the length only; the records are read-only until the next advance), so its return trip
+// overlaps the solves instead of ending the kernel; the last working block empties the sub-queue
+// at its end.
+template <class Visit>
+__device__ __forceinline__ void drain_subq_groups(int32_t* __restrict__ hardq, int per_q, Visit&& visit) {
+    const int q = blockIdx.x % kSubQ, k = blockIdx.x / kSubQ;
+    const int nq = hardq[32 * (1 + q)];
+    const int need = (nq + 7) / 8;
+    const int nwork = need < per_q ? need : per_q;
+    if (k >= nwork) return;
+    int done = 0;
+    if (threadIdx.x == 0) done = atomicAdd(&hardq[32 * (1 + kSubQ + q)], 1);
+    const int g = (threadIdx.x & 63) >> 3;
+    for (int i0 = k * 8; i0 < nq; i0 += nwork * 8) visit(q, i0 + g, i0 + g < nq);
+    if (threadIdx.x == 0 && done == nwork - 1) {
         hardq[32 * (1 + q)] = 0;
         hardq[32 * (1 + kSubQ + q)] = 0;
     }

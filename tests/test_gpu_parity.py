@@ -857,3 +857,43 @@ def test_allpairs_spilled_variant_is_bit_identical():
                 C.byref(_lib.CbfDiag()), _lib.stream_handle()) == 0
     torch.cuda.synchronize()
     assert torch.equal(u, ref["u"]) and torch.equal(st, ref["status"]) and torch.equal(cnt, ref["nbr_count"])
+
+
+@pytest.mark.parametrize("mode", [1, 2])
+@pytest.mark.parametrize("nominal", [None, ("random", 1.0, 5)])
+def test_cooperative_hard_solve_is_bit_identical(mode, nominal):
+    """The wave-cooperative exact solve of the QPs solve_fast cannot settle (coop_solve_ego: 8 lanes
+    per QP, ballots + shuffles; CBF_HARD_MODE 1 = inside the filter, 2 = in the queue kernel; test
+    builds tests/_lib/libcbf_hardcoop{1,2}.so) gives the shipped one-lane Seidel solve's results
+    bit for bit over a chained rollout: positions, last-step controls and statuses, and every
+    statistics word -- on the consensus lattice at spacing 0.2 and on cfg4r's random walk (10 %
+    of the QPs through the full solve)."""
+    import ctypes as C
+    import os
+    from cbf_amd import _lib
+    V = C.CDLL(os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", f"libcbf_hardcoop{mode}.so"))
+    for name in ("cbf_lattice_run", "cbf_lattice_set_nominal"):
+        f = getattr(V, name)
+        f.restype, f.argtypes = _lib.SIGNATURES[name]
+    W, H, steps = 160, 128, 8
+    pos = scenarios.lattice(W, H, seed=13, spacing=0.2 if nominal is None else 0.22)
+    A = swarm.LatticeSwarm(pos, W, H, nominal=nominal)
+    A.run(steps)
+    torch.cuda.synchronize()
+    ws = torch.zeros_like(A.ws)
+    if nominal is not None:
+        assert V.cbf_lattice_set_nominal(_lib.ptr(ws), ws.numel(), 1, nominal[1], nominal[2],
+                                         _lib.stream_handle()) == 0
+    P = _t(pos)
+    vel, u = torch.empty_like(P), torch.empty_like(P)
+    st = torch.empty((W * H,), dtype=torch.int32, device="cuda")
+    cnt = torch.empty_like(st)
+    stats = torch.zeros(1024, dtype=torch.int64, device="cuda")
+    assert V.cbf_lattice_run(A.cp, C.byref(A.grid), W, H, _lib.ptr(P), A.gain, A.T, steps, _lib.ptr(vel), _lib.ptr(u),
+                             _lib.ptr(st), _lib.ptr(cnt), _lib.ptr(stats), _lib.ptr(ws), ws.numel(),
+                             _lib.stream_handle()) == 0
+    torch.cuda.synchronize()
+    assert torch.equal(P, A.pos) and torch.equal(u, A.u) and torch.equal(st, A.status)
+    assert torch.equal(vel, A.vel) and torch.equal(cnt, A.nbr_count)
+    got, want = _lib.decode_stats(stats.cpu().numpy()), A.stats_summary()
+    assert got == want and want["seidel"] > 0, (got, want)
