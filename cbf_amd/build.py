@@ -93,7 +93,7 @@ def build_torch_ops(verbose: bool = False) -> str:
 # Test-only builds of the library with a compile switch flipped in some sources (never loaded by
 # the package): name -> (sources, defines).  CBF_SCAN_TEST_TIMEOUT makes every scan look-back give
 # up, so tests/test_gpu_parity.py can check that the failure is reported, not silent.
-TEST_VARIANTS = {"scantimeout": (["cells.hip"], ["CBF_SCAN_TEST_TIMEOUT=1"]),
+TEST_VARIANTS = {"scantimeout": (["cells.hip", "swarm.hip", "hocbf.hip", "filter.hip"], ["CBF_SCAN_TEST_TIMEOUT=1"]),
                  "apwpe8": (["filter.hip"], ["CBF_AP_WPE=8"]),
                  # the wave-cooperative exact solve of the queued QPs, in the filter (1) and in the
                  # queue kernel (2): kept bit-identical to the shipped one-lane solve by a GPU test

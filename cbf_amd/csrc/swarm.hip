@@ -259,31 +259,53 @@ __global__ void __launch_bounds__(kBlock) k_lattice_nominal_bin_ordered(
     bcs[t] = cell < 0 ? make_int3(-1, 0, (int)w) : make_int3(cell, rank, (int)w);
 }
 
-// Lattice step K3: counting-sort scatter of the binned window agents into the cell-sorted copies,
-// with each agent's lattice-Laplacian nominal control (cross_and_rescue.py:121-125 shape) computed
-// here: the agent's position is loaded anyway and its 4 lattice neighbours are mostly L2 hits
-// (cell order ~ lattice order), so the control never makes an HBM round trip.
-__global__ void __launch_bounds__(kBlock) k_lattice_scatter_ordered(long nwin, long nrec, const int3* __restrict__ bcs,
-                                                                    const int32_t* __restrict__ start,
-                                                                    const double2* __restrict__ pos,
-                                                                    double2* __restrict__ spos,
-                                                                    double2* __restrict__ svel,
-                                                                    int32_t* __restrict__ sidx,
-                                                                    int32_t* __restrict__ order_state, long ncell,
-                                                                    int win_row0, int H, int W, int row_begin,
-                                                                    int row_end, double gain,
-                                                                    double2* __restrict__ vel_out,
-                                                                    const int32_t* __restrict__ sctl,
-                                                                    unsigned long long* __restrict__ ext_keys, ExtSpec X) {
-    // ext_keys (a chained build of the sharded cycle, whose bin pass ran in the previous advance):
-    // the halo-guard extents of this build's input positions, as the bin kernel computes them
+#ifndef CBF_TILE_SPIN_LIMIT
+#define CBF_TILE_SPIN_LIMIT (1l << 22)
+#endif
+
+// Logical block index of physical block b of nb (nb a multiple of 8 or not) with one contiguous
+// range of logical blocks per XCD (xcd_block() for a sub-range of a grid that starts at an XCD
+// boundary: physical block b runs on XCD b mod 8).
+__device__ __forceinline__ int xcd_remap(int b, int nb) {
+    const int q = nb >> 3, rem = nb & 7, x = b & 7, j = b >> 3;
+    return (x < rem ? x * (q + 1) : rem * (q + 1) + (x - rem) * q) + j;
+}
+
+// Lattice build K2+K3, scan and scatter in one launch.  Blocks [0, ntiles) are the single-pass
+// scan's tiles (scan_tile), each publishing a done word once its starts are written; blocks from
+// ntiles8 (ntiles rounded up to the XCD count, so the scatter blocks keep their XCD-aware order)
+// are the counting-sort scatter of the binned window agents into the cell-sorted copies, with each
+// agent's lattice-Laplacian nominal control (cross_and_rescue.py:121-125 shape) computed on the
+// way: the agent's position is loaded anyway and its 4 lattice neighbours are mostly L2 hits (cell
+// order ~ lattice order), so the control never makes an HBM round trip.  A scatter wave first
+// loads its records, the positions and the neighbours -- the bulk of its memory traffic,
+// overlapping the scan -- and only then waits, one lane polling, for the done words of the tiles
+// holding its cells (the records arrive in the previous step's cell order, so a wave's cells span
+// one tile or two), then reads the starts (sc1 loads of write-through stores, scan_tile's
+// hand-off) and stores.  Every wait points at a lower block index, which the dispatcher has
+// already made resident (the single-pass scan relies on the same order).  A wait
+// that runs out of spins sets the build's error flag (sctl[2], as a scan look-back that gives up);
+// the filters then report CBF_STATUS_WORKSPACE_ERROR for the step, and the stores stay in bounds.
+__global__ void __launch_bounds__(kBlock) k_lattice_scan_scatter(
+    int32_t* __restrict__ count, long ncell, int ntiles, int ntiles8, int32_t* __restrict__ start,
+    unsigned long long* __restrict__ tstate, int32_t* __restrict__ tdone, int32_t* __restrict__ sctl, long nwin,
+    long nrec, const int3* __restrict__ bcs, const double2* __restrict__ pos, double2* __restrict__ spos,
+    double2* __restrict__ svel, int32_t* __restrict__ sidx, int32_t* __restrict__ order_state, int win_row0, int H,
+    int W, int row_begin, int row_end, double gain, double2* __restrict__ vel_out,
+    unsigned long long* __restrict__ ext_keys, ExtSpec X) {
+    if ((int)blockIdx.x < ntiles8) {
+        if ((int)blockIdx.x < ntiles) scan_tile(count, ncell, ntiles, start, tstate, sctl, blockIdx.x, tdone);
+        return;
+    }
     __shared__ unsigned long long red[6][kBlock / 64];
     __shared__ int arrive;
     if (ext_keys) {
         if (threadIdx.x == 0) arrive = 0;
         __syncthreads();
     }
-    const long t = (long)xcd_block() * kBlock + threadIdx.x;
+    const int lb = xcd_remap((int)blockIdx.x - ntiles8, (int)gridDim.x - ntiles8);
+    const long t = (long)lb * kBlock + threadIdx.x;
+    const unsigned epoch = (unsigned)__hip_atomic_load(&sctl[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (t == 0 && sctl[2] == 0) {  // the cell order now exists for this window and grid: the next build walks it
         order_state[0] = 1;
         order_state[1] = (int)nwin;
@@ -295,21 +317,46 @@ __global__ void __launch_bounds__(kBlock) k_lattice_scatter_ordered(long nwin, l
     double e[6] = {INFINITY, -INFINITY, -INFINITY, INFINITY, INFINITY, -INFINITY};
     int any = 0;
     double py = 0.0;
-    // an unusable build (build_begin / scan timeout): no scatter
     const int3 b = (t < nrec && sctl[2] == 0) ? bcs[t] : make_int3(-1, 0, 0);
-    const int d = b.x >= 0 ? start[b.x] + b.y : -1;
     const NominalSpec N = nominal_spec(sctl);
-    if (d >= 0 && d < nwin) {
-        const double2 p = pos[b.z];
-        spos[d] = p;
-        const int r = win_row0 + b.z / W, c = b.z % W;
-        double2 u0;
+    const bool live = b.x >= 0 && b.x < ncell && b.z >= 0 && b.z < nwin;
+    double2 p = make_double2(0.0, 0.0), u0 = make_double2(0.0, 0.0);
+    int r = 0, c = 0;
+    if (live) {
+        p = pos[b.z];
+        r = win_row0 + b.z / W;
+        c = b.z % W;
         if (N.mode == CBF_NOMINAL_RANDOM) {
             u0 = random_nominal(N, (long)win_row0 * W + b.z, p);
         } else {
             const double2 a = lattice_sum(pos, b.z, r, c, W, H);
             u0 = make_double2(a.x * gain, a.y * gain);
         }
+    }
+    // the wave's tiles: one lane polls their done words, then every lane acquires
+    const int tlo = wave_min_i(live ? b.x / kScanTile : INT_MAX), thi = wave_max_i(live ? b.x / kScanTile : -1);
+    if ((threadIdx.x & 63) == 0 && tlo <= thi) {
+        const int32_t want = tile_done_word(epoch);
+        bool failed = false;
+        for (int tt = tlo; tt <= thi && !failed; ++tt) {
+            long spins = 0;
+            while (__hip_atomic_load(&tdone[tt], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != want) {
+                if (++spins > CBF_TILE_SPIN_LIMIT) {
+                    __hip_atomic_store(&sctl[2], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    failed = true;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(1);
+            }
+        }
+    }
+    // the polling wave's loads of the handed-off words, all sc1, after its poll matched (scan_tile)
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("" ::: "memory");
+    const bool ok = __hip_atomic_load(&sctl[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0;
+    const int d = (live && ok) ? __hip_atomic_load(&start[b.x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + b.y : -1;
+    if (d >= 0 && d < nwin) {
+        spos[d] = p;
         svel[d] = u0;
         if (vel_out && r >= row_begin && r < row_end) vel_out[(long)(r - row_begin) * W + c] = u0;
         sidx[d] = b.z;
@@ -325,7 +372,7 @@ __global__ void __launch_bounds__(kBlock) k_lattice_scatter_ordered(long nwin, l
             any = 1;
         }
     }
-    if (ext_keys) ext_keys_flush<kBlock / 64>(e, any, py, ext_keys, blockIdx.x, red, &arrive);
+    if (ext_keys) ext_keys_flush<kBlock / 64>(e, any, py, ext_keys, lb, red, &arrive);
 }
 
 // Per-ego outcome of the lattice filter for the statistics.
@@ -936,11 +983,11 @@ static void lattice_scan_scatter(const CellWs& Wk, int W, int H, int row_begin, 
                                  const double2* pos, double gain, double* vel_out, hipStream_t s, long nrec = -1,
                                  unsigned long long* ext_keys = nullptr, ExtSpec X = ExtSpec{0, 0, 0}) {
     if (nrec < 0) nrec = n;
-    launch_scan(Wk, s);
-    hipLaunchKernelGGL(k_lattice_scatter_ordered, dim3(nblk(nrec)), dim3(kBlock), 0, s, n, nrec, lattice_bcs(Wk),
-                       Wk.start, pos,
-                       Wk.spos, Wk.svel, Wk.sidx, Wk.hardq + 2, Wk.ncell, win_row0, H, W, row_begin, row_end, gain,
-                       reinterpret_cast<double2*>(vel_out), Wk.sctl, ext_keys, X);
+    const int ntiles8 = (Wk.ntiles + 7) & ~7;
+    hipLaunchKernelGGL(k_lattice_scan_scatter, dim3(ntiles8 + nblk(nrec)), dim3(kBlock), 0, s, Wk.count, Wk.ncell,
+                       Wk.ntiles, ntiles8, Wk.start, Wk.tstate, Wk.tdone, Wk.sctl, n, nrec, lattice_bcs(Wk),
+                       pos, Wk.spos, Wk.svel, Wk.sidx, Wk.hardq + 2, win_row0, H, W, row_begin, row_end, gain,
+                       reinterpret_cast<double2*>(vel_out), ext_keys, X);
 }
 
 static int lattice_build(const cbf_params* p, const cbf_grid* grid, int32_t W, int32_t H, int32_t row_begin,
