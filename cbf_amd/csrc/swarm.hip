@@ -399,6 +399,15 @@ struct EgoOut {
 #ifndef CBF_HARD_MODE
 #define CBF_HARD_MODE 0
 #endif
+// Windows of at most this many agents run the filter instantiation with the full solve inline
+// (IN = true: no queue kernel); larger ones queue (CBF_HARD_MODE).  Measured crossover (cbf_lattice_run,
+// W = 1024, spacing 0.145, run(10) per timestep, inline vs queue): 64 rows 25.2 vs 30.2 us, 128
+// rows 27.7 vs 32.6 us, 256 rows 42.5 vs 38.9 us, 512 rows 55 vs 55 (and the inline form at 1024
+// rows 118.5 vs 79.5): the inline instantiation holds 165 VGPRs (3 waves/SIMD), which costs nothing
+// while the window fills no more than that.
+#ifndef CBF_INLINE_MAX
+#define CBF_INLINE_MAX 196608
+#endif
 #define CBF_HARD_COOP (CBF_HARD_MODE == 1)
 #if CBF_HARD_COOP
 static_assert(kHitCap >= 16, "the cooperative solve stages 8 doubles in each lane's hit-list column");
@@ -439,9 +448,10 @@ __device__ __forceinline__ void ego_output(const KP& P, const Ego& E, const Sol&
 
 // Tail of the lattice filter for one owned ego (output index k) whose QP rows are accumulated in
 // E: solve in place when solve_fast can (origin, or one Seidel event that stays put); otherwise
-// return false (CBF_HARD_COOP: the wave solves it cooperatively) or queue it to the hard kernel
-// (sub-queue q: header hardq, records qr).  Then clip, Euler, outputs.
-template <bool FZ, bool ST>
+// run the full solve_ego right here (IN: the small-window instantiation, below), return false
+// (CBF_HARD_COOP: the wave solves it cooperatively) or queue it to the hard kernel (sub-queue q:
+// header hardq, records qr).  Then clip, Euler, outputs.
+template <bool FZ, bool ST, bool IN>
 __device__ __forceinline__ bool ego_finish(const KP& P, Ego& E, int w, int k, int slot, double T,
                                            double2* __restrict__ pos_out, double2* __restrict__ u,
                                            int32_t* __restrict__ status, int32_t* __restrict__ cnt,
@@ -451,6 +461,11 @@ __device__ __forceinline__ bool ego_finish(const KP& P, Ego& E, int w, int k, in
     const bool idle = E.count == 0;
     if (!idle && !solve_fast(P, E, S)) {
         O.seidel = true;
+        if (IN) {
+            S = solve_ego(P, E);
+            ego_output<ST>(P, E, S, false, k, T, pos_out, u, status, cnt, O);
+            return true;
+        }
 #if CBF_HARD_COOP
         return false;
 #else
@@ -485,7 +500,7 @@ __device__ __forceinline__ bool ego_finish(const KP& P, Ego& E, int w, int k, in
 // whose quadrant terms are not all finite, or whose hit list overflowed, is assembled row by row
 // with row_b (scan_range_direct).  Returns false when the ego's QP is left to the wave's
 // cooperative solve (E holds it).
-template <bool FZ, bool ST>
+template <bool FZ, bool ST, bool IN>
 __device__ __forceinline__ bool lattice_ego(const KP& P, const CellGrid& G, const WinBounds& B, int slot,
                                             const double2* __restrict__ spos, const double2* __restrict__ svel,
                                             const int32_t* __restrict__ sidx, const int32_t* __restrict__ start,
@@ -529,7 +544,7 @@ __device__ __forceinline__ bool lattice_ego(const KP& P, const CellGrid& G, cons
     }
     O.nbrs = E.count;
     if (ST) O.d2 = d2;
-    return ego_finish<FZ, ST>(P, E, w, w - B.own_lo, slot, T, pos_out, u, status, cnt, hardq, q, qr, O);
+    return ego_finish<FZ, ST, IN>(P, E, w, w - B.own_lo, slot, T, pos_out, u, status, cnt, hardq, q, qr, O);
 }
 
 // The wave's QPs that solve_fast could not settle (lanes with `need`), solved by coop_solve_ego
@@ -614,7 +629,7 @@ __device__ __forceinline__ void wave_coop_finish(const KP& P, const Ego& E, bool
 // that stays put) are finished in place.  The others (CBF_HARD_COOP) are solved by the wave
 // cooperatively after every lane's scan (wave_coop_finish), or (round 2's form) appended with
 // their assembled state to the hard queue for K5.
-template <bool FZ, bool ST>
+template <bool FZ, bool ST, bool IN>
 __global__ void __launch_bounds__(kBlock) k_lattice_filter(KP P, CellGrid G, WinBounds B, int W, int row_begin,
                                                            int row_end, int win_row0, long nwin, long ncell,
                                                            const double2* __restrict__ spos,
@@ -632,17 +647,17 @@ __global__ void __launch_bounds__(kBlock) k_lattice_filter(KP P, CellGrid G, Win
     __shared__ int hit_lds[kHitCap * kBlock + 8 * kBlock];
     const int bx = xcd_block();
     const int slot = bx * kBlock + threadIdx.x;
-#if CBF_HARD_COOP
-    // no queue kernel follows: a chained advance starts the next build's scan epoch here (an error
-    // flag of this build stays set, so the rest of the run reports it; the scan reads the epoch
-    // only after this kernel), and the last block refreshes the statistics snapshot (values read
-    // mid-update are earlier ones, still valid lower bounds)
-    if (C.bcs && bx == 0 && threadIdx.x == 0) {
-        C.sctl[1] = (C.sctl[1] + 1) & 0x3FFFFFFF;
-        if (C.sctl != sctl) C.sctl[2] = sctl[2];
+    if (IN || CBF_HARD_COOP) {
+        // no queue kernel follows: a chained advance starts the next build's scan epoch here (an
+        // error flag of this build stays set, so the rest of the run reports it; the scan reads the
+        // epoch only after this kernel), and the last block refreshes the statistics snapshot
+        // (values read mid-update are earlier ones, still valid lower bounds)
+        if (C.bcs && bx == 0 && threadIdx.x == 0) {
+            C.sctl[1] = (C.sctl[1] + 1) & 0x3FFFFFFF;
+            if (C.sctl != sctl) C.sctl[2] = sctl[2];
+        }
+        if (ST && stats && (int)blockIdx.x == (int)gridDim.x - 1 && threadIdx.x < 64) stat_snapshot(stats);
     }
-    if (ST && stats && (int)blockIdx.x == (int)gridDim.x - 1 && threadIdx.x < 64) stat_snapshot(stats);
-#endif
     if (sctl[2] != 0) {  // unusable cell list (build_begin / scan timeout): touch none of it
         lattice_error_tail(W, row_begin, row_end, win_row0, nwin, slot, u, status, cnt, stats, ext_part,
                            (long)bx * (kBlock / 64) + (threadIdx.x >> 6), hardq);
@@ -662,8 +677,8 @@ __global__ void __launch_bounds__(kBlock) k_lattice_filter(KP P, CellGrid G, Win
     Ego E;
     bool done = true;
     if (slot < total)
-        done = lattice_ego<FZ, ST>(P, G, B, slot, spos, svel, sidx, start, T, pos_out, u, status, cnt, hardq,
-                                   bx % kSubQ, qrec + (long)(bx % kSubQ) * qcap, hit_lds, E, O);
+        done = lattice_ego<FZ, ST, IN>(P, G, B, slot, spos, svel, sidx, start, T, pos_out, u, status, cnt, hardq,
+                                       bx % kSubQ, qrec + (long)(bx % kSubQ) * qcap, hit_lds, E, O);
 #if CBF_HARD_COOP
     wave_coop_finish<ST>(P, E, !done, B, T, hit_lds, slot, spos, svel, pos_out, u, status, cnt, O);
 #else
@@ -1055,8 +1070,15 @@ static int lattice_advance(const cbf_params* p, const cbf_grid* grid, int32_t W,
     unsigned long long* st = reinterpret_cast<unsigned long long*>(stats);
     const WinBounds B = make_win_bounds(W, win_row0, n, row_begin, row_end, cnt_begin, cnt_end, guard_rows);
     // without a statistics array the filter is the instantiation that computes none of them
-    const auto filter = st ? (p->f_is_zero ? k_lattice_filter<true, true> : k_lattice_filter<false, true>)
-                           : (p->f_is_zero ? k_lattice_filter<true, false> : k_lattice_filter<false, false>);
+    // small windows (a few waves per SIMD, e.g. one stripe of a strong-scaled swarm): the
+    // instantiation that runs the full solve in the filter itself -- its registers would halve the
+    // big filter's occupancy, but a small window never fills the chip anyway -- and no queue kernel
+    const bool in = !CBF_HARD_COOP && n <= CBF_INLINE_MAX;
+    const auto filter =
+        in ? (st ? (p->f_is_zero ? k_lattice_filter<true, true, true> : k_lattice_filter<false, true, true>)
+                 : (p->f_is_zero ? k_lattice_filter<true, false, true> : k_lattice_filter<false, false, true>))
+           : (st ? (p->f_is_zero ? k_lattice_filter<true, true, false> : k_lattice_filter<false, true, false>)
+                 : (p->f_is_zero ? k_lattice_filter<true, false, false> : k_lattice_filter<false, false, false>));
     hipLaunchKernelGGL(filter, dim3(nb), dim3(kBlock), 0, s,
                        kp, G, B, W, row_begin, row_end, win_row0, n, Wk.ncell, Wk.spos, Wk.svel, Wk.sidx, Wk.start,
                        Wk.sctl, T, po, uo, status, nbr_count, ext_part, st, Wk.hardq, Wk.qrec, Wk.qcap,
@@ -1066,6 +1088,10 @@ static int lattice_advance(const cbf_params* p, const cbf_grid* grid, int32_t W,
 #if CBF_HARD_COOP
     if (extents) launch_extents_finalize((int)lattice_ext_waves(n), ext_part, extents, s);
 #else
+    if (in) {
+        if (extents) launch_extents_finalize((int)lattice_ext_waves(n), ext_part, extents, s);
+        return (int)hipGetLastError();
+    }
     hipLaunchKernelGGL(CBF_HARD_MODE == 2 ? k_lattice_filter_hard_coop : k_lattice_filter_hard, dim3(hb), dim3(64), 0, s,
                        kp, G, B, T, po, uo, status, nbr_count,
                        ext_part ? ext_part + 4l * lattice_ext_waves(n) : nullptr, st, Wk.hardq, Wk.qrec, Wk.qcap,

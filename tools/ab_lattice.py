@@ -1,6 +1,6 @@
 """A/B timing of the fused lattice step for two source trees (tools/_ab/<tree>): the same
 jittered lattice, hipGraph replay, step time and advance-phase time by HIP events.
-Usage: python tools/ab_lattice.py <tree-root> <spacing> [steps]"""
+Usage: python tools/ab_lattice.py <tree-root> <spacing> [steps] [rows]  (1024 x rows agents)"""
 import sys
 import time
 
@@ -11,7 +11,8 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 from cbf_amd import scenarios, swarm  # noqa: E402
 
-W = H = 1024
+W = 1024
+H = int(sys.argv[4]) if len(sys.argv) > 4 else 1024
 rng = np.random.default_rng(0)
 r, c = np.divmod(np.arange(W * H), W)
 pos = np.stack([c * spacing, r * spacing], axis=1).astype(np.float64)
@@ -47,4 +48,4 @@ if hasattr(L, "run"):  # trees with cbf_lattice_run: graphs of 10-timestep calls
         L.run(10)
     torch.cuda.synchronize()
     run = f", run(10) {(time.perf_counter() - t0) / (steps // 10 * 10) * 1e6:.1f} us/step"
-print(f"{root} spacing {spacing}: step {dt * 1e6:.1f} us, advance {adv:.1f} us{run}")
+print(f"{root} spacing {spacing} rows {H}: step {dt * 1e6:.1f} us, advance {adv:.1f} us{run}")
