@@ -571,11 +571,6 @@ def bench_mc(args, ws, rank, local):
     return {"metric": METRIC, "value": tot["calls"] / elapsed, "unit": "agent-QP solves/s", "n_gpus": ws,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
             "ms_per_step_with_stats": None if elapsed_stats is None else elapsed_stats / args.steps * 1e3,
-        "ms_per_step_outputs_every_step": None if elapsed_hist is None else elapsed_hist / args.steps * 1e3,
-        "outputs_every_step_note": "the timed steps replayed with every timestep's filtered control, status, nominal "
-                                   "control and neighbour count stored (cbf_lattice_run_ex CBF_RUN_OUTPUT_HISTORY: "
-                                   "the reference's per-step si_velocities); the headline run stores positions every "
-                                   "timestep and the other outputs on each call's last timestep",
             "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f64",
             "data": "synthetic",
             "config": {"workload": f"cfg5: {args.mc_scenarios} independent 16+16 rendezvous scenarios, "

@@ -98,7 +98,9 @@ TEST_VARIANTS = {"scantimeout": (["cells.hip", "swarm.hip", "hocbf.hip", "filter
                  # the wave-cooperative exact solve of the queued QPs, in the filter (1) and in the
                  # queue kernel (2): kept bit-identical to the shipped one-lane solve by a GPU test
                  "hardcoop1": (["swarm.hip"], ["CBF_HARD_MODE=1"]),
-                 "hardcoop2": (["swarm.hip"], ["CBF_HARD_MODE=2"])}
+                 "hardcoop2": (["swarm.hip"], ["CBF_HARD_MODE=2", "CBF_INLINE_MAX=0"]),
+                 # small windows through the queue kernel too (the shipped build solves them inline)
+                 "noinline": (["swarm.hip"], ["CBF_INLINE_MAX=0"])}
 TEST_LIB_DIR = os.path.join(ROOT, "tests", "_lib")
 
 

@@ -279,9 +279,10 @@ __device__ __forceinline__ void lattice_error_tail(int W, int row_begin, int row
     if (slot < nwin) {
         const int r = win_row0 + (int)(slot / W), c = (int)(slot % W);
         if (r >= row_begin && r < row_end) {
+            // u / status / cnt are null in the inner timesteps of a run or an exchange cycle
             const long k = (long)(r - row_begin) * W + c;
-            u[k] = make_double2(0.0, 0.0);
-            status[k] = CBF_STATUS_WORKSPACE_ERROR;
+            if (u) u[k] = make_double2(0.0, 0.0);
+            if (status) status[k] = CBF_STATUS_WORKSPACE_ERROR;
             if (cnt) cnt[k] = 0;
         }
     }

@@ -119,11 +119,24 @@ class HipBackend:
     def tensor(self, a):
         return self.torch.as_tensor(np.ascontiguousarray(a), device=self.dev)
 
+    # CBF_SYNC_CHECK=1 (diagnostics): synchronise after every device call, so that a device fault is
+    # reported by the call that caused it (with the rank and the sub-step range) instead of by a
+    # later one; the kernels' order and arguments are unchanged.
+    _sync_check = __import__("os").environ.get("CBF_SYNC_CHECK", "0") == "1"
+
+    def _checked(self, what, S):
+        if self._sync_check and not self.torch.cuda.is_current_stream_capturing():
+            try:
+                self.torch.cuda.synchronize()
+            except Exception as e:  # noqa: BLE001
+                raise RuntimeError(f"rank {S.rank}: device fault in {what}") from e
+
     def pack(self, S):
         L, P = self._lib, self._lib.ptr
         if S.exchange_mode == "neighbour":
             L.check(L.lib.cbf_halo_pack_nbr(self.W, S.G, S.n_owned, P(S.own), P(self.ext_keys), self.nsub, S.ws,
                                             S.rank, P(S.send), L.stream_handle()), "cbf_halo_pack_nbr")
+            self._checked("cbf_halo_pack_nbr", S)
             return
         L.check(L.lib.cbf_halo_pack(self.W, S.G, S.n_owned, P(S.own), P(self.ext_keys), self.nsub, P(S.send),
                                     L.stream_handle()), "cbf_halo_pack")
@@ -134,6 +147,7 @@ class HipBackend:
             L.check(L.lib.cbf_halo_unpack_nbr(self.W, S.G, S.rb - S.w0, S.w1 - S.re, S.re - S.w0, P(S.recv), S.ws,
                                               S.rank, self.radius, self.nsub, P(S.wpos), P(self.flag),
                                               L.stream_handle()), "cbf_halo_unpack_nbr")
+            self._checked("cbf_halo_unpack_nbr", S)
             return
         L.check(L.lib.cbf_halo_unpack(self.W, S.G, S.rb - S.w0, S.w1 - S.re, S.re - S.w0, P(S.recv), S.stride,
                                       S.ws, S.rank, self.radius, self.nsub, P(S.wpos), P(self.flag),
@@ -157,6 +171,7 @@ class HipBackend:
             self.cp, L.C.byref(self.grid), self.W, self.H, S.rb, S.re, S.halo, self.nsub, s0, s1, S.w0, S.win_rows,
             P(S.wpos), self.gain, self.T, P(S.wvel), P(S.wu), P(S.wstatus), P(S.wcnt), P(self.ext_keys),
             P(S.stats_ptr()), P(self.ws_all), self.ws_bytes, L.stream_handle()), "cbf_lattice_cycle_sharded")
+        self._checked(f"cbf_lattice_cycle_sharded (sub-steps {s0}..{s1 - 1}, stats {S.collect_stats})", S)
 
     def lattice_build(self, S):
         L, P = self._lib, self._lib.ptr

@@ -859,19 +859,21 @@ def test_allpairs_spilled_variant_is_bit_identical():
     assert torch.equal(u, ref["u"]) and torch.equal(st, ref["status"]) and torch.equal(cnt, ref["nbr_count"])
 
 
-@pytest.mark.parametrize("mode", [1, 2])
+@pytest.mark.parametrize("variant", ["hardcoop1", "hardcoop2", "noinline"])
 @pytest.mark.parametrize("nominal", [None, ("random", 1.0, 5)])
-def test_cooperative_hard_solve_is_bit_identical(mode, nominal):
-    """The wave-cooperative exact solve of the QPs solve_fast cannot settle (coop_solve_ego: 8 lanes
-    per QP, ballots + shuffles; CBF_HARD_MODE 1 = inside the filter, 2 = in the queue kernel; test
-    builds tests/_lib/libcbf_hardcoop{1,2}.so) gives the shipped one-lane Seidel solve's results
-    bit for bit over a chained rollout: positions, last-step controls and statuses, and every
-    statistics word -- on the consensus lattice at spacing 0.2 and on cfg4r's random walk (10 %
-    of the QPs through the full solve)."""
+def test_full_solve_placements_are_bit_identical(variant, nominal):
+    """Every placement of the full solve of the QPs solve_fast cannot settle gives the same results
+    bit for bit over a chained rollout (positions, last-step controls and statuses, every statistics
+    word), on the consensus lattice at spacing 0.2 and on cfg4r's random walk (10 % of the QPs
+    through the full solve).  The shipped build solves this small window inside the filter, one
+    lane per QP (CBF_INLINE_MAX); the test builds (tests/_lib/libcbf_<variant>.so) queue it for the
+    one-lane queue kernel (noinline, the path of large windows), or run the wave-cooperative solve
+    (coop_solve_ego: 8 lanes per QP, ballots + shuffles) inside the filter (hardcoop1) or in the
+    queue kernel (hardcoop2)."""
     import ctypes as C
     import os
     from cbf_amd import _lib
-    V = C.CDLL(os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", f"libcbf_hardcoop{mode}.so"))
+    V = C.CDLL(os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", f"libcbf_{variant}.so"))
     for name in ("cbf_lattice_run", "cbf_lattice_set_nominal"):
         f = getattr(V, name)
         f.restype, f.argtypes = _lib.SIGNATURES[name]
