@@ -277,15 +277,23 @@ __device__ __forceinline__ int xcd_remap(int b, int nb) {
 // are the counting-sort scatter of the binned window agents into the cell-sorted copies, with each
 // agent's lattice-Laplacian nominal control (cross_and_rescue.py:121-125 shape) computed on the
 // way: the agent's position is loaded anyway and its 4 lattice neighbours are mostly L2 hits (cell
-// order ~ lattice order), so the control never makes an HBM round trip.  A scatter wave first
-// loads its records, the positions and the neighbours -- the bulk of its memory traffic,
-// overlapping the scan -- and only then waits, one lane polling, for the done words of the tiles
-// holding its cells (the records arrive in the previous step's cell order, so a wave's cells span
-// one tile or two), then reads the starts (sc1 loads of write-through stores, scan_tile's
-// hand-off) and stores.  Every wait points at a lower block index, which the dispatcher has
-// already made resident (the single-pass scan relies on the same order).  A wait
-// that runs out of spins sets the build's error flag (sctl[2], as a scan look-back that gives up);
-// the filters then report CBF_STATUS_WORKSPACE_ERROR for the step, and the stores stay in bounds.
+// order ~ lattice order), so the control never makes an HBM round trip.  A scatter thread takes
+// CBF_SCATTER_A records (one per kBlock-wide sub-block, so every load stays coalesced) and issues
+// ALL their loads -- records, positions, neighbours: the bulk of the scatter's memory traffic --
+// before it waits, so that with CBF_SCATTER_A records per thread the whole scatter's grid fits on
+// the chip at once and its loads overlap the scan (one record per thread left half the grid
+// waiting for residency behind the scan: 22 us = scan + scatter back to back).  Then one lane per
+// wave polls the done words of the tiles holding the wave's cells (the records arrive in the
+// previous step's cell order, so they span one tile or two), and every lane reads its starts (sc1
+// loads of write-through stores, scan_tile's hand-off) and stores.  Every wait points at a lower
+// block index, which the dispatcher has already made resident (the single-pass scan relies on the
+// same order).  A wait that runs out of spins sets the build's error flag (sctl[2], as a scan
+// look-back that gives up); the filters then report CBF_STATUS_WORKSPACE_ERROR for the step, and
+// the stores stay in bounds.
+#ifndef CBF_SCATTER_A
+#define CBF_SCATTER_A 2
+#endif
+constexpr int kScatterA = CBF_SCATTER_A;
 __global__ void __launch_bounds__(kBlock) k_lattice_scan_scatter(
     int32_t* __restrict__ count, long ncell, int ntiles, int ntiles8, int32_t* __restrict__ start,
     unsigned long long* __restrict__ tstate, int32_t* __restrict__ tdone, int32_t* __restrict__ sctl, long nwin,
@@ -304,9 +312,10 @@ __global__ void __launch_bounds__(kBlock) k_lattice_scan_scatter(
         __syncthreads();
     }
     const int lb = xcd_remap((int)blockIdx.x - ntiles8, (int)gridDim.x - ntiles8);
-    const long t = (long)lb * kBlock + threadIdx.x;
+    const long t0 = (long)lb * (kBlock * kScatterA) + threadIdx.x;
     const unsigned epoch = (unsigned)__hip_atomic_load(&sctl[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (t == 0 && sctl[2] == 0) {  // the cell order now exists for this window and grid: the next build walks it
+    const bool usable = sctl[2] == 0;
+    if (t0 == 0 && usable) {  // the cell order now exists for this window and grid: the next build walks it
         order_state[0] = 1;
         order_state[1] = (int)nwin;
         order_state[2] = (int)ncell;
@@ -314,27 +323,41 @@ __global__ void __launch_bounds__(kBlock) k_lattice_scan_scatter(
         order_state[4] = H;
         order_state[5] = W;
     }
-    double e[6] = {INFINITY, -INFINITY, -INFINITY, INFINITY, INFINITY, -INFINITY};
-    int any = 0;
-    double py = 0.0;
-    const int3 b = (t < nrec && sctl[2] == 0) ? bcs[t] : make_int3(-1, 0, 0);
     const NominalSpec N = nominal_spec(sctl);
-    const bool live = b.x >= 0 && b.x < ncell && b.z >= 0 && b.z < nwin;
-    double2 p = make_double2(0.0, 0.0), u0 = make_double2(0.0, 0.0);
-    int r = 0, c = 0;
-    if (live) {
-        p = pos[b.z];
-        r = win_row0 + b.z / W;
-        c = b.z % W;
-        if (N.mode == CBF_NOMINAL_RANDOM) {
-            u0 = random_nominal(N, (long)win_row0 * W + b.z, p);
-        } else {
-            const double2 a = lattice_sum(pos, b.z, r, c, W, H);
-            u0 = make_double2(a.x * gain, a.y * gain);
+    int3 b[kScatterA];
+    double2 p[kScatterA], u0[kScatterA];
+    bool live[kScatterA];
+#pragma unroll
+    for (int a = 0; a < kScatterA; ++a) {
+        const long t = t0 + (long)a * kBlock;
+        b[a] = (t < nrec && usable) ? bcs[t] : make_int3(-1, 0, 0);
+        live[a] = b[a].x >= 0 && b[a].x < ncell && b[a].z >= 0 && b[a].z < nwin;
+    }
+#pragma unroll
+    for (int a = 0; a < kScatterA; ++a) {
+        p[a] = make_double2(0.0, 0.0);
+        u0[a] = make_double2(0.0, 0.0);
+        if (live[a]) {
+            const int z = b[a].z, r = win_row0 + z / W, c = z % W;
+            p[a] = pos[z];
+            if (N.mode == CBF_NOMINAL_RANDOM) {
+                u0[a] = random_nominal(N, (long)win_row0 * W + z, p[a]);
+            } else {
+                const double2 s = lattice_sum(pos, z, r, c, W, H);
+                u0[a] = make_double2(s.x * gain, s.y * gain);
+            }
         }
     }
-    // the wave's tiles: one lane polls their done words, then every lane acquires
-    const int tlo = wave_min_i(live ? b.x / kScanTile : INT_MAX), thi = wave_max_i(live ? b.x / kScanTile : -1);
+    // the wave's tiles: one lane polls their done words, then every lane reads the starts
+    int tl = INT_MAX, th = -1;
+#pragma unroll
+    for (int a = 0; a < kScatterA; ++a)
+        if (live[a]) {
+            const int tt = b[a].x / kScanTile;
+            tl = tt < tl ? tt : tl;
+            th = tt > th ? tt : th;
+        }
+    const int tlo = wave_min_i(tl), thi = wave_max_i(th);
     if ((threadIdx.x & 63) == 0 && tlo <= thi) {
         const int32_t want = tile_done_word(epoch);
         bool failed = false;
@@ -354,25 +377,42 @@ __global__ void __launch_bounds__(kBlock) k_lattice_scan_scatter(
     __builtin_amdgcn_wave_barrier();
     asm volatile("" ::: "memory");
     const bool ok = __hip_atomic_load(&sctl[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0;
-    const int d = (live && ok) ? __hip_atomic_load(&start[b.x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + b.y : -1;
-    if (d >= 0 && d < nwin) {
-        spos[d] = p;
-        svel[d] = u0;
-        if (vel_out && r >= row_begin && r < row_end) vel_out[(long)(r - row_begin) * W + c] = u0;
-        sidx[d] = b.z;
-        py = p.y;
-        if (r >= row_begin && r < row_end) {
-            e[0] = e[1] = p.y;
-            any = 1;
-        }
-        if (r >= X.own_begin && r < X.own_end) {
-            if (r < X.own_end - X.guard) e[2] = p.y;
-            if (r >= X.own_begin + X.guard) e[3] = p.y;
-            e[4] = e[5] = p.y;
-            any = 1;
+    int d[kScatterA];
+#pragma unroll
+    for (int a = 0; a < kScatterA; ++a)
+        d[a] = (live[a] && ok) ? __hip_atomic_load(&start[b[a].x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + b[a].y
+                               : -1;
+    // halo-guard extents over the lane's agents; the maxima keep a NaN y (dkey orders it above +inf,
+    // so it fails the guard, as with one agent per lane)
+    double e[6] = {INFINITY, -INFINITY, -INFINITY, INFINITY, INFINITY, -INFINITY};
+    auto nmax = [](double m, double y) { return (y > m || y != y) ? y : m; };
+    int any = 0;
+    double py = 0.0;
+#pragma unroll
+    for (int a = 0; a < kScatterA; ++a) {
+        if (!(d[a] >= 0 && d[a] < nwin)) continue;
+        const int z = b[a].z, r = win_row0 + z / W, c = z % W;
+        spos[d[a]] = p[a];
+        svel[d[a]] = u0[a];
+        if (vel_out && r >= row_begin && r < row_end) vel_out[(long)(r - row_begin) * W + c] = u0[a];
+        sidx[d[a]] = z;
+        if (ext_keys) {
+            py = p[a].y;
+            if (r >= row_begin && r < row_end) {
+                e[0] = pmin(e[0], p[a].y);
+                e[1] = nmax(e[1], p[a].y);
+                any = 1;
+            }
+            if (r >= X.own_begin && r < X.own_end) {
+                if (r < X.own_end - X.guard) e[2] = nmax(e[2], p[a].y);
+                if (r >= X.own_begin + X.guard) e[3] = pmin(e[3], p[a].y);
+                e[4] = pmin(e[4], p[a].y);
+                e[5] = nmax(e[5], p[a].y);
+                any = 1;
+            }
         }
     }
-    if (ext_keys) ext_keys_flush<kBlock / 64>(e, any, py, ext_keys, lb, red, &arrive);
+    if (ext_keys) ext_keys_flush<kBlock / 64, kScatterA == 1>(e, any, py, ext_keys, lb, red, &arrive);
 }
 
 // Per-ego outcome of the lattice filter for the statistics.
@@ -999,7 +1039,8 @@ static void lattice_scan_scatter(const CellWs& Wk, int W, int H, int row_begin, 
                                  unsigned long long* ext_keys = nullptr, ExtSpec X = ExtSpec{0, 0, 0}) {
     if (nrec < 0) nrec = n;
     const int ntiles8 = (Wk.ntiles + 7) & ~7;
-    hipLaunchKernelGGL(k_lattice_scan_scatter, dim3(ntiles8 + nblk(nrec)), dim3(kBlock), 0, s, Wk.count, Wk.ncell,
+    const int nsb = (int)((nrec + (long)kBlock * kScatterA - 1) / ((long)kBlock * kScatterA));
+    hipLaunchKernelGGL(k_lattice_scan_scatter, dim3(ntiles8 + nsb), dim3(kBlock), 0, s, Wk.count, Wk.ncell,
                        Wk.ntiles, ntiles8, Wk.start, Wk.tstate, Wk.tdone, Wk.sctl, n, nrec, lattice_bcs(Wk),
                        pos, Wk.spos, Wk.svel, Wk.sidx, Wk.hardq + 2, win_row0, H, W, row_begin, row_end, gain,
                        reinterpret_cast<double2*>(vel_out), ext_keys, X);

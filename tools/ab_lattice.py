@@ -1,6 +1,7 @@
 """A/B timing of the fused lattice step for two source trees (tools/_ab/<tree>): the same
 jittered lattice, hipGraph replay, step time and advance-phase time by HIP events.
-Usage: python tools/ab_lattice.py <tree-root> <spacing> [steps] [rows]  (1024 x rows agents)"""
+Usage: python tools/ab_lattice.py <tree-root> <spacing> [steps] [rows] [rw]  (1024 x rows agents;
+rw: cfg4r's random-walk nominal control, amplitude 1, seed 5)"""
 import sys
 import time
 
@@ -17,7 +18,8 @@ rng = np.random.default_rng(0)
 r, c = np.divmod(np.arange(W * H), W)
 pos = np.stack([c * spacing, r * spacing], axis=1).astype(np.float64)
 pos += rng.uniform(-spacing / 2, spacing / 2, size=pos.shape)
-L = swarm.LatticeSwarm(pos, W, H, gain=0.25)
+rw = len(sys.argv) > 5 and sys.argv[5] == "rw"
+L = swarm.LatticeSwarm(pos, W, H, gain=0.25, nominal=("random", 1.0, 5) if rw else None)
 L.capture()
 for _ in range(20):
     L.step()
@@ -48,4 +50,4 @@ if hasattr(L, "run"):  # trees with cbf_lattice_run: graphs of 10-timestep calls
         L.run(10)
     torch.cuda.synchronize()
     run = f", run(10) {(time.perf_counter() - t0) / (steps // 10 * 10) * 1e6:.1f} us/step"
-print(f"{root} spacing {spacing} rows {H}: step {dt * 1e6:.1f} us, advance {adv:.1f} us{run}")
+print(f"{root} spacing {spacing} rows {H}{' rw' if rw else ''}: step {dt * 1e6:.1f} us, advance {adv:.1f} us{run}")
