@@ -104,8 +104,16 @@ def load_pmc(config):
         return {}
 
 
-# the timed advance phase: the filter instantiation without statistics (f = 0) and the queue kernel
-ADVANCE_KERNELS = ("k_lattice_filter<true, false>", "k_lattice_filter_hard")
+# the timed advance phase: the filter instantiation without statistics (f = 0, large window: the
+# full solve queued) and the queue kernel
+ADVANCE_KERNELS = ("k_lattice_filter<true, false, false>", "k_lattice_filter_hard")
+
+
+def load_pmc_valu(config, kernel=ADVANCE_KERNELS[0]):
+    """The kernel's VALU issue fraction from the committed PMC summary (SQ_ACTIVE_INST_VALU x 4 over
+    the SIMD cycles of its dispatches, tools/summarize_profile.py), if profiled."""
+    v = load_pmc(config).get(kernel, {}).get("valu_busy")
+    return None if v is None else float(v)
 
 
 def load_pmc_traffic(config, kernels=ADVANCE_KERNELS):
@@ -471,6 +479,10 @@ def bench_lattice(args, ws, rank, local):
                      "advance_phase": {"kernels": "k_lattice_filter + k_lattice_filter_hard", "ms": k_ms,
                                        "achieved": achieved_adv, "frac": achieved_adv / HBM_PEAK_GBS,
                                        "traffic": traffic_adv},
+                     "valu_busy": load_pmc_valu(args.config) if args.barrier == "reference" else None,
+                     "valu_busy_note": "the dominant kernel's VALU issue fraction (rocprofv3 SQ_ACTIVE_INST_VALU, "
+                                       "profiles/pmc_summary.json): beside the HBM fraction, the limit it works "
+                                       "against",
                      "algorithmic_bytes_per_launch": FILTER_BYTES_PER_AGENT * n_local,
                      "step_algorithmic_GBps": STEP_BYTES_PER_AGENT * n_local * args.steps / elapsed / 1e9 / ws},
     }
