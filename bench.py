@@ -219,7 +219,11 @@ def lattice_geometry(args, ws):
             raise SystemExit(f"bench.py: --rows {args.rows} is not divisible into {ws} stripes (or use --weak)")
         R = args.rows // ws
     halo = 10 if args.nominal is not None else 4
-    k = args.substeps if args.substeps else max(1, min(8, R // (2 * halo)))
+    # sub-steps per exchange: a stripe of <= 512 rows does not fill the chip, so ghost rows are nearly
+    # free and fewer exchanges pay (128 rows: 30.2 vs 32.3 us/step at 16 vs 8; 256: 41.8-42.2 vs 43.7;
+    # 512: 57.5-57.9 vs 58.4-60.0; tools/gpu_r03r.sh, gpu_r03s.sh); 1024-row stripes keep 8
+    cap = 16 if R <= 512 else 8
+    k = args.substeps if args.substeps else max(1, min(cap, R // (2 * halo)))
     if halo * k > R:
         raise SystemExit(f"bench.py: {k} sub-steps x {halo} halo rows do not fit a stripe of {R} rows")
     return R, R * ws, halo, k
@@ -744,7 +748,8 @@ def main():
                     help="sharded cfg4: ghost rows by one all-to-all to the two neighbours (default) or by one "
                          "all-gather to every rank")
     ap.add_argument("--substeps", type=int, default=None,
-                    help="sharded cfg4: timesteps per halo exchange (default: min(8, rows per rank / (2 halo)))")
+                    help="sharded cfg4: timesteps per halo exchange (default: min(16 for stripes of <= 512 rows, "
+                         "else 8, rows per rank / (2 halo)))")
     ap.add_argument("--shard", action="store_true",
                     help="cfg4: run the sharded step (halo pack + collective + unpack) even on one rank")
     args = ap.parse_args()
