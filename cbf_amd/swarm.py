@@ -261,6 +261,7 @@ class LatticeSwarm:
         if barrier != "reference" and method != "cells":
             raise ValueError("the Euclidean HOCBF lattice step uses the cell list (method='cells')")
         self.barrier = barrier
+        self.alpha = (float(alpha[0]), float(alpha[1]))
         self.hp = _lib.CbfHocbf(float(alpha[0]), float(alpha[1]))
         self.params = params or FilterParams()
         self.cp = self.params.c()
@@ -432,6 +433,52 @@ class LatticeSwarm:
 
     def _state(self):
         return [self.pos, self.vel, self.u, self.status, self.nbr_count, self.ws, self.stats, self.ap_ws]
+
+    # ---- rollout checkpoints ("save the SoA state .npz every K steps") ---------------------
+    def save_checkpoint(self, path: str) -> None:
+        """Write the swarm's whole device state (snapshot(): positions, nominal controls, outputs, the
+        workspace with the cell order and the nominal-control spec, statistics) and what defines the
+        step (shape, grid, gain, T, method, barrier, filter parameters) to an .npz.
+        LatticeSwarm.from_checkpoint(path) resumes the rollout: its next steps are bit-identical to
+        the ones this swarm would take.  Synchronises the device."""
+        import json
+        torch = _lib.require_gpu()
+        torch.cuda.synchronize()
+        meta = {"W": self.W, "H": self.H, "gain": self.gain, "T": self.T, "method": self.method,
+                "barrier": self.barrier, "alpha": list(self.alpha), "nominal": self.nominal,
+                "grid": [self.grid.x0, self.grid.y0, self.grid.inv_h, self.grid.nx, self.grid.ny],
+                "params": {"max_speed": self.params.max_speed, "dmin": self.params.dmin, "k": self.params.k,
+                           "safety_distance": self.params.safety_distance,
+                           "f": np.asarray(self.params.f, dtype=np.float64).tolist(),
+                           "g": np.asarray(self.params.g, dtype=np.float64).tolist()}}
+        arrays = {f"state{i}": t.cpu().numpy() for i, t in enumerate(self._state())}
+        arrays["meta"] = np.frombuffer(json.dumps(meta).encode(), dtype=np.uint8)
+        with open(path, "wb") as f:
+            np.savez(f, **arrays)
+
+    @classmethod
+    def from_checkpoint(cls, path: str) -> "LatticeSwarm":
+        """A swarm rebuilt from save_checkpoint()'s file (no pickles: the metadata is JSON).  Steps
+        and runs continue the saved rollout bit for bit; graphs are captured afresh as usual."""
+        import json
+        with np.load(path, allow_pickle=False) as z:
+            meta = json.loads(bytes(z["meta"]).decode())
+            states = [z[f"state{i}"] for i in range(8)]
+        pr = meta["params"]
+        params = FilterParams(max_speed=pr["max_speed"], dmin=pr["dmin"], k=pr["k"],
+                              safety_distance=pr["safety_distance"], f=np.array(pr["f"]), g=np.array(pr["g"]))
+        g = CbfGrid()
+        g.x0, g.y0, g.inv_h = (float(v) for v in meta["grid"][:3])
+        g.nx, g.ny = int(meta["grid"][3]), int(meta["grid"][4])
+        nominal = meta["nominal"]
+        S = cls(states[0], meta["W"], meta["H"], gain=meta["gain"], params=params, T=meta["T"], grid=g,
+                method=meta["method"], barrier=meta["barrier"], alpha=tuple(meta["alpha"]),
+                nominal=tuple(nominal) if isinstance(nominal, list) else nominal)
+        for t, a in zip(S._state(), states):
+            if tuple(t.shape) != a.shape or str(t.dtype).replace("torch.", "") != str(a.dtype):
+                raise ValueError(f"checkpoint {path}: a state array does not fit this swarm ({a.shape}, {a.dtype})")
+            t.copy_(_lib.require_gpu().from_numpy(a))
+        return S
 
     def step(self):
         g = self.graphs.get(self.collect_stats)

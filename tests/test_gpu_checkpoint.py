@@ -1,0 +1,50 @@
+"""Rollout checkpoints (save the SoA state .npz every K steps): a lattice swarm saved
+mid-rollout and rebuilt from the file continues the rollout bit for bit -- positions, controls,
+statuses, neighbour counts and the statistics totals -- for the consensus and the random-walk
+nominal controls, through step() and run()."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+if not torch.cuda.is_available():  # collected on CPU boxes but never run there
+    pytest.skip("needs a ROCm GPU", allow_module_level=True)
+
+from cbf_amd import _lib, scenarios, swarm  # noqa: E402
+
+
+@pytest.mark.parametrize("nominal,spacing", [(None, 0.145), (("random", 1.0, 5), 0.22)])
+def test_lattice_checkpoint_resumes_bit_identical(tmp_path, nominal, spacing):
+    W, H = 96, 64
+    A = swarm.LatticeSwarm(scenarios.lattice(W, H, seed=3, spacing=spacing), W, H, nominal=nominal)
+    A.run(7)
+    A.step()
+    path = str(tmp_path / "ck.npz")
+    A.save_checkpoint(path)
+    B = swarm.LatticeSwarm.from_checkpoint(path)
+    for S in (A, B):
+        S.run(9)
+        S.step()
+    torch.cuda.synchronize()
+    for a, b in ((A.pos, B.pos), (A.u, B.u), (A.status, B.status), (A.nbr_count, B.nbr_count),
+                 (A.vel, B.vel)):
+        assert torch.equal(a, b)
+    # the statistics words are spread over slots by the order of the queue's atomics; their totals
+    # and extrema (what decode_stats reads) are deterministic
+    assert _lib.decode_stats(A.stats.cpu().numpy()) == _lib.decode_stats(B.stats.cpu().numpy())
+    assert B.grid.nx == A.grid.nx and B.grid.inv_h == A.grid.inv_h and B.nominal == A.nominal
+
+
+def test_checkpoint_refuses_another_shape(tmp_path):
+    A = swarm.LatticeSwarm(scenarios.lattice(32, 32, seed=1), 32, 32)
+    A.step()
+    path = str(tmp_path / "ck.npz")
+    A.save_checkpoint(path)
+    with np.load(path, allow_pickle=False) as z:
+        arrays = {k: z[k] for k in z.files}
+    arrays["state0"] = arrays["state0"][:-1]
+    bad = str(tmp_path / "bad.npz")
+    np.savez(bad, **arrays)
+    with pytest.raises(ValueError):
+        swarm.LatticeSwarm.from_checkpoint(bad)
