@@ -19,7 +19,7 @@ def _bench(*args, n=1, steps=3):
     env.update(MASTER_ADDR="127.0.0.1", MASTER_PORT="29561")
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--width", "256", "--rows", "256",
                         "--steps", str(steps), "--warmup", "1", "--kernel-iters", "2", "--no-cpu-baseline", *args],
-                       cwd=ROOT, env=env, capture_output=True, text=True, timeout=110)
+                       cwd=ROOT, env=env, capture_output=True, text=True, timeout=170)
     assert r.returncode == 0, r.stderr[-2000:]
     lines = r.stdout.splitlines()
     assert len(lines) == 1, r.stdout[-2000:]
@@ -55,3 +55,17 @@ def test_bench_gpus2_launches_two_ranks_strong_scaling():
     assert two["scaling"] == "strong" and "x2" in two["config"]["parallelism"]
     assert two["end_state_sha256"] == one["end_state_sha256"]
     assert two["solves_per_step"] == one["solves_per_step"]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [4, 8])
+def test_bench_gpus_n_rehearsal_matches_one_rank(n):
+    """The 4- and 8-rank row splits of the strong-scaling bench (64 and 32 rows per rank of a
+    256 x 256 lattice: interior ranks with two neighbours, fewer sub-steps per exchange), rehearsed
+    with gloo on this one-GPU box (8 processes on the card), end in the 1-rank state bit for bit."""
+    one = _bench(steps=8)
+    many = _bench("--gpus", str(n), "--backend", "gloo", n=n, steps=8)
+    assert many["config"]["agents_total"] == 256 * 256
+    assert many["config"]["agents_per_gpu"] == 256 * 256 // n
+    assert many["end_state_sha256"] == one["end_state_sha256"]
+    assert many["solves_per_step"] == one["solves_per_step"]
