@@ -51,10 +51,20 @@ class ControlBarrierFunction:
         r = np.asarray(robot_state, dtype=np.float64).reshape(4)
         obs = np.asarray(obs_states, dtype=np.float64).reshape(-1, 4)
         u0 = np.asarray(u0, dtype=np.float64).reshape(2)
-        dev = torch.device("cuda")
-        u, _, _ = self.get_safe_control_batch(torch.from_numpy(r).reshape(1, 4).to(dev),
-                                              [torch.from_numpy(obs).to(dev)],
-                                              torch.from_numpy(u0).reshape(1, 2).to(dev), f, g)
+        m = obs.shape[0]
+        # one host buffer, one copy to the device: [state (4), u0 (2), obstacles (4 m, at least 4)]
+        # as float64, then the neighbour offsets {0, m} as int32 in the last 8 bytes
+        nf = 6 + 4 * max(m, 1)
+        host = np.zeros(8 * nf + 8, dtype=np.uint8)
+        hf = host[:8 * nf].view(np.float64)
+        hf[:4] = r
+        hf[4:6] = u0
+        hf[6:6 + 4 * m] = obs.reshape(-1)
+        host[8 * nf:].view(np.int32)[:] = (0, m)
+        dev_buf = torch.from_numpy(host).to(torch.device("cuda"))
+        df = dev_buf[:8 * nf].view(torch.float64)
+        off = dev_buf[8 * nf:].view(torch.int32)
+        u, _, _ = self.get_safe_control_batch(df[:4].view(1, 4), (off, df[6:].view(-1, 4)), df[4:6].view(1, 2), f, g)
         return u[0].cpu().numpy()
 
     def get_safe_control_batch(self, robot_states, obs_list, u0, f=None, g=None, return_x=False):
