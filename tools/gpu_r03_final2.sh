@@ -3,7 +3,7 @@
 set -u
 cd /root/repo
 export TMPDIR=/tmp
-O=gpurun_out/r03_final2; mkdir -p $O
+O=gpurun_out/${FINAL_OUT:-r03_final2}; mkdir -p $O
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > $O/pytest.log 2>&1 || { tail -60 $O/pytest.log; exit 1; }
 tail -1 $O/pytest.log
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { tail -20 $O/smoke.log; exit 2; }
