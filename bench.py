@@ -221,7 +221,7 @@ def lattice_geometry(args, ws):
     halo = 10 if args.nominal is not None else 4
     # sub-steps per exchange: a stripe of <= 512 rows does not fill the chip, so ghost rows are nearly
     # free and fewer exchanges pay (128 rows: 30.2 vs 32.3 us/step at 16 vs 8; 256: 41.8-42.2 vs 43.7;
-    # 512: 57.5-57.9 vs 58.4-60.0; tools/gpu_r03r.sh, gpu_r03s.sh); 1024-row stripes keep 8
+    # 512: 57.5-57.9 vs 58.4-60.0; tools/records/gpu_r03r.sh, gpu_r03s.sh); 1024-row stripes keep 8
     cap = 16 if R <= 512 else 8
     k = args.substeps if args.substeps else max(1, min(cap, R // (2 * halo)))
     if halo * k > R:
