@@ -443,7 +443,7 @@ struct EgoOut {
 // (IN = true: no queue kernel); larger ones queue (CBF_HARD_MODE).  Measured crossover (cbf_lattice_run,
 // W = 1024, spacing 0.145, run(10) per timestep, inline vs queue): 64 rows 25.2 vs 30.2 us, 128
 // rows 27.7 vs 32.6 us, 256 rows 42.5 vs 38.9 us, 512 rows 55 vs 55 (and the inline form at 1024
-// rows 118.5 vs 79.5).  Between 128 and 192 rows (tools/gpu_r03g2.sh): 128 rows 27.8-27.9 vs
+// rows 118.5 vs 79.5).  Between 128 and 192 rows (tools/records/gpu_r03g2.sh): 128 rows 27.8-27.9 vs
 // 32.5-32.7, 136 rows 34.2 vs 32.9-33.1, 144 35.0 vs 33.8, 160 35.6 vs 33.8, 192 38.5-38.8 vs
 // 34.0-34.6.  So the inline form pays only while every SIMD holds at most 2 of the window's waves:
 // 256 CUs x 4 SIMDs x 2 waves x 64 lanes = 131072 agents (one 1024-wide row more puts a third
