@@ -15,7 +15,7 @@ PKG = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(PKG, "libcbf_amd.so")
 
 CBF_EINVAL = -1
-ABI_VERSION = 3  # include/cbf_amd.h CBF_ABI_VERSION
+ABI_VERSION = 4  # include/cbf_amd.h CBF_ABI_VERSION
 STATUS_IDLE, STATUS_OPTIMAL, STATUS_RELAXED, STATUS_BOX_INFEASIBLE, STATUS_RELAX_CAP = 0, 1, 2, 3, 4
 STATUS_NBR_OVERFLOW = 5
 STATUS_WORKSPACE_ERROR = 6
@@ -29,7 +29,8 @@ _DIST_KEY_TOP = 0x7FF0000000000000
 class CbfParams(C.Structure):
     _fields_ = [("max_speed", C.c_double), ("dmin", C.c_double), ("k", C.c_double), ("gamma", C.c_double),
                 ("f", C.c_double * 16), ("g", C.c_double * 8), ("cull_t", C.c_double),
-                ("nrm", (C.c_double * 2) * 4), ("f_is_zero", C.c_int32), ("relax_cap", C.c_int32)]
+                ("nrm", (C.c_double * 2) * 4), ("f_is_zero", C.c_int32), ("relax_cap", C.c_int32),
+                ("solve_inline_max", C.c_int32), ("reserved0", C.c_int32)]
 
 
 class CbfGrid(C.Structure):
@@ -67,6 +68,7 @@ _HP = C.POINTER(CbfHocbf)
 _CP, _UP = C.POINTER(CbfCertParams), C.POINTER(CbfUnicycleParams)
 SIGNATURES = {
     "cbf_abi_version": (C.c_int, []),
+    "cbf_workspace_layout": (C.c_int, []),
     "cbf_params_init": (C.c_int, [_P, _d, _d, _d, _vp, _vp, _d]),
     "cbf_get_safe_control_batch": (C.c_int, [_P, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "cbf_assemble_rows": (C.c_int, [_P, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),

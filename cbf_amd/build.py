@@ -94,13 +94,7 @@ def build_torch_ops(verbose: bool = False) -> str:
 # the package): name -> (sources, defines).  CBF_SCAN_TEST_TIMEOUT makes every scan look-back give
 # up, so tests/test_gpu_parity.py can check that the failure is reported, not silent.
 TEST_VARIANTS = {"scantimeout": (["cells.hip", "swarm.hip", "hocbf.hip", "filter.hip"], ["CBF_SCAN_TEST_TIMEOUT=1"]),
-                 "apwpe8": (["filter.hip"], ["CBF_AP_WPE=8"]),
-                 # the wave-cooperative exact solve of the queued QPs, in the filter (1) and in the
-                 # queue kernel (2): kept bit-identical to the shipped one-lane solve by a GPU test
-                 "hardcoop1": (["swarm.hip"], ["CBF_HARD_MODE=1"]),
-                 "hardcoop2": (["swarm.hip"], ["CBF_HARD_MODE=2", "CBF_INLINE_MAX=0"]),
-                 # small windows through the queue kernel too (the shipped build solves them inline)
-                 "noinline": (["swarm.hip"], ["CBF_INLINE_MAX=0"])}
+                 "apwpe8": (["filter.hip"], ["CBF_AP_WPE=8"])}
 TEST_LIB_DIR = os.path.join(ROOT, "tests", "_lib")
 
 

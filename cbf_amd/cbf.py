@@ -12,6 +12,8 @@ h = |p_i - p_j|^2 - dmin^2 with psi1 = h' + alpha1 h, psi2 = psi1' + alpha2 psi1
 """
 from __future__ import annotations
 
+import threading
+
 import numpy as np
 
 from . import _lib
@@ -33,7 +35,11 @@ class ControlBarrierFunction:
         self.barrier = barrier
         self.alpha1 = float(alpha1)
         self.alpha2 = float(alpha2)
-        self._io = None  # get_safe_control's pinned host / device buffers
+        # get_safe_control's pinned host / device buffers, one set per device (the call uses the
+        # current device's stream); the lock makes the call reentrant across threads sharing one
+        # instance, as the stateless reference call is
+        self._io = {}
+        self._io_lock = threading.Lock()
 
     def _params(self, f, g):
         f = np.asarray(f, dtype=np.float64)
@@ -55,31 +61,37 @@ class ControlBarrierFunction:
         m = obs.shape[0]
         # one pinned host buffer, one copy to the device: [state (4), u0 (2), obstacles (4 m, at
         # least 4)] as float64, then the neighbour offsets {0, m} as int32 in the last 8 bytes.
-        # The buffers are kept per instance and grown as needed; every call ends synchronised (the
-        # result is read back), so the next call may overwrite them.
+        # The buffers are kept per instance and device and grown as needed; every call ends
+        # synchronised (the result is read back) before the lock is released, so the next call
+        # may overwrite them.
         nf = 6 + 4 * max(m, 1)
         nbytes = 8 * nf + 8
-        if self._io is None or self._io[0].numel() < nbytes:
-            cap = max(nbytes, 8 * (6 + 4 * 64) + 8)
-            self._io = (torch.empty(cap, dtype=torch.uint8, pin_memory=True),
-                        torch.empty(cap, dtype=torch.uint8, device="cuda"),
-                        torch.empty(2, dtype=torch.float64, pin_memory=True))
-        pin, dev_buf, out = self._io
-        host = pin.numpy()
-        hf = host[:8 * nf].view(np.float64)
-        hf[:4] = r
-        hf[4:6] = u0
-        hf[6:6 + 4 * m] = obs.reshape(-1)
-        if m == 0:
-            hf[6:10] = 0.0
-        host[8 * nf:nbytes].view(np.int32)[:] = (0, m)
-        dev_buf[:nbytes].copy_(pin[:nbytes], non_blocking=True)
-        df = dev_buf[:8 * nf].view(torch.float64)
-        off = dev_buf[8 * nf:nbytes].view(torch.int32)
-        u, _, _ = self.get_safe_control_batch(df[:4].view(1, 4), (off, df[6:].view(-1, 4)), df[4:6].view(1, 2), f, g)
-        out.copy_(u[0], non_blocking=True)
-        torch.cuda.current_stream().synchronize()
-        return out.numpy().copy()
+        dev = torch.cuda.current_device()
+        with self._io_lock:
+            io = self._io.get(dev)
+            if io is None or io[0].numel() < nbytes:
+                cap = max(nbytes, 8 * (6 + 4 * 64) + 8)
+                io = (torch.empty(cap, dtype=torch.uint8, pin_memory=True),
+                      torch.empty(cap, dtype=torch.uint8, device=f"cuda:{dev}"),
+                      torch.empty(2, dtype=torch.float64, pin_memory=True))
+                self._io[dev] = io
+            pin, dev_buf, out = io
+            host = pin.numpy()
+            hf = host[:8 * nf].view(np.float64)
+            hf[:4] = r
+            hf[4:6] = u0
+            hf[6:6 + 4 * m] = obs.reshape(-1)
+            if m == 0:
+                hf[6:10] = 0.0
+            host[8 * nf:nbytes].view(np.int32)[:] = (0, m)
+            dev_buf[:nbytes].copy_(pin[:nbytes], non_blocking=True)
+            df = dev_buf[:8 * nf].view(torch.float64)
+            off = dev_buf[8 * nf:nbytes].view(torch.int32)
+            u, _, _ = self.get_safe_control_batch(df[:4].view(1, 4), (off, df[6:].view(-1, 4)), df[4:6].view(1, 2),
+                                                  f, g)
+            out.copy_(u[0], non_blocking=True)
+            torch.cuda.current_stream().synchronize()
+            return out.numpy().copy()
 
     def get_safe_control_batch(self, robot_states, obs_list, u0, f=None, g=None, return_x=False):
         """Batched get_safe_control.  robot_states (B,4), u0 (B,2) float64 CUDA tensors; obs_list is

@@ -30,6 +30,7 @@ extern "C" int cbf_params_init(cbf_params* p, double max_speed, double dmin, dou
     p->f_is_zero = fz;
     p->cull_t = cull_threshold(safety_distance);
     p->relax_cap = 1 << 16;
+    p->solve_inline_max = -1;  // the library's threshold (swarm.hip kSolveInlineDefault)
     // L_g = -hs_p @ g per sign quadrant, numpy's pairwise order (cbf.py:56)
     for (int q = 0; q < 4; ++q) {
         const double sx = (q & 1) ? -1.0 : 1.0, sy = (q & 2) ? -1.0 : 1.0;

@@ -480,208 +480,6 @@ __device__ __forceinline__ Sol solve_ego(const KP& P, const Ego& E) {
     return S;
 }
 
-// ---- the wave-cooperative exact solve (north star: "one wavefront per agent-batch ... exact
-// active-set solve with wavefront-reduce primitives") ------------------------------------------
-// solve_ego by the 8 lanes of a lane group (lane & 7 = plane slot: 0..3 the merged box rows,
-// 4..7 the CBF quadrants), a wave solving up to 8 QPs at once, bit-identical to solve_ego (and so
-// to oracle/cbf_oracle.c:solve_ego): the same expressions evaluated in the same order, only
-// spread over lanes.
-//   * the next violated plane: every lane tests its own plane at the current x, a group ballot
-//     picks the lowest violated slot above the last event -- solve8's sequential scan, since x
-//     does not change between its tests;
-//   * the event at plane h: every lane computes its own (a.d, b - a.p); the bound search of
-//     solve8 is a SEQUENTIAL fold over j < h (cross-multiplied comparisons are not associative
-//     under rounding), done redundantly by every lane of the group from the other lanes' values
-//     (shuffles), so the chosen bound is solve8's;
-//   * the feasibility check of planes j <= h: one test per lane, a group ballot;
-//   * the strip pre-check and the +1 relaxation loop (cbf.py:84-87): group-uniform control.
-// Work per event is O(h) shuffles + O(1) arithmetic per lane, against solve8's fully unrolled
-// O(N^2) per lane, which a wave of 64 different QPs executes for the union of their paths.
-// Inputs per lane: its slot's ORIGINAL rhs (box: pmin of the saturated rows, quadrant: the
-// per-quadrant minimum row) and the group's mask (bit s: slot s present); active = the group has
-// a QP.  Every lane of the wave must call it (shuffles and ballots); returns the group's Sol in
-// every lane of the group (viol over the solved rows, viol_orig over the original rows).
-__device__ __forceinline__ unsigned group_ballot(bool p) {
-    return (unsigned)((__ballot(p) >> (threadIdx.x & 56)) & 0xFFull);
-}
-
-__device__ __forceinline__ double group_shfl(double v, int slot) {
-    return __shfl(v, (int)(threadIdx.x & 56) | slot, 64);
-}
-
-// the normal of plane slot gl (solve_ego's a0 / a1 tables), from the uniform parameters
-__device__ __forceinline__ double slot_a0(const KP& P, int gl) {
-    return gl >= 4 ? (gl == 4 ? P.n0[0] : gl == 5 ? P.n0[1] : gl == 6 ? P.n0[2] : P.n0[3])
-                   : (gl == 0 ? 1.0 : (gl == 2 ? -1.0 : 0.0));
-}
-__device__ __forceinline__ double slot_a1(const KP& P, int gl) {
-    return gl >= 4 ? (gl == 4 ? P.n1[0] : gl == 5 ? P.n1[1] : gl == 6 ? P.n1[2] : P.n1[3])
-                   : (gl == 1 ? 1.0 : (gl == 3 ? -1.0 : 0.0));
-}
-
-// UNROLL: the bound fold's shuffles all issued up front (one shuffle latency per event; more
-// registers: for the queue kernel) instead of one candidate at a time (the in-filter form).
-template <bool UNROLL = false>
-__device__ __forceinline__ Sol coop_solve_ego(const KP& P, double bslot, unsigned mask8, bool active) {
-    const int gl = threadIdx.x & 7;
-    const double a0 = slot_a0(P, gl), a1 = slot_a1(P, gl);
-    const bool pres = active && ((mask8 >> gl) & 1u);
-    double b = bslot;
-    Sol S;
-    S.status = CBF_STATUS_OPTIMAL;
-    S.iters = 0;
-    S.x0 = S.x1 = 0.0;
-    // strip pre-check (solve_ego): the group's quadrant rhs relaxed together, in every lane
-    const unsigned present = mask8 >> 4;
-    if (active && ((present & 9u) == 9u || (present & 6u) == 6u)) {
-        double c4 = group_shfl(b, 4), c5 = group_shfl(b, 5), c6 = group_shfl(b, 6), c7 = group_shfl(b, 7);
-        for (;;) {
-            bool dead = false;
-            if ((present & 9u) == 9u) {
-                const double s = c4 + c7;
-                const double tb = FEAS_TOL * (pmax(1.0, fabs(c4)) + pmax(1.0, fabs(c7)));
-                dead = dead || (s < -tb - 1e-9 * (1.0 + fabs(c4) + fabs(c7)));
-            }
-            if ((present & 6u) == 6u) {
-                const double s = c5 + c6;
-                const double tb = FEAS_TOL * (pmax(1.0, fabs(c5)) + pmax(1.0, fabs(c6)));
-                dead = dead || (s < -tb - 1e-9 * (1.0 + fabs(c5) + fabs(c6)));
-            }
-            if (!dead || S.iters >= P.relax_cap) break;
-            c4 = c4 + 1.0;
-            c5 = c5 + 1.0;
-            c6 = c6 + 1.0;
-            c7 = c7 + 1.0;
-            S.iters++;
-        }
-        if (gl >= 4) b = gl == 4 ? c4 : (gl == 5 ? c5 : (gl == 6 ? c6 : c7));
-    }
-    if (active) {
-        for (;;) {
-            // one solve8 over the group's planes at the current rhs
-            const double tb = FEAS_TOL * pmax(1.0, fabs(b));
-            double x0 = 0.0, x1 = 0.0;
-            int fail = -1, hcur = -1;
-            for (;;) {
-                const bool v = pres && gl > hcur && !((a0 * x0 + a1 * x1) - b <= tb);
-                const unsigned m = group_ballot(v);
-                if (!m) break;
-                const int h = __ffs(m) - 1;
-                const double a0h = group_shfl(a0, h), a1h = group_shfl(a1, h), bh = group_shfl(b, h);
-                const double n2 = a0h * a0h + a1h * a1h;
-                if (!(n2 > 0)) {
-                    fail = h;
-                    break;
-                }
-                const double t = bh / n2;
-                const double p0 = t * a0h, p1 = t * a1h;
-                const double d0 = -a1h, d1 = a0h;
-                const double adl = a0 * d0 + a1 * d1;
-                const double rl_ = b - (a0 * p0 + a1 * p1);
-                double rh = 0.0, ah = 0.0, rl = 0.0, al = 0.0;
-                bool has_hi = false, has_lo = false;
-                auto fold = [&](int j, double ad, double r) {
-                    if (ad > 0) {
-                        if (!has_hi || r * ah < rh * ad) {
-                            rh = r;
-                            ah = ad;
-                        }
-                        has_hi = true;
-                    } else if (ad < 0) {
-                        if (!has_lo || r * al > rl * ad) {
-                            rl = r;
-                            al = ad;
-                        }
-                        has_lo = true;
-                    }
-                };
-                if (UNROLL) {
-                    double adj[7], rj[7];
-#pragma unroll
-                    for (int j = 0; j < 7; ++j) {
-                        adj[j] = group_shfl(adl, j);
-                        rj[j] = group_shfl(rl_, j);
-                    }
-#pragma unroll
-                    for (int j = 0; j < 7; ++j)
-                        if (j < h && ((mask8 >> j) & 1u)) fold(j, adj[j], rj[j]);
-                } else {
-                    // rolled: one candidate's shuffles in flight at a time (register budget)
-#pragma unroll 1
-                    for (int j = 0; j < h; ++j) {
-                        const double ad = group_shfl(adl, j), r = group_shfl(rl_, j);
-                        if ((mask8 >> j) & 1u) fold(j, ad, r);
-                    }
-                }
-                double s = 0.0;
-                bool s_hi = false;
-                if (has_hi && rh < 0) {
-                    s = rh / ah;
-                    s_hi = true;
-                }
-                if (has_lo && (s_hi ? (rh * al > rl * ah) : (rl < 0))) s = rl / al;
-                x0 = p0 + s * d0;
-                x1 = p1 + s * d1;
-                if (group_ballot(pres && gl <= h && !((a0 * x0 + a1 * x1) - b <= tb))) {
-                    fail = h;
-                    break;
-                }
-                hcur = h;
-            }
-            if (fail < 0) {
-                S.x0 = x0;
-                S.x1 = x1;
-                break;
-            }
-            if (fail < 4) {  // reported as at the first solve: no relaxation applied
-                S.status = CBF_STATUS_BOX_INFEASIBLE;
-                S.iters = 0;
-                S.x0 = S.x1 = 0.0;
-                b = bslot;
-                break;
-            }
-            if (S.iters >= P.relax_cap) {
-                S.status = CBF_STATUS_RELAX_CAP;
-                S.x0 = S.x1 = 0.0;
-                break;
-            }
-            if (gl >= 4) b = b + 1.0;
-            S.iters++;
-        }
-        if (S.status == CBF_STATUS_OPTIMAL && S.iters > 0) S.status = CBF_STATUS_RELAXED;
-    }
-    // the largest violation of the solved rows (solve_ego's max from 0 in slot order; a max of
-    // values >= 0 does not depend on the order), and of the ORIGINAL rows for a relaxed QP
-    // (orig_violation: the merged box rows and the unrelaxed quadrant minima = every slot's bslot)
-    const double ax = a0 * S.x0 + a1 * S.x1;
-    const double d = ax - b, dor = ax - bslot;
-    double v = (pres && d > 0.0) ? d : 0.0;
-    double vo = (pres && dor > 0.0) ? dor : 0.0;
-#pragma unroll
-    for (int o = 1; o < 8; o <<= 1) {
-        const double w = __shfl_xor(v, o, 64), wo = __shfl_xor(vo, o, 64);
-        v = w > v ? w : v;
-        vo = wo > vo ? wo : vo;
-    }
-    S.viol = v;
-    S.viol_orig = S.iters > 0 ? vo : v;
-    return S;
-}
-
-// This lane's slot rhs for the group solving ego E (box slots: solve_ego's merged box rows,
-// quadrant slots: the per-quadrant minima), evaluated in the lane that holds E.
-__device__ __forceinline__ double ego_slot_b(const KP& P, double u0x, double u0y, double r2, double r3, double bq0,
-                                             double bq1, double bq2, double bq3, int gl) {
-    const double ms = P.ms;
-    double b;
-    if (gl == 0) b = pmin(ms - u0x, (ms - r2) - u0x);
-    else if (gl == 1) b = pmin(ms + u0x, (ms - r3) - u0y);
-    else if (gl == 2) b = pmin(ms - u0y, (ms + r2) + u0x);
-    else if (gl == 3) b = pmin(ms + u0y, (ms + r3) + u0y);
-    else b = gl == 4 ? bq0 : (gl == 5 ? bq1 : (gl == 6 ? bq2 : bq3));
-    return b;
-}
-
 // The common cases of solve_ego without the full Seidel machinery, bit-identical to it.  After the
 // strip pre-relaxation, solve_ego's first solve8 call either finds the origin feasible (no plane
 // violated: x = 0), or meets exactly one violated plane h whose projection p = (b_h / |a_h|^2) a_h

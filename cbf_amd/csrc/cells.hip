@@ -68,3 +68,5 @@ int build_cells(const CellGrid& G, const CellWs& W, int n, const double2* pos, c
 }
 
 }  // namespace cbf
+
+extern "C" int cbf_workspace_layout(void) { return cbf::kWorkspaceLayout; }

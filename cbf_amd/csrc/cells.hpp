@@ -49,6 +49,11 @@ inline CellGrid make_grid(const cbf_grid* g) {
 
 inline size_t align256(size_t b) { return (b + 255) & ~size_t(255); }
 
+// Version of the workspace carve-up below and of its control words (cbf_workspace_layout): bump it
+// with ANY change to CellWs, HardRec, the control-word assignments or the queue header, so that a
+// saved workspace is never restored into a library that reads it differently.
+constexpr int kWorkspaceLayout = 4;
+
 // Workspace carve-up (all segments 256-byte aligned).  The control words come first, at a fixed
 // offset, so that the shape signature they hold can be checked whatever shape a call assumes.
 struct CellWs {

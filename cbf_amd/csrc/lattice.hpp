@@ -170,30 +170,6 @@ __device__ __forceinline__ void drain_subq(int32_t* __restrict__ hardq, int per_
     }
 }
 
-// drain_subq for the cooperative queue kernel: lane group g (8 lanes) of the k-th working block
-// of sub-queue q takes entries 8 k + g, then + 8 nwork, ...; visit(q, i, act) is called by EVERY
-// lane of the wave in each pass (the solve's shuffles and ballots need the whole wave), act =
-// the group has an entry.  The done counter is taken as soon as the length is read (a block
-// needs the length only; the records are read-only until the next advance), so its return trip
-// overlaps the solves instead of ending the kernel; the last working block empties the sub-queue
-// at its end.
-template <class Visit>
-__device__ __forceinline__ void drain_subq_groups(int32_t* __restrict__ hardq, int per_q, Visit&& visit) {
-    const int q = blockIdx.x % kSubQ, k = blockIdx.x / kSubQ;
-    const int nq = hardq[32 * (1 + q)];
-    const int need = (nq + 7) / 8;
-    const int nwork = need < per_q ? need : per_q;
-    if (k >= nwork) return;
-    int done = 0;
-    if (threadIdx.x == 0) done = atomicAdd(&hardq[32 * (1 + kSubQ + q)], 1);
-    const int g = (threadIdx.x & 63) >> 3;
-    for (int i0 = k * 8; i0 < nq; i0 += nwork * 8) visit(q, i0 + g, i0 + g < nq);
-    if (threadIdx.x == 0 && done == nwork - 1) {
-        hardq[32 * (1 + q)] = 0;
-        hardq[32 * (1 + kSubQ + q)] = 0;
-    }
-}
-
 // Rollout statistics of the lattice step (`stats`, device uint64[1024] = 64 slots of 16 words,
 // one 128-B line each; a wave adds into slot (its index & 63), the host sums or maxes over the
 // slots).  Counted over the egos of the counted rows.  The two violations are the bits of

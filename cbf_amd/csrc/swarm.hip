@@ -422,39 +422,27 @@ struct EgoOut {
     int nbrs;         // neighbours
     int code;         // final status code (res == 1)
     bool binding;     // the minimiser is not the origin (res == 1)
-    bool seidel;      // the QP took the full Seidel solve (the cooperative one, or the queue)
+    bool seidel;      // the QP took the full Seidel solve (inline, or through the queue)
     double viol, vorig, d2, nx, ny;
 };
 
-// Where the QPs that solve_fast cannot settle go (CBF_HARD_MODE; DESIGN.md sec. 4 has the A/B):
-//   0 (default): queued with their assembled state for k_lattice_filter_hard, one lane per QP;
-//   1: solved inside the filter by the wave-cooperative exact solve (coop_solve_ego: 8 lanes per
-//      QP, up to 8 QPs per pass; no queue kernel).  Bit-identical, slower: run(10) 90 vs 79 us per
-//      timestep at cfg4, 110 vs 78 at cfg4f -- the latency-bound solve holds the filter wave's CU
-//      slot, and the solver's registers cut the filter's occupancy from 6 to 5 waves/SIMD;
-//   2: queued, and the queue kernel k_lattice_filter_hard_coop solves them cooperatively (8 QPs
-//      per wave and pass).  Bit-identical, slower: 14.0 vs 10.1 us per launch at cfg4, 82.6 vs
-//      14.9 at cfg4r (8 lanes each re-running the event loop and the sequential bound fold cost
-//      more issue slots per QP than one lane's unrolled solve, and the shuffles add latency).
-#ifndef CBF_HARD_MODE
-#define CBF_HARD_MODE 0
-#endif
-// Windows of at most this many agents run the filter instantiation with the full solve inline
-// (IN = true: no queue kernel); larger ones queue (CBF_HARD_MODE).  Measured crossover (cbf_lattice_run,
-// W = 1024, spacing 0.145, run(10) per timestep, inline vs queue): 64 rows 25.2 vs 30.2 us, 128
-// rows 27.7 vs 32.6 us, 256 rows 42.5 vs 38.9 us, 512 rows 55 vs 55 (and the inline form at 1024
-// rows 118.5 vs 79.5).  Between 128 and 192 rows (tools/records/gpu_r03g2.sh): 128 rows 27.8-27.9 vs
-// 32.5-32.7, 136 rows 34.2 vs 32.9-33.1, 144 35.0 vs 33.8, 160 35.6 vs 33.8, 192 38.5-38.8 vs
-// 34.0-34.6.  So the inline form pays only while every SIMD holds at most 2 of the window's waves:
-// 256 CUs x 4 SIMDs x 2 waves x 64 lanes = 131072 agents (one 1024-wide row more puts a third
-// 165-VGPR wave on some SIMDs, and the kernel ends with the most loaded one).
-#ifndef CBF_INLINE_MAX
-#define CBF_INLINE_MAX 131072
-#endif
-#define CBF_HARD_COOP (CBF_HARD_MODE == 1)
-#if CBF_HARD_COOP
-static_assert(kHitCap >= 16, "the cooperative solve stages 8 doubles in each lane's hit-list column");
-#endif
+// Where the QPs that solve_fast cannot settle are solved: windows of at most
+// cbf_params.solve_inline_max agents (a runtime setting; < 0 = kSolveInlineDefault) run the filter
+// instantiation with the full solve inline (IN = true: no queue kernel); larger ones queue the QPs
+// with their assembled state for k_lattice_filter_hard, one lane per QP.  Measured crossover
+// (cbf_lattice_run, W = 1024, spacing 0.145, run(10) per timestep, inline vs queue): 64 rows 25.2 vs
+// 30.2 us, 128 rows 27.7 vs 32.6 us, 256 rows 42.5 vs 38.9 us, 512 rows 55 vs 55 (and the inline
+// form at 1024 rows 118.5 vs 79.5).  Between 128 and 192 rows (tools/records/gpu_r03g2.sh): 128 rows
+// 27.8-27.9 vs 32.5-32.7, 136 rows 34.2 vs 32.9-33.1, 144 35.0 vs 33.8, 160 35.6 vs 33.8, 192
+// 38.5-38.8 vs 34.0-34.6.  So the inline form pays only while every SIMD holds at most 2 of the
+// window's waves: 256 CUs x 4 SIMDs x 2 waves x 64 lanes = 131072 agents (one 1024-wide row more
+// puts a third 165-VGPR wave on some SIMDs, and the kernel ends with the most loaded one).  The two
+// placements are bit-identical (tests run both).  The wave-cooperative solves measured slower in
+// either place; their code is on branch exp/coop-solve-variants.
+constexpr long kSolveInlineDefault = 131072;
+inline bool solve_inline(const cbf_params* p, long n) {
+    return n <= (p->solve_inline_max < 0 ? kSolveInlineDefault : (long)p->solve_inline_max);
+}
 
 // Outputs of one owned ego (output index k) once its QP is solved (or it has no neighbour):
 // clip, Euler, stores, statistics record.
@@ -491,11 +479,10 @@ __device__ __forceinline__ void ego_output(const KP& P, const Ego& E, const Sol&
 
 // Tail of the lattice filter for one owned ego (output index k) whose QP rows are accumulated in
 // E: solve in place when solve_fast can (origin, or one Seidel event that stays put); otherwise
-// run the full solve_ego right here (IN: the small-window instantiation, below), return false
-// (CBF_HARD_COOP: the wave solves it cooperatively) or queue it to the hard kernel (sub-queue q:
-// header hardq, records qr).  Then clip, Euler, outputs.
+// run the full solve_ego right here (IN: the small-window instantiation, below) or queue it to the
+// hard kernel (sub-queue q: header hardq, records qr).  Then clip, Euler, outputs.
 template <bool FZ, bool ST, bool IN>
-__device__ __forceinline__ bool ego_finish(const KP& P, Ego& E, int w, int k, int slot, double T,
+__device__ __forceinline__ void ego_finish(const KP& P, Ego& E, int w, int k, int slot, double T,
                                            double2* __restrict__ pos_out, double2* __restrict__ u,
                                            int32_t* __restrict__ status, int32_t* __restrict__ cnt,
                                            int32_t* __restrict__ hardq, int q, HardRec* __restrict__ qr,
@@ -507,11 +494,8 @@ __device__ __forceinline__ bool ego_finish(const KP& P, Ego& E, int w, int k, in
         if (IN) {
             S = solve_ego(P, E);
             ego_output<ST>(P, E, S, false, k, T, pos_out, u, status, cnt, O);
-            return true;
+            return;
         }
-#if CBF_HARD_COOP
-        return false;
-#else
         HardRec& h = qr[subq_append(hardq, q)];
         h.r0 = E.r0;
         h.r1 = E.r1;
@@ -529,11 +513,9 @@ __device__ __forceinline__ bool ego_finish(const KP& P, Ego& E, int w, int k, in
         h.row = w;
         h.slot = slot;
         O.res = 2;
-        return true;
-#endif
+        return;
     }
     ego_output<ST>(P, E, S, idle, k, T, pos_out, u, status, cnt, O);
-    return true;
 }
 
 // Lattice step K4 for one cell-sorted slot: 3x3-cell cull (the three cell rows scanned as one
@@ -541,10 +523,9 @@ __device__ __forceinline__ bool ego_finish(const KP& P, Ego& E, int w, int k, in
 // divergent lanes do not pay assembly for every candidate iteration of the wave), then the tail.
 // Rows are assembled as row_g and the quadrant terms added per quadrant (row_g's note); an ego
 // whose quadrant terms are not all finite, or whose hit list overflowed, is assembled row by row
-// with row_b (scan_range_direct).  Returns false when the ego's QP is left to the wave's
-// cooperative solve (E holds it).
+// with row_b (scan_range_direct).
 template <bool FZ, bool ST, bool IN>
-__device__ __forceinline__ bool lattice_ego(const KP& P, const CellGrid& G, const WinBounds& B, int slot,
+__device__ __forceinline__ void lattice_ego(const KP& P, const CellGrid& G, const WinBounds& B, int slot,
                                             const double2* __restrict__ spos, const double2* __restrict__ svel,
                                             const int32_t* __restrict__ sidx, const int32_t* __restrict__ start,
                                             double T, double2* __restrict__ pos_out, double2* __restrict__ u,
@@ -553,7 +534,7 @@ __device__ __forceinline__ bool lattice_ego(const KP& P, const CellGrid& G, cons
                                             int* hit_lds, Ego& E, EgoOut& O) {
     const int w = sidx[slot];
     O.w = w;
-    if (!(w >= B.own_lo && w < B.own_hi)) return true;
+    if (!(w >= B.own_lo && w < B.own_hi)) return;
     const double2 pe = ld_slot(spos, slot), ve = ld_slot(svel, slot);
     ego_init(P, E, pe.x, pe.y, ve.x, ve.y, ve.x, ve.y);
     const int cx = cell_coord(pe.x, G.x0, G.inv_h, G.nx);
@@ -587,91 +568,12 @@ __device__ __forceinline__ bool lattice_ego(const KP& P, const CellGrid& G, cons
     }
     O.nbrs = E.count;
     if (ST) O.d2 = d2;
-    return ego_finish<FZ, ST, IN>(P, E, w, w - B.own_lo, slot, T, pos_out, u, status, cnt, hardq, q, qr, O);
-}
-
-// The wave's QPs that solve_fast could not settle (lanes with `need`), solved by coop_solve_ego
-// in passes of up to 8 (lane group g takes the pass's g-th of them), then their outputs.  Before
-// the first pass every such lane stages its 8 plane rhs in its own (dead, flushed) hit-list LDS
-// column (slot s in rows 2s, 2s + 1 as two 32-bit halves), from which the lanes of the group that
-// solves it read their slot; the ego's registers are then free during the solve, and the state the
-// outputs need is reloaded from the sorted copies afterwards.  Every lane of the wave must call it.
-template <bool ST>
-__device__ __forceinline__ void wave_coop_finish(const KP& P, const Ego& E, bool need, const WinBounds& B, double T,
-                                                 int* hit_lds, int slot, const double2* __restrict__ spos,
-                                                 const double2* __restrict__ svel, double2* __restrict__ pos_out,
-                                                 double2* __restrict__ u, int32_t* __restrict__ status,
-                                                 int32_t* __restrict__ cnt, EgoOut& O) {
-    unsigned long long hard = __ballot(need);
-    if (!hard) return;
-    const int lane = threadIdx.x & 63, g = lane >> 3, gl = lane & 7, wbase = threadIdx.x & ~63;
-    const unsigned long long below = (1ull << lane) - 1ull;
-    const unsigned present = E.present;
-    if (need) {
-        const Box Bx = box_rhs(P, E);
-        const double bs[8] = {pmin(Bx.S[0], Bx.S[4]), pmin(Bx.S[1], Bx.S[6]), pmin(Bx.S[2], Bx.S[5]),
-                              pmin(Bx.S[3], Bx.S[7]), E.bq0, E.bq1, E.bq2, E.bq3};
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            const unsigned long long v = (unsigned long long)__double_as_longlong(bs[k]);
-            hit_lds[(2 * k) * kBlock + threadIdx.x] = (int)(unsigned)v;
-            hit_lds[(2 * k + 1) * kBlock + threadIdx.x] = (int)(unsigned)(v >> 32);
-        }
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    Sol S;
-    S.x0 = S.x1 = 0.0;
-    S.status = CBF_STATUS_OPTIMAL;
-    S.iters = 0;
-    S.viol = S.viol_orig = 0.0;
-    while (hard) {
-        unsigned long long m = hard;
-        for (int i = 0; i < g && m; ++i) m &= m - 1;   // the g-th QP of this pass
-        const bool act = m != 0;
-        const int src = act ? __ffsll((long long)m) - 1 : 0;
-        const unsigned pres = (unsigned)__shfl((int)present, src, 64);
-        double bs = 0.0;
-        if (act) {
-            const unsigned lo = (unsigned)hit_lds[(2 * gl) * kBlock + wbase + src];
-            const unsigned hi = (unsigned)hit_lds[(2 * gl + 1) * kBlock + wbase + src];
-            bs = __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
-        }
-        const Sol Sg = coop_solve_ego(P, bs, act ? (0xFu | (pres << 4)) : 0u, act);
-        // the owner of group r's QP: the r-th lane of this pass takes group r's result
-        const int rank = __popcll(hard & below);
-        const int from = (rank < 8 ? rank : 7) * 8;
-        const double x0 = __shfl(Sg.x0, from, 64), x1 = __shfl(Sg.x1, from, 64);
-        const int stc = __shfl(Sg.status, from, 64), it = __shfl(Sg.iters, from, 64);
-        const double vi = __shfl(Sg.viol, from, 64), vo = __shfl(Sg.viol_orig, from, 64);
-        if (need && rank < 8) {
-            S.x0 = x0;
-            S.x1 = x1;
-            S.status = stc;
-            S.iters = it;
-            S.viol = vi;
-            S.viol_orig = vo;
-            need = false;
-        }
-        for (int i = 0; i < 8 && hard; ++i) hard &= hard - 1;
-    }
-    if (O.seidel && O.res == 0 && O.w >= B.own_lo && O.w < B.own_hi) {
-        const double2 pe = ld_slot(spos, slot), ve = ld_slot(svel, slot);
-        Ego Eo;
-        Eo.r0 = pe.x;
-        Eo.r1 = pe.y;
-        Eo.u0x = ve.x;
-        Eo.u0y = ve.y;
-        Eo.count = O.nbrs;
-        ego_output<ST>(P, Eo, S, false, O.w - B.own_lo, T, pos_out, u, status, cnt, O);
-    }
+    ego_finish<FZ, ST, IN>(P, E, w, w - B.own_lo, slot, T, pos_out, u, status, cnt, hardq, q, qr, O);
 }
 
 // K4: one lane per cell-sorted slot; QPs that solve_fast settles (the origin, or one Seidel event
-// that stays put) are finished in place.  The others (CBF_HARD_COOP) are solved by the wave
-// cooperatively after every lane's scan (wave_coop_finish), or (round 2's form) appended with
-// their assembled state to the hard queue for K5.
+// that stays put) are finished in place.  The others are solved right there by solve_ego (IN, the
+// small-window instantiation) or appended with their assembled state to the hard queue for K5.
 template <bool FZ, bool ST, bool IN>
 __global__ void __launch_bounds__(kBlock) k_lattice_filter(KP P, CellGrid G, WinBounds B, int W, int row_begin,
                                                            int row_end, int win_row0, long nwin, long ncell,
@@ -690,7 +592,7 @@ __global__ void __launch_bounds__(kBlock) k_lattice_filter(KP P, CellGrid G, Win
     __shared__ int hit_lds[kHitCap * kBlock + 8 * kBlock];
     const int bx = xcd_block();
     const int slot = bx * kBlock + threadIdx.x;
-    if (IN || CBF_HARD_COOP) {
+    if (IN) {
         // no queue kernel follows: a chained advance starts the next build's scan epoch here (an
         // error flag of this build stays set, so the rest of the run reports it; the scan reads the
         // epoch only after this kernel), and the last block refreshes the statistics snapshot
@@ -718,15 +620,9 @@ __global__ void __launch_bounds__(kBlock) k_lattice_filter(KP P, CellGrid G, Win
     O.viol = O.vorig = 0.0;
     O.d2 = INFINITY;
     Ego E;
-    bool done = true;
-    if (slot < total)
-        done = lattice_ego<FZ, ST, IN>(P, G, B, slot, spos, svel, sidx, start, T, pos_out, u, status, cnt, hardq,
-                                       bx % kSubQ, qrec + (long)(bx % kSubQ) * qcap, hit_lds, E, O);
-#if CBF_HARD_COOP
-    wave_coop_finish<ST>(P, E, !done, B, T, hit_lds, slot, spos, svel, pos_out, u, status, cnt, O);
-#else
-    (void)done;  // queued (O.res == 2) or finished
-#endif
+    if (slot < total)  // finished (O.res == 1) or queued (O.res == 2)
+        lattice_ego<FZ, ST, IN>(P, G, B, slot, spos, svel, sidx, start, T, pos_out, u, status, cnt, hardq,
+                                bx % kSubQ, qrec + (long)(bx % kSubQ) * qcap, hit_lds, E, O);
     if (ext_part && O.res == 1) ext_accumulate_w(O.w, B, O.ny, e0, e1, e2, e3);
     if (C.bcs) {  // chained binning: the next build's record of this agent (queued egos: K5)
         // indexed by this advance's slot (the next scatter then reads its records in cell order and
@@ -806,73 +702,6 @@ __global__ void __launch_bounds__(64) k_lattice_filter_hard(KP P, CellGrid G, Wi
             C.bcs[h.slot] = comp ? make_int3(cell, atomicAdd(&C.count[cell], 1), wn) : make_int3(-1, 0, wn);
         }
         if (h.row >= B.cnt_lo && h.row < B.cnt_hi) {
-            n_bnd += (S.x0 != 0.0 || S.x1 != 0.0) ? 1 : 0;
-            if (S.status == CBF_STATUS_OPTIMAL) {
-                ++n_opt;
-                vo = pmax(vo, S.viol);
-            } else if (S.status == CBF_STATUS_RELAXED) {
-                ++n_rel;
-                vr = pmax(vr, S.viol_orig);
-            } else {
-                ++n_inf;
-            }
-        }
-    });
-    if (stats) wave_stats_counts(stats, blockIdx.x, n_opt, n_rel, n_inf, n_bnd, vo, vr);
-    if (ext_part) wave_extents(e0, e1, e2, e3, ext_part, blockIdx.x);
-}
-
-// K5, cooperative form: the queued hard QPs solved by coop_solve_ego, lane group g of a wave on
-// one entry per pass (8 per wave), the sub-queues drained by drain_subq_groups.  Group lane 0
-// finishes its entry as k_lattice_filter_hard does (clip, Euler, outputs, chained binning,
-// statistics).
-__global__ void __launch_bounds__(64) k_lattice_filter_hard_coop(KP P, CellGrid G, WinBounds B, double T,
-                                                                 double2* __restrict__ pos_out,
-                                                                 double2* __restrict__ u, int32_t* __restrict__ status,
-                                                                 int32_t* __restrict__ cnt,
-                                                                 double* __restrict__ ext_part,
-                                                                 unsigned long long* __restrict__ stats,
-                                                                 int32_t* __restrict__ hardq,
-                                                                 const HardRec* __restrict__ qrec, long qcap,
-                                                                 ChainSpec C, const int32_t* __restrict__ sctl) {
-    if (C.bcs && blockIdx.x == 0 && threadIdx.x == 0) {
-        C.sctl[1] = (C.sctl[1] + 1) & 0x3FFFFFFF;
-        if (C.sctl != sctl) C.sctl[2] = sctl[2];
-    }
-    if (stats && blockIdx.x == gridDim.x - 1) stat_snapshot(stats);
-    double e0 = INFINITY, e1 = -INFINITY, e2 = -INFINITY, e3 = INFINITY;
-    int n_opt = 0, n_rel = 0, n_inf = 0, n_bnd = 0;
-    double vo = 0.0, vr = 0.0;
-    const int gl = threadIdx.x & 7;
-    drain_subq_groups(hardq, kHardPerQ, [&](int q, int i, bool act) {
-        const HardRec* h = qrec + (long)q * qcap + (act ? i : 0);
-        const double u0x = h->u0x, u0y = h->u0y, r2 = h->r2, r3 = h->r3;
-        const double bq = gl == 4 ? h->bq0 : gl == 5 ? h->bq1 : gl == 6 ? h->bq2 : h->bq3;
-        const unsigned pres = (unsigned)h->present;
-        const double bs = ego_slot_b(P, u0x, u0y, r2, r3, bq, bq, bq, bq, gl);
-        const Sol S = coop_solve_ego<true>(P, bs, act ? (0xFu | (pres << 4)) : 0u, act);
-        if (!act || gl != 0) return;
-        Ego E;
-        E.r0 = h->r0;
-        E.r1 = h->r1;
-        E.u0x = u0x;
-        E.u0y = u0y;
-        double ux, uy;
-        clip_u(P, S, E, ux, uy);
-        const int k = h->k, row = h->row, slot = h->slot;
-        const double2 pn = make_double2(E.r0 + T * ux, E.r1 + T * uy);
-        pos_out[k] = pn;
-        if (u) u[k] = make_double2(ux, uy);
-        if (status) status[k] = pack_status(S);
-        if (cnt) cnt[k] = h->count;
-        ext_accumulate_w(row, B, pn.y, e0, e1, e2, e3);
-        if (C.bcs) {
-            const int wn = row - C.shift;
-            const bool comp = wn >= C.comp_lo && wn < C.comp_hi;
-            const int cell = comp ? cell_of(G, pn.x, pn.y) : -1;
-            C.bcs[slot] = comp ? make_int3(cell, atomicAdd(&C.count[cell], 1), wn) : make_int3(-1, 0, wn);
-        }
-        if (row >= B.cnt_lo && row < B.cnt_hi) {
             n_bnd += (S.x0 != 0.0 || S.x1 != 0.0) ? 1 : 0;
             if (S.status == CBF_STATUS_OPTIMAL) {
                 ++n_opt;
@@ -1105,9 +934,7 @@ static int lattice_advance(const cbf_params* p, const cbf_grid* grid, int32_t W,
     CellWs Wk(workspace, n, (long)G.nx * G.ny);
     double* ext_part = extents ? (double*)((char*)workspace + CellWs::bytes(n, Wk.ncell)) : nullptr;
     const int nb = nblk(n);
-#if !CBF_HARD_COOP
     const int hb = lattice_hard_blocks(n);
-#endif
     const KP kp = make_kp(p);
     double2* po = reinterpret_cast<double2*>(pos_out);
     double2* uo = reinterpret_cast<double2*>(u);
@@ -1117,7 +944,7 @@ static int lattice_advance(const cbf_params* p, const cbf_grid* grid, int32_t W,
     // small windows (a few waves per SIMD, e.g. one stripe of a strong-scaled swarm): the
     // instantiation that runs the full solve in the filter itself -- its registers would halve the
     // big filter's occupancy, but a small window never fills the chip anyway -- and no queue kernel
-    const bool in = !CBF_HARD_COOP && n <= CBF_INLINE_MAX;
+    const bool in = solve_inline(p, n);
     const auto filter =
         in ? (st ? (p->f_is_zero ? k_lattice_filter<true, true, true> : k_lattice_filter<false, true, true>)
                  : (p->f_is_zero ? k_lattice_filter<true, false, true> : k_lattice_filter<false, false, true>))
@@ -1129,19 +956,15 @@ static int lattice_advance(const cbf_params* p, const cbf_grid* grid, int32_t W,
                        chain ? *chain : ChainSpec{});
     if (filter_done)
         if (hipError_t e = hipEventRecord(filter_done, s)) return (int)e;
-#if CBF_HARD_COOP
-    if (extents) launch_extents_finalize((int)lattice_ext_waves(n), ext_part, extents, s);
-#else
     if (in) {
         if (extents) launch_extents_finalize((int)lattice_ext_waves(n), ext_part, extents, s);
         return (int)hipGetLastError();
     }
-    hipLaunchKernelGGL(CBF_HARD_MODE == 2 ? k_lattice_filter_hard_coop : k_lattice_filter_hard, dim3(hb), dim3(64), 0, s,
+    hipLaunchKernelGGL(k_lattice_filter_hard, dim3(hb), dim3(64), 0, s,
                        kp, G, B, T, po, uo, status, nbr_count,
                        ext_part ? ext_part + 4l * lattice_ext_waves(n) : nullptr, st, Wk.hardq, Wk.qrec, Wk.qcap,
                        chain ? *chain : ChainSpec{}, Wk.sctl);
     if (extents) launch_extents_finalize((int)lattice_ext_waves(n) + hb, ext_part, extents, s);
-#endif
     return (int)hipGetLastError();
 }
 

@@ -26,9 +26,28 @@ class FilterParams:
     safety_distance: float = 0.2         # cross_and_rescue.py:134
     f: np.ndarray = field(default_factory=lambda: np.zeros((4, 4)))                                  # :31
     g: np.ndarray = field(default_factory=lambda: 0.1 * np.array([[1, 0], [0, 1], [0, 0], [0, 0]]))  # :32
+    # lattice steps only: where the QPs that neither the origin nor one projection settles are solved
+    # (cbf_params.solve_inline_max): "auto" (inline in the filter for windows of <= 131072 agents,
+    # queued for the second kernel above), "inline" (always in the filter), "queued" (always the
+    # queue kernel), or an int threshold.  Results are bit-identical; only the speed differs.
+    solve_placement: object = "auto"
 
     def c(self):
-        return _lib.make_params(self.max_speed, self.dmin, self.k, self.f, self.g, self.safety_distance)
+        p = _lib.make_params(self.max_speed, self.dmin, self.k, self.f, self.g, self.safety_distance)
+        p.solve_inline_max = solve_inline_max(self.solve_placement)
+        return p
+
+
+def solve_inline_max(placement) -> int:
+    """cbf_params.solve_inline_max for a FilterParams.solve_placement value."""
+    if isinstance(placement, (int, np.integer)) and not isinstance(placement, bool):
+        if not 0 <= int(placement) < 2 ** 31:
+            raise ValueError(f"solve_placement threshold out of range: {placement}")
+        return int(placement)
+    table = {"auto": -1, "inline": 2 ** 31 - 1, "queued": 0}
+    if placement not in table:
+        raise ValueError(f"solve_placement must be 'auto', 'inline', 'queued' or an int, got {placement!r}")
+    return table[placement]
 
 
 def make_grid(xmin, ymin, xmax, ymax, cell):
@@ -444,13 +463,18 @@ class LatticeSwarm:
         import json
         torch = _lib.require_gpu()
         torch.cuda.synchronize()
-        meta = {"W": self.W, "H": self.H, "gain": self.gain, "T": self.T, "method": self.method,
+        # what the opaque workspace bytes mean: a library with another ABI, workspace layout or size
+        # must not restore them (from_checkpoint refuses)
+        meta = {"abi_version": int(lib.cbf_abi_version()), "workspace_layout": int(lib.cbf_workspace_layout()),
+                "ws_bytes": int(self.ws_bytes),
+                "W": self.W, "H": self.H, "gain": self.gain, "T": self.T, "method": self.method,
                 "barrier": self.barrier, "alpha": list(self.alpha), "nominal": self.nominal,
                 "grid": [self.grid.x0, self.grid.y0, self.grid.inv_h, self.grid.nx, self.grid.ny],
                 "params": {"max_speed": self.params.max_speed, "dmin": self.params.dmin, "k": self.params.k,
                            "safety_distance": self.params.safety_distance,
                            "f": np.asarray(self.params.f, dtype=np.float64).tolist(),
-                           "g": np.asarray(self.params.g, dtype=np.float64).tolist()}}
+                           "g": np.asarray(self.params.g, dtype=np.float64).tolist(),
+                           "solve_placement": self.params.solve_placement}}
         arrays = {f"state{i}": t.cpu().numpy() for i, t in enumerate(self._state())}
         arrays["meta"] = np.frombuffer(json.dumps(meta).encode(), dtype=np.uint8)
         with open(path, "wb") as f:
@@ -464,9 +488,14 @@ class LatticeSwarm:
         with np.load(path, allow_pickle=False) as z:
             meta = json.loads(bytes(z["meta"]).decode())
             states = [z[f"state{i}"] for i in range(8)]
+        for key, have in (("abi_version", lib.cbf_abi_version()), ("workspace_layout", lib.cbf_workspace_layout())):
+            if meta.get(key) != have:
+                raise ValueError(f"checkpoint {path}: written with {key} {meta.get(key)}, this library has {have}: "
+                                 "its workspace bytes cannot be restored")
         pr = meta["params"]
         params = FilterParams(max_speed=pr["max_speed"], dmin=pr["dmin"], k=pr["k"],
-                              safety_distance=pr["safety_distance"], f=np.array(pr["f"]), g=np.array(pr["g"]))
+                              safety_distance=pr["safety_distance"], f=np.array(pr["f"]), g=np.array(pr["g"]),
+                              solve_placement=pr.get("solve_placement", "auto"))
         g = CbfGrid()
         g.x0, g.y0, g.inv_h = (float(v) for v in meta["grid"][:3])
         g.nx, g.ny = int(meta["grid"][3]), int(meta["grid"][4])
@@ -474,9 +503,13 @@ class LatticeSwarm:
         S = cls(states[0], meta["W"], meta["H"], gain=meta["gain"], params=params, T=meta["T"], grid=g,
                 method=meta["method"], barrier=meta["barrier"], alpha=tuple(meta["alpha"]),
                 nominal=tuple(nominal) if isinstance(nominal, list) else nominal)
-        for t, a in zip(S._state(), states):
+        if meta.get("ws_bytes") != S.ws_bytes:
+            raise ValueError(f"checkpoint {path}: workspace of {meta.get('ws_bytes')} bytes, this swarm's is "
+                             f"{S.ws_bytes}")
+        for i, (t, a) in enumerate(zip(S._state(), states)):
             if tuple(t.shape) != a.shape or str(t.dtype).replace("torch.", "") != str(a.dtype):
-                raise ValueError(f"checkpoint {path}: a state array does not fit this swarm ({a.shape}, {a.dtype})")
+                raise ValueError(f"checkpoint {path}: state{i} does not fit this swarm ({a.shape}, {a.dtype} vs "
+                                 f"{tuple(t.shape)}, {t.dtype})")
             t.copy_(_lib.require_gpu().from_numpy(a))
         return S
 

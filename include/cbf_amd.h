@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define CBF_ABI_VERSION 3
+#define CBF_ABI_VERSION 4
 
 #define CBF_EINVAL (-1)
 
@@ -81,6 +81,13 @@ typedef struct cbf_params {
     double nrm[4][2]; /* derived: L_g = -hs_p @ g per sign quadrant q = (dx<0) | (dy<0)<<1 (cbf.py:56) */
     int32_t f_is_zero;/* derived */
     int32_t relax_cap;/* max +1 relaxations before CBF_STATUS_RELAX_CAP (default 65536) */
+    /* Lattice steps (cbf_lattice_*): where the QPs that neither the origin nor one projection settles
+     * are solved.  A window of at most solve_inline_max agents solves them inside the filter kernel;
+     * a larger one queues them for a second kernel (one lane per QP).  Results are bit-identical
+     * either way; only the speed differs.  < 0 (cbf_params_init's default): the library's own
+     * threshold, 131072 agents (2 waves per SIMD on 256 CUs); 0: always queue.  ABI 4. */
+    int32_t solve_inline_max;
+    int32_t reserved0;
 } cbf_params;
 
 /* Fill *p (host).  f16 / g8 may be NULL for the callers' f = 0, g = 0.1 [I2; 0]. */
@@ -460,6 +467,11 @@ int cbf_unicycle_advance(const cbf_unicycle_params* u, int32_t n, double* poses,
 
 /* ABI version of the loaded library (== CBF_ABI_VERSION). */
 int cbf_abi_version(void);
+
+/* Layout version of the lattice / cells workspaces (the control words, cell counts and starts, scan
+ * tile words, sorted copies and queues a workspace holds between calls).  A saved workspace (e.g. a
+ * rollout checkpoint) may be restored only into a library reporting the same version and size. */
+int cbf_workspace_layout(void);
 
 #ifdef __cplusplus
 }

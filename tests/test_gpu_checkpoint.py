@@ -36,15 +36,42 @@ def test_lattice_checkpoint_resumes_bit_identical(tmp_path, nominal, spacing):
     assert B.grid.nx == A.grid.nx and B.grid.inv_h == A.grid.inv_h and B.nominal == A.nominal
 
 
+def _tamper(tmp_path, path, name, fn):
+    with np.load(path, allow_pickle=False) as z:
+        arrays = {k: z[k] for k in z.files}
+    fn(arrays)
+    bad = str(tmp_path / f"bad_{name}.npz")
+    np.savez(bad, **arrays)
+    return bad
+
+
 def test_checkpoint_refuses_another_shape(tmp_path):
+    """from_checkpoint's own checks (not the constructor's): a truncated workspace array, a state
+    array of another dtype, and metadata from another workspace layout or ABI are refused with the
+    checkpoint's error."""
+    import json
     A = swarm.LatticeSwarm(scenarios.lattice(32, 32, seed=1), 32, 32)
     A.step()
     path = str(tmp_path / "ck.npz")
     A.save_checkpoint(path)
-    with np.load(path, allow_pickle=False) as z:
-        arrays = {k: z[k] for k in z.files}
-    arrays["state0"] = arrays["state0"][:-1]
-    bad = str(tmp_path / "bad.npz")
-    np.savez(bad, **arrays)
-    with pytest.raises(ValueError):
-        swarm.LatticeSwarm.from_checkpoint(bad)
+    B = swarm.LatticeSwarm.from_checkpoint(path)     # the untouched file loads
+    assert torch.equal(A.ws, B.ws)
+
+    def meta(**kw):
+        def f(arrays):
+            m = json.loads(bytes(arrays["meta"]).decode())
+            m.update(kw)
+            arrays["meta"] = np.frombuffer(json.dumps(m).encode(), dtype=np.uint8)
+        return f
+
+    def trunc(arrays):
+        arrays["state5"] = arrays["state5"][:-256]      # the workspace
+
+    def dtype(arrays):
+        arrays["state6"] = arrays["state6"].astype(np.float64)   # the statistics words
+    for name, fn, msg in (("ws", trunc, "state5"), ("dtype", dtype, "state6"),
+                          ("layout", meta(workspace_layout=-1), "workspace_layout"),
+                          ("abi", meta(abi_version=-1), "abi_version"),
+                          ("bytes", meta(ws_bytes=1), "workspace of 1 bytes")):
+        with pytest.raises(ValueError, match=msg):
+            swarm.LatticeSwarm.from_checkpoint(_tamper(tmp_path, path, name, fn))

@@ -94,6 +94,30 @@ def test_compat_get_safe_control(golden):
         c.get_safe_control(np.zeros(2), np.zeros((1, 2)), np.zeros((2, 2)), np.eye(2), [0.0, 0.0])
 
 
+def test_compat_get_safe_control_sizes_and_threads():
+    """get_safe_control's per-instance pinned buffers: no obstacle (m = 0), more than the initial
+    64 obstacles (the buffers grow), and 8 threads sharing one instance (a lock keeps the call
+    reentrant) -- every answer equal to the oracle's."""
+    c = cbf_amd.ControlBarrierFunction(15)
+    rng = np.random.default_rng(44)
+    p = po.Params(15)
+    cases = []
+    for m in (0, 3, 65, 200, 1):
+        r = np.concatenate([rng.uniform(-1, 1, 2), rng.normal(0, 0.3, 2)])
+        obs = np.concatenate([r[:2] + rng.uniform(-0.3, 0.3, (m, 2)), rng.normal(0, 0.3, (m, 2))], axis=1)
+        cases.append((r, obs, rng.normal(0, 1.0, 2)))
+    want = [coracle.filter_one(p, r, obs, u0)["u"] for r, obs, u0 in cases]
+    for (r, obs, u0), w in zip(cases, want):
+        assert np.array_equal(c.get_safe_control(r, obs, np.zeros((4, 4)), GX, u0), w)
+
+    def call(i):
+        r, obs, u0 = cases[i % len(cases)]
+        return i, c.get_safe_control(r, obs, np.zeros((4, 4)), GX, u0)
+    with cf.ThreadPoolExecutor(8) as ex:
+        for i, u in ex.map(call, range(80)):
+            assert np.array_equal(u, want[i % len(cases)]), i
+
+
 def _random_swarm(rng, n, n_obs, spread):
     pos = rng.uniform(-spread, spread, (n, 2))
     vel = rng.normal(0, 0.3, (n, 2))
@@ -249,14 +273,26 @@ def _check_stats(got, want):
     assert got["errors"] == 0
 
 
+# Both placements of the full QP solve (cbf_params.solve_inline_max): inline in the filter (what
+# the shipped library picks for windows of <= 131072 agents) and queued for k_lattice_filter_hard
+# (its pick above that: the path the 1 M-agent bench times).  Every lattice test against the oracle
+# runs both, so each is anchored to the oracle on its own.
+PLACEMENTS = ["inline", "queued"]
+
+
+def _fp(placement):
+    return swarm.FilterParams(solve_placement=placement)
+
+
+@pytest.mark.parametrize("placement", PLACEMENTS)
 @pytest.mark.parametrize("spacing", [scenarios.LATTICE_SPACING, 0.2])
-def test_lattice_step_vs_oracle(spacing):
+def test_lattice_step_vs_oracle(spacing, placement):
     """Fused lattice steps == oracle steps bit for bit, and the device rollout statistics (status
     counts, OPTIMAL-only and original-row violations, minimum neighbour distance) equal the same
     quantities restated from the oracle's outputs.  Spacing 0.2 is the feasible regime (cfg4f)."""
     W, H = 48, 40
     pos = scenarios.lattice(W, H, seed=5, spacing=spacing)
-    L = swarm.LatticeSwarm(pos, W, H, gain=0.25)
+    L = swarm.LatticeSwarm(pos, W, H, gain=0.25, params=_fp(placement))
     ref = pos.copy()
     outs = []
     for step in range(8):
@@ -276,14 +312,16 @@ def test_lattice_step_vs_oracle(spacing):
         assert want["optimal"] > 0.5 * want["solves"] and want["binding"] > 0.1 * want["solves"]
 
 
-def test_lattice_random_nominal_vs_oracle():
+@pytest.mark.parametrize("placement", PLACEMENTS)
+def test_lattice_random_nominal_vs_oracle(placement):
     """The random-walk nominal control (CBF_NOMINAL_RANDOM, the exact-QP regime cfg4r): fused
     steps == oracle steps bit for bit (nominal controls, controls, statuses, positions, rollout
     statistics); most QPs are feasible with a binding row; cbf_lattice_run (chained binning) and
     a hipGraph of run(4) give the same rollout."""
     W, H, amp, seed = 48, 40, 1.0, 3
     pos = scenarios.lattice(W, H, seed=5, spacing=0.22)
-    L = swarm.LatticeSwarm(pos, W, H, nominal=("random", amp, seed))
+    fp = _fp(placement)
+    L = swarm.LatticeSwarm(pos, W, H, nominal=("random", amp, seed), params=fp)
     ref = pos.copy()
     outs = []
     for step in range(8):
@@ -299,12 +337,12 @@ def test_lattice_random_nominal_vs_oracle():
     want = _oracle_stats(outs)
     _check_stats(L.stats_summary(), want)
     assert want["optimal"] > 0.6 * want["solves"] and want["binding"] > 0.4 * want["solves"]
-    B = swarm.LatticeSwarm(pos, W, H, nominal=("random", amp, seed))
+    B = swarm.LatticeSwarm(pos, W, H, nominal=("random", amp, seed), params=fp)
     B.run(3)
     B.run(5)
     for a, b in zip(_lattice_state(L), _lattice_state(B)):
         assert np.array_equal(a, b)
-    D = swarm.LatticeSwarm(pos, W, H, nominal=("random", amp, seed))
+    D = swarm.LatticeSwarm(pos, W, H, nominal=("random", amp, seed), params=fp)
     D.capture(steps=4)              # the capture's warm-up launch runs steps 1-4
     D.run(4)
     for a, b in zip(_lattice_state(L), _lattice_state(D)):
@@ -335,15 +373,18 @@ def _lattice_state(L):
         [np.array([st[k] for k in sorted(st)], dtype=object)]
 
 
+@pytest.mark.parametrize("placement", PLACEMENTS)
 @pytest.mark.parametrize("spacing", [scenarios.LATTICE_SPACING, 0.2])
-def test_lattice_run_matches_steps(spacing):
+def test_lattice_run_matches_steps(spacing, placement):
     """cbf_lattice_run (chained binning: each advance bins the next timestep) == the same number of
     cbf_lattice_step calls, bit for bit: positions, last-step outputs and every statistics word,
     in one call, split over calls, and replayed from a hipGraph of run(4).  The first 3 steps of
-    the reference run are also checked against the oracle, so the chain is anchored to it."""
+    the reference run are also checked against the oracle, so the chain is anchored to it.  With
+    the queued placement the chained binning of the queued egos runs in the queue kernel."""
     W, H = 256, 192
     pos = scenarios.lattice(W, H, seed=11, spacing=spacing)
-    A = swarm.LatticeSwarm(pos, W, H)
+    fp = _fp(placement)
+    A = swarm.LatticeSwarm(pos, W, H, params=fp)
     ref = pos.copy()
     states = {}
     for k in range(1, 17):
@@ -354,16 +395,16 @@ def test_lattice_run_matches_steps(spacing):
             assert np.array_equal(A.pos.cpu().numpy(), ref), k
         if k in (12, 16):
             states[k] = _lattice_state(A)
-    B = swarm.LatticeSwarm(pos, W, H)
+    B = swarm.LatticeSwarm(pos, W, H, params=fp)
     B.run(12)
     for a, b in zip(states[12], _lattice_state(B)):
         assert np.array_equal(a, b)
-    C = swarm.LatticeSwarm(pos, W, H)
+    C = swarm.LatticeSwarm(pos, W, H, params=fp)
     for n in (1, 5, 6):
         C.run(n)
     for a, b in zip(states[12], _lattice_state(C)):
         assert np.array_equal(a, b)
-    D = swarm.LatticeSwarm(pos, W, H)
+    D = swarm.LatticeSwarm(pos, W, H, params=fp)
     D.capture(steps=4)              # the capture's warm-up launch runs steps 1-4
     for _ in range(3):
         D.run(4)
@@ -372,7 +413,9 @@ def test_lattice_run_matches_steps(spacing):
     st = B.stats_summary()
     assert st["errors"] == 0 and st["solves"] > 0
     if spacing == 0.2:
-        assert st["seidel"] > 0      # the hard-QP kernel's chained binning is exercised
+        # full solves happen; queued, the queue kernel bins them for the next timestep (the chained
+        # binning of k_lattice_filter_hard), inline the filter does
+        assert st["seidel"] > 0
 
 
 def test_lattice_run_output_history():
@@ -405,17 +448,18 @@ def test_lattice_run_output_history():
     assert torch.equal(C.pos, B.pos) and torch.equal(C.u, B.history(5)[1][4])
 
 
+@pytest.mark.parametrize("placement", PLACEMENTS)
 @pytest.mark.parametrize("nominal", [None, ("random", 0.05, 3)])
-def test_lattice_stats_off_and_replay(nominal):
+def test_lattice_stats_off_and_replay(nominal, placement):
     """The bench's timed path: run() with stats=NULL (graphs of both modes captured) gives the same
     trajectory bit for bit as with the statistics on, and snapshot()/restore() makes the statistics
     replay repeat a stats-off rollout exactly (positions, outputs), with the replay's statistics
     equal to those of a stats-on rollout from the start (incl. the random-walk nominal state)."""
     W, H = 128, 96
     pos = scenarios.lattice(W, H, seed=5, spacing=0.2)
-    A = swarm.LatticeSwarm(pos, W, H, nominal=nominal)
+    A = swarm.LatticeSwarm(pos, W, H, nominal=nominal, params=_fp(placement))
     A.run(6)
-    B = swarm.LatticeSwarm(pos, W, H, nominal=nominal)
+    B = swarm.LatticeSwarm(pos, W, H, nominal=nominal, params=_fp(placement))
     B.collect_stats = False
     B.capture(steps=3)              # runs steps 1-3 (stats off)
     B.collect_stats = True
@@ -424,7 +468,7 @@ def test_lattice_stats_off_and_replay(nominal):
     torch.cuda.synchronize()
     assert torch.equal(A.pos, B.pos) and torch.equal(A.u, B.u) and torch.equal(A.status, B.status)
     snap = B.snapshot()
-    ref = swarm.LatticeSwarm(pos, W, H, nominal=nominal)
+    ref = swarm.LatticeSwarm(pos, W, H, nominal=nominal, params=_fp(placement))
     ref.run(6)
     ref.reset_solves()
     ref.run(8)                      # the statistics of steps 7-14 alone
@@ -859,43 +903,74 @@ def test_allpairs_spilled_variant_is_bit_identical():
     assert torch.equal(u, ref["u"]) and torch.equal(st, ref["status"]) and torch.equal(cnt, ref["nbr_count"])
 
 
-@pytest.mark.parametrize("variant", ["hardcoop1", "hardcoop2", "noinline"])
 @pytest.mark.parametrize("nominal", [None, ("random", 1.0, 5)])
-def test_full_solve_placements_are_bit_identical(variant, nominal):
-    """Every placement of the full solve of the QPs solve_fast cannot settle gives the same results
-    bit for bit over a chained rollout (positions, last-step controls and statuses, every statistics
-    word), on the consensus lattice at spacing 0.2 and on cfg4r's random walk (10 % of the QPs
-    through the full solve).  The shipped build solves this small window inside the filter, one
-    lane per QP (CBF_INLINE_MAX); the test builds (tests/_lib/libcbf_<variant>.so) queue it for the
-    one-lane queue kernel (noinline, the path of large windows), or run the wave-cooperative solve
-    (coop_solve_ego: 8 lanes per QP, ballots + shuffles) inside the filter (hardcoop1) or in the
-    queue kernel (hardcoop2)."""
-    import ctypes as C
-    import os
-    from cbf_amd import _lib
-    V = C.CDLL(os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", f"libcbf_{variant}.so"))
-    for name in ("cbf_lattice_run", "cbf_lattice_set_nominal"):
-        f = getattr(V, name)
-        f.restype, f.argtypes = _lib.SIGNATURES[name]
+def test_full_solve_placements_are_bit_identical(nominal):
+    """The two placements of the full solve of the QPs solve_fast cannot settle (inline in the
+    filter, queued for the one-lane queue kernel; cbf_params.solve_inline_max) and the automatic
+    pick give the same results bit for bit over a chained rollout (positions, last-step controls and
+    statuses, every statistics word), on the consensus lattice at spacing 0.2 and on cfg4r's random
+    walk (10 % of the QPs through the full solve)."""
     W, H, steps = 160, 128, 8
     pos = scenarios.lattice(W, H, seed=13, spacing=0.2 if nominal is None else 0.22)
-    A = swarm.LatticeSwarm(pos, W, H, nominal=nominal)
-    A.run(steps)
+    runs = {}
+    for placement in ("auto", "inline", "queued"):
+        A = swarm.LatticeSwarm(pos, W, H, nominal=nominal, params=_fp(placement))
+        A.run(steps)
+        runs[placement] = _lattice_state(A)
+        st = A.stats_summary()
+        assert st["seidel"] > 0 and st["errors"] == 0
+    for placement in ("inline", "queued"):
+        for a, b in zip(runs["auto"], runs[placement]):
+            assert np.array_equal(a, b), placement
+
+
+def _oracle_window_step(pos, W, H, gain, threads=16):
+    """One timestep of the whole W x H lattice by the C oracle, its egos split over `threads` ego
+    ranges (the O(N) reference cull per ego, cross_and_rescue.py:141-150, on the host's cores)."""
+    vel = coracle.consensus_lattice(W, H, 0, H, pos, gain)
+    p = po.Params(15)
+    bounds = np.linspace(0, W * H, threads + 1).astype(int)
+
+    def run(k):
+        return coracle.filter_swarm(p, pos, vel, 0, int(bounds[k]), int(bounds[k + 1]))
+    with cf.ThreadPoolExecutor(threads) as ex:
+        parts = list(ex.map(run, range(threads)))
+    out = {key: np.concatenate([q[key] for q in parts]) for key in ("u", "status", "cnt")}
+    return coracle.euler(pos, out["u"], 1 / 30), vel, out
+
+
+@pytest.mark.parametrize("placement", ["auto", "inline"])
+def test_large_window_run_vs_oracle_every_timestep(placement):
+    """The bench's timed path on a window above the inline threshold (1024 x 136 = 139,264 agents >
+    131,072): the shipped cbf_lattice_run with stats = NULL -- auto places the full solves in the
+    queue kernel, whose chained binning feeds the next timestep -- checked bit for bit against the
+    oracle at EVERY timestep (nominal control, filtered control, status, neighbour count, and the
+    positions they imply), through run(4, history=True) (every timestep's outputs stored) and a
+    plain run(4) (the bench's form: outputs of the last timestep only).  "inline" forces the other
+    placement on the same window."""
+    W, H, steps = 1024, 136, 4
+    pos = scenarios.lattice(W, H, seed=17)
+    fp = _fp(placement)
+    A = swarm.LatticeSwarm(pos, W, H, params=fp)
+    A.collect_stats = False
+    A.run(steps, history=True)
+    B = swarm.LatticeSwarm(pos, W, H, params=fp)
+    B.collect_stats = False
+    B.run(steps)
     torch.cuda.synchronize()
-    ws = torch.zeros_like(A.ws)
-    if nominal is not None:
-        assert V.cbf_lattice_set_nominal(_lib.ptr(ws), ws.numel(), 1, nominal[1], nominal[2],
-                                         _lib.stream_handle()) == 0
-    P = _t(pos)
-    vel, u = torch.empty_like(P), torch.empty_like(P)
-    st = torch.empty((W * H,), dtype=torch.int32, device="cuda")
-    cnt = torch.empty_like(st)
-    stats = torch.zeros(1024, dtype=torch.int64, device="cuda")
-    assert V.cbf_lattice_run(A.cp, C.byref(A.grid), W, H, _lib.ptr(P), A.gain, A.T, steps, _lib.ptr(vel), _lib.ptr(u),
-                             _lib.ptr(st), _lib.ptr(cnt), _lib.ptr(stats), _lib.ptr(ws), ws.numel(),
-                             _lib.stream_handle()) == 0
-    torch.cuda.synchronize()
-    assert torch.equal(P, A.pos) and torch.equal(u, A.u) and torch.equal(st, A.status)
-    assert torch.equal(vel, A.vel) and torch.equal(cnt, A.nbr_count)
-    got, want = _lib.decode_stats(stats.cpu().numpy()), A.stats_summary()
-    assert got == want and want["seidel"] > 0, (got, want)
+    hv, hu, hs, hc = (t.cpu().numpy() for t in A.history(steps))
+    ref = pos.copy()
+    for t in range(steps):
+        nxt, vel, out = _oracle_window_step(ref, W, H, scenarios.LATTICE_GAIN)
+        assert np.array_equal(hv[t], vel), t
+        assert np.array_equal(hu[t], out["u"]), t
+        assert np.array_equal(hs[t], out["status"]), t
+        assert np.array_equal(hc[t], out["cnt"]), t
+        ref = nxt
+    assert np.array_equal(A.pos.cpu().numpy(), ref)
+    assert np.array_equal(B.pos.cpu().numpy(), ref)
+    assert np.array_equal(B.u.cpu().numpy(), out["u"]) and np.array_equal(B.status.cpu().numpy(), out["status"])
+    # the window holds full solves (the queue kernel has work under "auto")
+    C = swarm.LatticeSwarm(pos, W, H, params=fp)
+    C.run(steps)
+    assert C.stats_summary()["seidel"] > 0

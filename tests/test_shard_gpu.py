@@ -25,9 +25,10 @@ def _free_port():
     return p
 
 
-def _worker(rank, ws, port, W, R, steps, q, k=4, graph=False, run=False, nominal=None, exchange="neighbour"):
+def _worker(rank, ws, port, W, R, steps, q, k=4, graph=False, run=False, nominal=None, exchange="neighbour",
+            placement="auto"):
     try:
-        _work(rank, ws, port, W, R, steps, q, k, graph, run, nominal, exchange)
+        _work(rank, ws, port, W, R, steps, q, k, graph, run, nominal, exchange, placement)
     except BaseException as e:   # report instead of leaving the test waiting on the queue
         q.put((rank, "error", repr(e)))
         raise
@@ -38,16 +39,18 @@ def _spacing(nominal):
     return scenarios.LATTICE_SPACING if nominal is None else 0.22   # random walk: the cfg4r spacing
 
 
-def _work(rank, ws, port, W, R, steps, q, k, graph, run, nominal, exchange):
+def _work(rank, ws, port, W, R, steps, q, k, graph, run, nominal, exchange, placement):
     import datetime
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     torch.cuda.set_device(0)
     dist.init_process_group("gloo", rank=rank, world_size=ws, timeout=datetime.timedelta(seconds=60))
     from cbf_amd.shard import ShardedLattice
+    from cbf_amd.swarm import FilterParams
     # the random walk's RELAXED QPs can move an agent up to T * max_speed = 0.5 per step (the
     # guard catches it with the default 4-row halo): 10 rows per sub-step cover it
     S = ShardedLattice(W, R, seed=7, substeps=k, nominal=nominal, spacing=_spacing(nominal),
-                       halo=4 if nominal is None else 10, exchange=exchange)
+                       halo=4 if nominal is None else 10, exchange=exchange,
+                       params=FilterParams(solve_placement=placement))
     if graph == "cycle":   # whole exchange cycles replayed as one hipGraph each
         S.capture_cycle()
     elif graph:
@@ -89,21 +92,26 @@ def _work(rank, ws, port, W, R, steps, q, k, graph, run, nominal, exchange):
 RANDOM = ("random", 1.0, 3)   # the random-walk nominal control (CBF_NOMINAL_RANDOM)
 
 
-@pytest.mark.parametrize("ws,k,graph,run,nominal,exchange", [
-    (2, 1, False, False, None, "neighbour"), (3, 4, False, False, None, "neighbour"),
-    (2, 4, True, False, None, "neighbour"), (3, 4, False, True, None, "neighbour"),
-    (2, 2, False, True, None, "neighbour"), (2, 4, "cycle", True, None, "neighbour"),
-    (2, 2, False, True, RANDOM, "neighbour"), (3, 4, False, "mixed", None, "neighbour"),
-    (2, 4, False, "replay", None, "neighbour"), (3, 4, "cycle", "replay", None, "neighbour"),
-    (4, 2, False, True, None, "neighbour"), (3, 4, False, True, None, "allgather")])
-def test_sharded_equals_single_gpu(ws, k, graph, run, nominal, exchange):
+# placement: where the full QP solves run (cbf_params.solve_inline_max).  These small windows pick
+# "inline" under "auto"; the "queued" cases run the queue kernel and its chained binning into the
+# next sub-step's workspace (the path of windows above 131,072 agents).
+@pytest.mark.parametrize("ws,k,graph,run,nominal,exchange,placement", [
+    (2, 1, False, False, None, "neighbour", "auto"), (3, 4, False, False, None, "neighbour", "auto"),
+    (2, 4, True, False, None, "neighbour", "auto"), (3, 4, False, True, None, "neighbour", "auto"),
+    (2, 2, False, True, None, "neighbour", "auto"), (2, 4, "cycle", True, None, "neighbour", "auto"),
+    (2, 2, False, True, RANDOM, "neighbour", "auto"), (3, 4, False, "mixed", None, "neighbour", "auto"),
+    (2, 4, False, "replay", None, "neighbour", "auto"), (3, 4, "cycle", "replay", None, "neighbour", "auto"),
+    (4, 2, False, True, None, "neighbour", "auto"), (3, 4, False, True, None, "allgather", "auto"),
+    (3, 4, False, True, None, "neighbour", "queued"), (2, 2, False, True, RANDOM, "neighbour", "queued"),
+    (3, 4, "cycle", "replay", None, "neighbour", "queued"), (2, 1, False, False, None, "neighbour", "queued")])
+def test_sharded_equals_single_gpu(ws, k, graph, run, nominal, exchange, placement):
     from cbf_amd import scenarios, swarm
     W, R, steps = 96, 40, 6
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, ws, port, W, R, steps, q, k, graph, run, nominal, exchange))
-             for r in range(ws)]
+    procs = [ctx.Process(target=_worker, args=(r, ws, port, W, R, steps, q, k, graph, run, nominal, exchange,
+                                               placement)) for r in range(ws)]
     for p in procs:
         p.start()
     res = sorted([q.get(timeout=120) for _ in range(ws)], key=lambda t: t[0])
@@ -130,7 +138,8 @@ def test_sharded_equals_single_gpu(ws, k, graph, run, nominal, exchange):
     assert sum(r[4]["solves"] for r in res) == solves
     assert sum(r[4]["optimal"] for r in res) == optimal and sum(r[4]["relaxed"] for r in res) == relaxed
     # and the single-GPU fused step of the whole lattice
-    L = swarm.LatticeSwarm(scenarios.lattice(W, H, seed=7, spacing=_spacing(nominal)), W, H, nominal=nominal)
+    L = swarm.LatticeSwarm(scenarios.lattice(W, H, seed=7, spacing=_spacing(nominal)), W, H, nominal=nominal,
+                           params=swarm.FilterParams(solve_placement=placement))
     for _ in range(steps):
         L.step()
     torch.cuda.synchronize()
