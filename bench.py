@@ -49,12 +49,33 @@ def _free_port():
     return port
 
 
-def launch_ranks(n, argv, timeout_s=None):
+def progress(msg):
+    """One progress line on stderr (the driver's liveness signal; under launch_ranks every rank's
+    stderr is relayed with a rank prefix).  Names the pid, so a rank can be found and signalled."""
+    ws, rank, _ = _dist_env()
+    sys.stderr.write(f"bench.py rank {rank}/{ws} (pid {os.getpid()}): {msg}\n")
+    sys.stderr.flush()
+
+
+def default_rank_timeout(args):
+    """Overall limit for launch_ranks: a fresh box's first `import torch` (1-2 min), communicator
+    set-up and graph captures, the timed steps and their statistics / per-step-output replays
+    (generously 25 ms per step at any size), and the collective timeout once more so that a rank
+    blocked in a collective has raised before the parent gives up on it."""
+    return 300 + 0.025 * 4 * (args.steps + args.warmup) + args.collective_timeout
+
+
+def launch_ranks(n, argv, timeout_s, grace_s=30.0):
     """--gpus N without a launcher: start N copies of this script as child processes, one rank
-    each (RANK = LOCAL_RANK = r, WORLD_SIZE = N, rendezvous on 127.0.0.1), and relay rank 0's
-    one JSON line.  This parent never touches the GPU.  If a rank fails, the others are given a
-    grace period (they may be blocked in a collective) and then terminated; the exit status is
-    non-zero whenever any rank failed."""
+    each (RANK = LOCAL_RANK = r, WORLD_SIZE = N, rendezvous on 127.0.0.1), relay every rank's
+    stderr (and any stdout but rank 0's JSON line) to this stderr with a "[rank r]" prefix, and
+    print rank 0's one JSON line.  This parent never touches the GPU.
+
+    Failure handling: the first rank to exit non-zero is named at once; the others get grace_s
+    seconds to finish or fail on their own (a peer blocked in a collective raises at the collective
+    timeout or when the connection drops), then are terminated and named.  After timeout_s seconds
+    overall every rank still running is terminated and named.  Any failure makes the exit status
+    non-zero (124 for the overall timeout)."""
     import threading
     port = _free_port()
     procs = []
@@ -62,36 +83,75 @@ def launch_ranks(n, argv, timeout_s=None):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
                    MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY="0")
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv, env=env,
-                                      stdout=subprocess.PIPE if r == 0 else subprocess.DEVNULL))
+                                      stdout=subprocess.PIPE, stderr=subprocess.PIPE))
     out = []
-    reader = threading.Thread(target=lambda: out.append(procs[0].stdout.read()), daemon=True)
-    reader.start()
+    lock = threading.Lock()
+
+    def relay(r, stream, keep):
+        for line in iter(stream.readline, b""):
+            if keep:
+                out.append(line)
+                continue
+            with lock:
+                sys.stderr.buffer.write(f"[rank {r}] ".encode() + line)
+                sys.stderr.flush()
+    threads = [threading.Thread(target=relay, args=(r, p.stdout, r == 0), daemon=True) for r, p in enumerate(procs)]
+    threads += [threading.Thread(target=relay, args=(r, p.stderr, False), daemon=True) for r, p in enumerate(procs)]
+    for t in threads:
+        t.start()
+
+    def note(msg):
+        with lock:
+            sys.stderr.write(f"bench.py (launcher): {msg}\n")
+            sys.stderr.flush()
+
+    def stop_running(why):
+        running = [r for r, p in enumerate(procs) if p.poll() is None]
+        if running:
+            note(f"terminating rank(s) {running} ({why})")
+        for r in running:
+            procs[r].terminate()
+        for r in running:
+            try:
+                procs[r].wait(timeout=20)
+            except subprocess.TimeoutExpired:
+                procs[r].kill()
+                procs[r].wait()
+        return running
+
     t0 = time.time()
-    failed_at = None
+    first_fail = None
+    killed, timed_out = [], False
     while any(p.poll() is None for p in procs):
-        if failed_at is None and any(p.poll() not in (None, 0) for p in procs):
-            failed_at = time.time()
-        if (failed_at is not None and time.time() - failed_at > 60) or \
-                (timeout_s is not None and time.time() - t0 > timeout_s):
-            for p in procs:
-                if p.poll() is None:
-                    p.terminate()
-            for p in procs:
-                try:
-                    p.wait(timeout=20)
-                except subprocess.TimeoutExpired:
-                    p.kill()
-                    p.wait()
+        if first_fail is None:
+            bad = [(r, p.returncode) for r, p in enumerate(procs) if p.poll() not in (None, 0)]
+            if bad:
+                first_fail = (bad[0][0], bad[0][1], time.time())
+                code = bad[0][1]
+                how = f"signal {-code}" if code < 0 else f"exit code {code}"
+                note(f"rank {bad[0][0]} failed first ({how}); the other ranks get {grace_s:.0f} s")
+        if first_fail is not None and time.time() - first_fail[2] > grace_s:
+            killed = stop_running(f"rank {first_fail[0]} failed {grace_s:.0f} s ago")
             break
-        time.sleep(0.2)
-    reader.join(timeout=30)
+        if time.time() - t0 > timeout_s:
+            timed_out = True
+            killed = stop_running(f"overall limit of {timeout_s:.0f} s reached")
+            break
+        time.sleep(0.1)
+    for t in threads:
+        t.join(timeout=10)
     codes = [p.returncode for p in procs]
     if all(c == 0 for c in codes):
         sys.stdout.write(b"".join(out).decode())
         sys.stdout.flush()
         return 0
-    sys.stderr.write(f"bench.py: rank exit codes {codes}\n")
-    return next(c for c in codes if c != 0)
+    failed = [r for r, c in enumerate(codes) if c != 0 and r not in killed]
+    note(f"FAILED: rank exit codes {codes}; failed on their own: {failed}; terminated: {killed}"
+         + (f"; first failure: rank {first_fail[0]}" if first_fail else "")
+         + ("; overall time limit reached" if timed_out else ""))
+    if timed_out:
+        return 124
+    return next(c for c in codes if c != 0) if first_fail is None else (first_fail[1] if first_fail[1] > 0 else 1)
 
 
 def load_pmc(config):
@@ -261,6 +321,7 @@ def bench_lattice(args, ws, rank, local):
     else:
         pos = scenarios.lattice(W, rows, seed=args.seed, spacing=args.spacing)
         S = swarm.LatticeSwarm(pos, W, rows, gain=args.gain, barrier=args.barrier, nominal=args.nominal)
+    progress(f"{args.config}: {W}x{rows_total} lattice built ({rows} rows on this rank)")
     use_graph = not args.eager
     # single GPU, reference barrier: the timesteps run as cbf_lattice_run calls of `chunk`
     # timesteps (bit-identical to as many cbf_lattice_step calls; each advance bins the next
@@ -313,10 +374,12 @@ def bench_lattice(args, ws, rank, local):
             S.check_guard()
         S.restore(snap0)
         del snap0
+    progress(f"{args.config}: graphs captured; {args.warmup} warm-up steps")
     advance(args.warmup)
     torch.cuda.synchronize()
     snap = S.snapshot() if len(modes) > 1 else None
     S.reset_solves()
+    progress(f"{args.config}: timed region ({args.steps} steps)")
 
     def timed(history=False):
         if ws > 1:
@@ -341,6 +404,7 @@ def bench_lattice(args, ws, rank, local):
         return float(t[0])
 
     elapsed = max_over_ranks(timed())
+    progress(f"{args.config}: timed region done ({elapsed / args.steps * 1e6:.1f} us/step); replays")
     own = S.own if sharded else S.pos
     end_state = (own.clone(), S.u.clone(), S.status.clone())
     if ws > 1:
@@ -398,6 +462,24 @@ def bench_lattice(args, ws, rank, local):
         stat.update(viol_optimal=float(m[0]), viol_original_relaxed=float(m[1]),
                     min_dist2=None if not np.isfinite(m[2].item()) else -float(m[2]))
     safety = safety_report(stat, args.steps) if args.barrier == "reference" else None
+    exchange = None
+    if sharded:
+        # each rank's exchange (pack + collective + unpack with the guard), timed alone after the
+        # rollout, gathered to rank 0: the per-rank cost the strong-scaled step pays per timestep
+        ex = S.time_exchange(10)
+        keys = ("pack_us", "collective_us", "unpack_guard_us", "exchange_us", "exchange_us_per_timestep")
+        mine = torch.tensor([ex[k] for k in keys], dtype=torch.float64, device="cuda")
+        rows_all = [mine]
+        if ws > 1:
+            rows_all = [torch.empty_like(mine) for _ in range(ws)]
+            torch.distributed.all_gather(rows_all, mine)
+        per_rank = [dict(zip(keys, (float(v) for v in r.tolist()))) for r in rows_all]
+        exchange = {"per_rank": per_rank,
+                    "max_exchange_us_per_timestep": max(r["exchange_us_per_timestep"] for r in per_rank),
+                    "timesteps_per_exchange": k, "bytes_sent_per_rank": S.exchange_bytes(),
+                    "note": "pack + collective + unpack/guard, each closed by a device synchronize, mean of 10 "
+                            "exchanges timed after the rollout (state restored); the timed steps overlap none of "
+                            "it with compute, so it is part of ms_per_step"}
     comm = ("RCCL" if args.backend == "nccl" else "gloo (host-staged rehearsal)") if ws > 1 else "single-rank"
     # dominant kernel (filter + clip + Euler) timed alone with HIP events on the launch stream
     S.collect_stats = modes[0]  # as in the timed region
@@ -463,10 +545,12 @@ def bench_lattice(args, ws, rank, local):
                                       if args.exchange == "neighbour" else "all-gather of ghost-row slabs")
                                    + f" per {k} steps ({halo * k} ghost rows per side)") if sharded else "single GPU",
                    "exchange_bytes_per_rank": S.exchange_bytes() if sharded else 0,
+                   "solve_placement": "inline in the filter" if rows * W <= 131072 else "queued (k_lattice_filter_hard)",
                    "graph": use_graph,
                    "timesteps_per_call": max(plan) if chunk > 1 else 1},
         "timesteps_per_s": args.steps / elapsed,
         "solves_per_step": solves / args.steps,
+        "exchange": exchange,
         "feasible_fraction": safety["feasible_fraction"] if safety else None,
         "safety": safety,
         "full_size_check": check,
@@ -491,6 +575,29 @@ def bench_lattice(args, ws, rank, local):
                      "step_algorithmic_GBps": STEP_BYTES_PER_AGENT * n_local * args.steps / elapsed / 1e9 / ws},
     }
     return res
+
+
+def exact_qp_regime(args):
+    """cfg4r inside the default cfg4 line: the same 1M-agent lattice at spacing 0.22 with the
+    random-walk nominal control (CBF_NOMINAL_RANDOM), the same --steps / --warmup, its own timed
+    region -- the regime where most QPs are feasible with a binding row, i.e. where the reference
+    (cbf.py:75-92) defines the answer.  `value` stays cfg4's; this record is beside it."""
+    import copy
+    a = copy.copy(args)
+    a.config, a.spacing, a.nominal = "cfg4r", 0.22, ("random", 1.0, args.seed)
+    r = bench_lattice(a, 1, 0, 0)
+    sf = r["safety"]
+    return {"config": "cfg4r", "workload": r["config"]["workload"], "value": r["value"], "unit": r["unit"],
+            "ms_per_step": r["ms_per_step"], "ms_per_step_with_stats": r["ms_per_step_with_stats"],
+            "steps": a.steps, "warmup": a.warmup, "timesteps_per_s": r["timesteps_per_s"],
+            "feasible_fraction": sf["feasible_fraction"], "binding_fraction": sf["binding_fraction"],
+            "relaxed_fraction": sf["relaxed_fraction"], "seidel_fraction": sf["seidel_fraction"],
+            "max_violation_optimal": sf["max_violation_optimal"],
+            "full_size_check": r["full_size_check"], "end_state_sha256": r["end_state_sha256"],
+            "roofline": {k: r["roofline"][k] for k in ("bound", "achieved", "peak", "unit", "frac", "traffic",
+                                                          "kernel_ms", "advance_phase")},
+            "note": "the exact-QP regime timed by the same command (bench.py --config cfg4r alone gives the same "
+                    "line); no CPU baseline here (profiles/r0*_bench_cfg4r.json carry one)"}
 
 
 def bench_allpairs(args, ws, rank, local):
@@ -736,6 +843,8 @@ def main():
     ap.add_argument("--chunk", type=int, default=50,
                     help="timesteps per cbf_lattice_run call (single-GPU graph path; 1 = one cbf_lattice_step per step)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-exact-qp", action="store_true",
+                    help="cfg4 single GPU: skip the exact_qp_regime record (cfg4r timed beside the headline)")
     ap.add_argument("--barrier", default="reference", choices=["reference", "euclidean_hocbf"],
                     help="cfg4 single-GPU: the reference's L1 barrier rows or the Euclidean HOCBF mode")
     ap.add_argument("--cpu-budget", type=float, default=10.0, help="seconds per CPU-baseline process and shape")
@@ -750,6 +859,14 @@ def main():
     ap.add_argument("--substeps", type=int, default=None,
                     help="sharded cfg4: timesteps per halo exchange (default: min(16 for stripes of <= 512 rows, "
                          "else 8, rows per rank / (2 halo)))")
+    ap.add_argument("--rank-timeout", type=float, default=None,
+                    help="--gpus N without a launcher: overall seconds before the ranks still running are "
+                         "terminated and named (default: from --steps / --warmup and --collective-timeout)")
+    ap.add_argument("--rank-grace", type=float, default=30.0,
+                    help="--gpus N without a launcher: seconds the other ranks get after one fails")
+    ap.add_argument("--collective-timeout", type=float, default=300.0,
+                    help="N > 1: torch.distributed timeout (s) of every collective; a rank blocked on a dead "
+                         "peer raises after it")
     ap.add_argument("--shard", action="store_true",
                     help="cfg4: run the sharded step (halo pack + collective + unpack) even on one rank")
     args = ap.parse_args()
@@ -757,7 +874,9 @@ def main():
         raise SystemExit("bench.py: --gpus must be >= 1")
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         # no launcher: this process starts the ranks and relays rank 0's line (it never touches the GPU)
-        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:],
+                              args.rank_timeout if args.rank_timeout else default_rank_timeout(args),
+                              args.rank_grace))
     ws, rank, local = _dist_env()
     if ws != args.gpus:
         raise SystemExit(f"bench.py: WORLD_SIZE={ws} from the launcher but --gpus {args.gpus}")
@@ -780,11 +899,14 @@ def main():
         os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", str(_free_port()) if ws == 1 else "29533")
+        import datetime
+        tmo = datetime.timedelta(seconds=args.collective_timeout)
+        progress(f"init_process_group({args.backend}) on cuda:{dev}")
         if args.backend == "gloo":
-            torch.distributed.init_process_group("gloo", rank=rank, world_size=ws)
+            torch.distributed.init_process_group("gloo", rank=rank, world_size=ws, timeout=tmo)
         else:
             torch.distributed.init_process_group("nccl", device_id=torch.device("cuda", local), rank=rank,
-                                                 world_size=ws)
+                                                 world_size=ws, timeout=tmo)
     else:
         torch.cuda.set_device(0)
     if args.config == "cfg3":
@@ -797,10 +919,14 @@ def main():
         res = bench_cert(args, ws, rank, local)
     else:
         res = bench_lattice(args, ws, rank, local)
+        if args.config == "cfg4" and ws == 1 and not args.shard and args.barrier == "reference" and \
+                not args.no_exact_qp:
+            res["exact_qp_regime"] = exact_qp_regime(args)
     if rank == 0:
         sample = res.pop("_cert_sample", None)
         res["cpu_baseline"] = None
         if ws == 1 and not args.no_cpu_baseline:
+            progress("CPU baseline (oracle/, after the timed region)")
             res["cpu_baseline"] = cpu_baseline_for(args, sample)
         json_out.write(json.dumps(res) + "\n")
         json_out.flush()

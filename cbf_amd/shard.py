@@ -36,6 +36,7 @@ all-gathered once per timestep.
 from __future__ import annotations
 
 import math
+import time
 
 import numpy as np
 
@@ -331,6 +332,34 @@ class ShardedLattice:
         self._collective()
         self.be.unpack_guard(self)
         self.be.arm_guard_readback()
+
+    def time_exchange(self, reps=10):
+        """Wall time of this rank's exchange, split into its parts (µs per exchange, mean over reps):
+        pack (device), the collective (RCCL; gloo: incl. its host staging), unpack + guard (device),
+        each part closed by a device synchronize, every repetition opened by a barrier so that the
+        ranks start together.  Untimed diagnostics: the state is snapshot and restored around it."""
+        torch, dist = self.torch, self.dist
+        snap = self.snapshot()
+        parts = np.zeros(3)
+        for _ in range(reps):
+            dist.barrier(group=self.group)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            self.be.pack(self)
+            torch.cuda.synchronize()
+            t1 = time.perf_counter()
+            self._collective()
+            torch.cuda.synchronize()
+            t2 = time.perf_counter()
+            self.be.unpack_guard(self)
+            torch.cuda.synchronize()
+            t3 = time.perf_counter()
+            parts += (t1 - t0, t2 - t1, t3 - t2)
+        self.restore(snap)
+        us = parts / reps * 1e6
+        return {"pack_us": float(us[0]), "collective_us": float(us[1]), "unpack_guard_us": float(us[2]),
+                "exchange_us": float(us.sum()), "exchange_us_per_timestep": float(us.sum()) / self.k,
+                "timesteps_per_exchange": self.k, "bytes_sent": self.exchange_bytes()}
 
     def exchange_bytes(self):
         """Bytes this rank sends per exchange (rows + guard records, self excluded)."""

@@ -175,8 +175,17 @@ def run(kind, budget_s, procs=None, shape=None):
     procs = procs or cores
     args = [(kind, shape, r, procs, budget_s) for r in range(procs)]
     t0 = time.perf_counter()
-    with mp.get_context("spawn").Pool(procs) as pool:
+    # close + join (not the `with` block's terminate): the workers exit on their own, so no
+    # SIGTERM traces land in a profiler's log
+    pool = mp.get_context("spawn").Pool(procs)
+    try:
         res = pool.map(_worker, args)
+        pool.close()
+    except BaseException:
+        pool.terminate()
+        raise
+    finally:
+        pool.join()
     wall = time.perf_counter() - t0
     done = sum(r[0] for r in res)
     solves = sum(r[1] for r in res)

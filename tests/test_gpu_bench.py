@@ -69,3 +69,46 @@ def test_bench_gpus_n_rehearsal_matches_one_rank(n):
     assert many["config"]["agents_per_gpu"] == 256 * 256 // n
     assert many["end_state_sha256"] == one["end_state_sha256"]
     assert many["solves_per_step"] == one["solves_per_step"]
+
+
+@pytest.mark.gpu
+def test_bench_rank_failure_is_named_and_fails_fast():
+    """`bench.py --gpus 2` (gloo, one GPU) with rank 1 killed (SIGKILL) in its timed region: the
+    launcher names rank 1 as the first failure at once, relays every rank's stderr with a rank
+    prefix, and exits non-zero within the grace period instead of waiting on rank 0, which is left
+    blocked in (or failing out of) the next collective."""
+    import re
+    import signal
+    import time
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK")}
+    grace = 20
+    p = subprocess.Popen([sys.executable, os.path.join(ROOT, "bench.py"), "--width", "256", "--rows", "256",
+                          "--steps", "20000", "--warmup", "1", "--kernel-iters", "2", "--no-cpu-baseline",
+                          "--gpus", "2", "--backend", "gloo", "--rank-grace", str(grace),
+                          "--collective-timeout", "60"],
+                         cwd=ROOT, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+    seen, victim, t_kill = [], None, None
+    t0 = time.time()
+    try:
+        for line in p.stderr:
+            seen.append(line)
+            m = re.search(r"^\[rank 1\] bench\.py rank 1/2 \(pid (\d+)\): cfg4: timed region \(", line)
+            if m:
+                victim = int(m.group(1))
+                os.kill(victim, signal.SIGKILL)
+                t_kill = time.time()
+                break
+            if time.time() - t0 > 150:
+                break
+        assert victim is not None, "".join(seen)[-3000:]
+        out, err = p.communicate(timeout=grace + 90)
+    finally:
+        if p.poll() is None:
+            p.kill()
+            p.wait()
+    err = "".join(seen) + err
+    assert p.returncode != 0 and out.strip() == "", (p.returncode, out[-500:])
+    assert time.time() - t_kill < grace + 60
+    assert "rank 1 failed first (signal 9)" in err, err[-3000:]
+    assert "FAILED: rank exit codes" in err and "first failure: rank 1" in err, err[-3000:]
+    assert "[rank 0] bench.py rank 0/2" in err        # rank 0's stderr is relayed with its prefix
