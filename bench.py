@@ -138,6 +138,13 @@ def launch_ranks(n, argv, timeout_s, grace_s=30.0):
             killed = stop_running(f"overall limit of {timeout_s:.0f} s reached")
             break
         time.sleep(0.1)
+    if first_fail is None:
+        # every rank ended between two polls: name the failure(s) now
+        bad = [(r, p.returncode) for r, p in enumerate(procs) if p.returncode != 0]
+        if bad:
+            first_fail = (bad[0][0], bad[0][1], time.time())
+            how = f"signal {-bad[0][1]}" if bad[0][1] < 0 else f"exit code {bad[0][1]}"
+            note(f"rank {bad[0][0]} failed first ({how}; ranks {[r for r, _ in bad]} ended in the same poll)")
     for t in threads:
         t.join(timeout=10)
     codes = [p.returncode for p in procs]
@@ -894,7 +901,10 @@ def main():
     import torch
     if ws > 1 or args.shard:
         # (gloo: a rehearsal of several ranks on fewer GPUs, exchanges staged through the host)
-        dev = local % torch.cuda.device_count() if args.backend == "gloo" else local
+        ndev = torch.cuda.device_count()
+        if ndev == 0:
+            raise SystemExit(f"bench.py rank {rank}: no GPU visible")
+        dev = local % ndev if args.backend == "gloo" else local
         torch.cuda.set_device(dev)
         os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
