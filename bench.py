@@ -174,6 +174,8 @@ def load_pmc(config):
 # the timed advance phase: the filter instantiation without statistics (f = 0, large window: the
 # full solve queued) and the queue kernel
 ADVANCE_KERNELS = ("k_lattice_filter<true, false, false>", "k_lattice_filter_hard")
+# ... of the lattice-window cull
+WINDOW_KERNELS = ("k_window_filter<true, false, false>", "k_lattice_filter_hard")
 
 
 def load_pmc_valu(config, kernel=ADVANCE_KERNELS[0]):
@@ -315,6 +317,20 @@ def gather_state_sha(own, ws):
     return hashlib.sha256(x.cpu().numpy().tobytes()).hexdigest()
 
 
+def lattice_cull(args, sharded):
+    """The cull of the single-GPU lattice step: --cull, or auto = the lattice-window cull
+    (CBF_RUN_WINDOW_CULL) where the swarm stays lattice-like (the consensus nominal control of
+    cfg4 / cfg4f), the cell list for the random walk of cfg4r (which scrambles the lattice), the
+    HOCBF barrier and the sharded step."""
+    if sharded or args.barrier != "reference" or not 4 <= args.width <= 2048:
+        if args.cull == "window":
+            raise SystemExit("--cull window: single GPU, reference barrier, 4 <= width <= 2048 only")
+        return "cells"
+    if args.cull != "auto":
+        return args.cull
+    return "window" if args.nominal is None else "cells"
+
+
 def bench_lattice(args, ws, rank, local):
     import torch
     from cbf_amd import scenarios, swarm
@@ -327,7 +343,8 @@ def bench_lattice(args, ws, rank, local):
                            nominal=args.nominal, exchange=args.exchange)
     else:
         pos = scenarios.lattice(W, rows, seed=args.seed, spacing=args.spacing)
-        S = swarm.LatticeSwarm(pos, W, rows, gain=args.gain, barrier=args.barrier, nominal=args.nominal)
+        S = swarm.LatticeSwarm(pos, W, rows, gain=args.gain, barrier=args.barrier, nominal=args.nominal,
+                               cull=lattice_cull(args, sharded))
     progress(f"{args.config}: {W}x{rows_total} lattice built ({rows} rows on this rank)")
     use_graph = not args.eager
     # single GPU, reference barrier: the timesteps run as cbf_lattice_run calls of `chunk`
@@ -493,6 +510,7 @@ def bench_lattice(args, ws, rank, local):
     # the dominant kernel (k_lattice_filter) alone: an event recorded by the advance call between
     # it and the queued-QP kernel, on their launch stream (reference barrier)
     marked = args.barrier == "reference"
+    cull = getattr(S, "cull", "cells")
     kt = []
     for _ in range(args.kernel_iters):
         S.build_phase()
@@ -502,7 +520,9 @@ def bench_lattice(args, ws, rank, local):
         if marked:
             m.record()   # creates the event; the advance call records it again after the filter
         a.record()
-        if marked:
+        if marked and cull == "window":
+            S.advance_phase(mark=m, commit=False)   # (the new positions into scratch: no copy timed)
+        elif marked:
             S.advance_phase(mark=m)
         else:
             S.advance_phase()
@@ -516,9 +536,10 @@ def bench_lattice(args, ws, rank, local):
     check = full_size_check(S, args) if (ws == 1 and not args.shard and args.barrier == "reference") else None
     achieved = FILTER_BYTES_PER_AGENT * n_local / (f_ms * 1e-3) / 1e9
     achieved_adv = FILTER_BYTES_PER_AGENT * n_local / (k_ms * 1e-3) / 1e9
-    traffic = load_pmc_traffic(args.config, ADVANCE_KERNELS[:1]) if args.barrier == "reference" else \
+    adv_kernels = WINDOW_KERNELS if cull == "window" else ADVANCE_KERNELS
+    traffic = load_pmc_traffic(args.config, adv_kernels[:1]) if args.barrier == "reference" else \
         load_pmc_traffic(args.config + "_hocbf", ("k_lattice_filter_hocbf", "k_lattice_filter_hocbf_wide"))
-    traffic_adv = load_pmc_traffic(args.config) if args.barrier == "reference" else traffic
+    traffic_adv = load_pmc_traffic(args.config, adv_kernels) if args.barrier == "reference" else traffic
     res = {
         "metric": METRIC,
         "value": solves / elapsed,
@@ -544,8 +565,11 @@ def bench_lattice(args, ws, rank, local):
         "config": {"workload": f"{args.config}: {W}x{rows_total} jittered lattice swarm (spacing {args.spacing}), "
                                + (f"lattice-Laplacian consensus (gain {args.gain})" if args.nominal is None else
                                   f"random-walk nominal control (amplitude {args.nominal[1]}, CBF_NOMINAL_RANDOM)")
-                               + " + radius-0.2 cell-list cull + CBF QP + clip + Euler, one fused timestep per step",
+                               + (" + radius-0.2 lattice-window cull" if cull == "window" else
+                                  " + radius-0.2 cell-list cull")
+                               + " + CBF QP + clip + Euler, one fused timestep per step",
                    "barrier": args.barrier,
+                   "cull": cull,
                    "agents_total": n_total, "agents_per_gpu": n_local,
                    "parallelism": (f"row-stripe shards x{ws} ({rows} rows each), one {comm} "
                                    + ("all-to-all (ghost rows to the 2 neighbours + guard records to all)"
@@ -567,14 +591,15 @@ def bench_lattice(args, ws, rank, local):
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS,
                      "traffic": traffic,
-                     "kernel": "k_lattice_filter<f=0, no statistics> (the dominant kernel; HIP events on its launch "
-                               "stream, the end event recorded by cbf_lattice_advance_marked)" if args.barrier == "reference"
+                     "kernel": (f"{adv_kernels[0].split('<')[0]}<f=0, no statistics> (the dominant kernel; HIP events "
+                                "on its launch stream, the end event recorded by the advance call between it and the "
+                                "queued-QP kernel)") if args.barrier == "reference"
                      else "advance phase: k_lattice_filter_hocbf + k_lattice_filter_hocbf_wide",
                      "kernel_ms": f_ms,
-                     "advance_phase": {"kernels": "k_lattice_filter + k_lattice_filter_hard", "ms": k_ms,
+                     "advance_phase": {"kernels": " + ".join(k.split("<")[0] for k in adv_kernels), "ms": k_ms,
                                        "achieved": achieved_adv, "frac": achieved_adv / HBM_PEAK_GBS,
                                        "traffic": traffic_adv},
-                     "valu_busy": load_pmc_valu(args.config) if args.barrier == "reference" else None,
+                     "valu_busy": load_pmc_valu(args.config, adv_kernels[0]) if args.barrier == "reference" else None,
                      "valu_busy_note": "the dominant kernel's VALU issue fraction (rocprofv3 SQ_ACTIVE_INST_VALU, "
                                        "profiles/pmc_summary.json): beside the HBM fraction, the limit it works "
                                        "against",
@@ -852,6 +877,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-exact-qp", action="store_true",
                     help="cfg4 single GPU: skip the exact_qp_regime record (cfg4r timed beside the headline)")
+    ap.add_argument("--cull", default="auto", choices=["auto", "cells", "window"],
+                    help="single-GPU lattice cull: auto = the lattice-window cull for the consensus lattice "
+                         "(cfg4, cfg4f), the cell list for cfg4r's random walk")
     ap.add_argument("--barrier", default="reference", choices=["reference", "euclidean_hocbf"],
                     help="cfg4 single-GPU: the reference's L1 barrier rows or the Euclidean HOCBF mode")
     ap.add_argument("--cpu-budget", type=float, default=10.0, help="seconds per CPU-baseline process and shape")

@@ -15,11 +15,12 @@ PKG = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(PKG, "libcbf_amd.so")
 
 CBF_EINVAL = -1
-ABI_VERSION = 4  # include/cbf_amd.h CBF_ABI_VERSION
+ABI_VERSION = 5  # include/cbf_amd.h CBF_ABI_VERSION
 STATUS_IDLE, STATUS_OPTIMAL, STATUS_RELAXED, STATUS_BOX_INFEASIBLE, STATUS_RELAX_CAP = 0, 1, 2, 3, 4
 STATUS_NBR_OVERFLOW = 5
 STATUS_WORKSPACE_ERROR = 6
 RUN_OUTPUT_HISTORY = 1  # cbf_lattice_run_ex flags (include/cbf_amd.h CBF_RUN_*)
+RUN_WINDOW_CULL = 2
 # words of a lattice-step statistics slot (include/cbf_amd.h CBF_STAT_*)
 (STAT_SOLVES, STAT_OPTIMAL, STAT_RELAXED, STAT_INFEASIBLE, STAT_SEIDEL, STAT_VIOL_OPTIMAL, STAT_VIOL_ORIGINAL,
  STAT_MIN_DIST2, STAT_ERRORS, STAT_BINDING) = range(10)
@@ -95,6 +96,9 @@ SIGNATURES = {
     "cbf_lattice_run": (C.c_int, [_P, _G, _i32, _i32, _vp, _d, _d, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _sz, _vp]),
     "cbf_lattice_run_ex": (C.c_int, [_P, _G, _i32, _i32, _vp, _d, _d, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _sz,
                                      C.c_uint32, _vp]),
+    "cbf_lattice_window_build": (C.c_int, [_P, _G, _i32, _i32, _vp, _d, _vp, _vp, _sz, _vp]),
+    "cbf_lattice_window_advance": (C.c_int, [_P, _G, _i32, _i32, _vp, _d, _vp, _vp, _vp, _vp, _vp, _vp, _sz, _vp,
+                                             _vp]),
     "cbf_lattice_build": (C.c_int, [_P, _G, _i32, _i32, _i32, _i32, _i32, _i32, _vp, _d, _vp, _vp, _sz, _vp]),
     "cbf_lattice_advance": (C.c_int, [_P, _G, _i32, _i32, _i32, _i32, _i32, _i32, _vp, _d, _vp, _vp, _vp, _vp,
                                       _i32, _vp, _vp, _vp, _sz, _vp]),

@@ -17,7 +17,7 @@ ROOT = os.path.dirname(PKG)
 CSRC = os.path.join(PKG, "csrc")
 BUILD = os.path.join(PKG, "_build")
 LIB = os.path.join(PKG, "libcbf_amd.so")
-SOURCES = ["abi.cpp", "cells.hip", "filter.hip", "swarm.hip", "mc.hip", "hocbf.hip", "rps.hip"]
+SOURCES = ["abi.cpp", "cells.hip", "filter.hip", "swarm.hip", "window.hip", "mc.hip", "hocbf.hip", "rps.hip"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("CBF_OFFLOAD_ARCH", "gfx950")
 FLAGS = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-Wall", "-Wno-unused-function",

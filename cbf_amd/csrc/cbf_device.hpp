@@ -37,6 +37,10 @@ struct KP {
     double n0[4], n1[4];  // quadrant normals L_g (host-computed with the reference's order)
     int f_zero;
     int relax_cap;
+    // window cull (CBF_RUN_WINDOW_CULL): the smallest double d with d * d >= cull_t, so that a
+    // coordinate difference e with |e| > d makes e * e >= cull_t (rounding is monotone), i.e. the
+    // candidate cannot pass the cull test s < cull_t of cross_and_rescue.py:141-150
+    double win_d;
 };
 
 inline KP make_kp(const cbf_params* p) {
@@ -54,6 +58,9 @@ inline KP make_kp(const cbf_params* p) {
     }
     k.f_zero = p->f_is_zero;
     k.relax_cap = p->relax_cap;
+    double d = sqrt(p->cull_t > 0 ? p->cull_t : 0.0);
+    while (d * d < p->cull_t) d = nextafter(d, INFINITY);
+    k.win_d = d;
     return k;
 }
 

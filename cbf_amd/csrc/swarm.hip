@@ -5,6 +5,7 @@
 #include "cbf_device.hpp"
 #include "cells.hpp"
 #include "lattice.hpp"
+#include "lattice_ego.hpp"
 
 using namespace cbf;
 
@@ -121,54 +122,6 @@ __global__ void __launch_bounds__(kBlock) k_consensus_csr(int n_dst, int self_of
         v1 = fma(a1, rc, a0 * rs);
     }
     out[k] = make_double2(v0 * scale, v1 * scale);
-}
-
-// Lattice Laplacian sum for window agent w (neighbours in ascending index order).
-__device__ __forceinline__ double2 lattice_sum(const double2* __restrict__ pos, long w, int r, int c, int W, int H) {
-    const double2 pi = pos[w];
-    double a0 = 0.0, a1 = 0.0;
-    if (r > 0) {
-        const double2 q = pos[w - W];
-        a0 = a0 + (q.x - pi.x);
-        a1 = a1 + (q.y - pi.y);
-    }
-    if (c > 0) {
-        const double2 q = pos[w - 1];
-        a0 = a0 + (q.x - pi.x);
-        a1 = a1 + (q.y - pi.y);
-    }
-    if (c < W - 1) {
-        const double2 q = pos[w + 1];
-        a0 = a0 + (q.x - pi.x);
-        a1 = a1 + (q.y - pi.y);
-    }
-    if (r < H - 1) {
-        const double2 q = pos[w + W];
-        a0 = a0 + (q.x - pi.x);
-        a1 = a1 + (q.y - pi.y);
-    }
-    return make_double2(a0, a1);
-}
-
-// CBF_NOMINAL_RANDOM: a random-walk nominal control, a pure function of (seed, global agent
-// index, the bits of the agent's current position): splitmix64 finalisers chained over the three
-// words; each component amp (2 U - 1) with U = (h >> 11) 2^-53 (2 U - 1 is exact, so the only
-// rounding is the product).  The position changes every step, so each step draws afresh, with no
-// step counter; any sharding of the lattice draws the same values.  Restated in
-// oracle/pyoracle.py:random_nominal.
-__device__ __forceinline__ unsigned long long mix64(unsigned long long z) {
-    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
-    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-    return z ^ (z >> 31);
-}
-__device__ __forceinline__ double2 random_nominal(const NominalSpec& N, long g, double2 p) {
-    unsigned long long h = mix64(N.seed + 0x9E3779B97F4A7C15ull * (unsigned long long)(g + 1));
-    h = mix64(h ^ (unsigned long long)__double_as_longlong(p.x));
-    h = mix64(h ^ (unsigned long long)__double_as_longlong(p.y));
-    const unsigned long long h2 = mix64(h + 0x9E3779B97F4A7C15ull);
-    const double v0 = 2.0 * ((double)(h >> 11) * 0x1p-53) - 1.0;
-    const double v1 = 2.0 * ((double)(h2 >> 11) * 0x1p-53) - 1.0;
-    return make_double2(N.amp * v0, N.amp * v1);
 }
 
 __global__ void __launch_bounds__(kBlock) k_consensus_lattice(int W, int H, int row_begin, int row_end, int pos_row0,
@@ -413,109 +366,6 @@ __global__ void __launch_bounds__(kBlock) k_lattice_scan_scatter(
         }
     }
     if (ext_keys) ext_keys_flush<kBlock / 64, kScatterA == 1>(e, any, py, ext_keys, lb, red, &arrive);
-}
-
-// Per-ego outcome of the lattice filter for the statistics.
-struct EgoOut {
-    int res;          // 0 not an owned ego, 1 done (outputs written), 2 queued for the full solve
-    int w;            // window index of the agent
-    int nbrs;         // neighbours
-    int code;         // final status code (res == 1)
-    bool binding;     // the minimiser is not the origin (res == 1)
-    bool seidel;      // the QP took the full Seidel solve (inline, or through the queue)
-    double viol, vorig, d2, nx, ny;
-};
-
-// Where the QPs that solve_fast cannot settle are solved: windows of at most
-// cbf_params.solve_inline_max agents (a runtime setting; < 0 = kSolveInlineDefault) run the filter
-// instantiation with the full solve inline (IN = true: no queue kernel); larger ones queue the QPs
-// with their assembled state for k_lattice_filter_hard, one lane per QP.  Measured crossover
-// (cbf_lattice_run, W = 1024, spacing 0.145, run(10) per timestep, inline vs queue): 64 rows 25.2 vs
-// 30.2 us, 128 rows 27.7 vs 32.6 us, 256 rows 42.5 vs 38.9 us, 512 rows 55 vs 55 (and the inline
-// form at 1024 rows 118.5 vs 79.5).  Between 128 and 192 rows (tools/records/gpu_r03g2.sh): 128 rows
-// 27.8-27.9 vs 32.5-32.7, 136 rows 34.2 vs 32.9-33.1, 144 35.0 vs 33.8, 160 35.6 vs 33.8, 192
-// 38.5-38.8 vs 34.0-34.6.  So the inline form pays only while every SIMD holds at most 2 of the
-// window's waves: 256 CUs x 4 SIMDs x 2 waves x 64 lanes = 131072 agents (one 1024-wide row more
-// puts a third 165-VGPR wave on some SIMDs, and the kernel ends with the most loaded one).  The two
-// placements are bit-identical (tests run both).  The wave-cooperative solves measured slower in
-// either place; their code is on branch exp/coop-solve-variants.
-constexpr long kSolveInlineDefault = 131072;
-inline bool solve_inline(const cbf_params* p, long n) {
-    return n <= (p->solve_inline_max < 0 ? kSolveInlineDefault : (long)p->solve_inline_max);
-}
-
-// Outputs of one owned ego (output index k) once its QP is solved (or it has no neighbour):
-// clip, Euler, stores, statistics record.
-template <bool ST>
-__device__ __forceinline__ void ego_output(const KP& P, const Ego& E, const Sol& S, bool idle, int k, double T,
-                                           double2* __restrict__ pos_out, double2* __restrict__ u,
-                                           int32_t* __restrict__ status, int32_t* __restrict__ cnt, EgoOut& O) {
-    double ux, uy;
-    int32_t st;
-    O.code = CBF_STATUS_IDLE;
-    if (idle) {
-        ux = E.u0x;
-        uy = E.u0y;
-        st = CBF_STATUS_IDLE;
-    } else {
-        clip_u(P, S, E, ux, uy);
-        st = pack_status(S);
-        O.code = S.status;
-        if (ST) {  // statistics only (a kernel without them compiles the violations away)
-            O.binding = S.x0 != 0.0 || S.x1 != 0.0;
-            O.viol = S.viol;
-            O.vorig = S.viol_orig;
-        }
-    }
-    const double2 pn = make_double2(E.r0 + T * ux, E.r1 + T * uy);
-    pos_out[k] = pn;
-    if (u) u[k] = make_double2(ux, uy);  // u / status / cnt: null in the inner timesteps of cbf_lattice_run
-    if (status) status[k] = st;
-    if (cnt) cnt[k] = E.count;
-    O.nx = pn.x;
-    O.ny = pn.y;
-    O.res = 1;
-}
-
-// Tail of the lattice filter for one owned ego (output index k) whose QP rows are accumulated in
-// E: solve in place when solve_fast can (origin, or one Seidel event that stays put); otherwise
-// run the full solve_ego right here (IN: the small-window instantiation, below) or queue it to the
-// hard kernel (sub-queue q: header hardq, records qr).  Then clip, Euler, outputs.
-template <bool FZ, bool ST, bool IN>
-__device__ __forceinline__ void ego_finish(const KP& P, Ego& E, int w, int k, int slot, double T,
-                                           double2* __restrict__ pos_out, double2* __restrict__ u,
-                                           int32_t* __restrict__ status, int32_t* __restrict__ cnt,
-                                           int32_t* __restrict__ hardq, int q, HardRec* __restrict__ qr,
-                                           EgoOut& O) {
-    Sol S;
-    const bool idle = E.count == 0;
-    if (!idle && !solve_fast(P, E, S)) {
-        O.seidel = true;
-        if (IN) {
-            S = solve_ego(P, E);
-            ego_output<ST>(P, E, S, false, k, T, pos_out, u, status, cnt, O);
-            return;
-        }
-        HardRec& h = qr[subq_append(hardq, q)];
-        h.r0 = E.r0;
-        h.r1 = E.r1;
-        h.r2 = E.r2;
-        h.r3 = E.r3;
-        h.u0x = E.u0x;
-        h.u0y = E.u0y;
-        h.bq0 = E.bq0;
-        h.bq1 = E.bq1;
-        h.bq2 = E.bq2;
-        h.bq3 = E.bq3;
-        h.present = (int)E.present;
-        h.count = E.count;
-        h.k = k;
-        h.row = w;
-        h.slot = slot;
-        O.res = 2;
-        return;
-    }
-    ego_output<ST>(P, E, S, idle, k, T, pos_out, u, status, cnt, O);
 }
 
 // Lattice step K4 for one cell-sorted slot: 3x3-cell cull (the three cell rows scanned as one
@@ -999,6 +849,88 @@ extern "C" int cbf_lattice_step(const cbf_params* p, const cbf_grid* grid, int32
                                nbr_count, guard_rows, extents, stats, workspace, workspace_bytes, stream);
 }
 
+// The queued-QP kernel of a whole-lattice advance without chained binning (window cull).
+static void launch_hard_plain(const cbf_params* p, const cbf_grid* grid, const CellWs& Wk, int W, int H, double T,
+                              double2* pos_out, double2* u, int32_t* status, int32_t* cnt, unsigned long long* stats,
+                              hipStream_t s) {
+    const long n = (long)W * H;
+    hipLaunchKernelGGL(k_lattice_filter_hard, dim3(lattice_hard_blocks(n)), dim3(64), 0, s, make_kp(p),
+                       make_grid(grid), make_win_bounds(W, 0, n, 0, H, 0, H, 0), T, pos_out, u, status, cnt,
+                       (double*)nullptr, stats, Wk.hardq, Wk.qrec, Wk.qcap, ChainSpec{}, Wk.sctl);
+}
+
+// cbf_lattice_run_ex with CBF_RUN_WINDOW_CULL: per timestep the window build (k_window_prep:
+// nominal controls and the guards), the window filter and, for a large window, the queued-QP
+// kernel.  The filter reads its input positions while writing new ones, so timesteps alternate
+// between pos and the workspace's spos: with an odd count the first build also copies pos to spos
+// and the first filter reads that copy, so the last timestep always writes pos.
+static int lattice_run_window(const cbf_params* p, const cbf_grid* grid, int32_t W, int32_t H, double* pos,
+                              double gain, double T, int32_t steps, double* vel_out, double* u, int32_t* status,
+                              int32_t* nbr_count, uint64_t* stats, void* workspace, bool hist, void* stream) {
+    hipStream_t s = (hipStream_t)stream;
+    const long n = (long)W * H;
+    CellWs Wk(workspace, n, (long)grid->nx * grid->ny);
+    if (!window_cull_ok(W, H, n, Wk)) return CBF_EINVAL;
+    const bool in = solve_inline(p, n);
+    double2* buf[2] = {reinterpret_cast<double2*>(pos), Wk.spos};
+    const int odd = steps & 1;
+    unsigned long long* st = reinterpret_cast<unsigned long long*>(stats);
+    for (int k = 0; k < steps; ++k) {
+        double2* src = buf[(k + odd) & 1];
+        double2* dst = buf[(k + 1 + odd) & 1];
+        const bool last = k + 1 == steps, out = last || hist;
+        const long o = hist ? (long)k * n : 0;
+        // an odd run's first build reads pos and leaves its copy in spos, which the filter then reads
+        window_prep(Wk, W, H, k == 0 && odd ? buf[0] : src, gain,
+                    out ? reinterpret_cast<double2*>(vel_out) + o : nullptr, k == 0 && odd ? buf[1] : nullptr, s);
+        double2* uo = out ? reinterpret_cast<double2*>(u) + o : nullptr;
+        int32_t* so = out ? status + o : nullptr;
+        int32_t* co = out && nbr_count ? nbr_count + o : nullptr;
+        window_filter(p, Wk, W, H, src, T, dst, uo, so, co, st, in, s);
+        if (!in) launch_hard_plain(p, grid, Wk, W, H, T, dst, uo, so, co, st, s);
+        if (int rc = (int)hipGetLastError()) return rc;
+    }
+    return 0;
+}
+
+// The two phases of one window-cull timestep as separate calls (the measurement hooks: the bench
+// times the filter kernel alone).  pos_out must not overlap pos.
+extern "C" int cbf_lattice_window_build(const cbf_params* p, const cbf_grid* grid, int32_t W, int32_t H,
+                                        const double* pos, double gain, double* vel_out, void* workspace,
+                                        size_t workspace_bytes, void* stream) {
+    int rc = check_lattice(p, grid, W, H, 0, H, 0, H, pos, workspace, workspace_bytes);
+    if (rc) return rc;
+    const long n = (long)W * H;
+    CellWs Wk(workspace, n, (long)grid->nx * grid->ny);
+    if (!window_cull_ok(W, H, n, Wk)) return CBF_EINVAL;
+    window_prep(Wk, W, H, reinterpret_cast<const double2*>(pos), gain, reinterpret_cast<double2*>(vel_out), nullptr,
+                (hipStream_t)stream);
+    return (int)hipGetLastError();
+}
+
+extern "C" int cbf_lattice_window_advance(const cbf_params* p, const cbf_grid* grid, int32_t W, int32_t H,
+                                          const double* pos, double T, double* pos_out, double* u, int32_t* status,
+                                          int32_t* nbr_count, uint64_t* stats, void* workspace,
+                                          size_t workspace_bytes, void* filter_done, void* stream) {
+    int rc = check_lattice(p, grid, W, H, 0, H, 0, H, pos, workspace, workspace_bytes);
+    if (rc) return rc;
+    const long n = (long)W * H;
+    if (!pos_out || !u || !status) return CBF_EINVAL;
+    if (pos_out < pos + 2 * n && pos < pos_out + 2 * n) return CBF_EINVAL;  // the filter reads pos throughout
+    CellWs Wk(workspace, n, (long)grid->nx * grid->ny);
+    if (!window_cull_ok(W, H, n, Wk)) return CBF_EINVAL;
+    hipStream_t s = (hipStream_t)stream;
+    const bool in = solve_inline(p, n);
+    double2* po = reinterpret_cast<double2*>(pos_out);
+    double2* uo = reinterpret_cast<double2*>(u);
+    unsigned long long* st = reinterpret_cast<unsigned long long*>(stats);
+    window_filter(p, Wk, W, H, reinterpret_cast<const double2*>(pos), T, po, uo, status, nbr_count, st, in, s);
+    if (filter_done)
+        if (hipError_t e = hipEventRecord((hipEvent_t)filter_done, s)) return (int)e;
+    if (!in) launch_hard_plain(p, grid, Wk, W, H, T, po, uo, status, nbr_count, st, s);
+    return (int)hipGetLastError();
+}
+
 // `steps` timesteps of the whole lattice in one call, bit-identical to as many cbf_lattice_step
 // calls: every advance but the last bins its new positions for the next build on the fly
 // (chained binning: run_rank in K4, one atomic per queued ego in K5), so only the first build
@@ -1010,8 +942,12 @@ extern "C" int cbf_lattice_run_ex(const cbf_params* p, const cbf_grid* grid, int
                                   uint32_t flags, void* stream) {
     int rc = check_lattice(p, grid, W, H, 0, H, 0, H, pos, workspace, workspace_bytes);
     if (rc) return rc;
-    if (steps < 0 || !vel_out || !u || !status || (flags & ~CBF_RUN_OUTPUT_HISTORY)) return CBF_EINVAL;
+    if (steps < 0 || !vel_out || !u || !status || (flags & ~(CBF_RUN_OUTPUT_HISTORY | CBF_RUN_WINDOW_CULL)))
+        return CBF_EINVAL;
     const bool hist = (flags & CBF_RUN_OUTPUT_HISTORY) != 0;
+    if (flags & CBF_RUN_WINDOW_CULL)
+        return lattice_run_window(p, grid, W, H, pos, gain, T, steps, vel_out, u, status, nbr_count, stats, workspace,
+                                  hist, stream);
     hipStream_t s = (hipStream_t)stream;
     const long n = (long)W * H;
     CellWs Wk(workspace, n, (long)grid->nx * grid->ny);

@@ -1,0 +1,479 @@
+// window.hip -- the lattice-window cull of a lattice swarm timestep (gfx950).
+//
+// The cull of cross_and_rescue.py:141-150 keeps, for each ego, the agents within the cull radius.
+// The cell-list path (swarm.hip) finds them through a counting sort of all positions by cell,
+// rebuilt every timestep.  An agent of a lattice swarm keeps its lattice index, and while the
+// swarm stays lattice-like its neighbours are lattice neighbours: this path takes the candidates
+// straight from the lattice-ordered positions (coalesced loads, no sort) and PROVES per ego that
+// every agent it does not test is out of range, so the neighbour sets -- and every result -- are
+// bit-identical to the cell-list path's (the per-quadrant minimum is order-independent).
+//
+// The proof uses two guards, both exact in fp64 (rounding is monotone, so a computed difference
+// beyond d = win_d makes e * e >= cull_t: the candidate fails s < cull_t):
+//   rows     per lattice row the min / max y over its agents; sylo[r] = min over rows >= r,
+//            pyhi[r] = max over rows <= r (k_window_prep, last block).  Rows r + k + 1 and beyond
+//            are out of range of an ego at y once sylo[r + k + 1] - y > d (and below likewise).
+//   columns  per agent of row r' the min x over the columns >= its own (rs) and the max x over the
+//            columns <= its own (rp), rounded outward to fp32.  Columns c' and beyond of row r'
+//            are out of range once rs(r', c') - x > d (and to the left likewise).
+// Agents with a non-finite coordinate can never pass the cull test and are left out of every
+// extent.  Each ego scans its rows (the row guard) over columns c - 1 .. c + 1 and checks the
+// column sentinels at c -+ 2; a wave whose lanes need it scans columns c -+ 2 too (sentinels at
+// c -+ 3); a lane that still needs more, or whose hit list overflows, walks its rows outward until
+// every sentinel holds, with direct row assembly (any swarm: slower the less lattice-like it is).
+#include "cbf_device.hpp"
+#include "cells.hpp"
+#include "lattice.hpp"
+#include "lattice_ego.hpp"
+
+using namespace cbf;
+
+namespace {
+
+constexpr int kPrepBlock = 256;
+constexpr int kPrepPer = 8;  // columns per prep thread: rows of up to 2048 agents
+constexpr int kWinMaxW = kPrepBlock * kPrepPer;
+
+// The guard arrays in the workspace's record area (cs, 16 B per agent, unused by this path).
+struct WinGuard {
+    int32_t* ticket;  // prep blocks done (a control word: the last block scans the row extents, then
+                      // re-zeroes it; a zero-filled workspace starts at 0 whatever its cs area held)
+    double* rowy;     // [2 H] {min y, max y} per row (finite agents)
+    double* sylo;     // [H + 1] min over rows >= r of the row minima (sylo[H] = +inf)
+    double* pyhi;     // [H] max over rows <= r of the row maxima
+};
+inline WinGuard win_guard(const CellWs& Wk, int H) {
+    WinGuard g;
+    char* p = reinterpret_cast<char*>(Wk.cs);
+    g.ticket = Wk.sctl + 16;
+    g.rowy = reinterpret_cast<double*>(p + 256);
+    g.sylo = g.rowy + 2l * H;
+    g.pyhi = g.sylo + (H + 1);
+    return g;
+}
+inline size_t win_guard_bytes(int H) { return 256 + 8 * (size_t)(4l * H + 1); }
+// the column extents, one float2 {rs, rp} per agent, in the scratch area (wvel, 16 B per agent)
+inline float2* win_rsp(const CellWs& Wk) { return reinterpret_cast<float2*>(Wk.wvel); }
+
+// fp32 bounds of a double: the largest float <= v / the smallest float >= v (outward rounding, so
+// the column guard built from them stays sound)
+__device__ __forceinline__ float f32_down(double v) {
+    float f = (float)v;
+    if ((double)f > v) {
+        const unsigned b = __float_as_uint(f);
+        f = f == 0.0f ? __uint_as_float(0x80000001u) : __uint_as_float(f > 0.0f ? b - 1u : b + 1u);
+    }
+    return f;
+}
+__device__ __forceinline__ float f32_up(double v) {
+    float f = (float)v;
+    if ((double)f < v) {
+        const unsigned b = __float_as_uint(f);
+        f = f == 0.0f ? __uint_as_float(0x00000001u) : __uint_as_float(f > 0.0f ? b + 1u : b - 1u);
+    }
+    return f;
+}
+
+// Block-wide exclusive scans over one value per thread (every thread must call them): the minimum
+// over the threads after this one, and the maximum over the threads before it; *tot gets the
+// block's total.
+__device__ __forceinline__ double block_after_min(double v, double* red, double* tot) {
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    double s = v;  // inclusive suffix minimum within the wave
+    for (int o = 1; o < 64; o <<= 1) {
+        const double y = __shfl_down(s, o, 64);
+        if (lane + o < 64) s = pmin(s, y);
+    }
+    double ex = __shfl_down(s, 1, 64);
+    if (lane == 63) ex = INFINITY;
+    if (lane == 0) red[wid] = s;
+    __syncthreads();
+    double after = INFINITY, all = INFINITY;
+    for (int q = 0; q < kPrepBlock / 64; ++q) {
+        if (q > wid) after = pmin(after, red[q]);
+        all = pmin(all, red[q]);
+    }
+    __syncthreads();
+    *tot = all;
+    return pmin(ex, after);
+}
+__device__ __forceinline__ double block_before_max(double v, double* red, double* tot) {
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    double s = v;  // inclusive prefix maximum within the wave
+    for (int o = 1; o < 64; o <<= 1) {
+        const double y = __shfl_up(s, o, 64);
+        if (lane >= o) s = pmax(s, y);
+    }
+    double ex = __shfl_up(s, 1, 64);
+    if (lane == 0) ex = -INFINITY;
+    if (lane == 63) red[wid] = s;
+    __syncthreads();
+    double before = -INFINITY, all = -INFINITY;
+    for (int q = 0; q < kPrepBlock / 64; ++q) {
+        if (q < wid) before = pmax(before, red[q]);
+        all = pmax(all, red[q]);
+    }
+    __syncthreads();
+    *tot = all;
+    return pmax(ex, before);
+}
+
+__device__ __forceinline__ void st_sc1_f64(double* p, double v) {
+    __hip_atomic_store(reinterpret_cast<unsigned long long*>(p), (unsigned long long)__double_as_longlong(v),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double ld_sc1_f64(const double* p) {
+    return __longlong_as_double((long long)__hip_atomic_load(reinterpret_cast<const unsigned long long*>(p),
+                                                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+
+// Window-cull build of one timestep: one block per lattice row.  Per agent the nominal control
+// (the lattice Laplacian of cross_and_rescue.py:121-125 shape scaled by gain, or the random walk
+// of CBF_NOMINAL_RANDOM: the scatter's arithmetic) into u0 (and vel_out), the column extents into
+// rsp; per row its y extents.  The last block to finish (a ticket; the guide's sc1 hand-off: sc1
+// stores, every storing wave's vmcnt(0), a block barrier, one agent-scope add, sc1 loads by the
+// block whose add came last) turns the row extents into sylo / pyhi.  copy_to (nullable) gets a
+// copy of the positions (the run's ping-pong start).
+__global__ void __launch_bounds__(kPrepBlock) k_window_prep(int W, int H, const double2* __restrict__ pos,
+                                                            double2* __restrict__ u0, float2* __restrict__ rsp,
+                                                            WinGuard Gd, double gain, double2* __restrict__ vel_out,
+                                                            double2* __restrict__ copy_to, int32_t* __restrict__ sctl,
+                                                            long ncell) {
+    __shared__ double red[kPrepBlock / 64];
+    __shared__ int last;
+    const int r = xcd_block();
+    const long nwin = (long)W * H;
+    if (r == 0 && threadIdx.x == 0) build_begin(sctl, nwin, ncell);
+    const NominalSpec N = nominal_spec(sctl);
+    const int m = (W + kPrepBlock - 1) / kPrepBlock;
+    const int c0 = threadIdx.x * m;
+    const long row = (long)r * W;
+    double xs[kPrepPer];
+    bool fin[kPrepPer];
+    double ylo = INFINITY, yhi = -INFINITY;
+#pragma unroll
+    for (int j = 0; j < kPrepPer; ++j) {
+        xs[j] = 0.0;
+        fin[j] = false;
+        const int c = c0 + j;
+        if (j < m && c < W) {
+            const long w = row + c;
+            const double2 p = pos[w];
+            double2 a;
+            if (N.mode == CBF_NOMINAL_RANDOM) {
+                a = random_nominal(N, w, p);
+            } else {
+                const double2 s = lattice_sum(pos, w, r, c, W, H);
+                a = make_double2(s.x * gain, s.y * gain);
+            }
+            u0[w] = a;
+            if (vel_out) vel_out[w] = a;
+            if (copy_to) copy_to[w] = p;
+            fin[j] = isfinite(p.x) && isfinite(p.y);
+            xs[j] = p.x;
+            if (fin[j]) {
+                ylo = pmin(ylo, p.y);
+                yhi = pmax(yhi, p.y);
+            }
+        }
+    }
+    // column extents: suffix minimum / prefix maximum of x along the row (finite agents)
+    double sm[kPrepPer], pm[kPrepPer];
+    double acc = INFINITY;
+#pragma unroll
+    for (int j = kPrepPer - 1; j >= 0; --j) {
+        if (fin[j]) acc = pmin(acc, xs[j]);
+        sm[j] = acc;
+    }
+    acc = -INFINITY;
+#pragma unroll
+    for (int j = 0; j < kPrepPer; ++j) {
+        if (fin[j]) acc = pmax(acc, xs[j]);
+        pm[j] = acc;
+    }
+    double tot;
+    const double after = block_after_min(sm[0], red, &tot);
+    const double before = block_before_max(pm[kPrepPer - 1], red, &tot);
+#pragma unroll
+    for (int j = 0; j < kPrepPer; ++j) {
+        const int c = c0 + j;
+        if (j < m && c < W) rsp[row + c] = make_float2(f32_down(pmin(sm[j], after)), f32_up(pmax(pm[j], before)));
+    }
+    // row y extents
+    double lo, hi;
+    (void)block_after_min(ylo, red, &lo);
+    (void)block_before_max(yhi, red, &hi);
+    if (threadIdx.x == 0) {
+        st_sc1_f64(&Gd.rowy[2l * r], lo);
+        st_sc1_f64(&Gd.rowy[2l * r + 1], hi);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) last = atomicAdd(Gd.ticket, 1) == (int)gridDim.x - 1;
+    __syncthreads();
+    if (!last) return;
+    // the last block: sylo (suffix minima from the last row down) and pyhi (prefix maxima), in
+    // chunks of kPrepBlock x kPrepPer rows
+    constexpr int CH = kPrepBlock * kPrepPer;
+    double carry = INFINITY;
+    for (int base = ((H - 1) / CH) * CH; base >= 0; base -= CH) {
+        double v[kPrepPer];
+        double a = INFINITY;
+#pragma unroll
+        for (int j = kPrepPer - 1; j >= 0; --j) {
+            const int rr = base + threadIdx.x * kPrepPer + j;
+            v[j] = rr < H ? ld_sc1_f64(&Gd.rowy[2l * rr]) : INFINITY;
+            a = pmin(a, v[j]);
+            v[j] = a;
+        }
+        double t;
+        const double aft = pmin(block_after_min(a, red, &t), carry);
+#pragma unroll
+        for (int j = 0; j < kPrepPer; ++j) {
+            const int rr = base + threadIdx.x * kPrepPer + j;
+            if (rr < H) Gd.sylo[rr] = pmin(v[j], aft);
+        }
+        carry = pmin(carry, t);
+    }
+    carry = -INFINITY;
+    for (int base = 0; base < H; base += CH) {
+        double v[kPrepPer];
+        double a = -INFINITY;
+#pragma unroll
+        for (int j = 0; j < kPrepPer; ++j) {
+            const int rr = base + threadIdx.x * kPrepPer + j;
+            v[j] = rr < H ? ld_sc1_f64(&Gd.rowy[2l * rr + 1]) : -INFINITY;
+            a = pmax(a, v[j]);
+            v[j] = a;
+        }
+        double t;
+        const double bef = pmax(block_before_max(a, red, &t), carry);
+#pragma unroll
+        for (int j = 0; j < kPrepPer; ++j) {
+            const int rr = base + threadIdx.x * kPrepPer + j;
+            if (rr < H) Gd.pyhi[rr] = pmax(v[j], bef);
+        }
+        carry = pmax(carry, t);
+    }
+    if (threadIdx.x == 0) {
+        Gd.sylo[H] = INFINITY;
+        *Gd.ticket = 0;
+    }
+}
+
+// One candidate of the window scan: the cull test of cross_and_rescue.py:141-150 for agents
+// (s > 0: the ego itself and coincident agents are out), hits into the lane's list.
+__device__ __forceinline__ void win_cand(const KP& P, const Ego& E, double2 p, int idx, HitList& Hl, int* lds,
+                                         double& smin) {
+    const double e0 = p.x - E.r0, e1 = p.y - E.r1;
+    const double s = e0 * e0 + e1 * e1;
+    if (s < P.cull_t && s > 0) {
+        Hl.push(lds, idx);
+        smin = pmin(smin, s);
+    }
+}
+
+// The rows of an ego at window row r, y: [r - Kd, r + Ku] (rows beyond are out of range).
+__device__ __forceinline__ void win_rows(const KP& P, const double* __restrict__ sylo,
+                                         const double* __restrict__ pyhi, int r, int H, double y, int& Kd, int& Ku) {
+    Ku = 0;
+    while (r + Ku + 1 < H && !(sylo[r + Ku + 1] - y > P.win_d)) ++Ku;
+    Kd = 0;
+    while (r - Kd - 1 >= 0 && !(y - pyhi[r - Kd - 1] > P.win_d)) ++Kd;
+}
+
+// The unbounded form for one lane (rare): every row of [r - Kd, r + Ku] walked outward from the
+// ego's column until its sentinels hold, hits assembled row by row (ego_add: the overflow path of
+// the cell-list filter, same rows, same minima).
+template <bool FZ>
+__device__ __forceinline__ void win_direct(const KP& P, Ego& E, long w, int r, int c, int W, int Kd, int Ku,
+                                        const double2* __restrict__ pos, const double2* __restrict__ u0,
+                                        const float2* __restrict__ rsp, double& smin) {
+    E.bq0 = E.bq1 = E.bq2 = E.bq3 = INFINITY;
+    E.present = 0u;
+    E.count = 0;
+    smin = INFINITY;
+    auto cand = [&](long j) {
+        const double2 p = pos[j];
+        const double e0 = p.x - E.r0, e1 = p.y - E.r1;
+        const double s = e0 * e0 + e1 * e1;
+        if (!(s < P.cull_t && s > 0)) return;
+        smin = pmin(smin, s);
+        const double2 v = u0[j];
+        ego_add<FZ>(P, E, p.x, p.y, v.x, v.y);
+    };
+    for (int dr = -Kd; dr <= Ku; ++dr) {
+        const long b = w + (long)dr * W;
+        for (int dc = 0; c + dc < W; ++dc) {  // the column itself, then right
+            cand(b + dc);
+            if (c + dc + 1 >= W || (double)rsp[b + dc + 1].x - E.r0 > P.win_d) break;
+        }
+        for (int dc = -1; c + dc >= 0; --dc) {  // left
+            cand(b + dc);
+            if (c + dc - 1 < 0 || E.r0 - (double)rsp[b + dc - 1].y > P.win_d) break;
+        }
+    }
+}
+
+// One ego (window index w = r W + c, owned) of the window-cull filter.  Every lane of the wave
+// calls it (the row window is a wave-wide loop); `act` says whether the lane holds an ego.
+template <bool FZ, bool ST, bool IN>
+__device__ __forceinline__ void window_ego(const KP& P, const WinBounds& B, int W, int H, long w, bool act,
+                                           const double2* __restrict__ pos, const double2* __restrict__ u0,
+                                           const float2* __restrict__ rsp, const double* __restrict__ sylo,
+                                           const double* __restrict__ pyhi, double T, double2* __restrict__ pos_out,
+                                           double2* __restrict__ u, int32_t* __restrict__ status,
+                                           int32_t* __restrict__ cnt, int32_t* __restrict__ hardq, int q,
+                                           HardRec* __restrict__ qr, int* hit_lds, Ego& E, EgoOut& O) {
+    int r = 0, c = 0;
+    bool fin = false;
+    if (act) {
+        r = (int)(w / W);
+        c = (int)(w - (long)r * W);
+        const double2 pe = pos[w], ve = u0[w];
+        ego_init(P, E, pe.x, pe.y, ve.x, ve.y, ve.x, ve.y);
+        fin = isfinite(pe.x) && isfinite(pe.y);  // otherwise no candidate can pass (s is inf or NaN)
+    }
+    int Kd = -1, Ku = -1;
+    if (fin) win_rows(P, sylo, pyhi, r, H, E.r1, Kd, Ku);
+    const int KdW = wave_max_i(Kd), KuW = wave_max_i(Ku);
+    HitList Hl;
+    double d2 = INFINITY;
+    // rows whose sentinel at c + 2 (R) / c - 2 (L) does not hold: bit dr + KdW
+    unsigned long long pR = 0, pL = 0;
+    bool slow = KdW + KuW + 1 > 64;  // (a window that tall takes the unbounded form)
+    if (!slow) {
+        for (int dr = -KdW; dr <= KuW; ++dr) {
+            if (!(fin && dr >= -Kd && dr <= Ku)) continue;
+            const long b = w + (long)dr * W;
+            const double2 pm = c > 0 ? pos[b - 1] : make_double2(INFINITY, INFINITY);
+            const double2 p0 = pos[b];
+            const double2 pp = c + 1 < W ? pos[b + 1] : make_double2(INFINITY, INFINITY);
+            const float rs = c + 2 < W ? rsp[b + 2].x : INFINITY;
+            const float rp = c - 2 >= 0 ? rsp[b - 2].y : -INFINITY;
+            win_cand(P, E, pm, (int)(b - 1), Hl, hit_lds, d2);
+            win_cand(P, E, p0, (int)b, Hl, hit_lds, d2);
+            win_cand(P, E, pp, (int)(b + 1), Hl, hit_lds, d2);
+            if (!((double)rs - E.r0 > P.win_d)) pR |= 1ull << (dr + KdW);
+            if (!(E.r0 - (double)rp > P.win_d)) pL |= 1ull << (dr + KdW);
+        }
+        if (__ballot((pR | pL) != 0)) {  // columns c -+ 2 where a sentinel did not hold
+            for (int dr = -KdW; dr <= KuW; ++dr) {
+                const bool gr = (pR >> (dr + KdW)) & 1ull, gl = (pL >> (dr + KdW)) & 1ull;
+                if (!(gr || gl)) continue;
+                const long b = w + (long)dr * W;
+                if (gr) {  // c + 2 < W here (the sentinel beyond the edge holds)
+                    const double2 p2 = pos[b + 2];
+                    const float rs = c + 3 < W ? rsp[b + 3].x : INFINITY;
+                    win_cand(P, E, p2, (int)(b + 2), Hl, hit_lds, d2);
+                    if (!((double)rs - E.r0 > P.win_d)) slow = true;
+                }
+                if (gl) {
+                    const double2 p2 = pos[b - 2];
+                    const float rp = c - 3 >= 0 ? rsp[b - 3].y : -INFINITY;
+                    win_cand(P, E, p2, (int)(b - 2), Hl, hit_lds, d2);
+                    if (!(E.r0 - (double)rp > P.win_d)) slow = true;
+                }
+            }
+        }
+    }
+    if (!act) return;
+    O.w = (int)w;
+    if (!(w >= B.own_lo && w < B.own_hi)) return;
+    const double c0 = quad_c(P, E, 0), c1 = quad_c(P, E, 1), c2 = quad_c(P, E, 2), c3 = quad_c(P, E, 3);
+    if (fin && !slow && !Hl.overflowed() && isfinite(c0) && isfinite(c1) && isfinite(c2) && isfinite(c3)) {
+        double* gq = reinterpret_cast<double*>(hit_lds + kHitCap * kBlock);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) gq[k * kBlock + threadIdx.x] = INFINITY;
+        Hl.template flush_gq<FZ>(hit_lds, gq, P, E, pos, u0);
+        E.bq0 = gq[threadIdx.x] + c0;
+        E.bq1 = gq[kBlock + threadIdx.x] + c1;
+        E.bq2 = gq[2 * kBlock + threadIdx.x] + c2;
+        E.bq3 = gq[3 * kBlock + threadIdx.x] + c3;
+    } else if (fin) {
+        win_direct<FZ>(P, E, w, r, c, W, Kd, Ku, pos, u0, rsp, d2);
+    }
+    O.nbrs = E.count;
+    if (ST) O.d2 = d2;
+    ego_finish<FZ, ST, IN>(P, E, (int)w, (int)(w - B.own_lo), (int)w, T, pos_out, u, status, cnt, hardq, q, qr, O);
+}
+
+// The window-cull filter: one lane per agent in lattice order (the tail of the cell-list filter:
+// solve_fast in place, the rest solved inline (IN) or queued for k_lattice_filter_hard).
+template <bool FZ, bool ST, bool IN>
+__global__ void __launch_bounds__(kBlock) k_window_filter(KP P, WinBounds B, int W, int H, long nwin,
+                                                          const double2* __restrict__ pos,
+                                                          const double2* __restrict__ u0,
+                                                          const float2* __restrict__ rsp,
+                                                          const double* __restrict__ sylo,
+                                                          const double* __restrict__ pyhi,
+                                                          const int32_t* __restrict__ sctl, double T,
+                                                          double2* __restrict__ pos_out, double2* __restrict__ u,
+                                                          int32_t* __restrict__ status, int32_t* __restrict__ cnt,
+                                                          unsigned long long* __restrict__ stats,
+                                                          int32_t* __restrict__ hardq, HardRec* __restrict__ qrec,
+                                                          long qcap) {
+    __shared__ int hit_lds[kHitCap * kBlock + 8 * kBlock];
+    const int bx = xcd_block();
+    const long w = (long)bx * kBlock + threadIdx.x;
+    if (IN && ST && stats && (int)blockIdx.x == (int)gridDim.x - 1 && threadIdx.x < 64) stat_snapshot(stats);
+    if (sctl[2] != 0) {  // the workspace is bound to another shape: report, touch nothing else
+        lattice_error_tail(W, 0, H, 0, nwin, w, u, status, cnt, stats, nullptr, 0, hardq);
+        return;
+    }
+    EgoOut O;
+    O.res = 0;
+    O.w = -1;
+    O.nbrs = 0;
+    O.code = CBF_STATUS_IDLE;
+    O.binding = false;
+    O.seidel = false;
+    O.viol = O.vorig = 0.0;
+    O.d2 = INFINITY;
+    Ego E;
+    window_ego<FZ, ST, IN>(P, B, W, H, w, w < nwin, pos, u0, rsp, sylo, pyhi, T, pos_out, u, status, cnt, hardq,
+                           bx % kSubQ, qrec + (long)(bx % kSubQ) * qcap, hit_lds, E, O);
+    if (ST && stats) {
+        const bool counted = O.res != 0 && O.w >= B.cnt_lo && O.w < B.cnt_hi;
+        wave_stats(stats, (long)bx * (kBlock / 64) + (threadIdx.x >> 6), counted && O.nbrs > 0,
+                   counted && O.seidel, counted && O.res == 1, O.code, O.binding, O.viol, O.vorig,
+                   counted ? O.d2 : INFINITY);
+    }
+}
+
+}  // namespace
+
+namespace cbf {
+
+// window-cull geometry a call can use: whole lattice (no halo), rows of 4 .. 2048 agents
+bool window_cull_ok(int W, int H, long n_ws, const CellWs& Wk) {
+    return W >= 4 && W <= kWinMaxW && H >= 1 && win_guard_bytes(H) <= 16 * (size_t)n_ws && Wk.cs != nullptr;
+}
+
+void window_prep(const CellWs& Wk, int W, int H, const double2* pos, double gain, double2* vel_out,
+                 double2* copy_to, hipStream_t s) {
+    hipLaunchKernelGGL(k_window_prep, dim3(H), dim3(kPrepBlock), 0, s, W, H, pos, Wk.svel, win_rsp(Wk),
+                       win_guard(Wk, H), gain, vel_out, copy_to, Wk.sctl, Wk.ncell);
+}
+
+// The filter kernel of a window-cull advance (pos_out must not overlap pos); the queued QPs are
+// then solved by k_lattice_filter_hard (the caller launches it unless the solve is inline).
+void window_filter(const cbf_params* p, const CellWs& Wk, int W, int H, const double2* pos, double T,
+                   double2* pos_out, double2* u, int32_t* status, int32_t* cnt, unsigned long long* stats, bool in,
+                   hipStream_t s) {
+    const long n = (long)W * H;
+    const KP kp = make_kp(p);
+    const WinBounds B = make_win_bounds(W, 0, n, 0, H, 0, H, 0);
+    const WinGuard Gd = win_guard(Wk, H);
+    const auto filter =
+        in ? (stats ? (p->f_is_zero ? k_window_filter<true, true, true> : k_window_filter<false, true, true>)
+                    : (p->f_is_zero ? k_window_filter<true, false, true> : k_window_filter<false, false, true>))
+           : (stats ? (p->f_is_zero ? k_window_filter<true, true, false> : k_window_filter<false, true, false>)
+                    : (p->f_is_zero ? k_window_filter<true, false, false> : k_window_filter<false, false, false>));
+    hipLaunchKernelGGL(filter, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, kp, B, W, H, n, pos,
+                       (const double2*)Wk.svel, (const float2*)win_rsp(Wk), (const double*)Gd.sylo,
+                       (const double*)Gd.pyhi, (const int32_t*)Wk.sctl, T, pos_out, u, status, cnt, stats, Wk.hardq,
+                       Wk.qrec, Wk.qcap);
+}
+
+}  // namespace cbf

@@ -269,8 +269,17 @@ class LatticeSwarm:
     hipGraph.  Single-GPU: the window is the whole lattice."""
 
     def __init__(self, pos, W, H, gain=0.25, params: FilterParams = None, T=1 / 30, grid=None, margin=1.0,
-                 method="cells", barrier="reference", alpha=(1.0, 1.0), nominal=None):
+                 method="cells", barrier="reference", alpha=(1.0, 1.0), nominal=None, cull="cells"):
         torch = _lib.require_gpu()
+        # cull (reference barrier, cell method): "cells" = the cell-list cull rebuilt every timestep;
+        # "window" = the lattice-window cull (include/cbf_amd.h CBF_RUN_WINDOW_CULL: candidates are the
+        # lattice neighbours, guards prove the rest out of range; bit-identical results, no cell-list
+        # build -- fast while the swarm stays lattice-like, e.g. under consensus)
+        if cull not in ("cells", "window"):
+            raise ValueError(f"cull must be 'cells' or 'window', got {cull!r}")
+        if cull == "window" and (method != "cells" or barrier != "reference" or not 4 <= W <= 2048):
+            raise ValueError("the window cull needs the reference barrier, method='cells' and 4 <= W <= 2048")
+        self.cull = cull
         self.dev = torch.device("cuda")
         pos = np.asarray(pos, dtype=np.float64).reshape(W * H, 2)
         self.W, self.H, self.gain, self.T = W, H, float(gain), float(T)
@@ -329,6 +338,9 @@ class LatticeSwarm:
             self.build_phase()
             self.advance_phase()
             return
+        if self.cull == "window":  # one window-cull timestep (pos advanced in place through the workspace)
+            self._launch_run(1)
+            return
         check(lib.cbf_lattice_step(self.cp, _lib.C.byref(self.grid), self.W, self.H, 0, self.H, 0, self.H,
                                    ptr(self.pos), self.gain, self.T, ptr(self.pos), ptr(self.vel), ptr(self.u),
                                    ptr(self.status), ptr(self.nbr_count), 0, None, self._st(), ptr(self.ws),
@@ -354,6 +366,8 @@ class LatticeSwarm:
             flags = _lib.RUN_OUTPUT_HISTORY
         else:
             vel, u, st, cnt, flags = self.vel, self.u, self.status, self.nbr_count, 0
+        if self.cull == "window":
+            flags |= _lib.RUN_WINDOW_CULL
         check(lib.cbf_lattice_run_ex(self.cp, _lib.C.byref(self.grid), self.W, self.H, ptr(self.pos), self.gain,
                                      self.T, steps, ptr(vel), ptr(u), ptr(st), ptr(cnt), self._st(), ptr(self.ws),
                                      self.ws_bytes, flags, stream_handle()), "cbf_lattice_run_ex")
@@ -365,7 +379,7 @@ class LatticeSwarm:
         control, status and neighbour count (the reference's per-step si_velocities,
         cross_and_rescue.py:159-160) in the arrays of history(steps) instead of the last one only."""
         if self.method != "cells" or self.barrier != "reference":
-            raise ValueError("run() is the fused multi-step path of the reference barrier on the cell list")
+            raise ValueError("run() is the fused multi-step path of the reference barrier (cell method)")
         g = self.run_graphs.get((steps, self.collect_stats, history))
         if g is not None:
             g.replay()
@@ -378,14 +392,33 @@ class LatticeSwarm:
         return self._history(steps)
 
     def build_phase(self):
-        """nominal control + cell list only (K1-K3)."""
+        """nominal control + cell list only (K1-K3); window cull: nominal control + guards."""
+        if self.cull == "window":
+            check(lib.cbf_lattice_window_build(self.cp, _lib.C.byref(self.grid), self.W, self.H, ptr(self.pos),
+                                               self.gain, ptr(self.vel), ptr(self.ws), self.ws_bytes,
+                                               stream_handle()), "cbf_lattice_window_build")
+            return
         check(lib.cbf_lattice_build(self.cp, _lib.C.byref(self.grid), self.W, self.H, 0, self.H, 0, self.H,
                                     ptr(self.pos), self.gain, ptr(self.vel), ptr(self.ws), self.ws_bytes,
                                     stream_handle()), "cbf_lattice_build")
 
-    def advance_phase(self, mark=None):
+    def advance_phase(self, mark=None, commit=True):
         """filter + clip + Euler only (the dominant kernel, K4, then the queued-QP kernel K5).
-        mark: a torch.cuda.Event (already recorded once) that is recorded between K4 and K5."""
+        mark: a torch.cuda.Event (already recorded once) that is recorded between K4 and K5.
+        Window cull: the new positions go to a scratch tensor (the filter reads pos throughout) and
+        are copied into pos unless commit=False (kernel timing)."""
+        if self.cull == "window":
+            torch = _lib.require_gpu()
+            if getattr(self, "_pos_next", None) is None:
+                self._pos_next = torch.empty_like(self.pos)
+            check(lib.cbf_lattice_window_advance(self.cp, _lib.C.byref(self.grid), self.W, self.H, ptr(self.pos),
+                                                 self.T, ptr(self._pos_next), ptr(self.u), ptr(self.status),
+                                                 ptr(self.nbr_count), self._st(), ptr(self.ws), self.ws_bytes,
+                                                 _lib.C.c_void_p(mark.cuda_event if mark is not None else 0),
+                                                 stream_handle()), "cbf_lattice_window_advance")
+            if commit:
+                self.pos.copy_(self._pos_next)
+            return
         if self.barrier == "euclidean_hocbf":
             check(lib.cbf_lattice_advance_hocbf(self.cp, _lib.C.byref(self.hp), _lib.C.byref(self.grid), self.W,
                                                 self.H, 0, self.H, 0, self.H, ptr(self.pos), self.T, ptr(self.pos),
@@ -468,7 +501,7 @@ class LatticeSwarm:
         meta = {"abi_version": int(lib.cbf_abi_version()), "workspace_layout": int(lib.cbf_workspace_layout()),
                 "ws_bytes": int(self.ws_bytes),
                 "W": self.W, "H": self.H, "gain": self.gain, "T": self.T, "method": self.method,
-                "barrier": self.barrier, "alpha": list(self.alpha), "nominal": self.nominal,
+                "barrier": self.barrier, "alpha": list(self.alpha), "nominal": self.nominal, "cull": self.cull,
                 "grid": [self.grid.x0, self.grid.y0, self.grid.inv_h, self.grid.nx, self.grid.ny],
                 "params": {"max_speed": self.params.max_speed, "dmin": self.params.dmin, "k": self.params.k,
                            "safety_distance": self.params.safety_distance,
@@ -502,7 +535,7 @@ class LatticeSwarm:
         nominal = meta["nominal"]
         S = cls(states[0], meta["W"], meta["H"], gain=meta["gain"], params=params, T=meta["T"], grid=g,
                 method=meta["method"], barrier=meta["barrier"], alpha=tuple(meta["alpha"]),
-                nominal=tuple(nominal) if isinstance(nominal, list) else nominal)
+                nominal=tuple(nominal) if isinstance(nominal, list) else nominal, cull=meta.get("cull", "cells"))
         if meta.get("ws_bytes") != S.ws_bytes:
             raise ValueError(f"checkpoint {path}: workspace of {meta.get('ws_bytes')} bytes, this swarm's is "
                              f"{S.ws_bytes}")

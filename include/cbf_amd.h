@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define CBF_ABI_VERSION 4
+#define CBF_ABI_VERSION 5
 
 #define CBF_EINVAL (-1)
 
@@ -280,9 +280,30 @@ int cbf_lattice_run(const cbf_params* p, const cbf_grid* grid, int32_t W, int32_
  * controller that consumes each step's filtered control.  flags = 0 is cbf_lattice_run.
  */
 #define CBF_RUN_OUTPUT_HISTORY 1u
+/* CBF_RUN_WINDOW_CULL: the lattice-window cull instead of the cell list (ABI 5).  Candidates come
+ * straight from the lattice-ordered positions (the lattice neighbours of each ego), and per ego
+ * two guards prove every agent it does not test out of cull range: row y-extents (suffix minima /
+ * prefix maxima over rows) and per-row column x-extents.  Same neighbour sets, bit-identical
+ * results; no cell-list build.  An ego whose neighbours are not lattice-near walks its rows
+ * outward until the guards hold, so any swarm is handled exactly, the faster the more
+ * lattice-like it stays (a consensus lattice: 5 rows x 3 columns of candidates; a scrambled one
+ * degrades towards a whole-row scan -- use the cell list there).  Whole-lattice calls with
+ * 4 <= W <= 2048; the grid argument still sizes and binds the workspace. */
+#define CBF_RUN_WINDOW_CULL 2u
 int cbf_lattice_run_ex(const cbf_params* p, const cbf_grid* grid, int32_t W, int32_t H, double* pos, double gain,
                        double T, int32_t steps, double* vel_out, double* u, int32_t* status, int32_t* nbr_count,
                        uint64_t* solves, void* workspace, size_t workspace_bytes, uint32_t flags, void* stream);
+
+/* The window-cull timestep in two calls, as cbf_lattice_build / cbf_lattice_advance_marked for the
+ * cell list: the build (nominal control into vel_out and the workspace, the guards) and the
+ * advance from the same pos into pos_out (which must not overlap pos), recording filter_done
+ * (nullable hipEvent_t) between the filter kernel and the queued-QP kernel. */
+int cbf_lattice_window_build(const cbf_params* p, const cbf_grid* grid, int32_t W, int32_t H, const double* pos,
+                             double gain, double* vel_out, void* workspace, size_t workspace_bytes, void* stream);
+int cbf_lattice_window_advance(const cbf_params* p, const cbf_grid* grid, int32_t W, int32_t H, const double* pos,
+                               double T, double* pos_out, double* u, int32_t* status, int32_t* nbr_count,
+                               uint64_t* stats, void* workspace, size_t workspace_bytes, void* filter_done,
+                               void* stream);
 
 int cbf_lattice_build(const cbf_params* p, const cbf_grid* grid, int32_t W, int32_t H, int32_t row_begin,
                       int32_t row_end, int32_t win_row0, int32_t win_rows, const double* pos, double gain,

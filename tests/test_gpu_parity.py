@@ -278,21 +278,29 @@ def _check_stats(got, want):
 # (its pick above that: the path the 1 M-agent bench times).  Every lattice test against the oracle
 # runs both, so each is anchored to the oracle on its own.
 PLACEMENTS = ["inline", "queued"]
+# ... and both culls of the lattice step: the cell list, and the lattice-window cull
+# (CBF_RUN_WINDOW_CULL: lattice neighbours as candidates, guards proving the rest out of range)
+VARIANTS = [(pl, cull) for cull in ("cells", "window") for pl in PLACEMENTS]
 
 
 def _fp(placement):
     return swarm.FilterParams(solve_placement=placement)
 
 
-@pytest.mark.parametrize("placement", PLACEMENTS)
+def _kw(variant):
+    placement, cull = variant
+    return {"params": _fp(placement), "cull": cull}
+
+
+@pytest.mark.parametrize("variant", VARIANTS)
 @pytest.mark.parametrize("spacing", [scenarios.LATTICE_SPACING, 0.2])
-def test_lattice_step_vs_oracle(spacing, placement):
+def test_lattice_step_vs_oracle(spacing, variant):
     """Fused lattice steps == oracle steps bit for bit, and the device rollout statistics (status
     counts, OPTIMAL-only and original-row violations, minimum neighbour distance) equal the same
     quantities restated from the oracle's outputs.  Spacing 0.2 is the feasible regime (cfg4f)."""
     W, H = 48, 40
     pos = scenarios.lattice(W, H, seed=5, spacing=spacing)
-    L = swarm.LatticeSwarm(pos, W, H, gain=0.25, params=_fp(placement))
+    L = swarm.LatticeSwarm(pos, W, H, gain=0.25, **_kw(variant))
     ref = pos.copy()
     outs = []
     for step in range(8):
@@ -312,16 +320,16 @@ def test_lattice_step_vs_oracle(spacing, placement):
         assert want["optimal"] > 0.5 * want["solves"] and want["binding"] > 0.1 * want["solves"]
 
 
-@pytest.mark.parametrize("placement", PLACEMENTS)
-def test_lattice_random_nominal_vs_oracle(placement):
+@pytest.mark.parametrize("variant", VARIANTS)
+def test_lattice_random_nominal_vs_oracle(variant):
     """The random-walk nominal control (CBF_NOMINAL_RANDOM, the exact-QP regime cfg4r): fused
     steps == oracle steps bit for bit (nominal controls, controls, statuses, positions, rollout
     statistics); most QPs are feasible with a binding row; cbf_lattice_run (chained binning) and
     a hipGraph of run(4) give the same rollout."""
     W, H, amp, seed = 48, 40, 1.0, 3
     pos = scenarios.lattice(W, H, seed=5, spacing=0.22)
-    fp = _fp(placement)
-    L = swarm.LatticeSwarm(pos, W, H, nominal=("random", amp, seed), params=fp)
+    kw = _kw(variant)
+    L = swarm.LatticeSwarm(pos, W, H, nominal=("random", amp, seed), **kw)
     ref = pos.copy()
     outs = []
     for step in range(8):
@@ -337,12 +345,12 @@ def test_lattice_random_nominal_vs_oracle(placement):
     want = _oracle_stats(outs)
     _check_stats(L.stats_summary(), want)
     assert want["optimal"] > 0.6 * want["solves"] and want["binding"] > 0.4 * want["solves"]
-    B = swarm.LatticeSwarm(pos, W, H, nominal=("random", amp, seed), params=fp)
+    B = swarm.LatticeSwarm(pos, W, H, nominal=("random", amp, seed), **kw)
     B.run(3)
     B.run(5)
     for a, b in zip(_lattice_state(L), _lattice_state(B)):
         assert np.array_equal(a, b)
-    D = swarm.LatticeSwarm(pos, W, H, nominal=("random", amp, seed), params=fp)
+    D = swarm.LatticeSwarm(pos, W, H, nominal=("random", amp, seed), **kw)
     D.capture(steps=4)              # the capture's warm-up launch runs steps 1-4
     D.run(4)
     for a, b in zip(_lattice_state(L), _lattice_state(D)):
@@ -373,9 +381,9 @@ def _lattice_state(L):
         [np.array([st[k] for k in sorted(st)], dtype=object)]
 
 
-@pytest.mark.parametrize("placement", PLACEMENTS)
+@pytest.mark.parametrize("variant", VARIANTS)
 @pytest.mark.parametrize("spacing", [scenarios.LATTICE_SPACING, 0.2])
-def test_lattice_run_matches_steps(spacing, placement):
+def test_lattice_run_matches_steps(spacing, variant):
     """cbf_lattice_run (chained binning: each advance bins the next timestep) == the same number of
     cbf_lattice_step calls, bit for bit: positions, last-step outputs and every statistics word,
     in one call, split over calls, and replayed from a hipGraph of run(4).  The first 3 steps of
@@ -383,8 +391,8 @@ def test_lattice_run_matches_steps(spacing, placement):
     the queued placement the chained binning of the queued egos runs in the queue kernel."""
     W, H = 256, 192
     pos = scenarios.lattice(W, H, seed=11, spacing=spacing)
-    fp = _fp(placement)
-    A = swarm.LatticeSwarm(pos, W, H, params=fp)
+    kw = _kw(variant)
+    A = swarm.LatticeSwarm(pos, W, H, **kw)
     ref = pos.copy()
     states = {}
     for k in range(1, 17):
@@ -395,16 +403,16 @@ def test_lattice_run_matches_steps(spacing, placement):
             assert np.array_equal(A.pos.cpu().numpy(), ref), k
         if k in (12, 16):
             states[k] = _lattice_state(A)
-    B = swarm.LatticeSwarm(pos, W, H, params=fp)
+    B = swarm.LatticeSwarm(pos, W, H, **kw)
     B.run(12)
     for a, b in zip(states[12], _lattice_state(B)):
         assert np.array_equal(a, b)
-    C = swarm.LatticeSwarm(pos, W, H, params=fp)
+    C = swarm.LatticeSwarm(pos, W, H, **kw)
     for n in (1, 5, 6):
         C.run(n)
     for a, b in zip(states[12], _lattice_state(C)):
         assert np.array_equal(a, b)
-    D = swarm.LatticeSwarm(pos, W, H, params=fp)
+    D = swarm.LatticeSwarm(pos, W, H, **kw)
     D.capture(steps=4)              # the capture's warm-up launch runs steps 1-4
     for _ in range(3):
         D.run(4)
@@ -448,18 +456,18 @@ def test_lattice_run_output_history():
     assert torch.equal(C.pos, B.pos) and torch.equal(C.u, B.history(5)[1][4])
 
 
-@pytest.mark.parametrize("placement", PLACEMENTS)
+@pytest.mark.parametrize("variant", VARIANTS)
 @pytest.mark.parametrize("nominal", [None, ("random", 0.05, 3)])
-def test_lattice_stats_off_and_replay(nominal, placement):
+def test_lattice_stats_off_and_replay(nominal, variant):
     """The bench's timed path: run() with stats=NULL (graphs of both modes captured) gives the same
     trajectory bit for bit as with the statistics on, and snapshot()/restore() makes the statistics
     replay repeat a stats-off rollout exactly (positions, outputs), with the replay's statistics
     equal to those of a stats-on rollout from the start (incl. the random-walk nominal state)."""
     W, H = 128, 96
     pos = scenarios.lattice(W, H, seed=5, spacing=0.2)
-    A = swarm.LatticeSwarm(pos, W, H, nominal=nominal, params=_fp(placement))
+    A = swarm.LatticeSwarm(pos, W, H, nominal=nominal, **_kw(variant))
     A.run(6)
-    B = swarm.LatticeSwarm(pos, W, H, nominal=nominal, params=_fp(placement))
+    B = swarm.LatticeSwarm(pos, W, H, nominal=nominal, **_kw(variant))
     B.collect_stats = False
     B.capture(steps=3)              # runs steps 1-3 (stats off)
     B.collect_stats = True
@@ -468,7 +476,7 @@ def test_lattice_stats_off_and_replay(nominal, placement):
     torch.cuda.synchronize()
     assert torch.equal(A.pos, B.pos) and torch.equal(A.u, B.u) and torch.equal(A.status, B.status)
     snap = B.snapshot()
-    ref = swarm.LatticeSwarm(pos, W, H, nominal=nominal, params=_fp(placement))
+    ref = swarm.LatticeSwarm(pos, W, H, nominal=nominal, **_kw(variant))
     ref.run(6)
     ref.reset_solves()
     ref.run(8)                      # the statistics of steps 7-14 alone
@@ -939,22 +947,22 @@ def _oracle_window_step(pos, W, H, gain, threads=16):
     return coracle.euler(pos, out["u"], 1 / 30), vel, out
 
 
-@pytest.mark.parametrize("placement", ["auto", "inline"])
-def test_large_window_run_vs_oracle_every_timestep(placement):
+@pytest.mark.parametrize("placement,cull", [("auto", "cells"), ("inline", "cells"), ("auto", "window")])
+def test_large_window_run_vs_oracle_every_timestep(placement, cull):
     """The bench's timed path on a window above the inline threshold (1024 x 136 = 139,264 agents >
     131,072): the shipped cbf_lattice_run with stats = NULL -- auto places the full solves in the
     queue kernel, whose chained binning feeds the next timestep -- checked bit for bit against the
     oracle at EVERY timestep (nominal control, filtered control, status, neighbour count, and the
     positions they imply), through run(4, history=True) (every timestep's outputs stored) and a
     plain run(4) (the bench's form: outputs of the last timestep only).  "inline" forces the other
-    placement on the same window."""
+    placement on the same window; "window" runs the lattice-window cull (its queued path)."""
     W, H, steps = 1024, 136, 4
     pos = scenarios.lattice(W, H, seed=17)
     fp = _fp(placement)
-    A = swarm.LatticeSwarm(pos, W, H, params=fp)
+    A = swarm.LatticeSwarm(pos, W, H, params=fp, cull=cull)
     A.collect_stats = False
     A.run(steps, history=True)
-    B = swarm.LatticeSwarm(pos, W, H, params=fp)
+    B = swarm.LatticeSwarm(pos, W, H, params=fp, cull=cull)
     B.collect_stats = False
     B.run(steps)
     torch.cuda.synchronize()
@@ -971,6 +979,6 @@ def test_large_window_run_vs_oracle_every_timestep(placement):
     assert np.array_equal(B.pos.cpu().numpy(), ref)
     assert np.array_equal(B.u.cpu().numpy(), out["u"]) and np.array_equal(B.status.cpu().numpy(), out["status"])
     # the window holds full solves (the queue kernel has work under "auto")
-    C = swarm.LatticeSwarm(pos, W, H, params=fp)
+    C = swarm.LatticeSwarm(pos, W, H, params=fp, cull=cull)
     C.run(steps)
     assert C.stats_summary()["seidel"] > 0

@@ -1,0 +1,172 @@
+"""The lattice-window cull (include/cbf_amd.h CBF_RUN_WINDOW_CULL, cbf_amd/csrc/window.hip) against
+the C oracle's O(N) reference cull (cross_and_rescue.py:141-150) on swarms chosen to break every
+shortcut the window takes: agents far from their lattice site, rows out of x order, a dense clump
+that overflows the hit list, coincident agents, non-finite positions, narrow and short lattices.
+The cull decides only which candidates are tested; results must be the cell list's and the
+oracle's bit for bit whatever the swarm looks like."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+if not torch.cuda.is_available():  # collected on CPU boxes but never run there
+    pytest.skip("needs a ROCm GPU", allow_module_level=True)
+
+from cbf_amd import scenarios, swarm  # noqa: E402
+from oracle import coracle, pyoracle as po  # noqa: E402
+
+GAIN = 0.25
+
+
+def _oracle_rollout(pos, W, H, steps):
+    ref = pos.copy()
+    outs = []
+    for _ in range(steps):
+        vel = coracle.consensus_lattice(W, H, 0, H, ref, GAIN)
+        out = coracle.filter_swarm(po.Params(15), ref, vel, 0)
+        ref = coracle.euler(ref, out["u"], 1 / 30)
+        outs.append((vel, out, ref.copy()))
+    return outs
+
+
+def _check_steps(pos, W, H, steps, placement="auto", equal_nan=False):
+    """step() of the window cull and of the cell list, every timestep against the oracle."""
+    runs = [swarm.LatticeSwarm(pos, W, H, gain=GAIN, params=swarm.FilterParams(solve_placement=placement), cull=c)
+            for c in ("window", "cells")]
+    for t, (vel, out, ref) in enumerate(_oracle_rollout(pos, W, H, steps)):
+        for L in runs:
+            L.step()
+            torch.cuda.synchronize()
+            tag = (L.cull, t)
+            assert np.array_equal(L.vel.cpu().numpy(), vel, equal_nan=equal_nan), tag
+            assert np.array_equal(L.u.cpu().numpy(), out["u"], equal_nan=equal_nan), tag
+            assert np.array_equal(L.status.cpu().numpy(), out["status"]), tag
+            assert np.array_equal(L.nbr_count.cpu().numpy(), out["cnt"]), tag
+            assert np.array_equal(L.pos.cpu().numpy(), ref, equal_nan=equal_nan), tag
+    return runs
+
+
+@pytest.mark.parametrize("placement", ["inline", "queued"])
+def test_window_scrambled_lattice_vs_oracle(placement):
+    """Agents swapped with far-away ones (a lattice index no longer says where an agent is), so
+    the row and column guards fail for their neighbours and those egos walk their rows outward;
+    plus coincident agents (s = 0: not neighbours) and an exact-cutoff pair."""
+    W, H = 64, 48
+    pos = scenarios.lattice(W, H, seed=21)
+    rng = np.random.default_rng(4)
+    a = rng.choice(W * H, 40, replace=False)
+    b = rng.choice(W * H, 40, replace=False)
+    pos[a], pos[b] = pos[b].copy(), pos[a].copy()
+    pos[100] = pos[101]                        # coincident pair
+    pos[300] = pos[301] + np.array([0.2, 0.0])  # s == 0.04 exactly is out (sqrt(s) < 0.2 fails)
+    _check_steps(pos, W, H, 5, placement)
+
+
+def test_window_dense_clump_overflows_hit_list():
+    """25 agents packed in a 0.1-wide square: > 16 hits per ego (the hit list's cap), so those
+    egos take the direct-assembly walk; the rows they sit in are far out of x order."""
+    W, H = 48, 40
+    pos = scenarios.lattice(W, H, seed=22)
+    rng = np.random.default_rng(5)
+    idx = rng.choice(W * H, 25, replace=False)
+    pos[idx] = np.array([1.0, 1.0]) + 0.1 * rng.random((25, 2))
+    runs = _check_steps(pos, W, H, 4)
+    assert runs[0].nbr_count.cpu().numpy().max() > 16
+
+
+def test_window_unsorted_rows_vs_oracle():
+    """Every other lattice row reversed in x (its column extents then exclude nothing nearby):
+    correct, by the unbounded walk, however un-lattice-like."""
+    W, H = 40, 24
+    pos = scenarios.lattice(W, H, seed=23).reshape(H, W, 2)
+    pos[1::2] = pos[1::2, ::-1]
+    _check_steps(pos.reshape(-1, 2).copy(), W, H, 3)
+
+
+@pytest.mark.parametrize("W,H", [(4, 1), (4, 6), (5, 3), (70, 9), (130, 2), (2048, 2)])
+def test_window_edge_shapes(W, H):
+    """Narrow, short and wide lattices: candidates and sentinels beyond the row ends and beyond the
+    first / last row, a window of one row, rows of several waves."""
+    pos = scenarios.lattice(W, H, seed=24, spacing=0.15)
+    _check_steps(pos, W, H, 3)
+
+
+def test_window_nonfinite_positions_match_cells():
+    """Non-finite positions (NaN, +-inf) never pass the cull test and are left out of the guards'
+    extents; the window cull then gives the cell list's results bit for bit (NaNs compared as
+    equal)."""
+    W, H = 48, 32
+    pos = scenarios.lattice(W, H, seed=25)
+    pos[10] = [np.nan, 0.3]
+    pos[500] = [np.inf, pos[500, 1]]
+    pos[900] = [pos[900, 0], -np.inf]
+    A = swarm.LatticeSwarm(pos, W, H, gain=GAIN, cull="window")
+    B = swarm.LatticeSwarm(pos, W, H, gain=GAIN, cull="cells")
+    for _ in range(3):
+        A.step()
+        B.step()
+        torch.cuda.synchronize()
+        for x, y in ((A.pos, B.pos), (A.u, B.u), (A.vel, B.vel)):
+            assert np.array_equal(x.cpu().numpy(), y.cpu().numpy(), equal_nan=True)
+        assert torch.equal(A.status, B.status) and torch.equal(A.nbr_count, B.nbr_count)
+
+
+@pytest.mark.parametrize("nominal", [None, ("random", 1.0, 5)])
+def test_window_run_equals_cells_run(nominal):
+    """run() (odd and even step counts: the ping-pong through the workspace), a hipGraph of run(4)
+    and the statistics are the cell list's bit for bit, on the consensus lattice and on cfg4r's
+    random walk (which scrambles the lattice: more and more egos walk their rows outward)."""
+    W, H = 160, 128
+    pos = scenarios.lattice(W, H, seed=26, spacing=0.145 if nominal is None else 0.22)
+    res = {}
+    for cull in ("cells", "window"):
+        A = swarm.LatticeSwarm(pos, W, H, gain=GAIN, nominal=nominal, cull=cull)
+        A.run(3)
+        A.capture(steps=4)   # warm-up launch: timesteps 4-7
+        A.run(4)             # replay: 8-11
+        A.run(1)
+        torch.cuda.synchronize()
+        st = A.stats_summary()
+        res[cull] = [t.cpu().numpy() for t in (A.pos, A.vel, A.u, A.status, A.nbr_count)] + \
+            [np.array([st[k] for k in sorted(st)], dtype=object)]
+    for a, b in zip(res["cells"], res["window"]):
+        assert np.array_equal(a, b)
+
+
+def test_window_advance_phase_marked_equals_step():
+    """build_phase() + advance_phase(mark) of the window cull (the bench's measurement hook) ==
+    one step(), and the event lands inside the advance."""
+    W, H = 96, 64
+    pos = scenarios.lattice(W, H, seed=27, spacing=0.2)
+    A = swarm.LatticeSwarm(pos, W, H, cull="window")
+    B = swarm.LatticeSwarm(pos, W, H, cull="window")
+    A.step()
+    B.build_phase()
+    a, m, b = (torch.cuda.Event(enable_timing=True) for _ in range(3))
+    m.record()
+    a.record()
+    B.advance_phase(mark=m)
+    b.record()
+    torch.cuda.synchronize()
+    assert torch.equal(A.pos, B.pos) and torch.equal(A.u, B.u) and torch.equal(A.status, B.status)
+    assert torch.equal(A.vel, B.vel)
+    assert 0 <= a.elapsed_time(m) <= a.elapsed_time(b)
+
+
+def test_window_full_size_cfg4_equals_cells():
+    """cfg4 at full size (1024 x 1024), 12 timesteps: the window cull's rollout == the cell list's
+    (which the oracle tests pin) bit for bit, statistics included."""
+    W = H = 1024
+    pos = scenarios.lattice(W, H, seed=0)
+    res = {}
+    for cull in ("cells", "window"):
+        A = swarm.LatticeSwarm(pos, W, H, cull=cull)
+        A.run(12)
+        torch.cuda.synchronize()
+        st = A.stats_summary()
+        res[cull] = [t.cpu().numpy() for t in (A.pos, A.vel, A.u, A.status, A.nbr_count)] + \
+            [np.array([st[k] for k in sorted(st)], dtype=object)]
+        del A
+    for a, b in zip(res["cells"], res["window"]):
+        assert np.array_equal(a, b)
