@@ -46,12 +46,12 @@ inline WinGuard win_guard(const CellWs& Wk, int H) {
     WinGuard g;
     char* p = reinterpret_cast<char*>(Wk.cs);
     g.ticket = Wk.sctl + 16;
-    g.rowy = reinterpret_cast<double*>(p + 256);
+    g.rowy = reinterpret_cast<double*>(p);
     g.sylo = g.rowy + 2l * H;
     g.pyhi = g.sylo + (H + 1);
     return g;
 }
-inline size_t win_guard_bytes(int H) { return 256 + 8 * (size_t)(4l * H + 1); }
+inline size_t win_guard_bytes(int H) { return 8 * (size_t)(4l * H + 1); }  // <= 16 W H for W >= 4
 // the column extents, one float2 {rs, rp} per agent, in the scratch area (wvel, 16 B per agent)
 inline float2* win_rsp(const CellWs& Wk) { return reinterpret_cast<float2*>(Wk.wvel); }
 
