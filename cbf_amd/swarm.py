@@ -59,8 +59,13 @@ def make_grid(xmin, ymin, xmax, ymax, cell):
 
 
 def grid_for_points(pos_np, cull_radius, margin=1.0, cell_factor=1.02):
-    lo = pos_np.min(axis=0) - margin
-    hi = pos_np.max(axis=0) + margin
+    """A grid over the finite points (+ margin); agents outside it are clamped into the edge cells,
+    and non-finite ones never pass the cull test anyway."""
+    fin = pos_np[np.isfinite(pos_np).all(axis=1)]
+    if fin.shape[0] == 0:
+        fin = np.zeros((1, 2))
+    lo = fin.min(axis=0) - margin
+    hi = fin.max(axis=0) + margin
     return make_grid(lo[0], lo[1], hi[0], hi[1], cull_radius * cell_factor)
 
 
