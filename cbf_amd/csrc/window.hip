@@ -30,6 +30,9 @@ using namespace cbf;
 
 namespace {
 
+#ifndef CBF_WIN_G
+#define CBF_WIN_G 3  // rows whose candidate loads the window filter issues together
+#endif
 constexpr int kPrepBlock = 256;
 constexpr int kPrepPer = 8;  // columns per prep thread: rows of up to 2048 agents
 constexpr int kWinMaxW = kPrepBlock * kPrepPer;
@@ -133,62 +136,96 @@ __device__ __forceinline__ double ld_sc1_f64(const double* p) {
 // rsp; per row its y extents.  The last block to finish (a ticket; the guide's sc1 hand-off: sc1
 // stores, every storing wave's vmcnt(0), a block barrier, one agent-scope add, sc1 loads by the
 // block whose add came last) turns the row extents into sylo / pyhi.  copy_to (nullable) gets a
-// copy of the positions (the run's ping-pong start).
+// copy of the positions (the run's ping-pong start).  The row is staged in LDS (dynamic, 24 B per
+// column): every global load and store is coalesced, and the row scans run over contiguous
+// chunks of it.
 __global__ void __launch_bounds__(kPrepBlock) k_window_prep(int W, int H, const double2* __restrict__ pos,
                                                             double2* __restrict__ u0, float2* __restrict__ rsp,
                                                             WinGuard Gd, double gain, double2* __restrict__ vel_out,
                                                             double2* __restrict__ copy_to, int32_t* __restrict__ sctl,
                                                             long ncell) {
+    extern __shared__ double2 srow[];  // [W] positions, then [W] float2 {rs, rp}
+    float2* srsp = reinterpret_cast<float2*>(srow + W);
     __shared__ double red[kPrepBlock / 64];
     __shared__ int last;
     const int r = xcd_block();
     const long nwin = (long)W * H;
     if (r == 0 && threadIdx.x == 0) build_begin(sctl, nwin, ncell);
     const NominalSpec N = nominal_spec(sctl);
-    const int m = (W + kPrepBlock - 1) / kPrepBlock;
-    const int c0 = threadIdx.x * m;
-    const long row = (long)r * W;
-    double xs[kPrepPer];
-    bool fin[kPrepPer];
+    const double2* prow = pos + (long)r * W;
+#pragma unroll
+    for (int j = 0; j < kPrepPer; ++j) {
+        const int c = threadIdx.x + j * kPrepBlock;
+        if (c < W) {
+            const double2 p = prow[c];
+            srow[c] = p;
+            if (copy_to) copy_to[(long)r * W + c] = p;
+        }
+    }
+    __syncthreads();
+    // nominal controls (coalesced: column c = thread + j * block) and the row's y extents
     double ylo = INFINITY, yhi = -INFINITY;
 #pragma unroll
     for (int j = 0; j < kPrepPer; ++j) {
-        xs[j] = 0.0;
-        fin[j] = false;
-        const int c = c0 + j;
-        if (j < m && c < W) {
-            const long w = row + c;
-            const double2 p = pos[w];
-            double2 a;
-            if (N.mode == CBF_NOMINAL_RANDOM) {
-                a = random_nominal(N, w, p);
-            } else {
-                const double2 s = lattice_sum(pos, w, r, c, W, H);
-                a = make_double2(s.x * gain, s.y * gain);
+        const int c = threadIdx.x + j * kPrepBlock;
+        if (c >= W) continue;
+        const long w = (long)r * W + c;
+        const double2 pi = srow[c];
+        double2 a;
+        if (N.mode == CBF_NOMINAL_RANDOM) {
+            a = random_nominal(N, w, pi);
+        } else {  // lattice_sum's neighbour order and arithmetic: (r-1, c), (r, c-1), (r, c+1), (r+1, c)
+            const double2 qu = r > 0 ? prow[c - W] : pi;
+            const double2 qd = r < H - 1 ? prow[c + W] : pi;
+            double a0 = 0.0, a1 = 0.0;
+            if (r > 0) {
+                a0 = a0 + (qu.x - pi.x);
+                a1 = a1 + (qu.y - pi.y);
             }
-            u0[w] = a;
-            if (vel_out) vel_out[w] = a;
-            if (copy_to) copy_to[w] = p;
-            fin[j] = isfinite(p.x) && isfinite(p.y);
-            xs[j] = p.x;
-            if (fin[j]) {
-                ylo = pmin(ylo, p.y);
-                yhi = pmax(yhi, p.y);
+            if (c > 0) {
+                const double2 q = srow[c - 1];
+                a0 = a0 + (q.x - pi.x);
+                a1 = a1 + (q.y - pi.y);
             }
+            if (c < W - 1) {
+                const double2 q = srow[c + 1];
+                a0 = a0 + (q.x - pi.x);
+                a1 = a1 + (q.y - pi.y);
+            }
+            if (r < H - 1) {
+                a0 = a0 + (qd.x - pi.x);
+                a1 = a1 + (qd.y - pi.y);
+            }
+            a = make_double2(a0 * gain, a1 * gain);
+        }
+        u0[w] = a;
+        if (vel_out) vel_out[w] = a;
+        if (isfinite(pi.x) && isfinite(pi.y)) {
+            ylo = pmin(ylo, pi.y);
+            yhi = pmax(yhi, pi.y);
         }
     }
-    // column extents: suffix minimum / prefix maximum of x along the row (finite agents)
+    // column extents: suffix minimum / prefix maximum of x along the row over the finite agents,
+    // each thread over its contiguous chunk of m columns, then across the threads
+    const int m = (W + kPrepBlock - 1) / kPrepBlock;
+    const int c0 = threadIdx.x * m;
     double sm[kPrepPer], pm[kPrepPer];
     double acc = INFINITY;
 #pragma unroll
     for (int j = kPrepPer - 1; j >= 0; --j) {
-        if (fin[j]) acc = pmin(acc, xs[j]);
+        if (j < m && c0 + j < W) {
+            const double2 p = srow[c0 + j];
+            if (isfinite(p.x) && isfinite(p.y)) acc = pmin(acc, p.x);
+        }
         sm[j] = acc;
     }
     acc = -INFINITY;
 #pragma unroll
     for (int j = 0; j < kPrepPer; ++j) {
-        if (fin[j]) acc = pmax(acc, xs[j]);
+        if (j < m && c0 + j < W) {
+            const double2 p = srow[c0 + j];
+            if (isfinite(p.x) && isfinite(p.y)) acc = pmax(acc, p.x);
+        }
         pm[j] = acc;
     }
     double tot;
@@ -197,12 +234,17 @@ __global__ void __launch_bounds__(kPrepBlock) k_window_prep(int W, int H, const 
 #pragma unroll
     for (int j = 0; j < kPrepPer; ++j) {
         const int c = c0 + j;
-        if (j < m && c < W) rsp[row + c] = make_float2(f32_down(pmin(sm[j], after)), f32_up(pmax(pm[j], before)));
+        if (j < m && c < W) srsp[c] = make_float2(f32_down(pmin(sm[j], after)), f32_up(pmax(pm[j], before)));
     }
     // row y extents
     double lo, hi;
-    (void)block_after_min(ylo, red, &lo);
+    (void)block_after_min(ylo, red, &lo);   // (its barriers also order the srsp writes above)
     (void)block_before_max(yhi, red, &hi);
+#pragma unroll
+    for (int j = 0; j < kPrepPer; ++j) {
+        const int c = threadIdx.x + j * kPrepBlock;
+        if (c < W) rsp[(long)r * W + c] = srsp[c];
+    }
     if (threadIdx.x == 0) {
         st_sc1_f64(&Gd.rowy[2l * r], lo);
         st_sc1_f64(&Gd.rowy[2l * r + 1], hi);
@@ -273,13 +315,35 @@ __device__ __forceinline__ void win_cand(const KP& P, const Ego& E, double2 p, i
     }
 }
 
-// The rows of an ego at window row r, y: [r - Kd, r + Ku] (rows beyond are out of range).
+// The rows of an ego at window row r, y: [r - Kd, r + Ku] (rows beyond are out of range).  The
+// first kWinPre bounds each way are loaded together (sylo is non-decreasing and pyhi
+// non-increasing away from r, so the test is monotone in k and Ku counts its failures); a window
+// taller than that continues one row at a time.
+constexpr int kWinPre = 4;
 __device__ __forceinline__ void win_rows(const KP& P, const double* __restrict__ sylo,
                                          const double* __restrict__ pyhi, int r, int H, double y, int& Kd, int& Ku) {
+    double su[kWinPre], pd[kWinPre];
+#pragma unroll
+    for (int k = 0; k < kWinPre; ++k) {
+        su[k] = r + k + 1 < H ? sylo[r + k + 1] : INFINITY;  // beyond the last row: nothing to exclude
+        pd[k] = r - k - 1 >= 0 ? pyhi[r - k - 1] : -INFINITY;
+    }
     Ku = 0;
-    while (r + Ku + 1 < H && !(sylo[r + Ku + 1] - y > P.win_d)) ++Ku;
     Kd = 0;
-    while (r - Kd - 1 >= 0 && !(y - pyhi[r - Kd - 1] > P.win_d)) ++Kd;
+#pragma unroll
+    for (int k = 0; k < kWinPre; ++k) {
+        Ku += !(su[k] - y > P.win_d) ? 1 : 0;
+        Kd += !(y - pd[k] > P.win_d) ? 1 : 0;
+    }
+    if (Ku == kWinPre)
+        while (r + Ku + 1 < H && !(sylo[r + Ku + 1] - y > P.win_d)) ++Ku;
+    if (Kd == kWinPre)
+        while (r - Kd - 1 >= 0 && !(y - pyhi[r - Kd - 1] > P.win_d)) ++Kd;
+}
+
+// 32-bit byte offsets into the lattice-ordered arrays (windows of < 2^28 agents, check_lattice)
+__device__ __forceinline__ float2 ld_rsp(const float2* __restrict__ a, int t) {
+    return *reinterpret_cast<const float2*>(reinterpret_cast<const char*>(a) + ((uint32_t)t << 3));
 }
 
 // The unbounded form for one lane (rare): every row of [r - Kd, r + Ku] walked outward from the
@@ -342,37 +406,69 @@ __device__ __forceinline__ void window_ego(const KP& P, const WinBounds& B, int 
     // rows whose sentinel at c + 2 (R) / c - 2 (L) does not hold: bit dr + KdW
     unsigned long long pR = 0, pL = 0;
     bool slow = KdW + KuW + 1 > 64;  // (a window that tall takes the unbounded form)
+    const int wi = (int)w;
     if (!slow) {
-        for (int dr = -KdW; dr <= KuW; ++dr) {
-            if (!(fin && dr >= -Kd && dr <= Ku)) continue;
-            const long b = w + (long)dr * W;
-            const double2 pm = c > 0 ? pos[b - 1] : make_double2(INFINITY, INFINITY);
-            const double2 p0 = pos[b];
-            const double2 pp = c + 1 < W ? pos[b + 1] : make_double2(INFINITY, INFINITY);
-            const float rs = c + 2 < W ? rsp[b + 2].x : INFINITY;
-            const float rp = c - 2 >= 0 ? rsp[b - 2].y : -INFINITY;
-            win_cand(P, E, pm, (int)(b - 1), Hl, hit_lds, d2);
-            win_cand(P, E, p0, (int)b, Hl, hit_lds, d2);
-            win_cand(P, E, pp, (int)(b + 1), Hl, hit_lds, d2);
-            if (!((double)rs - E.r0 > P.win_d)) pR |= 1ull << (dr + KdW);
-            if (!(E.r0 - (double)rp > P.win_d)) pL |= 1ull << (dr + KdW);
+        // columns c - 1 .. c + 1 of every row, G rows' loads in flight at a time
+        constexpr int G = CBF_WIN_G;
+        for (int dr0 = -KdW; dr0 <= KuW; dr0 += G) {
+            double2 pm[G], p0[G], pp[G];
+            float rs[G], rp[G];
+            bool a[G];
+#pragma unroll
+            for (int i = 0; i < G; ++i) {
+                const int dr = dr0 + i;
+                a[i] = fin && dr <= KuW && dr >= -Kd && dr <= Ku;
+                if (a[i]) {
+                    const int b = wi + dr * W;
+                    pm[i] = c > 0 ? ld_slot(pos, b - 1) : make_double2(INFINITY, INFINITY);
+                    p0[i] = ld_slot(pos, b);
+                    pp[i] = c + 1 < W ? ld_slot(pos, b + 1) : make_double2(INFINITY, INFINITY);
+                    rs[i] = c + 2 < W ? ld_rsp(rsp, b + 2).x : INFINITY;
+                    rp[i] = c - 2 >= 0 ? ld_rsp(rsp, b - 2).y : -INFINITY;
+                }
+            }
+#pragma unroll
+            for (int i = 0; i < G; ++i) {
+                if (!a[i]) continue;
+                const int b = wi + (dr0 + i) * W;
+                win_cand(P, E, pm[i], b - 1, Hl, hit_lds, d2);
+                win_cand(P, E, p0[i], b, Hl, hit_lds, d2);
+                win_cand(P, E, pp[i], b + 1, Hl, hit_lds, d2);
+                if (!((double)rs[i] - E.r0 > P.win_d)) pR |= 1ull << (dr0 + i + KdW);
+                if (!(E.r0 - (double)rp[i] > P.win_d)) pL |= 1ull << (dr0 + i + KdW);
+            }
         }
         if (__ballot((pR | pL) != 0)) {  // columns c -+ 2 where a sentinel did not hold
-            for (int dr = -KdW; dr <= KuW; ++dr) {
-                const bool gr = (pR >> (dr + KdW)) & 1ull, gl = (pL >> (dr + KdW)) & 1ull;
-                if (!(gr || gl)) continue;
-                const long b = w + (long)dr * W;
-                if (gr) {  // c + 2 < W here (the sentinel beyond the edge holds)
-                    const double2 p2 = pos[b + 2];
-                    const float rs = c + 3 < W ? rsp[b + 3].x : INFINITY;
-                    win_cand(P, E, p2, (int)(b + 2), Hl, hit_lds, d2);
-                    if (!((double)rs - E.r0 > P.win_d)) slow = true;
+            for (int dr0 = -KdW; dr0 <= KuW; dr0 += G) {
+                double2 q2r[G], q2l[G];
+                float rs[G], rp[G];
+                bool gr[G], gl[G];
+#pragma unroll
+                for (int i = 0; i < G; ++i) {
+                    const int bit = dr0 + i + KdW;
+                    gr[i] = bit < 64 && ((pR >> bit) & 1ull);
+                    gl[i] = bit < 64 && ((pL >> bit) & 1ull);
+                    const int b = wi + (dr0 + i) * W;
+                    if (gr[i]) {  // c + 2 < W here (the sentinel beyond the row end holds)
+                        q2r[i] = ld_slot(pos, b + 2);
+                        rs[i] = c + 3 < W ? ld_rsp(rsp, b + 3).x : INFINITY;
+                    }
+                    if (gl[i]) {
+                        q2l[i] = ld_slot(pos, b - 2);
+                        rp[i] = c - 3 >= 0 ? ld_rsp(rsp, b - 3).y : -INFINITY;
+                    }
                 }
-                if (gl) {
-                    const double2 p2 = pos[b - 2];
-                    const float rp = c - 3 >= 0 ? rsp[b - 3].y : -INFINITY;
-                    win_cand(P, E, p2, (int)(b - 2), Hl, hit_lds, d2);
-                    if (!(E.r0 - (double)rp > P.win_d)) slow = true;
+#pragma unroll
+                for (int i = 0; i < G; ++i) {
+                    const int b = wi + (dr0 + i) * W;
+                    if (gr[i]) {
+                        win_cand(P, E, q2r[i], b + 2, Hl, hit_lds, d2);
+                        if (!((double)rs[i] - E.r0 > P.win_d)) slow = true;
+                    }
+                    if (gl[i]) {
+                        win_cand(P, E, q2l[i], b - 2, Hl, hit_lds, d2);
+                        if (!(E.r0 - (double)rp[i] > P.win_d)) slow = true;
+                    }
                 }
             }
         }
@@ -452,7 +548,7 @@ bool window_cull_ok(int W, int H, long n_ws, const CellWs& Wk) {
 
 void window_prep(const CellWs& Wk, int W, int H, const double2* pos, double gain, double2* vel_out,
                  double2* copy_to, hipStream_t s) {
-    hipLaunchKernelGGL(k_window_prep, dim3(H), dim3(kPrepBlock), 0, s, W, H, pos, Wk.svel, win_rsp(Wk),
+    hipLaunchKernelGGL(k_window_prep, dim3(H), dim3(kPrepBlock), 24 * (size_t)W, s, W, H, pos, Wk.svel, win_rsp(Wk),
                        win_guard(Wk, H), gain, vel_out, copy_to, Wk.sctl, Wk.ncell);
 }
 
