@@ -70,3 +70,15 @@ int build_cells(const CellGrid& G, const CellWs& W, int n, const double2* pos, c
 }  // namespace cbf
 
 extern "C" int cbf_workspace_layout(void) { return cbf::kWorkspaceLayout; }
+
+extern "C" int64_t cbf_lattice_workspace_view(int32_t W, int32_t win_rows, const cbf_grid* grid, int64_t* off) {
+    if (!grid || !off || W <= 0 || win_rows <= 0 || grid->nx <= 0 || grid->ny <= 0) return CBF_EINVAL;
+    const long n = (long)W * win_rows, ncell = (long)grid->nx * grid->ny;
+    const uintptr_t base = 4096;  // the carve-up only adds offsets to its base
+    cbf::CellWs Wk(reinterpret_cast<void*>(base), n, ncell);
+    off[0] = (int64_t)(reinterpret_cast<uintptr_t>(Wk.start) - base);
+    off[1] = (int64_t)(reinterpret_cast<uintptr_t>(Wk.spos) - base);
+    off[2] = (int64_t)(reinterpret_cast<uintptr_t>(Wk.svel) - base);
+    off[3] = (int64_t)(reinterpret_cast<uintptr_t>(Wk.sidx) - base);
+    return ncell;
+}

@@ -192,9 +192,16 @@ __device__ __forceinline__ void store_sc1_x4(int32_t* p, int4 v) {
 // a tile's done word for scan epoch e: never 0, so a zero-filled workspace holds no done tile
 __device__ __forceinline__ int32_t tile_done_word(unsigned e) { return (int32_t)((e & 0x3FFFFFFFu) | 0x40000000u); }
 
-// `tdone` (may be null): tile -> its done word (tile_done_word(epoch)), published once the tile's starts are written (with an
-// agent-scope release), for a kernel that consumes the starts while the scan runs
-// (k_lattice_scan_scatter).  Every thread of the block must call it.
+// `tdone` (may be null): tile -> its done word (tile_done_word(epoch)), published once the tile's
+// starts are written, for a kernel that consumes the starts while the scan runs
+// (k_lattice_scan_scatter).  The hand-off is the write-through (sc1) form of MI355X_MICROARCH.md
+// (inter-workgroup visibility, the table's first row), NOT an agent-scope release/acquire pair:
+// every start is stored with an sc1 store, every storing wave waits for its stores (vmcnt(0)),
+// a block barrier, then ONE lane's sc1 done-word store; the consumer polls the word with sc1
+// loads from one lane of the wave and that wave then reads the starts with sc1 loads only (no
+// acquire fence: the loads bypass L1, and one invalidate per polling wave cost more than the
+// launch this fusion saves).  tests/test_gpu_parity.py checks every start at full size against
+// a host exclusive scan of the cell counts.  Every thread of the block must call it.
 __device__ __forceinline__ void scan_tile(int32_t* __restrict__ count, long ncell, int ntiles,
                                           int32_t* __restrict__ start, unsigned long long* __restrict__ tstate,
                                           int32_t* __restrict__ sctl, int tile, int32_t* __restrict__ tdone) {
@@ -303,11 +310,10 @@ __device__ __forceinline__ void scan_tile(int32_t* __restrict__ count, long ncel
         }
     }
     if (tdone) {
-        // in-launch hand-off of the starts (MI355X_MICROARCH.md, inter-workgroup visibility, the
-        // sc1 form): write-through (sc1) start stores, every storing wave waits for them, a block
-        // barrier, then ONE lane's sc1 done-word store; the consumers poll it with sc1 loads and
-        // read the starts with sc1 loads only (no acquire fence: one per wave invalidating L1 cost
-        // more than the launch it saves).  A timed-out look-back's error flag is an sc1 store too.
+        // in-launch hand-off of the starts (the sc1 form above; relaxed agent-scope atomics lower
+        // to sc1 loads / stores): write-through start stores, every storing wave waits for them, a
+        // block barrier, then ONE lane's sc1 done-word store.  A timed-out look-back's error flag
+        // is an sc1 store too.
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         if (threadIdx.x == 0) __hip_atomic_store(&tdone[tile], tile_done_word(epoch), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

@@ -494,6 +494,13 @@ int cbf_abi_version(void);
  * rollout checkpoint) may be restored only into a library reporting the same version and size. */
 int cbf_workspace_layout(void);
 
+/* Byte offsets, inside a lattice workspace of this shape (cbf_lattice_workspace_size), of the cell
+ * list the last cell-list build left (a diagnostic view for tests and tools; the kernels never need
+ * it): off[0] start (int32[ncell + 1], the exclusive scan of the cell counts), off[1] the sorted
+ * positions (double[n][2]), off[2] the sorted nominal controls, off[3] the sorted agent indices
+ * (int32[n]); returns ncell, or CBF_EINVAL. */
+int64_t cbf_lattice_workspace_view(int32_t W, int32_t win_rows, const cbf_grid* grid, int64_t* off);
+
 #ifdef __cplusplus
 }
 #endif

@@ -982,3 +982,48 @@ def test_large_window_run_vs_oracle_every_timestep(placement, cull):
     C = swarm.LatticeSwarm(pos, W, H, params=fp, cull=cull)
     C.run(steps)
     assert C.stats_summary()["seidel"] > 0
+
+
+def _host_cells(pos, g):
+    """Cell of every position, as cell_coord / cell_of compute it (floor((v - o) inv_h), clamped)."""
+    def coord(v, o, n):
+        f = np.floor((v - o) * g.inv_h)
+        f = np.where(f >= 0.0, f, 0.0)
+        return np.minimum(f, n - 1).astype(np.int64)
+    return coord(pos[:, 1], g.y0, g.ny) * g.nx + coord(pos[:, 0], g.x0, g.nx)
+
+
+@pytest.mark.parametrize("steps", [1, 6])
+def test_cell_starts_full_size_equal_host_scan(steps):
+    """The in-launch hand-off of k_lattice_scan_scatter (cells.hpp scan_tile: sc1 start stores and
+    done words, sc1 loads by the scatter) at full size: after a build of the 1 M-agent lattice, every
+    cell start equals the host's exclusive scan of the cell counts of the positions binned, the
+    sorted indices are a permutation, and every sorted slot holds an agent of its own cell with its
+    own position.  steps = 6: five timesteps first, so the bin pass walks the previous cell order."""
+    import ctypes as C
+    from cbf_amd import _lib
+    W = H = 1024
+    pos = scenarios.lattice(W, H, seed=3)
+    L = swarm.LatticeSwarm(pos, W, H)
+    L.collect_stats = False
+    if steps > 1:
+        L.run(steps - 1)
+    torch.cuda.synchronize()
+    p_in = L.pos.cpu().numpy()
+    L.build_phase()
+    torch.cuda.synchronize()
+    off = (C.c_int64 * 4)()
+    ncell = _lib.lib.cbf_lattice_workspace_view(W, H, C.byref(L.grid), off)
+    assert ncell == L.grid.nx * L.grid.ny
+    ws = L.ws.cpu().numpy()
+    start = ws[off[0]:off[0] + 4 * (ncell + 1)].view(np.int32)
+    spos = ws[off[1]:off[1] + 16 * W * H].view(np.float64).reshape(-1, 2)
+    sidx = ws[off[3]:off[3] + 4 * W * H].view(np.int32)
+    cells = _host_cells(p_in, L.grid)
+    counts = np.bincount(cells, minlength=ncell)
+    want = np.concatenate([[0], np.cumsum(counts)]).astype(np.int64)
+    assert np.array_equal(start.astype(np.int64), want)
+    assert np.array_equal(np.sort(sidx), np.arange(W * H))
+    assert np.array_equal(spos, p_in[sidx])
+    slot_cell = np.repeat(np.arange(ncell), counts)
+    assert np.array_equal(cells[sidx], slot_cell)

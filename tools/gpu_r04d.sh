@@ -4,7 +4,7 @@ set -u
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
 O=gpurun_out/r04d; mkdir -p $O; : > $O/ab.txt
-timeout -k 10 600 python -u -m pytest tests/test_gpu_window.py -x -q --timeout 240 --timeout-method thread > $O/pytest_window.log 2>&1 || { tail -40 $O/pytest_window.log; exit 1; }
+timeout -k 10 600 python -u -m pytest tests/test_gpu_window.py tests/test_gpu_parity.py -k "window or cell_starts" -x -q --timeout 240 --timeout-method thread > $O/pytest_window.log 2>&1 || { tail -40 $O/pytest_window.log; exit 1; }
 tail -1 $O/pytest_window.log
 for rep in 1 2; do
   timeout -k 10 120 python tools/ab_window.py . cells >> $O/ab.txt || exit 2
