@@ -178,10 +178,12 @@ ADVANCE_KERNELS = ("k_lattice_filter<true, false, false>", "k_lattice_filter_har
 WINDOW_KERNELS = ("k_window_filter<true, false, false>", "k_lattice_filter_hard")
 
 
-def load_pmc_valu(config, kernel=ADVANCE_KERNELS[0]):
+def load_pmc_valu(config, kernel=ADVANCE_KERNELS[0], key="valu_busy"):
     """The kernel's VALU issue fraction from the committed PMC summary (SQ_ACTIVE_INST_VALU x 4 over
-    the SIMD cycles of its dispatches, tools/summarize_profile.py), if profiled."""
-    v = load_pmc(config).get(kernel, {}).get("valu_busy")
+    the SIMD cycles of its dispatches, tools/summarize_profile.py), if profiled.  key
+    "valu_busy_2p4ghz": the clock-corrected form (issue cycles over the traced duration at the
+    2.4 GHz peak clock, a lower bound; GRBM_GUI_ACTIVE reads high on short dispatches)."""
+    v = load_pmc(config).get(kernel, {}).get(key)
     return None if v is None else float(v)
 
 
@@ -600,9 +602,13 @@ def bench_lattice(args, ws, rank, local):
                                        "achieved": achieved_adv, "frac": achieved_adv / HBM_PEAK_GBS,
                                        "traffic": traffic_adv},
                      "valu_busy": load_pmc_valu(args.config, adv_kernels[0]) if args.barrier == "reference" else None,
+                     "valu_busy_2p4ghz": load_pmc_valu(args.config, adv_kernels[0], "valu_busy_2p4ghz")
+                     if args.barrier == "reference" else None,
                      "valu_busy_note": "the dominant kernel's VALU issue fraction (rocprofv3 SQ_ACTIVE_INST_VALU, "
-                                       "profiles/pmc_summary.json): beside the HBM fraction, the limit it works "
-                                       "against",
+                                       "profiles/pmc_summary.json) over GRBM_GUI_ACTIVE / 8 cycles (reads high on "
+                                       "short dispatches) and, valu_busy_2p4ghz, over its traced duration at the "
+                                       "2.4 GHz peak clock (a lower bound): beside the HBM fraction, the limit it "
+                                       "works against",
                      "algorithmic_bytes_per_launch": FILTER_BYTES_PER_AGENT * n_local,
                      "step_algorithmic_GBps": STEP_BYTES_PER_AGENT * n_local * args.steps / elapsed / 1e9 / ws},
     }

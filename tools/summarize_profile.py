@@ -72,6 +72,11 @@ def summarize(prof, cfg, rnd):
             e["valu_busy"] = e["SQ_ACTIVE_INST_VALU"] * 4 / (SIMDS * cyc)
             if e.get("avg_duration_ns"):
                 e["implied_clock_ghz"] = cyc / e["avg_duration_ns"]
+        if "SQ_ACTIVE_INST_VALU" in e and e.get("avg_duration_ns"):
+            # clock-corrected form (MI355X_MICROARCH.md, DVFS note: GRBM_GUI_ACTIVE / 8 reads high on
+            # dispatches shorter than ~0.3 ms): VALU issue cycles over the SIMD cycles the dispatch's
+            # traced duration holds at the 2.4 GHz peak clock -- a lower bound of the busy fraction
+            e["valu_busy_2p4ghz"] = e["SQ_ACTIVE_INST_VALU"] * 4 / (SIMDS * e["avg_duration_ns"] * 2.4)
         out[k] = e
     return out
 
@@ -99,7 +104,8 @@ def main(prof, rnd):
         print(cfg)
         for k, e in sorted(ks.items(), key=lambda kv: -(kv[1].get("avg_duration_ns") or 0)):
             print(f"  {k:30s} dur={((e.get('avg_duration_ns') or 0) / 1e3):8.2f} us  "
-                  f"hbm={(e.get('hbm_bytes_per_launch') or 0) / 1e6:8.2f} MB  valu_busy={e.get('valu_busy')}")
+                  f"hbm={(e.get('hbm_bytes_per_launch') or 0) / 1e6:8.2f} MB  valu_busy={e.get('valu_busy')} "
+                  f"(at 2.4 GHz {e.get('valu_busy_2p4ghz')})")
 
 
 if __name__ == "__main__":
