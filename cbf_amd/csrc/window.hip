@@ -33,6 +33,9 @@ namespace {
 #ifndef CBF_WIN_G
 #define CBF_WIN_G 3  // rows whose candidate loads the window filter issues together
 #endif
+#ifndef CBF_WIN_SPEC
+#define CBF_WIN_SPEC 0  // 1: rows r - 1 .. r + 1 loaded with the ego, before the row guard
+#endif
 constexpr int kPrepBlock = 256;
 constexpr int kPrepPer = 8;  // columns per prep thread: rows of up to 2048 agents
 constexpr int kWinMaxW = kPrepBlock * kPrepPer;
@@ -398,6 +401,25 @@ __device__ __forceinline__ void window_ego(const KP& P, const WinBounds& B, int 
         ego_init(P, E, pe.x, pe.y, ve.x, ve.y, ve.x, ve.y);
         fin = isfinite(pe.x) && isfinite(pe.y);  // otherwise no candidate can pass (s is inf or NaN)
     }
+    const int wi = (int)w;
+#if CBF_WIN_SPEC
+    // rows r - 1 .. r + 1 (nearly every ego's), loaded before the row guard is known (it needs y)
+    double2 xm[3], x0[3], xp[3];
+    float xrs[3], xrp[3];
+    bool xv[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        xv[i] = act && r + i - 1 >= 0 && r + i - 1 < H;
+        if (xv[i]) {
+            const int b = wi + (i - 1) * W;
+            xm[i] = c > 0 ? ld_slot(pos, b - 1) : make_double2(INFINITY, INFINITY);
+            x0[i] = ld_slot(pos, b);
+            xp[i] = c + 1 < W ? ld_slot(pos, b + 1) : make_double2(INFINITY, INFINITY);
+            xrs[i] = c + 2 < W ? ld_rsp(rsp, b + 2).x : INFINITY;
+            xrp[i] = c - 2 >= 0 ? ld_rsp(rsp, b - 2).y : -INFINITY;
+        }
+    }
+#endif
     int Kd = -1, Ku = -1;
     if (fin) win_rows(P, sylo, pyhi, r, H, E.r1, Kd, Ku);
     const int KdW = wave_max_i(Kd), KuW = wave_max_i(Ku);
@@ -406,8 +428,20 @@ __device__ __forceinline__ void window_ego(const KP& P, const WinBounds& B, int 
     // rows whose sentinel at c + 2 (R) / c - 2 (L) does not hold: bit dr + KdW
     unsigned long long pR = 0, pL = 0;
     bool slow = KdW + KuW + 1 > 64;  // (a window that tall takes the unbounded form)
-    const int wi = (int)w;
     if (!slow) {
+#if CBF_WIN_SPEC
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            const int dr = i - 1;
+            if (!(fin && xv[i] && dr >= -Kd && dr <= Ku)) continue;
+            const int b = wi + dr * W;
+            win_cand(P, E, xm[i], b - 1, Hl, hit_lds, d2);
+            win_cand(P, E, x0[i], b, Hl, hit_lds, d2);
+            win_cand(P, E, xp[i], b + 1, Hl, hit_lds, d2);
+            if (!((double)xrs[i] - E.r0 > P.win_d)) pR |= 1ull << (dr + KdW);
+            if (!(E.r0 - (double)xrp[i] > P.win_d)) pL |= 1ull << (dr + KdW);
+        }
+#endif
         // columns c - 1 .. c + 1 of every row, G rows' loads in flight at a time
         constexpr int G = CBF_WIN_G;
         for (int dr0 = -KdW; dr0 <= KuW; dr0 += G) {
@@ -417,7 +451,7 @@ __device__ __forceinline__ void window_ego(const KP& P, const WinBounds& B, int 
 #pragma unroll
             for (int i = 0; i < G; ++i) {
                 const int dr = dr0 + i;
-                a[i] = fin && dr <= KuW && dr >= -Kd && dr <= Ku;
+                a[i] = fin && dr <= KuW && dr >= -Kd && dr <= Ku && !(CBF_WIN_SPEC && dr >= -1 && dr <= 1);
                 if (a[i]) {
                     const int b = wi + dr * W;
                     pm[i] = c > 0 ? ld_slot(pos, b - 1) : make_double2(INFINITY, INFINITY);
