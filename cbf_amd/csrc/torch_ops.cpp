@@ -155,11 +155,12 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> lattice_step(
 
 // `steps` timesteps of the whole lattice in one call (cbf_lattice_run): positions advanced in place,
 // bit-identical to `steps` lattice_step calls; returns the last timestep's (nominal control,
-// filtered control, status, neighbour count).
+// filtered control, status, neighbour count).  window_cull: the lattice-window cull
+// (cbf_lattice_run_ex CBF_RUN_WINDOW_CULL), same results.
 std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> lattice_run(
     at::Tensor pos, int64_t W, int64_t H, double gain, double T, int64_t steps, double x0, double y0, double cell,
     int64_t nx, int64_t ny, at::Tensor workspace, c10::optional<at::Tensor> stats, double max_speed, double dmin, double k,
-    double safety_distance) {
+    double safety_distance, bool window_cull) {
     check_f64(pos, "pos", 2);
     TORCH_CHECK(pos.size(0) == W * H, "pos must hold W x H agents");
     TORCH_CHECK(steps >= 1, "steps must be >= 1 (the outputs are the last timestep's)");
@@ -176,11 +177,11 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> lattice_run(
     at::Tensor u = at::empty({n, 2}, pos.options());
     at::Tensor status = at::empty({n}, pos.options().dtype(at::kInt));
     at::Tensor cnt = at::empty({n}, pos.options().dtype(at::kInt));
-    check_rc(cbf_lattice_run(&p, &g, (int32_t)W, (int32_t)H, pos.data_ptr<double>(), gain, T, (int32_t)steps,
-                             vel.data_ptr<double>(), u.data_ptr<double>(), status.data_ptr<int32_t>(),
-                             cnt.data_ptr<int32_t>(), st,
-                             workspace.data_ptr(), (size_t)workspace.numel(), stream()),
-             "cbf_lattice_run");
+    check_rc(cbf_lattice_run_ex(&p, &g, (int32_t)W, (int32_t)H, pos.data_ptr<double>(), gain, T, (int32_t)steps,
+                                vel.data_ptr<double>(), u.data_ptr<double>(), status.data_ptr<int32_t>(),
+                                cnt.data_ptr<int32_t>(), st, workspace.data_ptr(), (size_t)workspace.numel(),
+                                window_cull ? CBF_RUN_WINDOW_CULL : 0u, stream()),
+             "cbf_lattice_run_ex");
     return {vel, u, status, cnt};
 }
 
@@ -206,7 +207,7 @@ TORCH_LIBRARY(cbf_amd, m) {
           "float k=1., float safety_distance=0.2) -> (Tensor, Tensor, Tensor, Tensor)");
     m.def("lattice_run(Tensor(a!) pos, int W, int H, float gain, float T, int steps, float x0, float y0, float cell, "
           "int nx, int ny, Tensor(b!) workspace, Tensor(c!)? stats=None, float max_speed=15., float dmin=0.2, "
-          "float k=1., float safety_distance=0.2) -> (Tensor, Tensor, Tensor, Tensor)");
+          "float k=1., float safety_distance=0.2, bool window_cull=False) -> (Tensor, Tensor, Tensor, Tensor)");
     m.def("lattice_workspace_size(int W, int H, float x0, float y0, float cell, int nx, int ny) -> int",
           &lattice_workspace_size);
     m.def("abi_version() -> int", []() -> int64_t { return cbf_abi_version(); });

@@ -88,8 +88,8 @@ def test_lattice_step_op_matches_ctypes_path_and_graph_captures():
 
 
 def test_lattice_run_op_equals_step_ops():
-    """torch.ops.cbf_amd.lattice_run(k) == k lattice_step ops, bit for bit (positions, the last
-    timestep's outputs, the decoded statistics)."""
+    """torch.ops.cbf_amd.lattice_run(k), with either cull, == k lattice_step ops, bit for bit
+    (positions, the last timestep's outputs, the decoded statistics)."""
     from cbf_amd import _lib
     W, H = 128, 96
     pos = scenarios.lattice(W, H, seed=6, spacing=0.2)
@@ -98,19 +98,20 @@ def test_lattice_run_op_equals_step_ops():
     geo = (g.x0, g.y0, 1 / g.inv_h, g.nx, g.ny)
     nb = OPS.lattice_workspace_size(W, H, *geo)
     outs = []
-    for run in (False, True):
+    for run in ("steps", "run", "run_window"):
         ws = torch.zeros(nb, dtype=torch.uint8, device=DEV)
         stats = torch.zeros(1024, dtype=torch.int64, device=DEV)
         P = _t(pos)
-        if run:
-            out = OPS.lattice_run(P, W, H, L.gain, L.T, 7, *geo, ws, stats)
-        else:
+        if run == "steps":
             for _ in range(7):
                 out = OPS.lattice_step(P, W, H, L.gain, L.T, *geo, ws, stats)
+        else:   # (window_cull: the lattice-window cull, CBF_RUN_WINDOW_CULL)
+            out = OPS.lattice_run(P, W, H, L.gain, L.T, 7, *geo, ws, stats, window_cull=run == "run_window")
         torch.cuda.synchronize()
         outs.append((P, out, _lib.decode_stats(stats.cpu().numpy())))
-    (pa, oa, sa), (pb, ob, sb) = outs
-    assert torch.equal(pa, pb) and all(torch.equal(x, y) for x, y in zip(oa, ob)) and sa == sb
+    pa, oa, sa = outs[0]
+    for pb, ob, sb in outs[1:]:
+        assert torch.equal(pa, pb) and all(torch.equal(x, y) for x, y in zip(oa, ob)) and sa == sb
     assert sa["solves"] > 0 and sa["errors"] == 0
 
 
