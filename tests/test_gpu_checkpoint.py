@@ -14,10 +14,11 @@ if not torch.cuda.is_available():  # collected on CPU boxes but never run there
 from cbf_amd import _lib, scenarios, swarm  # noqa: E402
 
 
-@pytest.mark.parametrize("nominal,spacing", [(None, 0.145), (("random", 1.0, 5), 0.22)])
-def test_lattice_checkpoint_resumes_bit_identical(tmp_path, nominal, spacing):
+@pytest.mark.parametrize("nominal,spacing,cull", [(None, 0.145, "cells"), (("random", 1.0, 5), 0.22, "cells"),
+                                                 (None, 0.145, "window")])
+def test_lattice_checkpoint_resumes_bit_identical(tmp_path, nominal, spacing, cull):
     W, H = 96, 64
-    A = swarm.LatticeSwarm(scenarios.lattice(W, H, seed=3, spacing=spacing), W, H, nominal=nominal)
+    A = swarm.LatticeSwarm(scenarios.lattice(W, H, seed=3, spacing=spacing), W, H, nominal=nominal, cull=cull)
     A.run(7)
     A.step()
     path = str(tmp_path / "ck.npz")
@@ -34,6 +35,7 @@ def test_lattice_checkpoint_resumes_bit_identical(tmp_path, nominal, spacing):
     # and extrema (what decode_stats reads) are deterministic
     assert _lib.decode_stats(A.stats.cpu().numpy()) == _lib.decode_stats(B.stats.cpu().numpy())
     assert B.grid.nx == A.grid.nx and B.grid.inv_h == A.grid.inv_h and B.nominal == A.nominal
+    assert B.cull == A.cull
 
 
 def _tamper(tmp_path, path, name, fn):
