@@ -33,6 +33,9 @@ namespace {
 #ifndef CBF_WIN_G
 #define CBF_WIN_G 3  // rows whose candidate loads the window filter issues together
 #endif
+#ifndef CBF_WIN_TILE
+#define CBF_WIN_TILE 1  // 0: the untiled window filter (k_window_filter), per-lane global loads
+#endif
 #ifndef CBF_WIN_SPEC
 #define CBF_WIN_SPEC 0  // 1: rows r - 1 .. r + 1 loaded with the ego, before the row guard
 #endif
@@ -571,6 +574,191 @@ __global__ void __launch_bounds__(kBlock) k_window_filter(KP P, WinBounds B, int
     }
 }
 
+// ---- the LDS-tiled form of the window filter (CBF_WIN_TILE) -----------------------------------
+// A block is a tile of kTileR lattice rows x kTileW columns (one wave per tile row).  It stages
+// the tile plus kTileKS halo rows and kTileKC halo columns of positions, nominal controls and
+// column extents in LDS with coalesced loads (one round trip), then every candidate, sentinel and
+// hit is read from LDS at a fixed offset from the ego's own slot: no per-lane gather chains.  Hits
+// are bits of a register mask over the (7 rows x 5 columns) window, assembled from LDS after the
+// scan.  An ego whose row window or column walk leaves the staged halo takes win_direct (global
+// memory, unbounded), as in the untiled form.
+constexpr int kTileW = 64;
+constexpr int kTileR = kBlock / kTileW;
+constexpr int kTileKS = 3;  // rows each side (the row guard's window up to +-3)
+constexpr int kTileKC = 3;  // columns each side (candidates to +-2, sentinels to +-3)
+constexpr int kTileRows = kTileR + 2 * kTileKS, kTileCols = kTileW + 2 * kTileKC, kTileN = kTileRows * kTileCols;
+constexpr int kTileGuard = kTileR + kWinPre - 1;  // sylo / pyhi values a tile needs
+struct TileLds {
+    double2 p[kTileN];
+    double2 u[kTileN];
+    float2 g[kTileN];
+    double sy[kTileGuard], py[kTileGuard];
+};
+
+template <bool FZ, bool ST, bool IN>
+__global__ void __launch_bounds__(kBlock) k_window_tile(KP P, WinBounds B, int W, int H, long nwin, int tiles_x,
+                                                        const double2* __restrict__ pos,
+                                                        const double2* __restrict__ u0,
+                                                        const float2* __restrict__ rsp,
+                                                        const double* __restrict__ sylo,
+                                                        const double* __restrict__ pyhi,
+                                                        const int32_t* __restrict__ sctl, double T,
+                                                        double2* __restrict__ pos_out, double2* __restrict__ u,
+                                                        int32_t* __restrict__ status, int32_t* __restrict__ cnt,
+                                                        unsigned long long* __restrict__ stats,
+                                                        int32_t* __restrict__ hardq, HardRec* __restrict__ qrec,
+                                                        long qcap) {
+    __shared__ TileLds L;
+    const int bx = xcd_block();
+    const int ty = bx / tiles_x, tx = bx - ty * tiles_x;
+    const int r0 = ty * kTileR, c0 = tx * kTileW;
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int r = r0 + wv, c = c0 + lane;
+    const long w = (long)r * W + c;
+    const bool inside = r < H && c < W;
+    if (IN && ST && stats && (int)blockIdx.x == (int)gridDim.x - 1 && threadIdx.x < 64) stat_snapshot(stats);
+    if (sctl[2] != 0) {  // the workspace is bound to another shape: report, touch nothing else
+        lattice_error_tail(W, 0, H, 0, nwin, inside ? w : nwin, u, status, cnt, stats, nullptr, 0, hardq);
+        return;
+    }
+    // stage the tile with its halo (beyond the lattice: +-inf positions, which no test passes, and
+    // column extents that exclude nothing beyond the row ends)
+    for (int i = threadIdx.x; i < kTileN; i += kBlock) {
+        const int lr = i / kTileCols, lc = i - lr * kTileCols;
+        const int rr = r0 - kTileKS + lr, cc = c0 - kTileKC + lc;
+        if (rr >= 0 && rr < H && cc >= 0 && cc < W) {
+            const int t = rr * W + cc;
+            L.p[i] = ld_slot(pos, t);
+            L.u[i] = ld_slot(u0, t);
+            L.g[i] = ld_rsp(rsp, t);
+        } else {
+            const double v = cc < 0 ? -INFINITY : INFINITY;
+            L.p[i] = make_double2(v, v);
+            L.u[i] = make_double2(0.0, 0.0);
+            L.g[i] = make_float2(INFINITY, -INFINITY);
+        }
+    }
+    if (threadIdx.x < kTileGuard) {
+        const int a = r0 + 1 + threadIdx.x, b = r0 - kWinPre + threadIdx.x;
+        L.sy[threadIdx.x] = a < H ? sylo[a] : INFINITY;
+        L.py[threadIdx.x] = b >= 0 ? pyhi[b] : -INFINITY;
+    }
+    __syncthreads();
+    const bool act = inside && w >= B.own_lo && w < B.own_hi;
+    const int e = (wv + kTileKS) * kTileCols + lane + kTileKC;  // the ego's slot in the tile
+    Ego E;
+    bool fin = false;
+    if (act) {
+        const double2 pe = L.p[e], ve = L.u[e];
+        ego_init(P, E, pe.x, pe.y, ve.x, ve.y, ve.x, ve.y);
+        fin = isfinite(pe.x) && isfinite(pe.y);
+    }
+    int Kd = -1, Ku = -1;
+    bool slow = false;
+    if (fin) {
+        Ku = 0;
+        Kd = 0;
+#pragma unroll
+        for (int k = 0; k < kWinPre; ++k) {
+            Ku += !(L.sy[wv + k] - E.r1 > P.win_d) ? 1 : 0;
+            Kd += !(E.r1 - L.py[wv + kWinPre - 1 - k] > P.win_d) ? 1 : 0;
+        }
+        if (Ku > kTileKS || Kd > kTileKS) slow = true;  // beyond the staged rows: the unbounded form
+    }
+    const int KuW = wave_max_i(slow ? -1 : Ku), KdW = wave_max_i(slow ? -1 : Kd);
+    unsigned long long hm = 0;  // hit bits (dr + 3) * 5 + (dc + 2)
+    double d2 = INFINITY;
+    auto cand = [&](int off, int bit) {
+        const double2 q = L.p[off];
+        const double e0 = q.x - E.r0, e1 = q.y - E.r1;
+        const double s = e0 * e0 + e1 * e1;
+        if (s < P.cull_t && s > 0) {
+            hm |= 1ull << bit;
+            d2 = pmin(d2, s);
+        }
+    };
+    unsigned pR = 0, pL = 0;  // rows (bit dr + 3) whose sentinel at c + 2 / c - 2 does not hold
+    for (int dr = -KdW; dr <= KuW; ++dr) {
+        if (!(fin && !slow && dr >= -Kd && dr <= Ku)) continue;
+        const int b = e + dr * kTileCols, bit = (dr + 3) * 5 + 2;
+        cand(b - 1, bit - 1);
+        cand(b, bit);
+        cand(b + 1, bit + 1);
+        if (!((double)L.g[b + 2].x - E.r0 > P.win_d)) pR |= 1u << (dr + 3);
+        if (!(E.r0 - (double)L.g[b - 2].y > P.win_d)) pL |= 1u << (dr + 3);
+    }
+    if (__ballot((pR | pL) != 0)) {  // columns c -+ 2 where a sentinel did not hold
+        for (int dr = -KdW; dr <= KuW; ++dr) {
+            const int b = e + dr * kTileCols, bit = (dr + 3) * 5 + 2;
+            if ((pR >> (dr + 3)) & 1u) {
+                cand(b + 2, bit + 2);
+                if (!((double)L.g[b + 3].x - E.r0 > P.win_d)) slow = true;
+            }
+            if ((pL >> (dr + 3)) & 1u) {
+                cand(b - 2, bit - 2);
+                if (!(E.r0 - (double)L.g[b - 3].y > P.win_d)) slow = true;
+            }
+        }
+    }
+    EgoOut O;
+    O.res = 0;
+    O.w = -1;
+    O.nbrs = 0;
+    O.code = CBF_STATUS_IDLE;
+    O.binding = false;
+    O.seidel = false;
+    O.viol = O.vorig = 0.0;
+    O.d2 = INFINITY;
+    if (act) {
+        O.w = (int)w;
+        const double q0 = quad_c(P, E, 0), q1 = quad_c(P, E, 1), q2 = quad_c(P, E, 2), q3 = quad_c(P, E, 3);
+        const bool qfin = isfinite(q0) && isfinite(q1) && isfinite(q2) && isfinite(q3);
+        if (fin && !slow) {
+            // the hits from LDS: per-quadrant minima of row_g plus the quadrant terms, or row by row
+            // (row_b) when a quadrant term is not finite -- the cell-list filter's two forms
+            double g0 = INFINITY, g1 = INFINITY, g2 = INFINITY, g3 = INFINITY;
+            if (qfin) E.count = __popcll(hm);  // (ego_add counts its hits itself)
+            while (hm) {
+                const int bit = __ffsll((long long)hm) - 1;
+                hm &= hm - 1;
+                const int dr = bit / 5 - 3, dc = bit - (bit / 5) * 5 - 2;
+                const int off = e + dr * kTileCols + dc;
+                const double2 q = L.p[off], v = L.u[off];
+                if (qfin) {
+                    int qd;
+                    const double g = row_g<FZ>(P, E, q.x, q.y, v.x, v.y, qd);
+                    g0 = (qd == 0 && g < g0) ? g : g0;
+                    g1 = (qd == 1 && g < g1) ? g : g1;
+                    g2 = (qd == 2 && g < g2) ? g : g2;
+                    g3 = (qd == 3 && g < g3) ? g : g3;
+                    E.present |= 1u << qd;
+                } else {
+                    ego_add<FZ>(P, E, q.x, q.y, v.x, v.y);
+                }
+            }
+            if (qfin) {
+                E.bq0 = g0 + q0;
+                E.bq1 = g1 + q1;
+                E.bq2 = g2 + q2;
+                E.bq3 = g3 + q3;
+            }
+        } else if (fin) {  // the unbounded form, over the full row window (beyond the staged halo too)
+            int kd, ku;
+            win_rows(P, sylo, pyhi, r, H, E.r1, kd, ku);
+            win_direct<FZ>(P, E, w, r, c, W, kd, ku, pos, u0, rsp, d2);
+        }
+        O.nbrs = E.count;
+        if (ST) O.d2 = d2;
+        ego_finish<FZ, ST, IN>(P, E, (int)w, (int)(w - B.own_lo), (int)w, T, pos_out, u, status, cnt, hardq,
+                               bx % kSubQ, qrec + (long)(bx % kSubQ) * qcap, O);
+    }
+    if (ST && stats) {
+        const bool counted = O.res != 0 && O.w >= B.cnt_lo && O.w < B.cnt_hi;
+        wave_stats(stats, (long)bx * (kBlock / 64) + wv, counted && O.nbrs > 0, counted && O.seidel,
+                   counted && O.res == 1, O.code, O.binding, O.viol, O.vorig, counted ? O.d2 : INFINITY);
+    }
+}
+
 }  // namespace
 
 namespace cbf {
@@ -595,6 +783,19 @@ void window_filter(const cbf_params* p, const CellWs& Wk, int W, int H, const do
     const KP kp = make_kp(p);
     const WinBounds B = make_win_bounds(W, 0, n, 0, H, 0, H, 0);
     const WinGuard Gd = win_guard(Wk, H);
+#if CBF_WIN_TILE
+    const int tiles_x = (W + kTileW - 1) / kTileW, tiles_y = (H + kTileR - 1) / kTileR;
+    const auto tile =
+        in ? (stats ? (p->f_is_zero ? k_window_tile<true, true, true> : k_window_tile<false, true, true>)
+                    : (p->f_is_zero ? k_window_tile<true, false, true> : k_window_tile<false, false, true>))
+           : (stats ? (p->f_is_zero ? k_window_tile<true, true, false> : k_window_tile<false, true, false>)
+                    : (p->f_is_zero ? k_window_tile<true, false, false> : k_window_tile<false, false, false>));
+    hipLaunchKernelGGL(tile, dim3((unsigned)(tiles_x * tiles_y)), dim3(kBlock), 0, s, kp, B, W, H, n, tiles_x, pos,
+                       (const double2*)Wk.svel, (const float2*)win_rsp(Wk), (const double*)Gd.sylo,
+                       (const double*)Gd.pyhi, (const int32_t*)Wk.sctl, T, pos_out, u, status, cnt, stats, Wk.hardq,
+                       Wk.qrec, Wk.qcap);
+    return;
+#endif
     const auto filter =
         in ? (stats ? (p->f_is_zero ? k_window_filter<true, true, true> : k_window_filter<false, true, true>)
                     : (p->f_is_zero ? k_window_filter<true, false, true> : k_window_filter<false, false, true>))

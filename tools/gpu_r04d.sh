@@ -4,12 +4,12 @@ set -u
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
 O=gpurun_out/r04d; mkdir -p $O; : > $O/ab.txt
-timeout -k 10 600 python -u -m pytest tests/test_gpu_window.py tests/test_gpu_parity.py -k "window or cell_starts" -x -q --timeout 240 --timeout-method thread > $O/pytest_window.log 2>&1 || { tail -40 $O/pytest_window.log; exit 1; }
+timeout -k 10 600 python -u -m pytest tests/test_gpu_window.py tests/test_gpu_parity.py tests/test_gpu_checkpoint.py tests/test_gpu_torch_ops.py -k "window or cell_starts or lattice_step_vs or run_matches or checkpoint or lattice_run_op" -x -q --timeout 240 --timeout-method thread > $O/pytest_window.log 2>&1 || { tail -40 $O/pytest_window.log; exit 1; }
 tail -1 $O/pytest_window.log
 for rep in 1 2; do
   for rows in 1024 128; do
     timeout -k 10 120 python tools/ab_window.py . cells 0.145 $rows >> $O/ab.txt || exit 2
-    for t in . tools/_abt/g2 tools/_abt/g1 tools/_abt/spec tools/_abt/spec2; do
+    for t in . tools/_abt/untiled tools/_abt/spec; do
       timeout -k 10 120 python tools/ab_window.py $t window 0.145 $rows >> $O/ab.txt || exit 3
     done
   done
