@@ -320,13 +320,12 @@ def gather_state_sha(own, ws):
 
 
 def lattice_cull(args, sharded):
-    """The cull of the single-GPU lattice step: --cull, or auto = the lattice-window cull
-    (CBF_RUN_WINDOW_CULL) where the swarm stays lattice-like (the consensus nominal control of
-    cfg4 / cfg4f), the cell list for the random walk of cfg4r (which scrambles the lattice), the
-    HOCBF barrier and the sharded step."""
-    if sharded or args.barrier != "reference" or not 4 <= args.width <= 2048:
+    """The cull of the lattice step: --cull, or auto = the lattice-window cull (CBF_RUN_WINDOW_CULL)
+    where the swarm stays lattice-like (the consensus nominal control of cfg4 / cfg4f), the cell
+    list for the random walk of cfg4r (which scrambles the lattice) and the HOCBF barrier."""
+    if args.barrier != "reference" or not 4 <= args.width <= 2048:
         if args.cull == "window":
-            raise SystemExit("--cull window: single GPU, reference barrier, 4 <= width <= 2048 only")
+            raise SystemExit("--cull window: reference barrier, 4 <= width <= 2048 only")
         return "cells"
     if args.cull != "auto":
         return args.cull
@@ -342,7 +341,7 @@ def bench_lattice(args, ws, rank, local):
     if sharded:
         from cbf_amd.shard import ShardedLattice
         S = ShardedLattice(W, rows, seed=args.seed, halo=halo, substeps=k, spacing=args.spacing, gain=args.gain,
-                           nominal=args.nominal, exchange=args.exchange)
+                           nominal=args.nominal, exchange=args.exchange, cull=lattice_cull(args, sharded))
     else:
         pos = scenarios.lattice(W, rows, seed=args.seed, spacing=args.spacing)
         S = swarm.LatticeSwarm(pos, W, rows, gain=args.gain, barrier=args.barrier, nominal=args.nominal,
@@ -512,7 +511,7 @@ def bench_lattice(args, ws, rank, local):
     # the dominant kernel (k_lattice_filter) alone: an event recorded by the advance call between
     # it and the queued-QP kernel, on their launch stream (reference barrier)
     marked = args.barrier == "reference"
-    cull = getattr(S, "cull", "cells")
+    cull = getattr(S, "cull", None) or getattr(getattr(S, "be", None), "cull", "cells")
     kt = []
     for _ in range(args.kernel_iters):
         S.build_phase()
@@ -522,7 +521,7 @@ def bench_lattice(args, ws, rank, local):
         if marked:
             m.record()   # creates the event; the advance call records it again after the filter
         a.record()
-        if marked and cull == "window":
+        if marked and cull == "window" and not sharded:
             S.advance_phase(mark=m, commit=False)   # (the new positions into scratch: no copy timed)
         elif marked:
             S.advance_phase(mark=m)

@@ -93,10 +93,16 @@ SIGNATURES = {
     "cbf_lattice_cycle_sharded": (C.c_int, [_P, _G, _i32, _i32, _i32, _i32, _i32, _i32, _i32, _i32, _i32, _i32,
                                             _vp, _d, _d,
                                             _vp, _vp, _vp, _vp, _vp, _vp, _vp, _sz, _vp]),
+    "cbf_lattice_cycle_sharded_ex": (C.c_int, [_P, _G, _i32, _i32, _i32, _i32, _i32, _i32, _i32, _i32, _i32, _i32,
+                                               _vp, _d, _d, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _sz, C.c_uint32, _vp]),
     "cbf_lattice_run": (C.c_int, [_P, _G, _i32, _i32, _vp, _d, _d, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _sz, _vp]),
     "cbf_lattice_run_ex": (C.c_int, [_P, _G, _i32, _i32, _vp, _d, _d, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _sz,
                                      C.c_uint32, _vp]),
     "cbf_lattice_workspace_view": (C.c_int64, [_i32, _i32, _G, C.POINTER(C.c_int64)]),
+    "cbf_lattice_window_build_ex": (C.c_int, [_P, _G, _i32, _i32, _i32, _i32, _i32, _i32, _vp, _d, _vp, _vp, _sz,
+                                              _vp]),
+    "cbf_lattice_window_advance_ex": (C.c_int, [_P, _G, _i32, _i32, _i32, _i32, _i32, _i32, _vp, _d, _vp, _vp, _vp,
+                                                _vp, _vp, _vp, _sz, _vp, _vp]),
     "cbf_lattice_window_build": (C.c_int, [_P, _G, _i32, _i32, _vp, _d, _vp, _vp, _sz, _vp]),
     "cbf_lattice_window_advance": (C.c_int, [_P, _G, _i32, _i32, _vp, _d, _vp, _vp, _vp, _vp, _vp, _vp, _sz, _vp,
                                              _vp]),

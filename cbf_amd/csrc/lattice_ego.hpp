@@ -8,6 +8,79 @@
 
 namespace cbf {
 
+constexpr int kExtSlotWords = 16;  // one 128-B line per extents slot (6 keys used)
+constexpr int kExtSlots = 64;      // extents slots per sub-step set
+constexpr int kExtVals = 6;        // {ego min, ego max, owned max below guard, owned min above guard, owned min, max}
+__host__ __device__ constexpr bool ext_is_min(int q) { return q == 0 || q == 3 || q == 4; }
+
+struct ExtSpec {
+    int own_begin, own_end, guard;
+};
+
+// Halo-guard y-extents of one block's agents into slot (slot & (kExtSlots - 1)) of an extents
+// set (e[] per lane: {min, max} over the computed rows, {max below the guard, min above it, min,
+// max} over the owned rows; y = the lane's y where any).  The values travel as dkey()s (order-
+// preserving uint64 keys, the form the slots hold), so each wave reduces them with 32-bit DPP
+// reductions (wave_umin64 / wave_umax64) instead of 64-bit shuffle trees through LDS; a NaN y
+// keys above +inf, so it wins a maximum and fails the guard (conservative).  The LAST wave of the
+// block to arrive (an LDS counter, `arrive`, zeroed by the caller before a block barrier at
+// kernel start) combines the NW partials and issues one atomic per non-identity value.  No
+// barrier at the end (it would hold every wave until the block's slowest is done), and a quarter
+// of the per-wave atomics.  ONE: each lane holds at most one agent (its e[] are y or infinite,
+// which allows a two-reduction fast path).  Every lane of the wave must call it.
+template <int NW, bool ONE = true>
+__device__ __forceinline__ void ext_keys_flush(double (&e)[6], int any, double y,
+                                               unsigned long long* __restrict__ ext_keys, long slot,
+                                               unsigned long long (*red)[NW], int* arrive) {
+    const unsigned long long kmin_id = dkey(INFINITY), kmax_id = dkey(-INFINITY);
+    const unsigned long long act = __ballot(any);
+    const unsigned code = any ? ((e[0] != INFINITY ? 1u : 0u) | (e[2] != -INFINITY ? 2u : 0u) |
+                                 (e[3] != INFINITY ? 4u : 0u) | (e[4] != INFINITY ? 8u : 0u))
+                              : 0u;
+    const unsigned c0 = (unsigned)__shfl((int)code, act ? __ffsll((long long)act) - 1 : 0, 64);
+    unsigned long long k[6];
+    if (!act) {
+#pragma unroll
+        for (int q = 0; q < 6; ++q) k[q] = ext_is_min(q) ? kmin_id : kmax_id;
+    } else if (ONE && __ballot(any && code != c0) == 0) {
+        // the common wave: one membership pattern for all its agents, two reductions instead of six
+        const unsigned long long ky = dkey(y);
+        const unsigned long long mn = wave_umin64(any ? ky : kmin_id), mx = wave_umax64(any ? ky : kmax_id);
+        k[0] = (c0 & 1u) ? mn : kmin_id;
+        k[1] = (c0 & 1u) ? mx : kmax_id;
+        k[2] = (c0 & 2u) ? mx : kmax_id;
+        k[3] = (c0 & 4u) ? mn : kmin_id;
+        k[4] = (c0 & 8u) ? mn : kmin_id;
+        k[5] = (c0 & 8u) ? mx : kmax_id;
+    } else {
+#pragma unroll
+        for (int q = 0; q < 6; ++q) k[q] = ext_is_min(q) ? wave_umin64(dkey(e[q])) : wave_umax64(dkey(e[q]));
+    }
+    if ((threadIdx.x & 63) != 0) return;
+    const int wid = threadIdx.x >> 6;
+#pragma unroll
+    for (int q = 0; q < 6; ++q) red[q][wid] = k[q];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    if (atomicAdd(arrive, 1) != NW - 1) return;  // not the last wave of the block
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    for (int v = 0; v < NW; ++v)
+#pragma unroll
+        for (int q = 0; q < 6; ++q) {
+            const unsigned long long x = red[q][v];
+            k[q] = ext_is_min(q) ? (x < k[q] ? x : k[q]) : (x > k[q] ? x : k[q]);
+        }
+    unsigned long long* ks = ext_keys + kExtSlotWords * (slot & (kExtSlots - 1));
+#pragma unroll
+    for (int q = 0; q < 6; ++q) {
+        if (ext_is_min(q)) {
+            if (k[q] != kmin_id) atomicMin(&ks[q], k[q]);
+        } else if (k[q] != kmax_id) {
+            atomicMax(&ks[q], k[q]);
+        }
+    }
+}
+
+
 // Lattice Laplacian sum for window agent w (neighbours in ascending index order).
 __device__ __forceinline__ double2 lattice_sum(const double2* __restrict__ pos, long w, int r, int c, int W, int H) {
     const double2 pi = pos[w];
@@ -159,15 +232,25 @@ __device__ __forceinline__ void ego_finish(const KP& P, Ego& E, int w, int k, in
     ego_output<ST>(P, E, S, idle, k, T, pos_out, u, status, cnt, O);
 }
 
-// The lattice-window cull (window.hip, CBF_RUN_WINDOW_CULL): whether a whole-lattice call of this
-// shape can use it, its build (nominal controls, guards; copy_to: a copy of pos, nullable) and its
-// filter kernel (pos_out must not overlap pos; the queued QPs are left for k_lattice_filter_hard
-// unless `in`).
-bool window_cull_ok(int W, int H, long n_ws, const CellWs& Wk);
-void window_prep(const CellWs& Wk, int W, int H, const double2* pos, double gain, double2* vel_out,
-                 double2* copy_to, hipStream_t s);
-void window_filter(const cbf_params* p, const CellWs& Wk, int W, int H, const double2* pos, double T,
-                   double2* pos_out, double2* u, int32_t* status, int32_t* cnt, unsigned long long* stats, bool in,
-                   hipStream_t s);
+// The lattice-window cull (window.hip, CBF_RUN_WINDOW_CULL).  Geometry of a call: arrays of `rows`
+// lattice rows from lattice row row0 of a W x Hl lattice, candidates in window rows [cr0, cr1).
+struct WinGeom {
+    int W, rows, row0, Hl, cr0, cr1;
+};
+inline WinGeom whole_lattice(int W, int H) { return WinGeom{W, H, 0, H, 0, H}; }
+// whether a call of this geometry can use it (rows of 4 .. 2048 agents, guard arrays in the
+// workspace's record area)
+bool window_cull_ok(int W, int rows, long n_ws, const CellWs& Wk);
+// The build: nominal controls (vel_out: index (r - row_begin) W + c for rows [row_begin, row_end),
+// nullable), the guards, the halo-guard extents (ext_keys, nullable: sharded), a copy of pos
+// (copy_to, nullable).
+void window_prep(const CellWs& Wk, const WinGeom& Q, const double2* pos, double gain, double2* vel_out,
+                 double2* copy_to, unsigned long long* ext_keys, int row_begin, int row_end, ExtSpec X,
+                 hipStream_t s);
+// The filter kernel for the egos of lattice rows [row_begin, row_end) (pos_out must not overlap pos;
+// the queued QPs are left for k_lattice_filter_hard unless `in`).
+void window_filter(const cbf_params* p, const CellWs& Wk, const WinGeom& Q, int row_begin, int row_end,
+                   int cnt_begin, int cnt_end, const double2* pos, double T, double2* pos_out, double2* u,
+                   int32_t* status, int32_t* cnt, unsigned long long* stats, bool in, hipStream_t s);
 
 }  // namespace cbf

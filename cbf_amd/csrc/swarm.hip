@@ -13,78 +13,6 @@ namespace {
 
 inline int nblk(long n) { return (int)((n + kBlock - 1) / kBlock); }
 
-constexpr int kExtSlotWords = 16;  // one 128-B line per extents slot (6 keys used)
-constexpr int kExtSlots = 64;      // extents slots per sub-step set
-constexpr int kExtVals = 6;        // {ego min, ego max, owned max below guard, owned min above guard, owned min, max}
-__host__ __device__ constexpr bool ext_is_min(int q) { return q == 0 || q == 3 || q == 4; }
-
-struct ExtSpec {
-    int own_begin, own_end, guard;
-};
-
-// Halo-guard y-extents of one block's agents into slot (slot & (kExtSlots - 1)) of an extents
-// set (e[] per lane: {min, max} over the computed rows, {max below the guard, min above it, min,
-// max} over the owned rows; y = the lane's y where any).  The values travel as dkey()s (order-
-// preserving uint64 keys, the form the slots hold), so each wave reduces them with 32-bit DPP
-// reductions (wave_umin64 / wave_umax64) instead of 64-bit shuffle trees through LDS; a NaN y
-// keys above +inf, so it wins a maximum and fails the guard (conservative).  The LAST wave of the
-// block to arrive (an LDS counter, `arrive`, zeroed by the caller before a block barrier at
-// kernel start) combines the NW partials and issues one atomic per non-identity value.  No
-// barrier at the end (it would hold every wave until the block's slowest is done), and a quarter
-// of the per-wave atomics.  ONE: each lane holds at most one agent (its e[] are y or infinite,
-// which allows a two-reduction fast path).  Every lane of the wave must call it.
-template <int NW, bool ONE = true>
-__device__ __forceinline__ void ext_keys_flush(double (&e)[6], int any, double y,
-                                               unsigned long long* __restrict__ ext_keys, long slot,
-                                               unsigned long long (*red)[NW], int* arrive) {
-    const unsigned long long kmin_id = dkey(INFINITY), kmax_id = dkey(-INFINITY);
-    const unsigned long long act = __ballot(any);
-    const unsigned code = any ? ((e[0] != INFINITY ? 1u : 0u) | (e[2] != -INFINITY ? 2u : 0u) |
-                                 (e[3] != INFINITY ? 4u : 0u) | (e[4] != INFINITY ? 8u : 0u))
-                              : 0u;
-    const unsigned c0 = (unsigned)__shfl((int)code, act ? __ffsll((long long)act) - 1 : 0, 64);
-    unsigned long long k[6];
-    if (!act) {
-#pragma unroll
-        for (int q = 0; q < 6; ++q) k[q] = ext_is_min(q) ? kmin_id : kmax_id;
-    } else if (ONE && __ballot(any && code != c0) == 0) {
-        // the common wave: one membership pattern for all its agents, two reductions instead of six
-        const unsigned long long ky = dkey(y);
-        const unsigned long long mn = wave_umin64(any ? ky : kmin_id), mx = wave_umax64(any ? ky : kmax_id);
-        k[0] = (c0 & 1u) ? mn : kmin_id;
-        k[1] = (c0 & 1u) ? mx : kmax_id;
-        k[2] = (c0 & 2u) ? mx : kmax_id;
-        k[3] = (c0 & 4u) ? mn : kmin_id;
-        k[4] = (c0 & 8u) ? mn : kmin_id;
-        k[5] = (c0 & 8u) ? mx : kmax_id;
-    } else {
-#pragma unroll
-        for (int q = 0; q < 6; ++q) k[q] = ext_is_min(q) ? wave_umin64(dkey(e[q])) : wave_umax64(dkey(e[q]));
-    }
-    if ((threadIdx.x & 63) != 0) return;
-    const int wid = threadIdx.x >> 6;
-#pragma unroll
-    for (int q = 0; q < 6; ++q) red[q][wid] = k[q];
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    if (atomicAdd(arrive, 1) != NW - 1) return;  // not the last wave of the block
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-    for (int v = 0; v < NW; ++v)
-#pragma unroll
-        for (int q = 0; q < 6; ++q) {
-            const unsigned long long x = red[q][v];
-            k[q] = ext_is_min(q) ? (x < k[q] ? x : k[q]) : (x > k[q] ? x : k[q]);
-        }
-    unsigned long long* ks = ext_keys + kExtSlotWords * (slot & (kExtSlots - 1));
-#pragma unroll
-    for (int q = 0; q < 6; ++q) {
-        if (ext_is_min(q)) {
-            if (k[q] != kmin_id) atomicMin(&ks[q], k[q]);
-        } else if (k[q] != kmax_id) {
-            atomicMax(&ks[q], k[q]);
-        }
-    }
-}
-
 // Chained binning: the build an advance bins its new positions for (the same window in
 // cbf_lattice_run; the next sub-step's window, its own workspace, in cbf_lattice_cycle_sharded).
 // Records are indexed by this advance's slots and name the agent by its index in the next window
@@ -849,14 +777,20 @@ extern "C" int cbf_lattice_step(const cbf_params* p, const cbf_grid* grid, int32
                                nbr_count, guard_rows, extents, stats, workspace, workspace_bytes, stream);
 }
 
-// The queued-QP kernel of a whole-lattice advance without chained binning (window cull).
+// The queued-QP kernel of an advance without chained binning (window cull): the egos of window
+// bounds B, n window agents.
+static void launch_hard_plain(const cbf_params* p, const cbf_grid* grid, const CellWs& Wk, const WinBounds& B, long n,
+                              double T, double2* pos_out, double2* u, int32_t* status, int32_t* cnt,
+                              unsigned long long* stats, hipStream_t s) {
+    hipLaunchKernelGGL(k_lattice_filter_hard, dim3(lattice_hard_blocks(n)), dim3(64), 0, s, make_kp(p),
+                       make_grid(grid), B, T, pos_out, u, status, cnt, (double*)nullptr, stats, Wk.hardq, Wk.qrec,
+                       Wk.qcap, ChainSpec{}, Wk.sctl);
+}
 static void launch_hard_plain(const cbf_params* p, const cbf_grid* grid, const CellWs& Wk, int W, int H, double T,
                               double2* pos_out, double2* u, int32_t* status, int32_t* cnt, unsigned long long* stats,
                               hipStream_t s) {
     const long n = (long)W * H;
-    hipLaunchKernelGGL(k_lattice_filter_hard, dim3(lattice_hard_blocks(n)), dim3(64), 0, s, make_kp(p),
-                       make_grid(grid), make_win_bounds(W, 0, n, 0, H, 0, H, 0), T, pos_out, u, status, cnt,
-                       (double*)nullptr, stats, Wk.hardq, Wk.qrec, Wk.qcap, ChainSpec{}, Wk.sctl);
+    launch_hard_plain(p, grid, Wk, make_win_bounds(W, 0, n, 0, H, 0, H, 0), n, T, pos_out, u, status, cnt, stats, s);
 }
 
 // cbf_lattice_run_ex with CBF_RUN_WINDOW_CULL: per timestep the window build (k_window_prep:
@@ -881,12 +815,13 @@ static int lattice_run_window(const cbf_params* p, const cbf_grid* grid, int32_t
         const bool last = k + 1 == steps, out = last || hist;
         const long o = hist ? (long)k * n : 0;
         // an odd run's first build reads pos and leaves its copy in spos, which the filter then reads
-        window_prep(Wk, W, H, k == 0 && odd ? buf[0] : src, gain,
-                    out ? reinterpret_cast<double2*>(vel_out) + o : nullptr, k == 0 && odd ? buf[1] : nullptr, s);
+        const WinGeom Q = whole_lattice(W, H);
+        window_prep(Wk, Q, k == 0 && odd ? buf[0] : src, gain, out ? reinterpret_cast<double2*>(vel_out) + o : nullptr,
+                    k == 0 && odd ? buf[1] : nullptr, nullptr, 0, H, ExtSpec{0, 0, 0}, s);
         double2* uo = out ? reinterpret_cast<double2*>(u) + o : nullptr;
         int32_t* so = out ? status + o : nullptr;
         int32_t* co = out && nbr_count ? nbr_count + o : nullptr;
-        window_filter(p, Wk, W, H, src, T, dst, uo, so, co, st, in, s);
+        window_filter(p, Wk, Q, 0, H, 0, H, src, T, dst, uo, so, co, st, in, s);
         if (!in) launch_hard_plain(p, grid, Wk, W, H, T, dst, uo, so, co, st, s);
         if (int rc = (int)hipGetLastError()) return rc;
     }
@@ -894,41 +829,69 @@ static int lattice_run_window(const cbf_params* p, const cbf_grid* grid, int32_t
 }
 
 // The two phases of one window-cull timestep as separate calls (the measurement hooks: the bench
-// times the filter kernel alone).  pos_out must not overlap pos.
+// times the filter kernel alone), for the owned rows [row_begin, row_end) of a window of win_rows
+// lattice rows from win_row0 (the whole lattice, or a sharded sub-step's window).  pos_out (index
+// (r - row_begin) W + c) must not overlap pos.
+static WinGeom window_geom(int W, int H, int win_row0, int win_rows) {
+    return WinGeom{W, win_rows, win_row0, H, win_row0 > 0 ? 1 : 0,
+                   win_row0 + win_rows < H ? win_rows - 1 : win_rows};
+}
+
+extern "C" int cbf_lattice_window_build_ex(const cbf_params* p, const cbf_grid* grid, int32_t W, int32_t H,
+                                           int32_t row_begin, int32_t row_end, int32_t win_row0, int32_t win_rows,
+                                           const double* pos, double gain, double* vel_out, void* workspace,
+                                           size_t workspace_bytes, void* stream) {
+    int rc = check_lattice(p, grid, W, H, row_begin, row_end, win_row0, win_rows, pos, workspace, workspace_bytes);
+    if (rc) return rc;
+    const long n = (long)W * win_rows;
+    CellWs Wk(workspace, n, (long)grid->nx * grid->ny);
+    if (!window_cull_ok(W, win_rows, n, Wk)) return CBF_EINVAL;
+    window_prep(Wk, window_geom(W, H, win_row0, win_rows), reinterpret_cast<const double2*>(pos), gain,
+                reinterpret_cast<double2*>(vel_out), nullptr, nullptr, row_begin, row_end, ExtSpec{0, 0, 0},
+                (hipStream_t)stream);
+    return (int)hipGetLastError();
+}
+
+extern "C" int cbf_lattice_window_advance_ex(const cbf_params* p, const cbf_grid* grid, int32_t W, int32_t H,
+                                             int32_t row_begin, int32_t row_end, int32_t win_row0, int32_t win_rows,
+                                             const double* pos, double T, double* pos_out, double* u,
+                                             int32_t* status, int32_t* nbr_count, uint64_t* stats, void* workspace,
+                                             size_t workspace_bytes, void* filter_done, void* stream) {
+    int rc = check_lattice(p, grid, W, H, row_begin, row_end, win_row0, win_rows, pos, workspace, workspace_bytes);
+    if (rc) return rc;
+    const long n = (long)W * win_rows, nown = (long)W * (row_end - row_begin);
+    if (!pos_out || !u || !status) return CBF_EINVAL;
+    if (pos_out < pos + 2 * n && pos < pos_out + 2 * nown) return CBF_EINVAL;  // the filter reads pos throughout
+    CellWs Wk(workspace, n, (long)grid->nx * grid->ny);
+    if (!window_cull_ok(W, win_rows, n, Wk)) return CBF_EINVAL;
+    hipStream_t s = (hipStream_t)stream;
+    const bool in = solve_inline(p, n);
+    double2* po = reinterpret_cast<double2*>(pos_out);
+    double2* uo = reinterpret_cast<double2*>(u);
+    unsigned long long* st = reinterpret_cast<unsigned long long*>(stats);
+    window_filter(p, Wk, window_geom(W, H, win_row0, win_rows), row_begin, row_end, row_begin, row_end,
+                  reinterpret_cast<const double2*>(pos), T, po, uo, status, nbr_count, st, in, s);
+    if (filter_done)
+        if (hipError_t e = hipEventRecord((hipEvent_t)filter_done, s)) return (int)e;
+    if (!in)
+        launch_hard_plain(p, grid, Wk, make_win_bounds(W, win_row0, n, row_begin, row_end, row_begin, row_end, 0), n,
+                          T, po, uo, status, nbr_count, st, s);
+    return (int)hipGetLastError();
+}
+
 extern "C" int cbf_lattice_window_build(const cbf_params* p, const cbf_grid* grid, int32_t W, int32_t H,
                                         const double* pos, double gain, double* vel_out, void* workspace,
                                         size_t workspace_bytes, void* stream) {
-    int rc = check_lattice(p, grid, W, H, 0, H, 0, H, pos, workspace, workspace_bytes);
-    if (rc) return rc;
-    const long n = (long)W * H;
-    CellWs Wk(workspace, n, (long)grid->nx * grid->ny);
-    if (!window_cull_ok(W, H, n, Wk)) return CBF_EINVAL;
-    window_prep(Wk, W, H, reinterpret_cast<const double2*>(pos), gain, reinterpret_cast<double2*>(vel_out), nullptr,
-                (hipStream_t)stream);
-    return (int)hipGetLastError();
+    return cbf_lattice_window_build_ex(p, grid, W, H, 0, H, 0, H, pos, gain, vel_out, workspace, workspace_bytes,
+                                       stream);
 }
 
 extern "C" int cbf_lattice_window_advance(const cbf_params* p, const cbf_grid* grid, int32_t W, int32_t H,
                                           const double* pos, double T, double* pos_out, double* u, int32_t* status,
                                           int32_t* nbr_count, uint64_t* stats, void* workspace,
                                           size_t workspace_bytes, void* filter_done, void* stream) {
-    int rc = check_lattice(p, grid, W, H, 0, H, 0, H, pos, workspace, workspace_bytes);
-    if (rc) return rc;
-    const long n = (long)W * H;
-    if (!pos_out || !u || !status) return CBF_EINVAL;
-    if (pos_out < pos + 2 * n && pos < pos_out + 2 * n) return CBF_EINVAL;  // the filter reads pos throughout
-    CellWs Wk(workspace, n, (long)grid->nx * grid->ny);
-    if (!window_cull_ok(W, H, n, Wk)) return CBF_EINVAL;
-    hipStream_t s = (hipStream_t)stream;
-    const bool in = solve_inline(p, n);
-    double2* po = reinterpret_cast<double2*>(pos_out);
-    double2* uo = reinterpret_cast<double2*>(u);
-    unsigned long long* st = reinterpret_cast<unsigned long long*>(stats);
-    window_filter(p, Wk, W, H, reinterpret_cast<const double2*>(pos), T, po, uo, status, nbr_count, st, in, s);
-    if (filter_done)
-        if (hipError_t e = hipEventRecord((hipEvent_t)filter_done, s)) return (int)e;
-    if (!in) launch_hard_plain(p, grid, Wk, W, H, T, po, uo, status, nbr_count, st, s);
-    return (int)hipGetLastError();
+    return cbf_lattice_window_advance_ex(p, grid, W, H, 0, H, 0, H, pos, T, pos_out, u, status, nbr_count, stats,
+                                         workspace, workspace_bytes, filter_done, stream);
 }
 
 // `steps` timesteps of the whole lattice in one call, bit-identical to as many cbf_lattice_step
@@ -988,6 +951,24 @@ extern "C" int cbf_lattice_run(const cbf_params* p, const cbf_grid* grid, int32_
 // the last bins the rows it computed straight into the next sub-step's build (whose window is
 // exactly those rows) and accumulates that build's guard extents.  Bit-identical to nsub
 // cbf_lattice_step_sharded calls with the same geometry.
+static int cycle_sharded(const cbf_params* p, const cbf_grid* grid, int32_t W, int32_t H, int32_t own_begin,
+                         int32_t own_end, int32_t halo, int32_t nsub, int32_t sub_begin, int32_t sub_end,
+                         int32_t win_row0, int32_t win_rows, double* wpos, double gain, double T, double* wvel,
+                         double* wu, int32_t* wstatus, int32_t* wcnt, uint64_t* ext_keys, uint64_t* stats,
+                         void* workspaces, size_t ws_bytes, bool window, void* stream);
+
+extern "C" int cbf_lattice_cycle_sharded_ex(const cbf_params* p, const cbf_grid* grid, int32_t W, int32_t H,
+                                            int32_t own_begin, int32_t own_end, int32_t halo, int32_t nsub,
+                                            int32_t sub_begin, int32_t sub_end, int32_t win_row0, int32_t win_rows,
+                                            double* wpos, double gain, double T, double* wvel, double* wu,
+                                            int32_t* wstatus, int32_t* wcnt, uint64_t* ext_keys, uint64_t* stats,
+                                            void* workspaces, size_t ws_bytes, uint32_t flags, void* stream) {
+    if (flags & ~CBF_RUN_WINDOW_CULL) return CBF_EINVAL;
+    return cycle_sharded(p, grid, W, H, own_begin, own_end, halo, nsub, sub_begin, sub_end, win_row0, win_rows, wpos,
+                         gain, T, wvel, wu, wstatus, wcnt, ext_keys, stats, workspaces, ws_bytes,
+                         (flags & CBF_RUN_WINDOW_CULL) != 0, stream);
+}
+
 extern "C" int cbf_lattice_cycle_sharded(const cbf_params* p, const cbf_grid* grid, int32_t W, int32_t H,
                                          int32_t own_begin, int32_t own_end, int32_t halo, int32_t nsub,
                                          int32_t sub_begin, int32_t sub_end,
@@ -995,6 +976,68 @@ extern "C" int cbf_lattice_cycle_sharded(const cbf_params* p, const cbf_grid* gr
                                          double* wvel, double* wu, int32_t* wstatus, int32_t* wcnt,
                                          uint64_t* ext_keys, uint64_t* stats, void* workspaces, size_t ws_bytes,
                                          void* stream) {
+    return cycle_sharded(p, grid, W, H, own_begin, own_end, halo, nsub, sub_begin, sub_end, win_row0, win_rows, wpos,
+                         gain, T, wvel, wu, wstatus, wcnt, ext_keys, stats, workspaces, ws_bytes, false, stream);
+}
+
+// The window-cull form of an exchange cycle: per sub-step the window build (nominal controls,
+// guards, and the halo-guard extents of its input, as the cell-list bin / scatter accumulate them),
+// the window filter and the queued-QP kernel.  Sub-step s reads its window from one buffer and
+// writes the rows it computes -- exactly the next sub-step's window -- to the other: wpos and
+// workspace 0's spos (sized for the whole cycle window), so that the call's last sub-step writes
+// wpos (with an odd count the first build copies its window to spos).  Same results as the
+// cell-list cycle whenever its halo guard holds (the guard is the same).
+template <class Sub>
+static int cycle_sharded_window(const cbf_params* p, const cbf_grid* grid, int32_t W, int32_t H, int32_t own_begin,
+                                int32_t own_end, int32_t nsub, int32_t sub_begin, int32_t sub_end, int32_t win_row0,
+                                int32_t win_rows, double* wpos, double gain, double T, double* wvel, double* wu,
+                                int32_t* wstatus, int32_t* wcnt, uint64_t* ext_keys, uint64_t* stats,
+                                void* workspaces, size_t ws_bytes, Sub&& sub, hipStream_t st) {
+    const long ncell = (long)grid->nx * grid->ny;
+    const CellWs W0(workspaces, (long)W * win_rows, ncell);
+    if (!window_cull_ok(W, win_rows, (long)W * win_rows, W0)) return CBF_EINVAL;
+    double2* buf[2] = {reinterpret_cast<double2*>(wpos), W0.spos};
+    const int n = sub_end - sub_begin, odd = n & 1;
+    const size_t set_words = cbf_halo_ext_bytes(1) / 8;
+    unsigned long long* stw = reinterpret_cast<unsigned long long*>(stats);
+    for (int j = 0; j < n; ++j) {
+        const int k = sub_begin + j;
+        int a, b, sw0, sw1, guard;
+        sub(k, a, b, sw0, sw1, guard);
+        const int rows = sw1 - sw0;
+        void* ws = (char*)workspaces + (size_t)k * ws_bytes;
+        int rc = check_lattice(p, grid, W, H, a, b, sw0, rows, wpos, ws, ws_bytes);
+        if (rc) return rc;
+        const CellWs Wk(ws, (long)W * rows, ncell);
+        if (!window_cull_ok(W, rows, (long)W * rows, Wk)) return CBF_EINVAL;
+        const WinGeom Q{W, rows, sw0, H, sw0 > 0 ? 1 : 0, sw1 < H ? rows - 1 : rows};
+        double2* src = buf[(j + odd) & 1] + (long)(sw0 - win_row0) * W;
+        double2* dst = buf[(j + 1 + odd) & 1] + (long)(a - win_row0) * W;
+        const bool last = j + 1 == n;
+        const long o = (long)(a - win_row0) * W;
+        unsigned long long* ek = reinterpret_cast<unsigned long long*>(ext_keys) + (size_t)k * set_words;
+        // an odd call's first build reads wpos and leaves the copy its filter reads in spos
+        window_prep(Wk, Q, j == 0 && odd ? buf[0] + (long)(sw0 - win_row0) * W : src, gain,
+                    last ? reinterpret_cast<double2*>(wvel) + o : nullptr, j == 0 && odd ? src : nullptr, ek, a, b,
+                    ExtSpec{own_begin, own_end, guard}, st);
+        double2* uo = last ? reinterpret_cast<double2*>(wu) + o : nullptr;
+        int32_t* so = last ? wstatus + o : nullptr;
+        int32_t* co = last && wcnt ? wcnt + o : nullptr;
+        const bool in = solve_inline(p, (long)W * rows);
+        window_filter(p, Wk, Q, a, b, own_begin, own_end, src, T, dst, uo, so, co, stw, in, st);
+        if (!in)
+            launch_hard_plain(p, grid, Wk, make_win_bounds(W, sw0, (long)W * rows, a, b, own_begin, own_end, 0),
+                              (long)W * rows, T, dst, uo, so, co, stw, st);
+        if (int e = (int)hipGetLastError()) return e;
+    }
+    return 0;
+}
+
+static int cycle_sharded(const cbf_params* p, const cbf_grid* grid, int32_t W, int32_t H, int32_t own_begin,
+                         int32_t own_end, int32_t halo, int32_t nsub, int32_t sub_begin, int32_t sub_end,
+                         int32_t win_row0, int32_t win_rows, double* wpos, double gain, double T, double* wvel,
+                         double* wu, int32_t* wstatus, int32_t* wcnt, uint64_t* ext_keys, uint64_t* stats,
+                         void* workspaces, size_t ws_bytes, bool window, void* stream) {
     if (!p || !grid || W <= 0 || H <= 0 || halo < 2 || nsub < 1 || own_begin < 0 || own_end > H ||
         own_begin >= own_end || sub_begin < 0 || sub_end > nsub || sub_begin >= sub_end)
         return CBF_EINVAL;
@@ -1023,6 +1066,10 @@ extern "C" int cbf_lattice_cycle_sharded(const cbf_params* p, const cbf_grid* gr
         sub(k - 1, pa, pb, pw0, pw1, pg);
         if (12l * (pw1 - pw0) > 16l * (w1k - w0k)) return CBF_EINVAL;
     }
+    if (window)
+        return cycle_sharded_window(p, grid, W, H, own_begin, own_end, nsub, sub_begin, sub_end, win_row0, win_rows,
+                                    wpos, gain, T, wvel, wu, wstatus, wcnt, ext_keys, stats, workspaces, ws_bytes,
+                                    sub, st);
     for (int k = sub_begin; k < sub_end; ++k) {
         int a, b, sw0, sw1, guard;
         sub(k, a, b, sw0, sw1, guard);

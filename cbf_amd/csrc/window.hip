@@ -61,6 +61,11 @@ inline WinGuard win_guard(const CellWs& Wk, int H) {
     return g;
 }
 inline size_t win_guard_bytes(int H) { return 8 * (size_t)(4l * H + 1); }  // <= 16 W H for W >= 4
+// Geometry (WinGeom, lattice_ego.hpp): candidates are the agents of window rows [cr0, cr1).  A
+// window edge that is not a lattice edge is not a candidate row (its agents' nominal controls
+// cannot be formed there; the cell-list builds skip them likewise, and the sharded step's halo
+// guard proves them out of range), so for the guards rows beyond [cr0, cr1) do not exist.
+
 // the column extents, one float2 {rs, rp} per agent, in the scratch area (wvel, 16 B per agent)
 inline float2* win_rsp(const CellWs& Wk) { return reinterpret_cast<float2*>(Wk.wvel); }
 
@@ -145,18 +150,23 @@ __device__ __forceinline__ double ld_sc1_f64(const double* p) {
 // copy of the positions (the run's ping-pong start).  The row is staged in LDS (dynamic, 24 B per
 // column): every global load and store is coalesced, and the row scans run over contiguous
 // chunks of it.
-__global__ void __launch_bounds__(kPrepBlock) k_window_prep(int W, int H, const double2* __restrict__ pos,
+__global__ void __launch_bounds__(kPrepBlock) k_window_prep(WinGeom Q, const double2* __restrict__ pos,
                                                             double2* __restrict__ u0, float2* __restrict__ rsp,
                                                             WinGuard Gd, double gain, double2* __restrict__ vel_out,
                                                             double2* __restrict__ copy_to, int32_t* __restrict__ sctl,
-                                                            long ncell) {
+                                                            long ncell, unsigned long long* __restrict__ ext_keys,
+                                                            int row_begin, int row_end, ExtSpec X) {
     extern __shared__ double2 srow[];  // [W] positions, then [W] float2 {rs, rp}
+    const int W = Q.W;
     float2* srsp = reinterpret_cast<float2*>(srow + W);
     __shared__ double red[kPrepBlock / 64];
-    __shared__ int last;
-    const int r = xcd_block();
-    const long nwin = (long)W * H;
-    if (r == 0 && threadIdx.x == 0) build_begin(sctl, nwin, ncell);
+    __shared__ unsigned long long ered[6][kPrepBlock / 64];
+    __shared__ int last, arrive;
+    const int r = Q.cr0 + xcd_block();      // window row
+    const int rl = Q.row0 + r;              // lattice row
+    const long nwin = (long)W * Q.rows;
+    if (r == Q.cr0 && threadIdx.x == 0) build_begin(sctl, nwin, ncell);
+    if (ext_keys && threadIdx.x == 0) arrive = 0;
     const NominalSpec N = nominal_spec(sctl);
     const double2* prow = pos + (long)r * W;
 #pragma unroll
@@ -179,12 +189,12 @@ __global__ void __launch_bounds__(kPrepBlock) k_window_prep(int W, int H, const 
         const double2 pi = srow[c];
         double2 a;
         if (N.mode == CBF_NOMINAL_RANDOM) {
-            a = random_nominal(N, w, pi);
+            a = random_nominal(N, (long)Q.row0 * W + w, pi);
         } else {  // lattice_sum's neighbour order and arithmetic: (r-1, c), (r, c-1), (r, c+1), (r+1, c)
-            const double2 qu = r > 0 ? prow[c - W] : pi;
-            const double2 qd = r < H - 1 ? prow[c + W] : pi;
+            const double2 qu = rl > 0 ? prow[c - W] : pi;
+            const double2 qd = rl < Q.Hl - 1 ? prow[c + W] : pi;
             double a0 = 0.0, a1 = 0.0;
-            if (r > 0) {
+            if (rl > 0) {
                 a0 = a0 + (qu.x - pi.x);
                 a1 = a1 + (qu.y - pi.y);
             }
@@ -198,14 +208,14 @@ __global__ void __launch_bounds__(kPrepBlock) k_window_prep(int W, int H, const 
                 a0 = a0 + (q.x - pi.x);
                 a1 = a1 + (q.y - pi.y);
             }
-            if (r < H - 1) {
+            if (rl < Q.Hl - 1) {
                 a0 = a0 + (qd.x - pi.x);
                 a1 = a1 + (qd.y - pi.y);
             }
             a = make_double2(a0 * gain, a1 * gain);
         }
         u0[w] = a;
-        if (vel_out) vel_out[w] = a;
+        if (vel_out && rl >= row_begin && rl < row_end) vel_out[(long)(rl - row_begin) * W + c] = a;
         if (isfinite(pi.x) && isfinite(pi.y)) {
             ylo = pmin(ylo, pi.y);
             yhi = pmax(yhi, pi.y);
@@ -246,6 +256,36 @@ __global__ void __launch_bounds__(kPrepBlock) k_window_prep(int W, int H, const 
     double lo, hi;
     (void)block_after_min(ylo, red, &lo);   // (its barriers also order the srsp writes above)
     (void)block_before_max(yhi, red, &hi);
+    if (ext_keys) {
+        // the sharded step's halo-guard extents of this build's input positions (as the cell-list
+        // bin kernel accumulates them, every agent of the row, non-finite ones included): {min,
+        // max} over the computed rows, {max below the guard, min above it, min, max} over the owned
+        double e[6] = {INFINITY, -INFINITY, -INFINITY, INFINITY, INFINITY, -INFINITY};
+        auto nmax = [](double m, double y) { return (y > m || y != y) ? y : m; };
+        int any = 0;
+        double py = 0.0;
+        const bool comp = rl >= row_begin && rl < row_end, own = rl >= X.own_begin && rl < X.own_end;
+#pragma unroll
+        for (int j = 0; j < kPrepPer; ++j) {
+            const int c = threadIdx.x + j * kPrepBlock;
+            if (c >= W) continue;
+            const double y = srow[c].y;
+            py = y;
+            if (comp) {
+                e[0] = pmin(e[0], y);
+                e[1] = nmax(e[1], y);
+                any = 1;
+            }
+            if (own) {
+                if (rl < X.own_end - X.guard) e[2] = nmax(e[2], y);
+                if (rl >= X.own_begin + X.guard) e[3] = pmin(e[3], y);
+                e[4] = pmin(e[4], y);
+                e[5] = nmax(e[5], y);
+                any = 1;
+            }
+        }
+        ext_keys_flush<kPrepBlock / 64, false>(e, any, py, ext_keys, r, ered, &arrive);
+    }
 #pragma unroll
     for (int j = 0; j < kPrepPer; ++j) {
         const int c = threadIdx.x + j * kPrepBlock;
@@ -263,8 +303,9 @@ __global__ void __launch_bounds__(kPrepBlock) k_window_prep(int W, int H, const 
     // the last block: sylo (suffix minima from the last row down) and pyhi (prefix maxima), in
     // chunks of kPrepBlock x kPrepPer rows
     constexpr int CH = kPrepBlock * kPrepPer;
+    const int H = Q.cr1;  // rows [cr0, cr1) hold extents; below cr0 nothing is read
     double carry = INFINITY;
-    for (int base = ((H - 1) / CH) * CH; base >= 0; base -= CH) {
+    for (int base = Q.cr0 + ((H - Q.cr0 - 1) / CH) * CH; base >= Q.cr0; base -= CH) {
         double v[kPrepPer];
         double a = INFINITY;
 #pragma unroll
@@ -284,7 +325,7 @@ __global__ void __launch_bounds__(kPrepBlock) k_window_prep(int W, int H, const 
         carry = pmin(carry, t);
     }
     carry = -INFINITY;
-    for (int base = 0; base < H; base += CH) {
+    for (int base = Q.cr0; base < H; base += CH) {
         double v[kPrepPer];
         double a = -INFINITY;
 #pragma unroll
@@ -327,12 +368,13 @@ __device__ __forceinline__ void win_cand(const KP& P, const Ego& E, double2 p, i
 // taller than that continues one row at a time.
 constexpr int kWinPre = 4;
 __device__ __forceinline__ void win_rows(const KP& P, const double* __restrict__ sylo,
-                                         const double* __restrict__ pyhi, int r, int H, double y, int& Kd, int& Ku) {
+                                         const double* __restrict__ pyhi, int r, int lo, int H, double y, int& Kd,
+                                         int& Ku) {
     double su[kWinPre], pd[kWinPre];
 #pragma unroll
     for (int k = 0; k < kWinPre; ++k) {
-        su[k] = r + k + 1 < H ? sylo[r + k + 1] : INFINITY;  // beyond the last row: nothing to exclude
-        pd[k] = r - k - 1 >= 0 ? pyhi[r - k - 1] : -INFINITY;
+        su[k] = r + k + 1 < H ? sylo[r + k + 1] : INFINITY;  // beyond the candidate rows: nothing to exclude
+        pd[k] = r - k - 1 >= lo ? pyhi[r - k - 1] : -INFINITY;
     }
     Ku = 0;
     Kd = 0;
@@ -344,7 +386,7 @@ __device__ __forceinline__ void win_rows(const KP& P, const double* __restrict__
     if (Ku == kWinPre)
         while (r + Ku + 1 < H && !(sylo[r + Ku + 1] - y > P.win_d)) ++Ku;
     if (Kd == kWinPre)
-        while (r - Kd - 1 >= 0 && !(y - pyhi[r - Kd - 1] > P.win_d)) ++Kd;
+        while (r - Kd - 1 >= lo && !(y - pyhi[r - Kd - 1] > P.win_d)) ++Kd;
 }
 
 // 32-bit byte offsets into the lattice-ordered arrays (windows of < 2^28 agents, check_lattice)
@@ -424,7 +466,7 @@ __device__ __forceinline__ void window_ego(const KP& P, const WinBounds& B, int 
     }
 #endif
     int Kd = -1, Ku = -1;
-    if (fin) win_rows(P, sylo, pyhi, r, H, E.r1, Kd, Ku);
+    if (fin) win_rows(P, sylo, pyhi, r, 0, H, E.r1, Kd, Ku);
     const int KdW = wave_max_i(Kd), KuW = wave_max_i(Ku);
     HitList Hl;
     double d2 = INFINITY;
@@ -596,7 +638,7 @@ struct TileLds {
 };
 
 template <bool FZ, bool ST, bool IN>
-__global__ void __launch_bounds__(kBlock) k_window_tile(KP P, WinBounds B, int W, int H, long nwin, int tiles_x,
+__global__ void __launch_bounds__(kBlock) k_window_tile(KP P, WinBounds B, WinGeom Q, int er0, int tiles_x,
                                                         const double2* __restrict__ pos,
                                                         const double2* __restrict__ u0,
                                                         const float2* __restrict__ rsp,
@@ -609,16 +651,19 @@ __global__ void __launch_bounds__(kBlock) k_window_tile(KP P, WinBounds B, int W
                                                         int32_t* __restrict__ hardq, HardRec* __restrict__ qrec,
                                                         long qcap) {
     __shared__ TileLds L;
+    const int W = Q.W;
+    const long nwin = (long)W * Q.rows;
     const int bx = xcd_block();
     const int ty = bx / tiles_x, tx = bx - ty * tiles_x;
-    const int r0 = ty * kTileR, c0 = tx * kTileW;
+    const int r0 = er0 + ty * kTileR, c0 = tx * kTileW;  // window rows
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int r = r0 + wv, c = c0 + lane;
     const long w = (long)r * W + c;
-    const bool inside = r < H && c < W;
+    const bool inside = r < Q.rows && c < W;
     if (IN && ST && stats && (int)blockIdx.x == (int)gridDim.x - 1 && threadIdx.x < 64) stat_snapshot(stats);
     if (sctl[2] != 0) {  // the workspace is bound to another shape: report, touch nothing else
-        lattice_error_tail(W, 0, H, 0, nwin, inside ? w : nwin, u, status, cnt, stats, nullptr, 0, hardq);
+        lattice_error_tail(W, Q.row0 + B.own_lo / W, Q.row0 + B.own_hi / W, Q.row0, nwin, inside ? w : nwin, u,
+                           status, cnt, stats, nullptr, 0, hardq);
         return;
     }
     // stage the tile with its halo (beyond the lattice: +-inf positions, which no test passes, and
@@ -626,7 +671,7 @@ __global__ void __launch_bounds__(kBlock) k_window_tile(KP P, WinBounds B, int W
     for (int i = threadIdx.x; i < kTileN; i += kBlock) {
         const int lr = i / kTileCols, lc = i - lr * kTileCols;
         const int rr = r0 - kTileKS + lr, cc = c0 - kTileKC + lc;
-        if (rr >= 0 && rr < H && cc >= 0 && cc < W) {
+        if (rr >= Q.cr0 && rr < Q.cr1 && cc >= 0 && cc < W) {
             const int t = rr * W + cc;
             L.p[i] = ld_slot(pos, t);
             L.u[i] = ld_slot(u0, t);
@@ -640,8 +685,8 @@ __global__ void __launch_bounds__(kBlock) k_window_tile(KP P, WinBounds B, int W
     }
     if (threadIdx.x < kTileGuard) {
         const int a = r0 + 1 + threadIdx.x, b = r0 - kWinPre + threadIdx.x;
-        L.sy[threadIdx.x] = a < H ? sylo[a] : INFINITY;
-        L.py[threadIdx.x] = b >= 0 ? pyhi[b] : -INFINITY;
+        L.sy[threadIdx.x] = a < Q.cr1 ? sylo[a] : INFINITY;
+        L.py[threadIdx.x] = b >= Q.cr0 ? pyhi[b] : -INFINITY;
     }
     __syncthreads();
     const bool act = inside && w >= B.own_lo && w < B.own_hi;
@@ -744,7 +789,7 @@ __global__ void __launch_bounds__(kBlock) k_window_tile(KP P, WinBounds B, int W
             }
         } else if (fin) {  // the unbounded form, over the full row window (beyond the staged halo too)
             int kd, ku;
-            win_rows(P, sylo, pyhi, r, H, E.r1, kd, ku);
+            win_rows(P, sylo, pyhi, r, Q.cr0, Q.cr1, E.r1, kd, ku);
             win_direct<FZ>(P, E, w, r, c, W, kd, ku, pos, u0, rsp, d2);
         }
         O.nbrs = E.count;
@@ -764,38 +809,45 @@ __global__ void __launch_bounds__(kBlock) k_window_tile(KP P, WinBounds B, int W
 namespace cbf {
 
 // window-cull geometry a call can use: whole lattice (no halo), rows of 4 .. 2048 agents
-bool window_cull_ok(int W, int H, long n_ws, const CellWs& Wk) {
-    return W >= 4 && W <= kWinMaxW && H >= 1 && win_guard_bytes(H) <= 16 * (size_t)n_ws && Wk.cs != nullptr;
+bool window_cull_ok(int W, int rows, long n_ws, const CellWs& Wk) {
+    return W >= 4 && W <= kWinMaxW && rows >= 1 && win_guard_bytes(rows) <= 16 * (size_t)n_ws && Wk.cs != nullptr;
 }
 
-void window_prep(const CellWs& Wk, int W, int H, const double2* pos, double gain, double2* vel_out,
-                 double2* copy_to, hipStream_t s) {
-    hipLaunchKernelGGL(k_window_prep, dim3(H), dim3(kPrepBlock), 24 * (size_t)W, s, W, H, pos, Wk.svel, win_rsp(Wk),
-                       win_guard(Wk, H), gain, vel_out, copy_to, Wk.sctl, Wk.ncell);
+void window_prep(const CellWs& Wk, const WinGeom& Q, const double2* pos, double gain, double2* vel_out,
+                 double2* copy_to, unsigned long long* ext_keys, int row_begin, int row_end, ExtSpec X,
+                 hipStream_t s) {
+    hipLaunchKernelGGL(k_window_prep, dim3(Q.cr1 - Q.cr0), dim3(kPrepBlock), 24 * (size_t)Q.W, s, Q, pos, Wk.svel,
+                       win_rsp(Wk), win_guard(Wk, Q.rows), gain, vel_out, copy_to, Wk.sctl, Wk.ncell, ext_keys,
+                       row_begin, row_end, X);
 }
 
-// The filter kernel of a window-cull advance (pos_out must not overlap pos); the queued QPs are
-// then solved by k_lattice_filter_hard (the caller launches it unless the solve is inline).
-void window_filter(const cbf_params* p, const CellWs& Wk, int W, int H, const double2* pos, double T,
-                   double2* pos_out, double2* u, int32_t* status, int32_t* cnt, unsigned long long* stats, bool in,
-                   hipStream_t s) {
-    const long n = (long)W * H;
+// The filter kernel of a window-cull advance of the egos of lattice rows [row_begin, row_end)
+// (statistics over rows [cnt_begin, cnt_end)); pos_out (index (r - row_begin) W + c) must not
+// overlap pos.  The queued QPs are then solved by k_lattice_filter_hard (the caller launches it
+// unless the solve is inline).
+void window_filter(const cbf_params* p, const CellWs& Wk, const WinGeom& Q, int row_begin, int row_end,
+                   int cnt_begin, int cnt_end, const double2* pos, double T, double2* pos_out, double2* u,
+                   int32_t* status, int32_t* cnt, unsigned long long* stats, bool in, hipStream_t s) {
+    const int W = Q.W;
+    const long n = (long)W * Q.rows;
     const KP kp = make_kp(p);
-    const WinBounds B = make_win_bounds(W, 0, n, 0, H, 0, H, 0);
-    const WinGuard Gd = win_guard(Wk, H);
+    const WinBounds B = make_win_bounds(W, Q.row0, n, row_begin, row_end, cnt_begin, cnt_end, 0);
+    const WinGuard Gd = win_guard(Wk, Q.rows);
 #if CBF_WIN_TILE
-    const int tiles_x = (W + kTileW - 1) / kTileW, tiles_y = (H + kTileR - 1) / kTileR;
+    const int tiles_x = (W + kTileW - 1) / kTileW, tiles_y = (row_end - row_begin + kTileR - 1) / kTileR;
     const auto tile =
         in ? (stats ? (p->f_is_zero ? k_window_tile<true, true, true> : k_window_tile<false, true, true>)
                     : (p->f_is_zero ? k_window_tile<true, false, true> : k_window_tile<false, false, true>))
            : (stats ? (p->f_is_zero ? k_window_tile<true, true, false> : k_window_tile<false, true, false>)
                     : (p->f_is_zero ? k_window_tile<true, false, false> : k_window_tile<false, false, false>));
-    hipLaunchKernelGGL(tile, dim3((unsigned)(tiles_x * tiles_y)), dim3(kBlock), 0, s, kp, B, W, H, n, tiles_x, pos,
-                       (const double2*)Wk.svel, (const float2*)win_rsp(Wk), (const double*)Gd.sylo,
+    hipLaunchKernelGGL(tile, dim3((unsigned)(tiles_x * tiles_y)), dim3(kBlock), 0, s, kp, B, Q, row_begin - Q.row0,
+                       tiles_x, pos, (const double2*)Wk.svel, (const float2*)win_rsp(Wk), (const double*)Gd.sylo,
                        (const double*)Gd.pyhi, (const int32_t*)Wk.sctl, T, pos_out, u, status, cnt, stats, Wk.hardq,
                        Wk.qrec, Wk.qcap);
     return;
 #endif
+    // the untiled form: whole lattices only
+    const int H = Q.rows;
     const auto filter =
         in ? (stats ? (p->f_is_zero ? k_window_filter<true, true, true> : k_window_filter<false, true, true>)
                     : (p->f_is_zero ? k_window_filter<true, false, true> : k_window_filter<false, false, true>))

@@ -88,10 +88,15 @@ class Sub:
 class HipBackend:
     """Device work of one rank through libcbf_amd.so."""
 
-    def __init__(self, W, H, gain, T, params, grid, win_rows, nsub=1, nominal=None):
+    def __init__(self, W, H, gain, T, params, grid, win_rows, nsub=1, nominal=None, cull="cells"):
         import torch
         from . import _lib, swarm
         self.torch, self._lib, self.swarm = torch, _lib, swarm
+        # "window": every sub-step through the lattice-window cull (cbf_lattice_cycle_sharded_ex,
+        # CBF_RUN_WINDOW_CULL); same results whenever the halo guard holds
+        if cull not in ("cells", "window"):
+            raise ValueError(f"cull must be 'cells' or 'window', got {cull!r}")
+        self.cull = cull
         self.dev = torch.device("cuda", torch.cuda.current_device())
         self.W, self.H, self.gain, self.T = W, H, gain, T
         self.cp = params.c()
@@ -155,6 +160,9 @@ class HipBackend:
                                       L.stream_handle()), "cbf_halo_unpack")
 
     def lattice_step(self, S, s, sub):
+        if self.cull == "window":   # one sub-step = a cycle call of one sub-step
+            self.lattice_cycle(S, s, s + 1)
+            return
         L, P, W = self._lib, self._lib.ptr, self.W
         o = (sub.a - S.w0) * W
         L.check(L.lib.cbf_lattice_step_sharded(
@@ -168,15 +176,22 @@ class HipBackend:
         the sub-steps after the first are binned by the previous sub-step's advance)."""
         L, P = self._lib, self._lib.ptr
         s1 = self.nsub if s1 is None else s1
-        L.check(L.lib.cbf_lattice_cycle_sharded(
+        L.check(L.lib.cbf_lattice_cycle_sharded_ex(
             self.cp, L.C.byref(self.grid), self.W, self.H, S.rb, S.re, S.halo, self.nsub, s0, s1, S.w0, S.win_rows,
             P(S.wpos), self.gain, self.T, P(S.wvel), P(S.wu), P(S.wstatus), P(S.wcnt), P(self.ext_keys),
-            P(S.stats_ptr()), P(self.ws_all), self.ws_bytes, L.stream_handle()), "cbf_lattice_cycle_sharded")
+            P(S.stats_ptr()), P(self.ws_all), self.ws_bytes, L.RUN_WINDOW_CULL if self.cull == "window" else 0,
+            L.stream_handle()), "cbf_lattice_cycle_sharded_ex")
         self._checked(f"cbf_lattice_cycle_sharded (sub-steps {s0}..{s1 - 1}, stats {S.collect_stats})", S)
 
     def lattice_build(self, S):
         L, P = self._lib, self._lib.ptr
         sub = S.subs[-1]
+        if self.cull == "window":
+            L.check(L.lib.cbf_lattice_window_build_ex(
+                self.cp, L.C.byref(self.grid), self.W, self.H, S.rb, S.re, sub.w0, sub.w1 - sub.w0,
+                P(S.wpos[(sub.w0 - S.w0) * self.W:]), self.gain, P(S.vel), P(self.wss[-1]), self.ws_bytes,
+                L.stream_handle()), "cbf_lattice_window_build_ex")
+            return
         L.check(L.lib.cbf_lattice_build(self.cp, L.C.byref(self.grid), self.W, self.H, S.rb, S.re, sub.w0,
                                         sub.w1 - sub.w0, P(S.wpos[(sub.w0 - S.w0) * self.W:]), self.gain, P(S.vel),
                                         P(self.wss[-1]), self.ws_bytes, L.stream_handle()), "cbf_lattice_build")
@@ -184,6 +199,16 @@ class HipBackend:
     def lattice_advance(self, S, mark=None):
         L, P = self._lib, self._lib.ptr
         sub = S.subs[-1]
+        if self.cull == "window":   # (new owned positions into scratch: kernel timing, the state stays)
+            if getattr(self, "_own_next", None) is None:
+                self._own_next = self.torch.empty_like(S.own)
+            L.check(L.lib.cbf_lattice_window_advance_ex(
+                self.cp, L.C.byref(self.grid), self.W, self.H, S.rb, S.re, sub.w0, sub.w1 - sub.w0,
+                P(S.wpos[(sub.w0 - S.w0) * self.W:]), self.T, P(self._own_next), P(S.u), P(S.status),
+                P(S.nbr_count), P(S.stats_ptr()), P(self.wss[-1]), self.ws_bytes,
+                L.C.c_void_p(mark.cuda_event if mark is not None else 0), L.stream_handle()),
+                "cbf_lattice_window_advance_ex")
+            return
         L.check(L.lib.cbf_lattice_advance_marked(
             self.cp, L.C.byref(self.grid), self.W, self.H, S.rb, S.re, sub.w0, sub.w1 - sub.w0,
             P(S.wpos[(sub.w0 - S.w0) * self.W:]), self.T, P(S.own), P(S.u), P(S.status), P(S.nbr_count), sub.guard,
@@ -224,7 +249,7 @@ class ShardedLattice:
 
     def __init__(self, W, rows_per_rank, seed=0, halo=4, substeps=4, gain=scenarios.LATTICE_GAIN, T=scenarios.T,
                  params=None, backend=None, group=None, pos_global=None, spacing=scenarios.LATTICE_SPACING,
-                 nominal=None, exchange="neighbour"):
+                 nominal=None, exchange="neighbour", cull="cells"):
         import torch
         import torch.distributed as dist
         from .swarm import FilterParams, make_grid
@@ -253,7 +278,7 @@ class ShardedLattice:
         grid = make_grid(-1.0 - a, self.w0 * a - 1.0 - a, W * a + 1.0, self.w1 * a + 1.0,
                          self.params.safety_distance * 1.02)
         if backend is None:
-            backend = HipBackend(W, self.H, gain, T, self.params, grid, self.win_rows, substeps, nominal)
+            backend = HipBackend(W, self.H, gain, T, self.params, grid, self.win_rows, substeps, nominal, cull)
         self.be = backend
         t = backend.tensor
         self.wpos = t(win)

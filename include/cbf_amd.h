@@ -304,6 +304,15 @@ int cbf_lattice_window_advance(const cbf_params* p, const cbf_grid* grid, int32_
                                double T, double* pos_out, double* u, int32_t* status, int32_t* nbr_count,
                                uint64_t* stats, void* workspace, size_t workspace_bytes, void* filter_done,
                                void* stream);
+/* The same for the owned rows [row_begin, row_end) of a window of win_rows lattice rows from
+ * win_row0 (one sub-step of a sharded stripe); pos holds the window, pos_out the owned rows. */
+int cbf_lattice_window_build_ex(const cbf_params* p, const cbf_grid* grid, int32_t W, int32_t H, int32_t row_begin,
+                                int32_t row_end, int32_t win_row0, int32_t win_rows, const double* pos, double gain,
+                                double* vel_out, void* workspace, size_t workspace_bytes, void* stream);
+int cbf_lattice_window_advance_ex(const cbf_params* p, const cbf_grid* grid, int32_t W, int32_t H, int32_t row_begin,
+                                  int32_t row_end, int32_t win_row0, int32_t win_rows, const double* pos, double T,
+                                  double* pos_out, double* u, int32_t* status, int32_t* nbr_count, uint64_t* stats,
+                                  void* workspace, size_t workspace_bytes, void* filter_done, void* stream);
 
 int cbf_lattice_build(const cbf_params* p, const cbf_grid* grid, int32_t W, int32_t H, int32_t row_begin,
                       int32_t row_end, int32_t win_row0, int32_t win_rows, const double* pos, double gain,
@@ -410,6 +419,15 @@ int cbf_lattice_cycle_sharded(const cbf_params* p, const cbf_grid* grid, int32_t
                               int32_t win_row0, int32_t win_rows, double* wpos, double gain, double T, double* wvel,
                               double* wu, int32_t* wstatus, int32_t* wcnt, uint64_t* ext_keys, uint64_t* stats,
                               void* workspaces, size_t ws_bytes, void* stream);
+/* cbf_lattice_cycle_sharded with flags: CBF_RUN_WINDOW_CULL runs every sub-step with the
+ * lattice-window cull (workspaces as for the cell list; the call alternates between wpos and
+ * workspace 0's sorted-position area, the last sub-step writing wpos).  Same results whenever the
+ * halo guard holds. */
+int cbf_lattice_cycle_sharded_ex(const cbf_params* p, const cbf_grid* grid, int32_t W, int32_t H, int32_t own_begin,
+                                 int32_t own_end, int32_t halo, int32_t nsub, int32_t sub_begin, int32_t sub_end,
+                                 int32_t win_row0, int32_t win_rows, double* wpos, double gain, double T, double* wvel,
+                                 double* wu, int32_t* wstatus, int32_t* wcnt, uint64_t* ext_keys, uint64_t* stats,
+                                 void* workspaces, size_t ws_bytes, uint32_t flags, void* stream);
 
 /*
  * Batched Monte-Carlo rendezvous (SURVEY cfg5): n_scen independent scenarios, each with

@@ -26,9 +26,9 @@ def _free_port():
 
 
 def _worker(rank, ws, port, W, R, steps, q, k=4, graph=False, run=False, nominal=None, exchange="neighbour",
-            placement="auto"):
+            placement="auto", cull="cells"):
     try:
-        _work(rank, ws, port, W, R, steps, q, k, graph, run, nominal, exchange, placement)
+        _work(rank, ws, port, W, R, steps, q, k, graph, run, nominal, exchange, placement, cull)
     except BaseException as e:   # report instead of leaving the test waiting on the queue
         q.put((rank, "error", repr(e)))
         raise
@@ -39,7 +39,7 @@ def _spacing(nominal):
     return scenarios.LATTICE_SPACING if nominal is None else 0.22   # random walk: the cfg4r spacing
 
 
-def _work(rank, ws, port, W, R, steps, q, k, graph, run, nominal, exchange, placement):
+def _work(rank, ws, port, W, R, steps, q, k, graph, run, nominal, exchange, placement, cull):
     import datetime
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     torch.cuda.set_device(0)
@@ -50,7 +50,7 @@ def _work(rank, ws, port, W, R, steps, q, k, graph, run, nominal, exchange, plac
     # guard catches it with the default 4-row halo): 10 rows per sub-step cover it
     S = ShardedLattice(W, R, seed=7, substeps=k, nominal=nominal, spacing=_spacing(nominal),
                        halo=4 if nominal is None else 10, exchange=exchange,
-                       params=FilterParams(solve_placement=placement))
+                       params=FilterParams(solve_placement=placement), cull=cull)
     if graph == "cycle":   # whole exchange cycles replayed as one hipGraph each
         S.capture_cycle()
     elif graph:
@@ -94,24 +94,32 @@ RANDOM = ("random", 1.0, 3)   # the random-walk nominal control (CBF_NOMINAL_RAN
 
 # placement: where the full QP solves run (cbf_params.solve_inline_max).  These small windows pick
 # "inline" under "auto"; the "queued" cases run the queue kernel and its chained binning into the
-# next sub-step's workspace (the path of windows above 131,072 agents).
-@pytest.mark.parametrize("ws,k,graph,run,nominal,exchange,placement", [
-    (2, 1, False, False, None, "neighbour", "auto"), (3, 4, False, False, None, "neighbour", "auto"),
-    (2, 4, True, False, None, "neighbour", "auto"), (3, 4, False, True, None, "neighbour", "auto"),
-    (2, 2, False, True, None, "neighbour", "auto"), (2, 4, "cycle", True, None, "neighbour", "auto"),
-    (2, 2, False, True, RANDOM, "neighbour", "auto"), (3, 4, False, "mixed", None, "neighbour", "auto"),
-    (2, 4, False, "replay", None, "neighbour", "auto"), (3, 4, "cycle", "replay", None, "neighbour", "auto"),
-    (4, 2, False, True, None, "neighbour", "auto"), (3, 4, False, True, None, "allgather", "auto"),
-    (3, 4, False, True, None, "neighbour", "queued"), (2, 2, False, True, RANDOM, "neighbour", "queued"),
-    (3, 4, "cycle", "replay", None, "neighbour", "queued"), (2, 1, False, False, None, "neighbour", "queued")])
-def test_sharded_equals_single_gpu(ws, k, graph, run, nominal, exchange, placement):
+# next sub-step's workspace (the path of windows above 131,072 agents).  cull "window": every
+# sub-step through the lattice-window cull (cbf_lattice_cycle_sharded_ex, CBF_RUN_WINDOW_CULL).
+NB = "neighbour"
+
+
+@pytest.mark.parametrize("ws,k,graph,run,nominal,exchange,placement,cull", [
+    (2, 1, False, False, None, NB, "auto", "cells"), (3, 4, False, False, None, NB, "auto", "cells"),
+    (2, 4, True, False, None, NB, "auto", "cells"), (3, 4, False, True, None, NB, "auto", "cells"),
+    (2, 2, False, True, None, NB, "auto", "cells"), (2, 4, "cycle", True, None, NB, "auto", "cells"),
+    (2, 2, False, True, RANDOM, NB, "auto", "cells"), (3, 4, False, "mixed", None, NB, "auto", "cells"),
+    (2, 4, False, "replay", None, NB, "auto", "cells"), (3, 4, "cycle", "replay", None, NB, "auto", "cells"),
+    (4, 2, False, True, None, NB, "auto", "cells"), (3, 4, False, True, None, "allgather", "auto", "cells"),
+    (3, 4, False, True, None, NB, "queued", "cells"), (2, 2, False, True, RANDOM, NB, "queued", "cells"),
+    (3, 4, "cycle", "replay", None, NB, "queued", "cells"), (2, 1, False, False, None, NB, "queued", "cells"),
+    (2, 1, False, False, None, NB, "auto", "window"), (3, 4, False, True, None, NB, "auto", "window"),
+    (2, 4, True, False, None, NB, "auto", "window"), (3, 4, "cycle", "replay", None, NB, "auto", "window"),
+    (3, 4, False, "mixed", None, NB, "queued", "window"), (2, 2, False, True, RANDOM, NB, "auto", "window"),
+    (4, 2, False, True, None, NB, "queued", "window")])
+def test_sharded_equals_single_gpu(ws, k, graph, run, nominal, exchange, placement, cull):
     from cbf_amd import scenarios, swarm
     W, R, steps = 96, 40, 6
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
     procs = [ctx.Process(target=_worker, args=(r, ws, port, W, R, steps, q, k, graph, run, nominal, exchange,
-                                               placement)) for r in range(ws)]
+                                               placement, cull)) for r in range(ws)]
     for p in procs:
         p.start()
     res = sorted([q.get(timeout=120) for _ in range(ws)], key=lambda t: t[0])
