@@ -1,11 +1,13 @@
-# GPU box, round 4: window tests, then A/B of window-filter variants (tools/_abt) against the cell
-# list, then a kernel trace of the default bench (window cull).
+# GPU box, round 4: window-cull tests (single GPU and sharded), then A/B of window-filter variants
+# (tools/_abt) against the cell list at 1024 and 128 rows, then a kernel trace of the default bench.
 set -u
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
 O=gpurun_out/r04d; mkdir -p $O; : > $O/ab.txt
-timeout -k 10 600 python -u -m pytest tests/test_gpu_window.py tests/test_gpu_parity.py tests/test_gpu_checkpoint.py tests/test_gpu_torch_ops.py -k "window or cell_starts or lattice_step_vs or run_matches or checkpoint or lattice_run_op" -x -q && timeout -k 10 900 python -u -m pytest tests/test_shard_gpu.py -k "window" -x -q --timeout 300 --timeout-method thread >> $O/pytest_window.log 2>&1 --timeout 240 --timeout-method thread > $O/pytest_window.log 2>&1 || { tail -40 $O/pytest_window.log; exit 1; }
+timeout -k 10 600 python -u -m pytest tests/test_gpu_window.py tests/test_gpu_parity.py tests/test_gpu_checkpoint.py tests/test_gpu_torch_ops.py -k "window or cell_starts or lattice_step_vs or run_matches or checkpoint or lattice_run_op" -x -q --timeout 240 --timeout-method thread > $O/pytest_window.log 2>&1 || { tail -40 $O/pytest_window.log; exit 1; }
 tail -1 $O/pytest_window.log
+timeout -k 10 900 python -u -m pytest tests/test_shard_gpu.py -k "window" -x -q --timeout 300 --timeout-method thread > $O/pytest_shard.log 2>&1 || { tail -40 $O/pytest_shard.log; exit 1; }
+tail -1 $O/pytest_shard.log
 for rep in 1 2; do
   for rows in 1024 128; do
     timeout -k 10 120 python tools/ab_window.py . cells 0.145 $rows >> $O/ab.txt || exit 2
