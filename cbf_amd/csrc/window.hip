@@ -11,7 +11,7 @@
 // The proof uses two guards, both exact in fp64 (rounding is monotone, so a computed difference
 // beyond d = win_d makes e * e >= cull_t: the candidate fails s < cull_t):
 //   rows     per lattice row the min / max y over its agents; sylo[r] = min over rows >= r,
-//            pyhi[r] = max over rows <= r (k_window_prep, last block).  Rows r + k + 1 and beyond
+//            pyhi[r] = max over rows <= r (k_window_rowscan).  Rows r + k + 1 and beyond
 //            are out of range of an ego at y once sylo[r + k + 1] - y > d (and below likewise).
 //   columns  per agent of row r' the min x over the columns >= its own (rs) and the max x over the
 //            columns <= its own (rp), rounded outward to fp32.  Columns c' and beyond of row r'
@@ -45,8 +45,6 @@ constexpr int kWinMaxW = kPrepBlock * kPrepPer;
 
 // The guard arrays in the workspace's record area (cs, 16 B per agent, unused by this path).
 struct WinGuard {
-    int32_t* ticket;  // prep blocks done (a control word: the last block scans the row extents, then
-                      // re-zeroes it; a zero-filled workspace starts at 0 whatever its cs area held)
     double* rowy;     // [2 H] {min y, max y} per row (finite agents)
     double* sylo;     // [H + 1] min over rows >= r of the row minima (sylo[H] = +inf)
     double* pyhi;     // [H] max over rows <= r of the row maxima
@@ -54,7 +52,6 @@ struct WinGuard {
 inline WinGuard win_guard(const CellWs& Wk, int H) {
     WinGuard g;
     char* p = reinterpret_cast<char*>(Wk.cs);
-    g.ticket = Wk.sctl + 16;
     g.rowy = reinterpret_cast<double*>(p);
     g.sylo = g.rowy + 2l * H;
     g.pyhi = g.sylo + (H + 1);
@@ -132,24 +129,13 @@ __device__ __forceinline__ double block_before_max(double v, double* red, double
     return pmax(ex, before);
 }
 
-__device__ __forceinline__ void st_sc1_f64(double* p, double v) {
-    __hip_atomic_store(reinterpret_cast<unsigned long long*>(p), (unsigned long long)__double_as_longlong(v),
-                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ double ld_sc1_f64(const double* p) {
-    return __longlong_as_double((long long)__hip_atomic_load(reinterpret_cast<const unsigned long long*>(p),
-                                                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-}
-
-// Window-cull build of one timestep: one block per lattice row.  Per agent the nominal control
+// Window-cull build of one timestep: one block per candidate row.  Per agent the nominal control
 // (the lattice Laplacian of cross_and_rescue.py:121-125 shape scaled by gain, or the random walk
 // of CBF_NOMINAL_RANDOM: the scatter's arithmetic) into u0 (and vel_out), the column extents into
-// rsp; per row its y extents.  The last block to finish (a ticket; the guide's sc1 hand-off: sc1
-// stores, every storing wave's vmcnt(0), a block barrier, one agent-scope add, sc1 loads by the
-// block whose add came last) turns the row extents into sylo / pyhi.  copy_to (nullable) gets a
-// copy of the positions (the run's ping-pong start).  The row is staged in LDS (dynamic, 24 B per
-// column): every global load and store is coalesced, and the row scans run over contiguous
-// chunks of it.
+// rsp; per row its y extents (turned into the row guard by k_window_rowscan); the sharded step's
+// halo-guard extents (ext_keys, nullable).  copy_to (nullable) gets a copy of the positions (the
+// run's ping-pong start).  The row is staged in LDS (dynamic, 24 B per column): every global load
+// and store is coalesced, and the row scans run over contiguous chunks of it.
 __global__ void __launch_bounds__(kPrepBlock) k_window_prep(WinGeom Q, const double2* __restrict__ pos,
                                                             double2* __restrict__ u0, float2* __restrict__ rsp,
                                                             WinGuard Gd, double gain, double2* __restrict__ vel_out,
@@ -161,7 +147,7 @@ __global__ void __launch_bounds__(kPrepBlock) k_window_prep(WinGeom Q, const dou
     float2* srsp = reinterpret_cast<float2*>(srow + W);
     __shared__ double red[kPrepBlock / 64];
     __shared__ unsigned long long ered[6][kPrepBlock / 64];
-    __shared__ int last, arrive;
+    __shared__ int arrive;
     const int r = Q.cr0 + xcd_block();      // window row
     const int rl = Q.row0 + r;              // lattice row
     const long nwin = (long)W * Q.rows;
@@ -292,18 +278,19 @@ __global__ void __launch_bounds__(kPrepBlock) k_window_prep(WinGeom Q, const dou
         if (c < W) rsp[(long)r * W + c] = srsp[c];
     }
     if (threadIdx.x == 0) {
-        st_sc1_f64(&Gd.rowy[2l * r], lo);
-        st_sc1_f64(&Gd.rowy[2l * r + 1], hi);
+        Gd.rowy[2l * r] = lo;
+        Gd.rowy[2l * r + 1] = hi;
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x == 0) last = atomicAdd(Gd.ticket, 1) == (int)gridDim.x - 1;
-    __syncthreads();
-    if (!last) return;
-    // the last block: sylo (suffix minima from the last row down) and pyhi (prefix maxima), in
-    // chunks of kPrepBlock x kPrepPer rows
+}
+
+// The row guard's arrays from the row extents k_window_prep wrote (one block, chunks of kPrepBlock
+// x kPrepPer rows): sylo[r] = min over candidate rows >= r of the row minima (sylo[cr1] = +inf),
+// pyhi[r] = max over candidate rows <= r of the row maxima.  (A ticket at the end of the prep
+// kernel, whose last block did this, serialised 1,024 same-address atomics: 29 us per build.)
+__global__ void __launch_bounds__(kPrepBlock) k_window_rowscan(WinGeom Q, WinGuard Gd) {
+    __shared__ double red[kPrepBlock / 64];
     constexpr int CH = kPrepBlock * kPrepPer;
-    const int H = Q.cr1;  // rows [cr0, cr1) hold extents; below cr0 nothing is read
+    const int H = Q.cr1;
     double carry = INFINITY;
     for (int base = Q.cr0 + ((H - Q.cr0 - 1) / CH) * CH; base >= Q.cr0; base -= CH) {
         double v[kPrepPer];
@@ -311,7 +298,7 @@ __global__ void __launch_bounds__(kPrepBlock) k_window_prep(WinGeom Q, const dou
 #pragma unroll
         for (int j = kPrepPer - 1; j >= 0; --j) {
             const int rr = base + threadIdx.x * kPrepPer + j;
-            v[j] = rr < H ? ld_sc1_f64(&Gd.rowy[2l * rr]) : INFINITY;
+            v[j] = rr < H ? Gd.rowy[2l * rr] : INFINITY;
             a = pmin(a, v[j]);
             v[j] = a;
         }
@@ -331,7 +318,7 @@ __global__ void __launch_bounds__(kPrepBlock) k_window_prep(WinGeom Q, const dou
 #pragma unroll
         for (int j = 0; j < kPrepPer; ++j) {
             const int rr = base + threadIdx.x * kPrepPer + j;
-            v[j] = rr < H ? ld_sc1_f64(&Gd.rowy[2l * rr + 1]) : -INFINITY;
+            v[j] = rr < H ? Gd.rowy[2l * rr + 1] : -INFINITY;
             a = pmax(a, v[j]);
             v[j] = a;
         }
@@ -344,10 +331,7 @@ __global__ void __launch_bounds__(kPrepBlock) k_window_prep(WinGeom Q, const dou
         }
         carry = pmax(carry, t);
     }
-    if (threadIdx.x == 0) {
-        Gd.sylo[H] = INFINITY;
-        *Gd.ticket = 0;
-    }
+    if (threadIdx.x == 0) Gd.sylo[H] = INFINITY;
 }
 
 // One candidate of the window scan: the cull test of cross_and_rescue.py:141-150 for agents
@@ -819,6 +803,7 @@ void window_prep(const CellWs& Wk, const WinGeom& Q, const double2* pos, double 
     hipLaunchKernelGGL(k_window_prep, dim3(Q.cr1 - Q.cr0), dim3(kPrepBlock), 24 * (size_t)Q.W, s, Q, pos, Wk.svel,
                        win_rsp(Wk), win_guard(Wk, Q.rows), gain, vel_out, copy_to, Wk.sctl, Wk.ncell, ext_keys,
                        row_begin, row_end, X);
+    hipLaunchKernelGGL(k_window_rowscan, dim3(1), dim3(kPrepBlock), 0, s, Q, win_guard(Wk, Q.rows));
 }
 
 // The filter kernel of a window-cull advance of the egos of lattice rows [row_begin, row_end)
