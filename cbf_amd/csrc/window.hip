@@ -136,6 +136,7 @@ __device__ __forceinline__ double block_before_max(double v, double* red, double
 // halo-guard extents (ext_keys, nullable).  copy_to (nullable) gets a copy of the positions (the
 // run's ping-pong start).  The row is staged in LDS (dynamic, 24 B per column): every global load
 // and store is coalesced, and the row scans run over contiguous chunks of it.
+template <int PER>  // columns per thread: W <= kPrepBlock x PER
 __global__ void __launch_bounds__(kPrepBlock) k_window_prep(WinGeom Q, const double2* __restrict__ pos,
                                                             double2* __restrict__ u0, float2* __restrict__ rsp,
                                                             WinGuard Gd, double gain, double2* __restrict__ vel_out,
@@ -145,7 +146,7 @@ __global__ void __launch_bounds__(kPrepBlock) k_window_prep(WinGeom Q, const dou
     extern __shared__ double2 srow[];  // [W] positions, then [W] float2 {rs, rp}
     const int W = Q.W;
     float2* srsp = reinterpret_cast<float2*>(srow + W);
-    __shared__ double red[kPrepBlock / 64];
+    __shared__ double red4[4][kPrepBlock / 64];
     __shared__ unsigned long long ered[6][kPrepBlock / 64];
     __shared__ int arrive;
     const int r = Q.cr0 + xcd_block();      // window row
@@ -154,35 +155,45 @@ __global__ void __launch_bounds__(kPrepBlock) k_window_prep(WinGeom Q, const dou
     if (r == Q.cr0 && threadIdx.x == 0) build_begin(sctl, nwin, ncell);
     if (ext_keys && threadIdx.x == 0) arrive = 0;
     const NominalSpec N = nominal_spec(sctl);
+    const bool lap = N.mode != CBF_NOMINAL_RANDOM;
     const double2* prow = pos + (long)r * W;
+    // every load of the block in one round trip: the row (coalesced: column c = thread + j * block)
+    // and, for the Laplacian, the rows above and below
+    double2 p[PER], qu[PER], qd[PER];
 #pragma unroll
-    for (int j = 0; j < kPrepPer; ++j) {
+    for (int j = 0; j < PER; ++j) {
         const int c = threadIdx.x + j * kPrepBlock;
         if (c < W) {
-            const double2 p = prow[c];
-            srow[c] = p;
-            if (copy_to) copy_to[(long)r * W + c] = p;
+            p[j] = prow[c];
+            if (lap && rl > 0) qu[j] = prow[c - W];
+            if (lap && rl < Q.Hl - 1) qd[j] = prow[c + W];
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+        const int c = threadIdx.x + j * kPrepBlock;
+        if (c < W) {
+            srow[c] = p[j];
+            if (copy_to) copy_to[(long)r * W + c] = p[j];
         }
     }
     __syncthreads();
-    // nominal controls (coalesced: column c = thread + j * block) and the row's y extents
+    // nominal controls and the row's y extents
     double ylo = INFINITY, yhi = -INFINITY;
 #pragma unroll
-    for (int j = 0; j < kPrepPer; ++j) {
+    for (int j = 0; j < PER; ++j) {
         const int c = threadIdx.x + j * kPrepBlock;
         if (c >= W) continue;
         const long w = (long)r * W + c;
-        const double2 pi = srow[c];
+        const double2 pi = p[j];
         double2 a;
-        if (N.mode == CBF_NOMINAL_RANDOM) {
+        if (!lap) {
             a = random_nominal(N, (long)Q.row0 * W + w, pi);
         } else {  // lattice_sum's neighbour order and arithmetic: (r-1, c), (r, c-1), (r, c+1), (r+1, c)
-            const double2 qu = rl > 0 ? prow[c - W] : pi;
-            const double2 qd = rl < Q.Hl - 1 ? prow[c + W] : pi;
             double a0 = 0.0, a1 = 0.0;
             if (rl > 0) {
-                a0 = a0 + (qu.x - pi.x);
-                a1 = a1 + (qu.y - pi.y);
+                a0 = a0 + (qu[j].x - pi.x);
+                a1 = a1 + (qu[j].y - pi.y);
             }
             if (c > 0) {
                 const double2 q = srow[c - 1];
@@ -195,8 +206,8 @@ __global__ void __launch_bounds__(kPrepBlock) k_window_prep(WinGeom Q, const dou
                 a1 = a1 + (q.y - pi.y);
             }
             if (rl < Q.Hl - 1) {
-                a0 = a0 + (qd.x - pi.x);
-                a1 = a1 + (qd.y - pi.y);
+                a0 = a0 + (qd[j].x - pi.x);
+                a1 = a1 + (qd[j].y - pi.y);
             }
             a = make_double2(a0 * gain, a1 * gain);
         }
@@ -208,54 +219,75 @@ __global__ void __launch_bounds__(kPrepBlock) k_window_prep(WinGeom Q, const dou
         }
     }
     // column extents: suffix minimum / prefix maximum of x along the row over the finite agents,
-    // each thread over its contiguous chunk of m columns, then across the threads
+    // each thread over its contiguous chunk of m columns, then across the threads; one block-wide
+    // exchange carries them and the row's y extents
     const int m = (W + kPrepBlock - 1) / kPrepBlock;
     const int c0 = threadIdx.x * m;
-    double sm[kPrepPer], pm[kPrepPer];
+    double sm[PER], pm[PER];
     double acc = INFINITY;
 #pragma unroll
-    for (int j = kPrepPer - 1; j >= 0; --j) {
+    for (int j = PER - 1; j >= 0; --j) {
         if (j < m && c0 + j < W) {
-            const double2 p = srow[c0 + j];
-            if (isfinite(p.x) && isfinite(p.y)) acc = pmin(acc, p.x);
+            const double2 q = srow[c0 + j];
+            if (isfinite(q.x) && isfinite(q.y)) acc = pmin(acc, q.x);
         }
         sm[j] = acc;
     }
     acc = -INFINITY;
 #pragma unroll
-    for (int j = 0; j < kPrepPer; ++j) {
+    for (int j = 0; j < PER; ++j) {
         if (j < m && c0 + j < W) {
-            const double2 p = srow[c0 + j];
-            if (isfinite(p.x) && isfinite(p.y)) acc = pmax(acc, p.x);
+            const double2 q = srow[c0 + j];
+            if (isfinite(q.x) && isfinite(q.y)) acc = pmax(acc, q.x);
         }
         pm[j] = acc;
     }
-    double tot;
-    const double after = block_after_min(sm[0], red, &tot);
-    const double before = block_before_max(pm[kPrepPer - 1], red, &tot);
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    double ss = sm[0], ps = pm[PER - 1], yl = ylo, yh = yhi;  // wave scans / reductions
+    for (int o = 1; o < 64; o <<= 1) {
+        const double a = __shfl_down(ss, o, 64), b = __shfl_up(ps, o, 64);
+        if (lane + o < 64) ss = pmin(ss, a);
+        if (lane >= o) ps = pmax(ps, b);
+        yl = pmin(yl, __shfl_xor(yl, o, 64));
+        yh = pmax(yh, __shfl_xor(yh, o, 64));
+    }
+    double sx = __shfl_down(ss, 1, 64), px = __shfl_up(ps, 1, 64);  // exclusive
+    if (lane == 63) sx = INFINITY;
+    if (lane == 0) px = -INFINITY;
+    if (lane == 0) red4[0][wid] = ss;
+    if (lane == 63) red4[1][wid] = ps;
+    if (lane == 0) {
+        red4[2][wid] = yl;
+        red4[3][wid] = yh;
+    }
+    __syncthreads();
+    double after = sx, before = px, lo = INFINITY, hi = -INFINITY;
 #pragma unroll
-    for (int j = 0; j < kPrepPer; ++j) {
+    for (int q = 0; q < kPrepBlock / 64; ++q) {
+        if (q > wid) after = pmin(after, red4[0][q]);
+        if (q < wid) before = pmax(before, red4[1][q]);
+        lo = pmin(lo, red4[2][q]);
+        hi = pmax(hi, red4[3][q]);
+    }
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
         const int c = c0 + j;
         if (j < m && c < W) srsp[c] = make_float2(f32_down(pmin(sm[j], after)), f32_up(pmax(pm[j], before)));
     }
-    // row y extents
-    double lo, hi;
-    (void)block_after_min(ylo, red, &lo);   // (its barriers also order the srsp writes above)
-    (void)block_before_max(yhi, red, &hi);
     if (ext_keys) {
         // the sharded step's halo-guard extents of this build's input positions (as the cell-list
         // bin kernel accumulates them, every agent of the row, non-finite ones included): {min,
         // max} over the computed rows, {max below the guard, min above it, min, max} over the owned
         double e[6] = {INFINITY, -INFINITY, -INFINITY, INFINITY, INFINITY, -INFINITY};
-        auto nmax = [](double m, double y) { return (y > m || y != y) ? y : m; };
+        auto nmax = [](double mm, double y) { return (y > mm || y != y) ? y : mm; };
         int any = 0;
         double py = 0.0;
         const bool comp = rl >= row_begin && rl < row_end, own = rl >= X.own_begin && rl < X.own_end;
 #pragma unroll
-        for (int j = 0; j < kPrepPer; ++j) {
+        for (int j = 0; j < PER; ++j) {
             const int c = threadIdx.x + j * kPrepBlock;
             if (c >= W) continue;
-            const double y = srow[c].y;
+            const double y = p[j].y;
             py = y;
             if (comp) {
                 e[0] = pmin(e[0], y);
@@ -272,8 +304,9 @@ __global__ void __launch_bounds__(kPrepBlock) k_window_prep(WinGeom Q, const dou
         }
         ext_keys_flush<kPrepBlock / 64, false>(e, any, py, ext_keys, r, ered, &arrive);
     }
+    __syncthreads();
 #pragma unroll
-    for (int j = 0; j < kPrepPer; ++j) {
+    for (int j = 0; j < PER; ++j) {
         const int c = threadIdx.x + j * kPrepBlock;
         if (c < W) rsp[(long)r * W + c] = srsp[c];
     }
@@ -283,53 +316,44 @@ __global__ void __launch_bounds__(kPrepBlock) k_window_prep(WinGeom Q, const dou
     }
 }
 
-// The row guard's arrays from the row extents k_window_prep wrote (one block, chunks of kPrepBlock
-// x kPrepPer rows): sylo[r] = min over candidate rows >= r of the row minima (sylo[cr1] = +inf),
+// The row guard's arrays from the row extents k_window_prep wrote (one block, one row per thread
+// and chunk): sylo[r] = min over candidate rows >= r of the row minima (sylo[cr1] = +inf),
 // pyhi[r] = max over candidate rows <= r of the row maxima.  (A ticket at the end of the prep
 // kernel, whose last block did this, serialised 1,024 same-address atomics: 29 us per build.)
-__global__ void __launch_bounds__(kPrepBlock) k_window_rowscan(WinGeom Q, WinGuard Gd) {
-    __shared__ double red[kPrepBlock / 64];
-    constexpr int CH = kPrepBlock * kPrepPer;
-    const int H = Q.cr1;
-    double carry = INFINITY;
-    for (int base = Q.cr0 + ((H - Q.cr0 - 1) / CH) * CH; base >= Q.cr0; base -= CH) {
-        double v[kPrepPer];
-        double a = INFINITY;
-#pragma unroll
-        for (int j = kPrepPer - 1; j >= 0; --j) {
-            const int rr = base + threadIdx.x * kPrepPer + j;
-            v[j] = rr < H ? Gd.rowy[2l * rr] : INFINITY;
-            a = pmin(a, v[j]);
-            v[j] = a;
+constexpr int kRowScanBlock = 1024;
+__global__ void __launch_bounds__(kRowScanBlock) k_window_rowscan(WinGeom Q, WinGuard Gd) {
+    __shared__ double red[2][kRowScanBlock / 64];
+    constexpr int NW = kRowScanBlock / 64;
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int lo = Q.cr0, H = Q.cr1;
+    // chunks of one row per thread; suffix minima run from the last chunk down, prefix maxima up
+    double carry_s = INFINITY, carry_p = -INFINITY;
+    const int nch = (H - lo + kRowScanBlock - 1) / kRowScanBlock;
+    for (int k = 0; k < nch; ++k) {
+        const int rs = lo + (nch - 1 - k) * kRowScanBlock + threadIdx.x;  // suffix pass row
+        const int rp = lo + k * kRowScanBlock + threadIdx.x;              // prefix pass row
+        double vs = rs < H ? Gd.rowy[2l * rs] : INFINITY;
+        double vp = rp < H ? Gd.rowy[2l * rp + 1] : -INFINITY;
+        for (int o = 1; o < 64; o <<= 1) {  // inclusive wave scans
+            const double a = __shfl_down(vs, o, 64), b = __shfl_up(vp, o, 64);
+            if (lane + o < 64) vs = pmin(vs, a);
+            if (lane >= o) vp = pmax(vp, b);
         }
-        double t;
-        const double aft = pmin(block_after_min(a, red, &t), carry);
-#pragma unroll
-        for (int j = 0; j < kPrepPer; ++j) {
-            const int rr = base + threadIdx.x * kPrepPer + j;
-            if (rr < H) Gd.sylo[rr] = pmin(v[j], aft);
+        if (lane == 0) red[0][wid] = vs;
+        if (lane == 63) red[1][wid] = vp;
+        __syncthreads();
+        double as = carry_s, bp = carry_p, ts = INFINITY, tp = -INFINITY;
+        for (int q = 0; q < NW; ++q) {
+            if (q > wid) as = pmin(as, red[0][q]);
+            if (q < wid) bp = pmax(bp, red[1][q]);
+            ts = pmin(ts, red[0][q]);
+            tp = pmax(tp, red[1][q]);
         }
-        carry = pmin(carry, t);
-    }
-    carry = -INFINITY;
-    for (int base = Q.cr0; base < H; base += CH) {
-        double v[kPrepPer];
-        double a = -INFINITY;
-#pragma unroll
-        for (int j = 0; j < kPrepPer; ++j) {
-            const int rr = base + threadIdx.x * kPrepPer + j;
-            v[j] = rr < H ? Gd.rowy[2l * rr + 1] : -INFINITY;
-            a = pmax(a, v[j]);
-            v[j] = a;
-        }
-        double t;
-        const double bef = pmax(block_before_max(a, red, &t), carry);
-#pragma unroll
-        for (int j = 0; j < kPrepPer; ++j) {
-            const int rr = base + threadIdx.x * kPrepPer + j;
-            if (rr < H) Gd.pyhi[rr] = pmax(v[j], bef);
-        }
-        carry = pmax(carry, t);
+        if (rs < H) Gd.sylo[rs] = pmin(vs, as);
+        if (rp < H) Gd.pyhi[rp] = pmax(vp, bp);
+        carry_s = pmin(carry_s, ts);
+        carry_p = pmax(carry_p, tp);
+        __syncthreads();
     }
     if (threadIdx.x == 0) Gd.sylo[H] = INFINITY;
 }
@@ -695,7 +719,7 @@ __global__ void __launch_bounds__(kBlock) k_window_tile(KP P, WinBounds B, WinGe
         if (Ku > kTileKS || Kd > kTileKS) slow = true;  // beyond the staged rows: the unbounded form
     }
     const int KuW = wave_max_i(slow ? -1 : Ku), KdW = wave_max_i(slow ? -1 : Kd);
-    unsigned long long hm = 0;  // hit bits (dr + 3) * 5 + (dc + 2)
+    unsigned long long hm = 0;  // hit bits (dr + 3) * 8 + (dc + 2): one byte per row
     double d2 = INFINITY;
     auto cand = [&](int off, int bit) {
         const double2 q = L.p[off];
@@ -709,7 +733,7 @@ __global__ void __launch_bounds__(kBlock) k_window_tile(KP P, WinBounds B, WinGe
     unsigned pR = 0, pL = 0;  // rows (bit dr + 3) whose sentinel at c + 2 / c - 2 does not hold
     for (int dr = -KdW; dr <= KuW; ++dr) {
         if (!(fin && !slow && dr >= -Kd && dr <= Ku)) continue;
-        const int b = e + dr * kTileCols, bit = (dr + 3) * 5 + 2;
+        const int b = e + dr * kTileCols, bit = (dr + 3) * 8 + 2;
         cand(b - 1, bit - 1);
         cand(b, bit);
         cand(b + 1, bit + 1);
@@ -718,7 +742,7 @@ __global__ void __launch_bounds__(kBlock) k_window_tile(KP P, WinBounds B, WinGe
     }
     if (__ballot((pR | pL) != 0)) {  // columns c -+ 2 where a sentinel did not hold
         for (int dr = -KdW; dr <= KuW; ++dr) {
-            const int b = e + dr * kTileCols, bit = (dr + 3) * 5 + 2;
+            const int b = e + dr * kTileCols, bit = (dr + 3) * 8 + 2;
             if ((pR >> (dr + 3)) & 1u) {
                 cand(b + 2, bit + 2);
                 if (!((double)L.g[b + 3].x - E.r0 > P.win_d)) slow = true;
@@ -750,7 +774,7 @@ __global__ void __launch_bounds__(kBlock) k_window_tile(KP P, WinBounds B, WinGe
             while (hm) {
                 const int bit = __ffsll((long long)hm) - 1;
                 hm &= hm - 1;
-                const int dr = bit / 5 - 3, dc = bit - (bit / 5) * 5 - 2;
+                const int dr = (bit >> 3) - 3, dc = (bit & 7) - 2;
                 const int off = e + dr * kTileCols + dc;
                 const double2 q = L.p[off], v = L.u[off];
                 if (qfin) {
@@ -800,10 +824,12 @@ bool window_cull_ok(int W, int rows, long n_ws, const CellWs& Wk) {
 void window_prep(const CellWs& Wk, const WinGeom& Q, const double2* pos, double gain, double2* vel_out,
                  double2* copy_to, unsigned long long* ext_keys, int row_begin, int row_end, ExtSpec X,
                  hipStream_t s) {
-    hipLaunchKernelGGL(k_window_prep, dim3(Q.cr1 - Q.cr0), dim3(kPrepBlock), 24 * (size_t)Q.W, s, Q, pos, Wk.svel,
+    const auto prep = Q.W <= 2 * kPrepBlock ? k_window_prep<2> : (Q.W <= 4 * kPrepBlock ? k_window_prep<4>
+                                                                                          : k_window_prep<kPrepPer>);
+    hipLaunchKernelGGL(prep, dim3(Q.cr1 - Q.cr0), dim3(kPrepBlock), 24 * (size_t)Q.W, s, Q, pos, Wk.svel,
                        win_rsp(Wk), win_guard(Wk, Q.rows), gain, vel_out, copy_to, Wk.sctl, Wk.ncell, ext_keys,
                        row_begin, row_end, X);
-    hipLaunchKernelGGL(k_window_rowscan, dim3(1), dim3(kPrepBlock), 0, s, Q, win_guard(Wk, Q.rows));
+    hipLaunchKernelGGL(k_window_rowscan, dim3(1), dim3(kRowScanBlock), 0, s, Q, win_guard(Wk, Q.rows));
 }
 
 // The filter kernel of a window-cull advance of the egos of lattice rows [row_begin, row_end)
