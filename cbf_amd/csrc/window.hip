@@ -633,7 +633,11 @@ __global__ void __launch_bounds__(kBlock) k_window_filter(KP P, WinBounds B, int
 // scan.  An ego whose row window or column walk leaves the staged halo takes win_direct (global
 // memory, unbounded), as in the untiled form.
 constexpr int kTileW = 64;
-constexpr int kTileR = kBlock / kTileW;
+#ifndef CBF_TILE_R
+#define CBF_TILE_R 4  // lattice rows (waves) per tile
+#endif
+constexpr int kTileR = CBF_TILE_R;
+constexpr int kTileT = kTileR * 64;  // threads per tile block
 constexpr int kTileKS = 3;  // rows each side (the row guard's window up to +-3)
 constexpr int kTileKC = 3;  // columns each side (candidates to +-2, sentinels to +-3)
 constexpr int kTileRows = kTileR + 2 * kTileKS, kTileCols = kTileW + 2 * kTileKC, kTileN = kTileRows * kTileCols;
@@ -646,7 +650,7 @@ struct TileLds {
 };
 
 template <bool FZ, bool ST, bool IN>
-__global__ void __launch_bounds__(kBlock) k_window_tile(KP P, WinBounds B, WinGeom Q, int er0, int tiles_x,
+__global__ void __launch_bounds__(kTileT) k_window_tile(KP P, WinBounds B, WinGeom Q, int er0, int tiles_x,
                                                         const double2* __restrict__ pos,
                                                         const double2* __restrict__ u0,
                                                         const float2* __restrict__ rsp,
@@ -676,7 +680,7 @@ __global__ void __launch_bounds__(kBlock) k_window_tile(KP P, WinBounds B, WinGe
     }
     // stage the tile with its halo (beyond the lattice: +-inf positions, which no test passes, and
     // column extents that exclude nothing beyond the row ends)
-    for (int i = threadIdx.x; i < kTileN; i += kBlock) {
+    for (int i = threadIdx.x; i < kTileN; i += kTileT) {
         const int lr = i / kTileCols, lc = i - lr * kTileCols;
         const int rr = r0 - kTileKS + lr, cc = c0 - kTileKC + lc;
         if (rr >= Q.cr0 && rr < Q.cr1 && cc >= 0 && cc < W) {
@@ -770,30 +774,47 @@ __global__ void __launch_bounds__(kBlock) k_window_tile(KP P, WinBounds B, WinGe
             // the hits from LDS: per-quadrant minima of row_g plus the quadrant terms, or row by row
             // (row_b) when a quadrant term is not finite -- the cell-list filter's two forms
             double g0 = INFINITY, g1 = INFINITY, g2 = INFINITY, g3 = INFINITY;
-            if (qfin) E.count = __popcll(hm);  // (ego_add counts its hits itself)
-            while (hm) {
-                const int bit = __ffsll((long long)hm) - 1;
-                hm &= hm - 1;
-                const int dr = (bit >> 3) - 3, dc = (bit & 7) - 2;
-                const int off = e + dr * kTileCols + dc;
-                const double2 q = L.p[off], v = L.u[off];
-                if (qfin) {
+            if (qfin) {
+                E.count = __popcll(hm);
+                // row_g<FZ> per hit (f = 0: its H with k's sign set by bit arithmetic -- -P.k flips
+                // exactly that bit -- instead of selects; same value bit for bit)
+                const unsigned long long kb = (unsigned long long)__double_as_longlong(P.k);
+                while (hm) {
+                    const int bit = __ffsll((long long)hm) - 1;
+                    hm &= hm - 1;
+                    const int off = e + ((bit >> 3) - 3) * kTileCols + (bit & 7) - 2;
+                    const double2 q = L.p[off], v = L.u[off];
                     int qd;
-                    const double g = row_g<FZ>(P, E, q.x, q.y, v.x, v.y, qd);
+                    double g;
+                    if (FZ) {
+                        const double d0 = E.r0 - q.x, d1 = E.r1 - q.y, d2 = E.r2 - v.x, d3 = E.r3 - v.y;
+                        const bool nx = d0 < 0, ny = d1 < 0;
+                        const double ksx = __longlong_as_double((long long)(kb ^ ((unsigned long long)nx << 63)));
+                        const double ksy = __longlong_as_double((long long)(kb ^ ((unsigned long long)ny << 63)));
+                        const double Hh = fma(ksy, d3, fma(ksx, d2, fabs(d0) + fabs(d1)));
+                        qd = (nx ? 1 : 0) | (ny ? 2 : 0);
+                        g = P.gamma * (Hh - P.dmin);
+                    } else {
+                        g = row_g<FZ>(P, E, q.x, q.y, v.x, v.y, qd);
+                    }
                     g0 = (qd == 0 && g < g0) ? g : g0;
                     g1 = (qd == 1 && g < g1) ? g : g1;
                     g2 = (qd == 2 && g < g2) ? g : g2;
                     g3 = (qd == 3 && g < g3) ? g : g3;
                     E.present |= 1u << qd;
-                } else {
-                    ego_add<FZ>(P, E, q.x, q.y, v.x, v.y);
                 }
-            }
-            if (qfin) {
                 E.bq0 = g0 + q0;
                 E.bq1 = g1 + q1;
                 E.bq2 = g2 + q2;
                 E.bq3 = g3 + q3;
+            } else {  // a quadrant term is not finite: row by row (row_b), as the cell-list filter
+                while (hm) {
+                    const int bit = __ffsll((long long)hm) - 1;
+                    hm &= hm - 1;
+                    const int off = e + ((bit >> 3) - 3) * kTileCols + (bit & 7) - 2;
+                    const double2 q = L.p[off], v = L.u[off];
+                    ego_add<FZ>(P, E, q.x, q.y, v.x, v.y);
+                }
             }
         } else if (fin) {  // the unbounded form, over the full row window (beyond the staged halo too)
             int kd, ku;
@@ -807,7 +828,7 @@ __global__ void __launch_bounds__(kBlock) k_window_tile(KP P, WinBounds B, WinGe
     }
     if (ST && stats) {
         const bool counted = O.res != 0 && O.w >= B.cnt_lo && O.w < B.cnt_hi;
-        wave_stats(stats, (long)bx * (kBlock / 64) + wv, counted && O.nbrs > 0, counted && O.seidel,
+        wave_stats(stats, (long)bx * kTileR + wv, counted && O.nbrs > 0, counted && O.seidel,
                    counted && O.res == 1, O.code, O.binding, O.viol, O.vorig, counted ? O.d2 : INFINITY);
     }
 }
@@ -851,7 +872,7 @@ void window_filter(const cbf_params* p, const CellWs& Wk, const WinGeom& Q, int 
                     : (p->f_is_zero ? k_window_tile<true, false, true> : k_window_tile<false, false, true>))
            : (stats ? (p->f_is_zero ? k_window_tile<true, true, false> : k_window_tile<false, true, false>)
                     : (p->f_is_zero ? k_window_tile<true, false, false> : k_window_tile<false, false, false>));
-    hipLaunchKernelGGL(tile, dim3((unsigned)(tiles_x * tiles_y)), dim3(kBlock), 0, s, kp, B, Q, row_begin - Q.row0,
+    hipLaunchKernelGGL(tile, dim3((unsigned)(tiles_x * tiles_y)), dim3(kTileT), 0, s, kp, B, Q, row_begin - Q.row0,
                        tiles_x, pos, (const double2*)Wk.svel, (const float2*)win_rsp(Wk), (const double*)Gd.sylo,
                        (const double*)Gd.pyhi, (const int32_t*)Wk.sctl, T, pos_out, u, status, cnt, stats, Wk.hardq,
                        Wk.qrec, Wk.qcap);
