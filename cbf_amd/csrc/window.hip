@@ -634,7 +634,7 @@ __global__ void __launch_bounds__(kBlock) k_window_filter(KP P, WinBounds B, int
 // memory, unbounded), as in the untiled form.
 constexpr int kTileW = 64;
 #ifndef CBF_TILE_R
-#define CBF_TILE_R 4  // lattice rows (waves) per tile
+#define CBF_TILE_R 8  // lattice rows (waves) per tile (4: 43.0 us, 8: 41.3 us per launch at 1 M agents)
 #endif
 constexpr int kTileR = CBF_TILE_R;
 constexpr int kTileT = kTileR * 64;  // threads per tile block
