@@ -515,6 +515,10 @@ def bench_lattice(args, ws, rank, local):
     marked = args.barrier == "reference"
     cull = getattr(S, "cull", None) or getattr(getattr(S, "be", None), "cull", "cells")
     kt = []
+    # the GPU is kept busy (a spin kernel) while the host enqueues the start event and the advance,
+    # so the events time the kernels and not the host's launch latency (a 20-us window-cull build
+    # can drain before the host has launched the advance)
+    spin = getattr(torch.cuda, "_sleep", None)
     for _ in range(args.kernel_iters):
         S.build_phase()
         a = torch.cuda.Event(enable_timing=True)
@@ -522,6 +526,8 @@ def bench_lattice(args, ws, rank, local):
         b = torch.cuda.Event(enable_timing=True)
         if marked:
             m.record()   # creates the event; the advance call records it again after the filter
+        if spin is not None:
+            spin(200000)
         a.record()
         if marked and cull == "window" and not sharded:
             S.advance_phase(mark=m, commit=False)   # (the new positions into scratch: no copy timed)

@@ -28,8 +28,10 @@ ev = []
 for _ in range(10):
     a, m, b, c = (torch.cuda.Event(enable_timing=True) for _ in range(4))
     m.record()
+    torch.cuda._sleep(200000)   # the GPU busy while the host enqueues: events time kernels, not launches
     a.record()
     L.build_phase()
+    torch.cuda._sleep(200000)
     b.record()
     L.advance_phase(mark=m, commit=False) if cull == "window" else L.advance_phase(mark=m)
     c.record()
