@@ -175,7 +175,7 @@ def load_pmc(config):
 # full solve queued) and the queue kernel
 ADVANCE_KERNELS = ("k_lattice_filter<true, false, false>", "k_lattice_filter_hard")
 # ... of the lattice-window cull
-WINDOW_KERNELS = ("k_window_filter<true, false, false>", "k_lattice_filter_hard")
+WINDOW_KERNELS = ("k_window_tile<true, false, false>", "k_lattice_filter_hard")
 
 
 def load_pmc_valu(config, kernel=ADVANCE_KERNELS[0], key="valu_busy"):
