@@ -39,6 +39,18 @@ namespace {
 #ifndef CBF_WIN_SPEC
 #define CBF_WIN_SPEC 0  // 1: rows r - 1 .. r + 1 loaded with the ego, before the row guard
 #endif
+#ifndef CBF_WIN_FOLD
+#define CBF_WIN_FOLD 1  // 1: the tiled filter's first block forms the row guard (no k_window_rowscan)
+#endif
+#ifndef CBF_TILE_WPE
+#define CBF_TILE_WPE 6  // waves per SIMD the timed tile kernels (queued solve, no statistics) are fitted to
+#endif
+#ifndef CBF_GUARD_PER
+#define CBF_GUARD_PER 2  // rows per thread of the tile launch's row-guard scan
+#endif
+#ifndef CBF_WIN_SPIN_LIMIT
+#define CBF_WIN_SPIN_LIMIT (1l << 22)  // polls of the row guard's done word before a block gives up
+#endif
 constexpr int kPrepBlock = 256;
 constexpr int kPrepPer = 8;  // columns per prep thread: rows of up to 2048 agents
 constexpr int kWinMaxW = kPrepBlock * kPrepPer;
@@ -48,6 +60,7 @@ struct WinGuard {
     double* rowy;     // [2 H] {min y, max y} per row (finite agents)
     double* sylo;     // [H + 1] min over rows >= r of the row minima (sylo[H] = +inf)
     double* pyhi;     // [H] max over rows <= r of the row maxima
+    int32_t* sync;    // [2] {the build's guard token, the token of the last guard formed}
 };
 inline WinGuard win_guard(const CellWs& Wk, int H) {
     WinGuard g;
@@ -55,9 +68,13 @@ inline WinGuard win_guard(const CellWs& Wk, int H) {
     g.rowy = reinterpret_cast<double*>(p);
     g.sylo = g.rowy + 2l * H;
     g.pyhi = g.sylo + (H + 1);
+    g.sync = reinterpret_cast<int32_t*>(g.pyhi + H);
     return g;
 }
-inline size_t win_guard_bytes(int H) { return 8 * (size_t)(4l * H + 1); }  // <= 16 W H for W >= 4
+// a build's guard token: a 24-bit count tagged in the top byte (the area is the cell list's record
+// area on other paths; its words never carry the tag)
+__host__ __device__ inline int32_t guard_token(int32_t v) { return (v & 0x00FFFFFF) | 0x5A000000; }
+inline size_t win_guard_bytes(int H) { return 8 * (size_t)(4l * H + 2); }  // <= 16 W H for W >= 4
 // Geometry (WinGeom, lattice_ego.hpp): candidates are the agents of window rows [cr0, cr1).  A
 // window edge that is not a lattice edge is not a candidate row (its agents' nominal controls
 // cannot be formed there; the cell-list builds skip them likewise, and the sharded step's halo
@@ -152,7 +169,10 @@ __global__ void __launch_bounds__(kPrepBlock) k_window_prep(WinGeom Q, const dou
     const int r = Q.cr0 + xcd_block();      // window row
     const int rl = Q.row0 + r;              // lattice row
     const long nwin = (long)W * Q.rows;
-    if (r == Q.cr0 && threadIdx.x == 0) build_begin(sctl, nwin, ncell);
+    if (r == Q.cr0 && threadIdx.x == 0) {
+        build_begin(sctl, nwin, ncell);
+        Gd.sync[0] = guard_token(Gd.sync[1] + 1);  // this build's guard token (not the last one formed)
+    }
     if (ext_keys && threadIdx.x == 0) arrive = 0;
     const NominalSpec N = nominal_spec(sctl);
     const bool lap = N.mode != CBF_NOMINAL_RANDOM;
@@ -321,41 +341,91 @@ __global__ void __launch_bounds__(kPrepBlock) k_window_prep(WinGeom Q, const dou
 // pyhi[r] = max over candidate rows <= r of the row maxima.  (A ticket at the end of the prep
 // kernel, whose last block did this, serialised 1,024 same-address atomics: 29 us per build.)
 constexpr int kRowScanBlock = 1024;
-__global__ void __launch_bounds__(kRowScanBlock) k_window_rowscan(WinGeom Q, WinGuard Gd) {
-    __shared__ double red[2][kRowScanBlock / 64];
-    constexpr int NW = kRowScanBlock / 64;
+template <bool PACK>  // PACK: {fp32 value, token} words (in-launch hand-off), else the double
+__device__ __forceinline__ void st_guard(double* p, double v, bool down, int32_t token) {
+    if (PACK) {
+        const float f = down ? f32_down(v) : f32_up(v);
+        const unsigned long long w = ((unsigned long long)(uint32_t)token << 32) | __float_as_uint(f);
+        __hip_atomic_store(reinterpret_cast<unsigned long long*>(p), w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+        *p = v;
+    }
+}
+template <int NT, int PER, bool PACK>  // threads of the block, rows per thread and chunk
+__device__ __forceinline__ void row_guard_scan(const WinGeom& Q, const WinGuard& Gd, double (*red)[NT / 64],
+                                               int32_t token) {
+    constexpr int NW = NT / 64, CH = NT * PER;
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const int lo = Q.cr0, H = Q.cr1;
-    // chunks of one row per thread; suffix minima run from the last chunk down, prefix maxima up
+    // chunks of PER consecutive rows per thread (all loads of a chunk in one round trip); suffix
+    // minima run from the last chunk down, prefix maxima up
     double carry_s = INFINITY, carry_p = -INFINITY;
-    const int nch = (H - lo + kRowScanBlock - 1) / kRowScanBlock;
+    const int nch = (H - lo + CH - 1) / CH;
     for (int k = 0; k < nch; ++k) {
-        const int rs = lo + (nch - 1 - k) * kRowScanBlock + threadIdx.x;  // suffix pass row
-        const int rp = lo + k * kRowScanBlock + threadIdx.x;              // prefix pass row
-        double vs = rs < H ? Gd.rowy[2l * rs] : INFINITY;
-        double vp = rp < H ? Gd.rowy[2l * rp + 1] : -INFINITY;
-        for (int o = 1; o < 64; o <<= 1) {  // inclusive wave scans
+        const int bs = lo + (nch - 1 - k) * CH + threadIdx.x * PER;  // suffix pass rows bs .. bs + PER - 1
+        const int bp = lo + k * CH + threadIdx.x * PER;              // prefix pass rows
+        double ls[PER], lp[PER];
+#pragma unroll
+        for (int j = 0; j < PER; ++j) {
+            ls[j] = bs + j < H ? Gd.rowy[2l * (bs + j)] : INFINITY;
+            lp[j] = bp + j < H ? Gd.rowy[2l * (bp + j) + 1] : -INFINITY;
+        }
+#pragma unroll
+        for (int j = PER - 2; j >= 0; --j) ls[j] = pmin(ls[j], ls[j + 1]);
+#pragma unroll
+        for (int j = 1; j < PER; ++j) lp[j] = pmax(lp[j], lp[j - 1]);
+        double vs = ls[0], vp = lp[PER - 1];
+        for (int o = 1; o < 64; o <<= 1) {  // inclusive wave scans of the thread totals
             const double a = __shfl_down(vs, o, 64), b = __shfl_up(vp, o, 64);
             if (lane + o < 64) vs = pmin(vs, a);
             if (lane >= o) vp = pmax(vp, b);
         }
+        double xs = __shfl_down(vs, 1, 64), xp = __shfl_up(vp, 1, 64);  // exclusive
+        if (lane == 63) xs = INFINITY;
+        if (lane == 0) xp = -INFINITY;
         if (lane == 0) red[0][wid] = vs;
         if (lane == 63) red[1][wid] = vp;
         __syncthreads();
-        double as = carry_s, bp = carry_p, ts = INFINITY, tp = -INFINITY;
+        double as = carry_s, bq = carry_p, ts = INFINITY, tp = -INFINITY;
         for (int q = 0; q < NW; ++q) {
             if (q > wid) as = pmin(as, red[0][q]);
-            if (q < wid) bp = pmax(bp, red[1][q]);
+            if (q < wid) bq = pmax(bq, red[1][q]);
             ts = pmin(ts, red[0][q]);
             tp = pmax(tp, red[1][q]);
         }
-        if (rs < H) Gd.sylo[rs] = pmin(vs, as);
-        if (rp < H) Gd.pyhi[rp] = pmax(vp, bp);
+        as = pmin(as, xs);
+        bq = pmax(bq, xp);
+#pragma unroll
+        for (int j = 0; j < PER; ++j) {
+            if (bs + j < H) st_guard<PACK>(&Gd.sylo[bs + j], pmin(ls[j], as), true, token);
+            if (bp + j < H) st_guard<PACK>(&Gd.pyhi[bp + j], pmax(lp[j], bq), false, token);
+        }
         carry_s = pmin(carry_s, ts);
         carry_p = pmax(carry_p, tp);
-        __syncthreads();
+        if (k + 1 < nch) __syncthreads();
     }
-    if (threadIdx.x == 0) Gd.sylo[H] = INFINITY;
+    if (threadIdx.x == 0) st_guard<PACK>(&Gd.sylo[H], INFINITY, true, token);
+}
+__global__ void __launch_bounds__(kRowScanBlock) k_window_rowscan(WinGeom Q, WinGuard Gd) {
+    __shared__ double red[2][kRowScanBlock / 64];
+    row_guard_scan<kRowScanBlock, 1, false>(Q, Gd, red, 0);
+}
+
+// A row-guard value.  Packed (formed in the same launch, k_window_tile): the word is polled with
+// sc1 loads until it carries this build's token; one that never does reads as `worst` (-inf for
+// sylo, +inf for pyhi: every row a candidate row, so the windows only grow and stay complete).
+// fp32 values rounded outward (sylo down, pyhi up) are sound bounds likewise.
+template <bool PACK>
+__device__ __forceinline__ double ld_guard(const double* p, int32_t token, double worst) {
+    if (!PACK) return *p;
+    if (CBF_WIN_SPIN_LIMIT < 0) return worst;  // (test build tests/_lib/libcbf_winnowait.so)
+    const unsigned long long* q = reinterpret_cast<const unsigned long long*>(p);
+    for (long spins = 0;; ++spins) {
+        const unsigned long long w = __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if ((int32_t)(w >> 32) == token) return (double)__uint_as_float((unsigned)w);
+        if (spins >= CBF_WIN_SPIN_LIMIT) return worst;
+        __builtin_amdgcn_s_sleep(1);
+    }
 }
 
 // One candidate of the window scan: the cull test of cross_and_rescue.py:141-150 for agents
@@ -375,14 +445,15 @@ __device__ __forceinline__ void win_cand(const KP& P, const Ego& E, double2 p, i
 // non-increasing away from r, so the test is monotone in k and Ku counts its failures); a window
 // taller than that continues one row at a time.
 constexpr int kWinPre = 4;
+template <bool PACK = false>
 __device__ __forceinline__ void win_rows(const KP& P, const double* __restrict__ sylo,
                                          const double* __restrict__ pyhi, int r, int lo, int H, double y, int& Kd,
-                                         int& Ku) {
+                                         int& Ku, int32_t token = 0) {
     double su[kWinPre], pd[kWinPre];
 #pragma unroll
     for (int k = 0; k < kWinPre; ++k) {
-        su[k] = r + k + 1 < H ? sylo[r + k + 1] : INFINITY;  // beyond the candidate rows: nothing to exclude
-        pd[k] = r - k - 1 >= lo ? pyhi[r - k - 1] : -INFINITY;
+        su[k] = r + k + 1 < H ? ld_guard<PACK>(sylo + r + k + 1, token, -INFINITY) : INFINITY;  // beyond: none
+        pd[k] = r - k - 1 >= lo ? ld_guard<PACK>(pyhi + r - k - 1, token, INFINITY) : -INFINITY;
     }
     Ku = 0;
     Kd = 0;
@@ -392,9 +463,9 @@ __device__ __forceinline__ void win_rows(const KP& P, const double* __restrict__
         Kd += !(y - pd[k] > P.win_d) ? 1 : 0;
     }
     if (Ku == kWinPre)
-        while (r + Ku + 1 < H && !(sylo[r + Ku + 1] - y > P.win_d)) ++Ku;
+        while (r + Ku + 1 < H && !(ld_guard<PACK>(sylo + r + Ku + 1, token, -INFINITY) - y > P.win_d)) ++Ku;
     if (Kd == kWinPre)
-        while (r - Kd - 1 >= lo && !(y - pyhi[r - Kd - 1] > P.win_d)) ++Kd;
+        while (r - Kd - 1 >= lo && !(y - ld_guard<PACK>(pyhi + r - Kd - 1, token, INFINITY) > P.win_d)) ++Kd;
 }
 
 // 32-bit byte offsets into the lattice-ordered arrays (windows of < 2^28 agents, check_lattice)
@@ -650,19 +721,19 @@ struct TileLds {
 };
 
 template <bool FZ, bool ST, bool IN>
-__global__ void __launch_bounds__(kTileT) k_window_tile(KP P, WinBounds B, WinGeom Q, int er0, int tiles_x,
+__global__ void __launch_bounds__(kTileT) __attribute__((amdgpu_waves_per_eu((IN || ST) ? 1 : CBF_TILE_WPE))) k_window_tile(KP P, WinBounds B, WinGeom Q, int er0, int tiles_x,
                                                         const double2* __restrict__ pos,
                                                         const double2* __restrict__ u0,
-                                                        const float2* __restrict__ rsp,
-                                                        const double* __restrict__ sylo,
-                                                        const double* __restrict__ pyhi,
-                                                        const int32_t* __restrict__ sctl, double T,
+                                                        const float2* __restrict__ rsp, WinGuard Gd,
+                                                        int32_t* __restrict__ sctl, double T,
                                                         double2* __restrict__ pos_out, double2* __restrict__ u,
                                                         int32_t* __restrict__ status, int32_t* __restrict__ cnt,
                                                         unsigned long long* __restrict__ stats,
                                                         int32_t* __restrict__ hardq, HardRec* __restrict__ qrec,
                                                         long qcap) {
     __shared__ TileLds L;
+    const double* __restrict__ sylo = Gd.sylo;
+    const double* __restrict__ pyhi = Gd.pyhi;
     const int W = Q.W;
     const long nwin = (long)W * Q.rows;
     const int bx = xcd_block();
@@ -678,6 +749,22 @@ __global__ void __launch_bounds__(kTileT) k_window_tile(KP P, WinBounds B, WinGe
                            status, cnt, stats, nullptr, 0, hardq);
         return;
     }
+#if CBF_WIN_FOLD
+    // The row guard without the k_window_rowscan launch: the launch's first block (dispatched
+    // first, so resident while any other block waits) forms sylo / pyhi from the build's row
+    // extents and stores each value as one 64-bit word {fp32 value rounded outward, the build's
+    // token} with an sc1 store; a reader polls the words it needs with sc1 loads until they carry
+    // the token (ld_guard), so a block that starts after the guard is formed pays no extra round
+    // trip and none waits on a done word.
+    __shared__ double gred[2][kTileT / 64];
+    const int32_t token = Gd.sync[0];  // written by the build (an earlier launch)
+    if (blockIdx.x == 0) {
+        row_guard_scan<kTileT, CBF_GUARD_PER, true>(Q, Gd, gred, token);
+        if (threadIdx.x == 0) Gd.sync[1] = token;  // (the next build's token follows it)
+    }
+#else
+    const int32_t token = 0;
+#endif
     // stage the tile with its halo (beyond the lattice: +-inf positions, which no test passes, and
     // column extents that exclude nothing beyond the row ends)
     for (int i = threadIdx.x; i < kTileN; i += kTileT) {
@@ -697,8 +784,8 @@ __global__ void __launch_bounds__(kTileT) k_window_tile(KP P, WinBounds B, WinGe
     }
     if (threadIdx.x < kTileGuard) {
         const int a = r0 + 1 + threadIdx.x, b = r0 - kWinPre + threadIdx.x;
-        L.sy[threadIdx.x] = a < Q.cr1 ? sylo[a] : INFINITY;
-        L.py[threadIdx.x] = b >= Q.cr0 ? pyhi[b] : -INFINITY;
+        L.sy[threadIdx.x] = a < Q.cr1 ? ld_guard<CBF_WIN_FOLD>(sylo + a, token, -INFINITY) : INFINITY;
+        L.py[threadIdx.x] = b >= Q.cr0 ? ld_guard<CBF_WIN_FOLD>(pyhi + b, token, INFINITY) : -INFINITY;
     }
     __syncthreads();
     const bool act = inside && w >= B.own_lo && w < B.own_hi;
@@ -818,7 +905,7 @@ __global__ void __launch_bounds__(kTileT) k_window_tile(KP P, WinBounds B, WinGe
             }
         } else if (fin) {  // the unbounded form, over the full row window (beyond the staged halo too)
             int kd, ku;
-            win_rows(P, sylo, pyhi, r, Q.cr0, Q.cr1, E.r1, kd, ku);
+            win_rows<CBF_WIN_FOLD>(P, sylo, pyhi, r, Q.cr0, Q.cr1, E.r1, kd, ku, token);
             win_direct<FZ>(P, E, w, r, c, W, kd, ku, pos, u0, rsp, d2);
         }
         O.nbrs = E.count;
@@ -850,7 +937,8 @@ void window_prep(const CellWs& Wk, const WinGeom& Q, const double2* pos, double 
     hipLaunchKernelGGL(prep, dim3(Q.cr1 - Q.cr0), dim3(kPrepBlock), 24 * (size_t)Q.W, s, Q, pos, Wk.svel,
                        win_rsp(Wk), win_guard(Wk, Q.rows), gain, vel_out, copy_to, Wk.sctl, Wk.ncell, ext_keys,
                        row_begin, row_end, X);
-    hipLaunchKernelGGL(k_window_rowscan, dim3(1), dim3(kRowScanBlock), 0, s, Q, win_guard(Wk, Q.rows));
+    if (!CBF_WIN_TILE || !CBF_WIN_FOLD)  // (else the filter's first block forms the row guard)
+        hipLaunchKernelGGL(k_window_rowscan, dim3(1), dim3(kRowScanBlock), 0, s, Q, win_guard(Wk, Q.rows));
 }
 
 // The filter kernel of a window-cull advance of the egos of lattice rows [row_begin, row_end)
@@ -873,9 +961,8 @@ void window_filter(const cbf_params* p, const CellWs& Wk, const WinGeom& Q, int 
            : (stats ? (p->f_is_zero ? k_window_tile<true, true, false> : k_window_tile<false, true, false>)
                     : (p->f_is_zero ? k_window_tile<true, false, false> : k_window_tile<false, false, false>));
     hipLaunchKernelGGL(tile, dim3((unsigned)(tiles_x * tiles_y)), dim3(kTileT), 0, s, kp, B, Q, row_begin - Q.row0,
-                       tiles_x, pos, (const double2*)Wk.svel, (const float2*)win_rsp(Wk), (const double*)Gd.sylo,
-                       (const double*)Gd.pyhi, (const int32_t*)Wk.sctl, T, pos_out, u, status, cnt, stats, Wk.hardq,
-                       Wk.qrec, Wk.qcap);
+                       tiles_x, pos, (const double2*)Wk.svel, (const float2*)win_rsp(Wk), Gd, Wk.sctl, T, pos_out,
+                       u, status, cnt, stats, Wk.hardq, Wk.qrec, Wk.qcap);
     return;
 #endif
     // the untiled form: whole lattices only

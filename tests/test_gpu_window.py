@@ -170,3 +170,33 @@ def test_window_full_size_cfg4_equals_cells():
         del A
     for a, b in zip(res["cells"], res["window"]):
         assert np.array_equal(a, b)
+
+
+def test_window_guard_words_never_ready():
+    """A row-guard word that never carries the build's token (the first block's hand-off not seen;
+    forced for every word by the test build tests/_lib/libcbf_winnowait.so, CBF_WIN_SPIN_LIMIT =
+    -1) reads as the worst bound (every row a candidate row): every ego then walks all rows, and
+    the results are the shipped library's bit for bit, on the scrambled lattice."""
+    import ctypes as C
+    import os
+    from cbf_amd import _lib
+    V = C.CDLL(os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "libcbf_winnowait.so"))
+    fn = V.cbf_lattice_run_ex
+    fn.restype, fn.argtypes = _lib.SIGNATURES["cbf_lattice_run_ex"]
+    W, H = 64, 48
+    pos = scenarios.lattice(W, H, seed=21)
+    rng = np.random.default_rng(4)
+    a = rng.choice(W * H, 40, replace=False)
+    b = rng.choice(W * H, 40, replace=False)
+    pos[a], pos[b] = pos[b].copy(), pos[a].copy()
+    A = swarm.LatticeSwarm(pos, W, H, gain=GAIN, cull="window")
+    B = swarm.LatticeSwarm(pos, W, H, gain=GAIN, cull="window")
+    A.run(3)
+    rc = fn(B.cp, C.byref(B.grid), W, H, _lib.ptr(B.pos), B.gain, B.T, 3, _lib.ptr(B.vel), _lib.ptr(B.u),
+            _lib.ptr(B.status), _lib.ptr(B.nbr_count), B._st(), _lib.ptr(B.ws), B.ws_bytes, _lib.RUN_WINDOW_CULL,
+            _lib.stream_handle())
+    assert rc == 0
+    torch.cuda.synchronize()
+    for x, y in ((A.pos, B.pos), (A.u, B.u), (A.vel, B.vel), (A.status, B.status), (A.nbr_count, B.nbr_count)):
+        assert torch.equal(x, y)
+    assert A.stats_summary() == B.stats_summary()
