@@ -1,19 +1,21 @@
 """A/B timing of the lattice step for a source tree (tools/_ab/<tree> or .): hipGraphs of run(10),
 per-timestep time, and the build / filter / advance kernels by HIP events (the filter's end event
-recorded by the advance call).  Usage: python tools/ab_window.py <tree-root> <cull> [spacing] [rows]"""
+recorded by the advance call).  Usage: python tools/ab_window.py <tree-root> <cull> [spacing] [rows] [placement]"""
 import sys
 import time
 
 root, cull = sys.argv[1], sys.argv[2]
 spacing = float(sys.argv[3]) if len(sys.argv) > 3 else 0.145
 H = int(sys.argv[4]) if len(sys.argv) > 4 else 1024
+placement = sys.argv[5] if len(sys.argv) > 5 else "auto"
 sys.path.insert(0, root)
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 from cbf_amd import scenarios, swarm  # noqa: E402
 
 W = 1024
-L = swarm.LatticeSwarm(scenarios.lattice(W, H, seed=0, spacing=spacing), W, H, gain=0.25, cull=cull)
+L = swarm.LatticeSwarm(scenarios.lattice(W, H, seed=0, spacing=spacing), W, H, gain=0.25, cull=cull,
+                       params=swarm.FilterParams(solve_placement=placement))
 L.collect_stats = False
 L.capture(steps=10)
 for _ in range(3):
@@ -40,5 +42,5 @@ torch.cuda.synchronize()
 bld = np.mean([a.elapsed_time(b) for a, m, b, c in ev]) * 1e3
 flt = np.mean([b.elapsed_time(m) for a, m, b, c in ev]) * 1e3
 adv = np.mean([b.elapsed_time(c) for a, m, b, c in ev]) * 1e3
-print(f"{root} {cull} spacing {spacing} rows {H}: run(10) {run:.1f} us/step, build {bld:.1f}, filter {flt:.1f}, "
+print(f"{root} {cull} {placement} spacing {spacing} rows {H}: run(10) {run:.1f} us/step, build {bld:.1f}, filter {flt:.1f}, "
       f"advance {adv:.1f} us", flush=True)
