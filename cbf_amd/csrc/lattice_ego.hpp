@@ -152,7 +152,7 @@ struct EgoOut {
 // window's waves: 256 CUs x 4 SIMDs x 2 waves x 64 lanes = 131072 agents (one 1024-wide row more
 // puts a third 165-VGPR wave on some SIMDs, and the kernel ends with the most loaded one).  The two
 // placements are bit-identical (tests run both).  The wave-cooperative solves measured slower in
-// either place; their code is on branch exp/coop-solve-variants.
+// either place: commit c7a6b09 and branch exp/coop-line-solve.
 constexpr long kSolveInlineDefault = 131072;
 inline bool solve_inline(const cbf_params* p, long n) {
     return n <= (p->solve_inline_max < 0 ? kSolveInlineDefault : (long)p->solve_inline_max);
