@@ -51,9 +51,15 @@ namespace {
 #ifndef CBF_WIN_SPIN_LIMIT
 #define CBF_WIN_SPIN_LIMIT (1l << 22)  // polls of the row guard's done word before a block gives up
 #endif
-constexpr int kPrepBlock = 256;
-constexpr int kPrepPer = 8;  // columns per prep thread: rows of up to 2048 agents
-constexpr int kWinMaxW = kPrepBlock * kPrepPer;
+#ifndef CBF_PREP_BLOCK
+#define CBF_PREP_BLOCK 256  // threads of a build block (one lattice row)
+#endif
+#ifndef CBF_PREP_WPE
+#define CBF_PREP_WPE 1  // waves per SIMD the build kernel's registers are fitted to (1: no fit)
+#endif
+constexpr int kPrepBlock = CBF_PREP_BLOCK;
+constexpr int kWinMaxW = 2048;                  // rows of up to 2048 agents
+constexpr int kPrepPer = kWinMaxW / kPrepBlock;  // columns per build thread at the widest
 
 // The guard arrays in the workspace's record area (cs, 16 B per agent, unused by this path).
 struct WinGuard {
@@ -154,7 +160,7 @@ __device__ __forceinline__ double block_before_max(double v, double* red, double
 // run's ping-pong start).  The row is staged in LDS (dynamic, 24 B per column): every global load
 // and store is coalesced, and the row scans run over contiguous chunks of it.
 template <int PER>  // columns per thread: W <= kPrepBlock x PER
-__global__ void __launch_bounds__(kPrepBlock) k_window_prep(WinGeom Q, const double2* __restrict__ pos,
+__global__ void __launch_bounds__(kPrepBlock) __attribute__((amdgpu_waves_per_eu(CBF_PREP_WPE))) k_window_prep(WinGeom Q, const double2* __restrict__ pos,
                                                             double2* __restrict__ u0, float2* __restrict__ rsp,
                                                             WinGuard Gd, double gain, double2* __restrict__ vel_out,
                                                             double2* __restrict__ copy_to, int32_t* __restrict__ sctl,
