@@ -11,16 +11,18 @@
 // The proof uses two guards, both exact in fp64 (rounding is monotone, so a computed difference
 // beyond d = win_d makes e * e >= cull_t: the candidate fails s < cull_t):
 //   rows     per lattice row the min / max y over its agents; sylo[r] = min over rows >= r,
-//            pyhi[r] = max over rows <= r (k_window_rowscan).  Rows r + k + 1 and beyond
-//            are out of range of an ego at y once sylo[r + k + 1] - y > d (and below likewise).
+//            pyhi[r] = max over rows <= r (formed by the filter launch's first block).  Rows
+//            r + k + 1 and beyond are out of range of an ego at y once sylo[r + k + 1] - y > d
+//            (and below likewise).
 //   columns  per agent of row r' the min x over the columns >= its own (rs) and the max x over the
 //            columns <= its own (rp), rounded outward to fp32.  Columns c' and beyond of row r'
 //            are out of range once rs(r', c') - x > d (and to the left likewise).
 // Agents with a non-finite coordinate can never pass the cull test and are left out of every
-// extent.  Each ego scans its rows (the row guard) over columns c - 1 .. c + 1 and checks the
-// column sentinels at c -+ 2; a wave whose lanes need it scans columns c -+ 2 too (sentinels at
-// c -+ 3); a lane that still needs more, or whose hit list overflows, walks its rows outward until
-// every sentinel holds, with direct row assembly (any swarm: slower the less lattice-like it is).
+// extent.  The filter (k_window_tile) stages a tile of rows and its halo in LDS; each ego scans
+// its rows (the row guard, up to -+3) over columns c - 1 .. c + 1 and checks the column sentinels
+// at c -+ 2; a wave whose lanes need it scans columns c -+ 2 too (sentinels at c -+ 3); a lane
+// that still needs more walks its rows outward until every sentinel holds, with direct row
+// assembly (win_direct: any swarm, slower the less lattice-like it is).
 #include "cbf_device.hpp"
 #include "cells.hpp"
 #include "lattice.hpp"
@@ -30,15 +32,6 @@ using namespace cbf;
 
 namespace {
 
-#ifndef CBF_WIN_G
-#define CBF_WIN_G 3  // rows whose candidate loads the window filter issues together
-#endif
-#ifndef CBF_WIN_TILE
-#define CBF_WIN_TILE 1  // 0: the untiled window filter (k_window_filter), per-lane global loads
-#endif
-#ifndef CBF_WIN_SPEC
-#define CBF_WIN_SPEC 0  // 1: rows r - 1 .. r + 1 loaded with the ego, before the row guard
-#endif
 #ifndef CBF_WIN_FOLD
 #define CBF_WIN_FOLD 1  // 1: the tiled filter's first block forms the row guard (no k_window_rowscan)
 #endif
@@ -108,54 +101,10 @@ __device__ __forceinline__ float f32_up(double v) {
     return f;
 }
 
-// Block-wide exclusive scans over one value per thread (every thread must call them): the minimum
-// over the threads after this one, and the maximum over the threads before it; *tot gets the
-// block's total.
-__device__ __forceinline__ double block_after_min(double v, double* red, double* tot) {
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    double s = v;  // inclusive suffix minimum within the wave
-    for (int o = 1; o < 64; o <<= 1) {
-        const double y = __shfl_down(s, o, 64);
-        if (lane + o < 64) s = pmin(s, y);
-    }
-    double ex = __shfl_down(s, 1, 64);
-    if (lane == 63) ex = INFINITY;
-    if (lane == 0) red[wid] = s;
-    __syncthreads();
-    double after = INFINITY, all = INFINITY;
-    for (int q = 0; q < kPrepBlock / 64; ++q) {
-        if (q > wid) after = pmin(after, red[q]);
-        all = pmin(all, red[q]);
-    }
-    __syncthreads();
-    *tot = all;
-    return pmin(ex, after);
-}
-__device__ __forceinline__ double block_before_max(double v, double* red, double* tot) {
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    double s = v;  // inclusive prefix maximum within the wave
-    for (int o = 1; o < 64; o <<= 1) {
-        const double y = __shfl_up(s, o, 64);
-        if (lane >= o) s = pmax(s, y);
-    }
-    double ex = __shfl_up(s, 1, 64);
-    if (lane == 0) ex = -INFINITY;
-    if (lane == 63) red[wid] = s;
-    __syncthreads();
-    double before = -INFINITY, all = -INFINITY;
-    for (int q = 0; q < kPrepBlock / 64; ++q) {
-        if (q < wid) before = pmax(before, red[q]);
-        all = pmax(all, red[q]);
-    }
-    __syncthreads();
-    *tot = all;
-    return pmax(ex, before);
-}
-
 // Window-cull build of one timestep: one block per candidate row.  Per agent the nominal control
 // (the lattice Laplacian of cross_and_rescue.py:121-125 shape scaled by gain, or the random walk
 // of CBF_NOMINAL_RANDOM: the scatter's arithmetic) into u0 (and vel_out), the column extents into
-// rsp; per row its y extents (turned into the row guard by k_window_rowscan); the sharded step's
+// rsp; per row its y extents (turned into the row guard by the filter launch); the sharded step's
 // halo-guard extents (ext_keys, nullable).  copy_to (nullable) gets a copy of the positions (the
 // run's ping-pong start).  The row is staged in LDS (dynamic, 24 B per column): every global load
 // and store is coalesced, and the row scans run over contiguous chunks of it.
@@ -434,18 +383,6 @@ __device__ __forceinline__ double ld_guard(const double* p, int32_t token, doubl
     }
 }
 
-// One candidate of the window scan: the cull test of cross_and_rescue.py:141-150 for agents
-// (s > 0: the ego itself and coincident agents are out), hits into the lane's list.
-__device__ __forceinline__ void win_cand(const KP& P, const Ego& E, double2 p, int idx, HitList& Hl, int* lds,
-                                         double& smin) {
-    const double e0 = p.x - E.r0, e1 = p.y - E.r1;
-    const double s = e0 * e0 + e1 * e1;
-    if (s < P.cull_t && s > 0) {
-        Hl.push(lds, idx);
-        smin = pmin(smin, s);
-    }
-}
-
 // The rows of an ego at window row r, y: [r - Kd, r + Ku] (rows beyond are out of range).  The
 // first kWinPre bounds each way are loaded together (sylo is non-decreasing and pyhi
 // non-increasing away from r, so the test is monotone in k and Ku counts its failures); a window
@@ -512,196 +449,7 @@ __device__ __forceinline__ void win_direct(const KP& P, Ego& E, long w, int r, i
     }
 }
 
-// One ego (window index w = r W + c, owned) of the window-cull filter.  Every lane of the wave
-// calls it (the row window is a wave-wide loop); `act` says whether the lane holds an ego.
-template <bool FZ, bool ST, bool IN>
-__device__ __forceinline__ void window_ego(const KP& P, const WinBounds& B, int W, int H, long w, bool act,
-                                           const double2* __restrict__ pos, const double2* __restrict__ u0,
-                                           const float2* __restrict__ rsp, const double* __restrict__ sylo,
-                                           const double* __restrict__ pyhi, double T, double2* __restrict__ pos_out,
-                                           double2* __restrict__ u, int32_t* __restrict__ status,
-                                           int32_t* __restrict__ cnt, int32_t* __restrict__ hardq, int q,
-                                           HardRec* __restrict__ qr, int* hit_lds, Ego& E, EgoOut& O) {
-    int r = 0, c = 0;
-    bool fin = false;
-    if (act) {
-        r = (int)(w / W);
-        c = (int)(w - (long)r * W);
-        const double2 pe = pos[w], ve = u0[w];
-        ego_init(P, E, pe.x, pe.y, ve.x, ve.y, ve.x, ve.y);
-        fin = isfinite(pe.x) && isfinite(pe.y);  // otherwise no candidate can pass (s is inf or NaN)
-    }
-    const int wi = (int)w;
-#if CBF_WIN_SPEC
-    // rows r - 1 .. r + 1 (nearly every ego's), loaded before the row guard is known (it needs y)
-    double2 xm[3], x0[3], xp[3];
-    float xrs[3], xrp[3];
-    bool xv[3];
-#pragma unroll
-    for (int i = 0; i < 3; ++i) {
-        xv[i] = act && r + i - 1 >= 0 && r + i - 1 < H;
-        if (xv[i]) {
-            const int b = wi + (i - 1) * W;
-            xm[i] = c > 0 ? ld_slot(pos, b - 1) : make_double2(INFINITY, INFINITY);
-            x0[i] = ld_slot(pos, b);
-            xp[i] = c + 1 < W ? ld_slot(pos, b + 1) : make_double2(INFINITY, INFINITY);
-            xrs[i] = c + 2 < W ? ld_rsp(rsp, b + 2).x : INFINITY;
-            xrp[i] = c - 2 >= 0 ? ld_rsp(rsp, b - 2).y : -INFINITY;
-        }
-    }
-#endif
-    int Kd = -1, Ku = -1;
-    if (fin) win_rows(P, sylo, pyhi, r, 0, H, E.r1, Kd, Ku);
-    const int KdW = wave_max_i(Kd), KuW = wave_max_i(Ku);
-    HitList Hl;
-    double d2 = INFINITY;
-    // rows whose sentinel at c + 2 (R) / c - 2 (L) does not hold: bit dr + KdW
-    unsigned long long pR = 0, pL = 0;
-    bool slow = KdW + KuW + 1 > 64;  // (a window that tall takes the unbounded form)
-    if (!slow) {
-#if CBF_WIN_SPEC
-#pragma unroll
-        for (int i = 0; i < 3; ++i) {
-            const int dr = i - 1;
-            if (!(fin && xv[i] && dr >= -Kd && dr <= Ku)) continue;
-            const int b = wi + dr * W;
-            win_cand(P, E, xm[i], b - 1, Hl, hit_lds, d2);
-            win_cand(P, E, x0[i], b, Hl, hit_lds, d2);
-            win_cand(P, E, xp[i], b + 1, Hl, hit_lds, d2);
-            if (!((double)xrs[i] - E.r0 > P.win_d)) pR |= 1ull << (dr + KdW);
-            if (!(E.r0 - (double)xrp[i] > P.win_d)) pL |= 1ull << (dr + KdW);
-        }
-#endif
-        // columns c - 1 .. c + 1 of every row, G rows' loads in flight at a time
-        constexpr int G = CBF_WIN_G;
-        for (int dr0 = -KdW; dr0 <= KuW; dr0 += G) {
-            double2 pm[G], p0[G], pp[G];
-            float rs[G], rp[G];
-            bool a[G];
-#pragma unroll
-            for (int i = 0; i < G; ++i) {
-                const int dr = dr0 + i;
-                a[i] = fin && dr <= KuW && dr >= -Kd && dr <= Ku && !(CBF_WIN_SPEC && dr >= -1 && dr <= 1);
-                if (a[i]) {
-                    const int b = wi + dr * W;
-                    pm[i] = c > 0 ? ld_slot(pos, b - 1) : make_double2(INFINITY, INFINITY);
-                    p0[i] = ld_slot(pos, b);
-                    pp[i] = c + 1 < W ? ld_slot(pos, b + 1) : make_double2(INFINITY, INFINITY);
-                    rs[i] = c + 2 < W ? ld_rsp(rsp, b + 2).x : INFINITY;
-                    rp[i] = c - 2 >= 0 ? ld_rsp(rsp, b - 2).y : -INFINITY;
-                }
-            }
-#pragma unroll
-            for (int i = 0; i < G; ++i) {
-                if (!a[i]) continue;
-                const int b = wi + (dr0 + i) * W;
-                win_cand(P, E, pm[i], b - 1, Hl, hit_lds, d2);
-                win_cand(P, E, p0[i], b, Hl, hit_lds, d2);
-                win_cand(P, E, pp[i], b + 1, Hl, hit_lds, d2);
-                if (!((double)rs[i] - E.r0 > P.win_d)) pR |= 1ull << (dr0 + i + KdW);
-                if (!(E.r0 - (double)rp[i] > P.win_d)) pL |= 1ull << (dr0 + i + KdW);
-            }
-        }
-        if (__ballot((pR | pL) != 0)) {  // columns c -+ 2 where a sentinel did not hold
-            for (int dr0 = -KdW; dr0 <= KuW; dr0 += G) {
-                double2 q2r[G], q2l[G];
-                float rs[G], rp[G];
-                bool gr[G], gl[G];
-#pragma unroll
-                for (int i = 0; i < G; ++i) {
-                    const int bit = dr0 + i + KdW;
-                    gr[i] = bit < 64 && ((pR >> bit) & 1ull);
-                    gl[i] = bit < 64 && ((pL >> bit) & 1ull);
-                    const int b = wi + (dr0 + i) * W;
-                    if (gr[i]) {  // c + 2 < W here (the sentinel beyond the row end holds)
-                        q2r[i] = ld_slot(pos, b + 2);
-                        rs[i] = c + 3 < W ? ld_rsp(rsp, b + 3).x : INFINITY;
-                    }
-                    if (gl[i]) {
-                        q2l[i] = ld_slot(pos, b - 2);
-                        rp[i] = c - 3 >= 0 ? ld_rsp(rsp, b - 3).y : -INFINITY;
-                    }
-                }
-#pragma unroll
-                for (int i = 0; i < G; ++i) {
-                    const int b = wi + (dr0 + i) * W;
-                    if (gr[i]) {
-                        win_cand(P, E, q2r[i], b + 2, Hl, hit_lds, d2);
-                        if (!((double)rs[i] - E.r0 > P.win_d)) slow = true;
-                    }
-                    if (gl[i]) {
-                        win_cand(P, E, q2l[i], b - 2, Hl, hit_lds, d2);
-                        if (!(E.r0 - (double)rp[i] > P.win_d)) slow = true;
-                    }
-                }
-            }
-        }
-    }
-    if (!act) return;
-    O.w = (int)w;
-    if (!(w >= B.own_lo && w < B.own_hi)) return;
-    const double c0 = quad_c(P, E, 0), c1 = quad_c(P, E, 1), c2 = quad_c(P, E, 2), c3 = quad_c(P, E, 3);
-    if (fin && !slow && !Hl.overflowed() && isfinite(c0) && isfinite(c1) && isfinite(c2) && isfinite(c3)) {
-        double* gq = reinterpret_cast<double*>(hit_lds + kHitCap * kBlock);
-#pragma unroll
-        for (int k = 0; k < 4; ++k) gq[k * kBlock + threadIdx.x] = INFINITY;
-        Hl.template flush_gq<FZ>(hit_lds, gq, P, E, pos, u0);
-        E.bq0 = gq[threadIdx.x] + c0;
-        E.bq1 = gq[kBlock + threadIdx.x] + c1;
-        E.bq2 = gq[2 * kBlock + threadIdx.x] + c2;
-        E.bq3 = gq[3 * kBlock + threadIdx.x] + c3;
-    } else if (fin) {
-        win_direct<FZ>(P, E, w, r, c, W, Kd, Ku, pos, u0, rsp, d2);
-    }
-    O.nbrs = E.count;
-    if (ST) O.d2 = d2;
-    ego_finish<FZ, ST, IN>(P, E, (int)w, (int)(w - B.own_lo), (int)w, T, pos_out, u, status, cnt, hardq, q, qr, O);
-}
-
-// The window-cull filter: one lane per agent in lattice order (the tail of the cell-list filter:
-// solve_fast in place, the rest solved inline (IN) or queued for k_lattice_filter_hard).
-template <bool FZ, bool ST, bool IN>
-__global__ void __launch_bounds__(kBlock) k_window_filter(KP P, WinBounds B, int W, int H, long nwin,
-                                                          const double2* __restrict__ pos,
-                                                          const double2* __restrict__ u0,
-                                                          const float2* __restrict__ rsp,
-                                                          const double* __restrict__ sylo,
-                                                          const double* __restrict__ pyhi,
-                                                          const int32_t* __restrict__ sctl, double T,
-                                                          double2* __restrict__ pos_out, double2* __restrict__ u,
-                                                          int32_t* __restrict__ status, int32_t* __restrict__ cnt,
-                                                          unsigned long long* __restrict__ stats,
-                                                          int32_t* __restrict__ hardq, HardRec* __restrict__ qrec,
-                                                          long qcap) {
-    __shared__ int hit_lds[kHitCap * kBlock + 8 * kBlock];
-    const int bx = xcd_block();
-    const long w = (long)bx * kBlock + threadIdx.x;
-    if (IN && ST && stats && (int)blockIdx.x == (int)gridDim.x - 1 && threadIdx.x < 64) stat_snapshot(stats);
-    if (sctl[2] != 0) {  // the workspace is bound to another shape: report, touch nothing else
-        lattice_error_tail(W, 0, H, 0, nwin, w, u, status, cnt, stats, nullptr, 0, hardq);
-        return;
-    }
-    EgoOut O;
-    O.res = 0;
-    O.w = -1;
-    O.nbrs = 0;
-    O.code = CBF_STATUS_IDLE;
-    O.binding = false;
-    O.seidel = false;
-    O.viol = O.vorig = 0.0;
-    O.d2 = INFINITY;
-    Ego E;
-    window_ego<FZ, ST, IN>(P, B, W, H, w, w < nwin, pos, u0, rsp, sylo, pyhi, T, pos_out, u, status, cnt, hardq,
-                           bx % kSubQ, qrec + (long)(bx % kSubQ) * qcap, hit_lds, E, O);
-    if (ST && stats) {
-        const bool counted = O.res != 0 && O.w >= B.cnt_lo && O.w < B.cnt_hi;
-        wave_stats(stats, (long)bx * (kBlock / 64) + (threadIdx.x >> 6), counted && O.nbrs > 0,
-                   counted && O.seidel, counted && O.res == 1, O.code, O.binding, O.viol, O.vorig,
-                   counted ? O.d2 : INFINITY);
-    }
-}
-
-// ---- the LDS-tiled form of the window filter (CBF_WIN_TILE) -----------------------------------
+// ---- the window filter: LDS tiles -----------------------------------
 // A block is a tile of kTileR lattice rows x kTileW columns (one wave per tile row).  It stages
 // the tile plus kTileKS halo rows and kTileKC halo columns of positions, nominal controls and
 // column extents in LDS with coalesced loads (one round trip), then every candidate, sentinel and
@@ -943,7 +691,7 @@ void window_prep(const CellWs& Wk, const WinGeom& Q, const double2* pos, double 
     hipLaunchKernelGGL(prep, dim3(Q.cr1 - Q.cr0), dim3(kPrepBlock), 24 * (size_t)Q.W, s, Q, pos, Wk.svel,
                        win_rsp(Wk), win_guard(Wk, Q.rows), gain, vel_out, copy_to, Wk.sctl, Wk.ncell, ext_keys,
                        row_begin, row_end, X);
-    if (!CBF_WIN_TILE || !CBF_WIN_FOLD)  // (else the filter's first block forms the row guard)
+    if (!CBF_WIN_FOLD)  // (else the filter's first block forms the row guard)
         hipLaunchKernelGGL(k_window_rowscan, dim3(1), dim3(kRowScanBlock), 0, s, Q, win_guard(Wk, Q.rows));
 }
 
@@ -959,7 +707,6 @@ void window_filter(const cbf_params* p, const CellWs& Wk, const WinGeom& Q, int 
     const KP kp = make_kp(p);
     const WinBounds B = make_win_bounds(W, Q.row0, n, row_begin, row_end, cnt_begin, cnt_end, 0);
     const WinGuard Gd = win_guard(Wk, Q.rows);
-#if CBF_WIN_TILE
     const int tiles_x = (W + kTileW - 1) / kTileW, tiles_y = (row_end - row_begin + kTileR - 1) / kTileR;
     const auto tile =
         in ? (stats ? (p->f_is_zero ? k_window_tile<true, true, true> : k_window_tile<false, true, true>)
@@ -969,19 +716,6 @@ void window_filter(const cbf_params* p, const CellWs& Wk, const WinGeom& Q, int 
     hipLaunchKernelGGL(tile, dim3((unsigned)(tiles_x * tiles_y)), dim3(kTileT), 0, s, kp, B, Q, row_begin - Q.row0,
                        tiles_x, pos, (const double2*)Wk.svel, (const float2*)win_rsp(Wk), Gd, Wk.sctl, T, pos_out,
                        u, status, cnt, stats, Wk.hardq, Wk.qrec, Wk.qcap);
-    return;
-#endif
-    // the untiled form: whole lattices only
-    const int H = Q.rows;
-    const auto filter =
-        in ? (stats ? (p->f_is_zero ? k_window_filter<true, true, true> : k_window_filter<false, true, true>)
-                    : (p->f_is_zero ? k_window_filter<true, false, true> : k_window_filter<false, false, true>))
-           : (stats ? (p->f_is_zero ? k_window_filter<true, true, false> : k_window_filter<false, true, false>)
-                    : (p->f_is_zero ? k_window_filter<true, false, false> : k_window_filter<false, false, false>));
-    hipLaunchKernelGGL(filter, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, kp, B, W, H, n, pos,
-                       (const double2*)Wk.svel, (const float2*)win_rsp(Wk), (const double*)Gd.sylo,
-                       (const double*)Gd.pyhi, (const int32_t*)Wk.sctl, T, pos_out, u, status, cnt, stats, Wk.hardq,
-                       Wk.qrec, Wk.qcap);
 }
 
 }  // namespace cbf
