@@ -52,7 +52,6 @@ namespace {
 #endif
 constexpr int kPrepBlock = CBF_PREP_BLOCK;
 constexpr int kWinMaxW = 2048;                  // rows of up to 2048 agents
-constexpr int kPrepPer = kWinMaxW / kPrepBlock;  // columns per build thread at the widest
 
 // The guard arrays in the workspace's record area (cs, 16 B per agent, unused by this path).
 struct WinGuard {
@@ -108,7 +107,7 @@ __device__ __forceinline__ float f32_up(double v) {
 // halo-guard extents (ext_keys, nullable).  copy_to (nullable) gets a copy of the positions (the
 // run's ping-pong start).  The row is staged in LDS (dynamic, 24 B per column): every global load
 // and store is coalesced, and the row scans run over contiguous chunks of it.
-template <int PER>  // columns per thread: W <= kPrepBlock x PER
+template <int PER>  // columns per thread: W <= kPrepBlock x PER (PER <= 16)
 __global__ void __launch_bounds__(kPrepBlock) __attribute__((amdgpu_waves_per_eu(CBF_PREP_WPE))) k_window_prep(WinGeom Q, const double2* __restrict__ pos,
                                                             double2* __restrict__ u0, float2* __restrict__ rsp,
                                                             WinGuard Gd, double gain, double2* __restrict__ vel_out,
@@ -686,8 +685,10 @@ bool window_cull_ok(int W, int rows, long n_ws, const CellWs& Wk) {
 void window_prep(const CellWs& Wk, const WinGeom& Q, const double2* pos, double gain, double2* vel_out,
                  double2* copy_to, unsigned long long* ext_keys, int row_begin, int row_end, ExtSpec X,
                  hipStream_t s) {
-    const auto prep = Q.W <= 2 * kPrepBlock ? k_window_prep<2> : (Q.W <= 4 * kPrepBlock ? k_window_prep<4>
-                                                                                          : k_window_prep<kPrepPer>);
+    const auto prep = Q.W <= 2 * kPrepBlock   ? k_window_prep<2>
+                      : Q.W <= 4 * kPrepBlock ? k_window_prep<4>
+                      : Q.W <= 8 * kPrepBlock ? k_window_prep<8>
+                                              : k_window_prep<16>;
     hipLaunchKernelGGL(prep, dim3(Q.cr1 - Q.cr0), dim3(kPrepBlock), 24 * (size_t)Q.W, s, Q, pos, Wk.svel,
                        win_rsp(Wk), win_guard(Wk, Q.rows), gain, vel_out, copy_to, Wk.sctl, Wk.ncell, ext_keys,
                        row_begin, row_end, X);
