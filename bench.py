@@ -1,8 +1,9 @@
 """Benchmark of the CBF safety-filter hot path on MI355X (BASELINE.json metric).
 
 Default workload (cfg4): a 1024 x 1024 jittered lattice swarm (N = 1,048,576 agents), one fused
-timestep (lattice-Laplacian nominal control + cell-list cull + barrier assembly + exact QP + clip
-+ Euler) per step, captured in hipGraphs.  value = agent-QP solves/s over the whole job (agents
+timestep (lattice-Laplacian nominal control + cull + barrier assembly + exact QP + clip + Euler)
+per step, captured in hipGraphs; the cull is the lattice-window cull on one GPU and the cell list
+for the sharded stripes and the random walk (--cull, lattice_cull).  value = agent-QP solves/s over the whole job (agents
 whose filter ran, counted on device).
 
 --gpus N: one rank per GPU.  Under a launcher (torchrun: RANK / WORLD_SIZE set) this process is
@@ -322,9 +323,11 @@ def gather_state_sha(own, ws):
 def lattice_cull(args, sharded):
     """The cull of the lattice step: --cull, or auto = the lattice-window cull (CBF_RUN_WINDOW_CULL)
     for a single-GPU lattice that stays lattice-like (the consensus nominal control of cfg4 /
-    cfg4f: 69.5-70.0 vs 71.8-72.2 us per timestep at 1 M agents, tools/ab_window.py), the cell list
-    for the random walk of cfg4r (which scrambles the lattice), the HOCBF barrier and the sharded
-    stripes (at 128 rows the cell list's step is 26.0 us against 29.7-30.7)."""
+    cfg4f: 66.1-67.9 vs 71.2-72.2 us per timestep at 1 M agents, profiles/r04_row_guard_ab.txt),
+    the cell list for the random walk of cfg4r (which scrambles each row's x order: 237.7 vs 84.9
+    us, profiles/r04_cfg4r_window_vs_cells.txt), the HOCBF barrier and the sharded stripes (128-256
+    rows per sub-step window: the cell list is faster below about 384 rows,
+    profiles/r04_window_vs_cells_by_rows.txt)."""
     if args.barrier != "reference" or not 4 <= args.width <= 2048:
         if args.cull == "window":
             raise SystemExit("--cull window: reference barrier, 4 <= width <= 2048 only")

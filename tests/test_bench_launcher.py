@@ -30,3 +30,25 @@ def test_default_rank_timeout_is_bounded():
     a = argparse.Namespace(steps=200, warmup=20, collective_timeout=300.0)
     t = bench.default_rank_timeout(a)
     assert 300 < t < 1800
+
+
+def test_lattice_cull_policy():
+    """bench.py --cull auto: the window cull for the single-GPU consensus lattice only."""
+    sys.path.insert(0, ROOT)
+    import argparse
+    import pytest
+    import bench
+
+    def a(**kw):
+        d = dict(barrier="reference", width=1024, cull="auto", nominal=None)
+        d.update(kw)
+        return argparse.Namespace(**d)
+    assert bench.lattice_cull(a(), sharded=False) == "window"
+    assert bench.lattice_cull(a(), sharded=True) == "cells"
+    assert bench.lattice_cull(a(nominal=("random", 1.0, 5)), sharded=False) == "cells"
+    assert bench.lattice_cull(a(barrier="euclidean_hocbf"), sharded=False) == "cells"
+    assert bench.lattice_cull(a(width=4096), sharded=False) == "cells"
+    assert bench.lattice_cull(a(cull="window"), sharded=True) == "window"
+    assert bench.lattice_cull(a(cull="cells"), sharded=False) == "cells"
+    with pytest.raises(SystemExit):
+        bench.lattice_cull(a(cull="window", barrier="euclidean_hocbf"), sharded=False)
