@@ -522,27 +522,37 @@ def bench_lattice(args, ws, rank, local):
     # so the events time the kernels and not the host's launch latency (a 20-us window-cull build
     # can drain before the host has launched the advance)
     spin = getattr(torch.cuda, "_sleep", None)
-    for _ in range(args.kernel_iters):
+    # single GPU: the filter is also launched with hipExtLaunchKernel start / stop events, which
+    # carry the dispatch's own start and end (as a kernel trace measures it); the stream events
+    # around it also cover the dispatch of the launch and its end-of-kernel cache flush
+    own = marked and not sharded
+    kt, ko = [], []
+    for it in range(args.kernel_iters * (2 if own else 1)):
+        timed_launch = own and it % 2 == 1
         S.build_phase()
-        a = torch.cuda.Event(enable_timing=True)
-        m = torch.cuda.Event(enable_timing=True)
-        b = torch.cuda.Event(enable_timing=True)
+        a, m, b, fs, fe = (torch.cuda.Event(enable_timing=True) for _ in range(5))
         if marked:
             m.record()   # creates the event; the advance call records it again after the filter
+        if timed_launch:
+            fs.record()  # created here; the filter's launch sets both
+            fe.record()
         if spin is not None:
             spin(200000)
         a.record()
-        if marked and cull == "window" and not sharded:
+        if timed_launch:
+            S.advance_phase(timing=(fs, fe), **({"commit": False} if cull == "window" else {}))
+        elif marked and cull == "window" and not sharded:
             S.advance_phase(mark=m, commit=False)   # (the new positions into scratch: no copy timed)
         elif marked:
             S.advance_phase(mark=m)
         else:
             S.advance_phase()
         b.record()
-        kt.append((a, m, b))
+        (ko if timed_launch else kt).append((a, m, b, fs, fe))
     torch.cuda.synchronize()
-    k_ms = float(np.mean([a.elapsed_time(b) for a, m, b in kt]))
-    f_ms = float(np.mean([a.elapsed_time(m) for a, m, b in kt])) if marked else k_ms
+    k_ms = float(np.mean([a.elapsed_time(b) for a, m, b, fs, fe in kt]))
+    f_stream_ms = float(np.mean([a.elapsed_time(m) for a, m, b, fs, fe in kt])) if marked else k_ms
+    f_ms = float(np.mean([fs.elapsed_time(fe) for a, m, b, fs, fe in ko])) if own else f_stream_ms
     status = S.status.cpu().numpy()
     codes = np.bincount(status & 0xFF, minlength=5)
     check = full_size_check(S, args) if (ws == 1 and not args.shard and args.barrier == "reference") else None
@@ -603,11 +613,14 @@ def bench_lattice(args, ws, rank, local):
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS,
                      "traffic": traffic,
-                     "kernel": (f"{adv_kernels[0].split('<')[0]}<f=0, no statistics> (the dominant kernel; HIP events "
-                                "on its launch stream, the end event recorded by the advance call between it and the "
-                                "queued-QP kernel)") if args.barrier == "reference"
+                     "kernel": (f"{adv_kernels[0].split('<')[0]}<f=0, no statistics> (the dominant kernel; "
+                                + ("the start / stop events of its own launch (hipExtLaunchKernel), as a kernel trace "
+                                   "times it" if own else "HIP events on its launch stream, the end event recorded "
+                                   "by the advance call between it and the queued-QP kernel") + ")")
+                     if args.barrier == "reference"
                      else "advance phase: k_lattice_filter_hocbf + k_lattice_filter_hocbf_wide",
                      "kernel_ms": f_ms,
+                     "kernel_ms_stream_events": f_stream_ms,
                      "advance_phase": {"kernels": " + ".join(k.split("<")[0] for k in adv_kernels), "ms": k_ms,
                                        "achieved": achieved_adv, "frac": achieved_adv / HBM_PEAK_GBS,
                                        "traffic": traffic_adv},

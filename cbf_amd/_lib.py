@@ -15,7 +15,7 @@ PKG = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(PKG, "libcbf_amd.so")
 
 CBF_EINVAL = -1
-ABI_VERSION = 5  # include/cbf_amd.h CBF_ABI_VERSION
+ABI_VERSION = 6  # include/cbf_amd.h CBF_ABI_VERSION
 STATUS_IDLE, STATUS_OPTIMAL, STATUS_RELAXED, STATUS_BOX_INFEASIBLE, STATUS_RELAX_CAP = 0, 1, 2, 3, 4
 STATUS_NBR_OVERFLOW = 5
 STATUS_WORKSPACE_ERROR = 6
@@ -111,6 +111,10 @@ SIGNATURES = {
                                       _i32, _vp, _vp, _vp, _sz, _vp]),
     "cbf_lattice_advance_marked": (C.c_int, [_P, _G, _i32, _i32, _i32, _i32, _i32, _i32, _vp, _d, _vp, _vp, _vp, _vp,
                                       _i32, _vp, _vp, _vp, _sz, _vp, _vp]),
+    "cbf_lattice_advance_timed": (C.c_int, [_P, _G, _i32, _i32, _i32, _i32, _i32, _i32, _vp, _d, _vp, _vp, _vp, _vp,
+                                            _i32, _vp, _vp, _vp, _sz, _vp, _vp, _vp]),
+    "cbf_lattice_window_advance_timed": (C.c_int, [_P, _G, _i32, _i32, _vp, _d, _vp, _vp, _vp, _vp, _vp, _vp, _sz,
+                                                   _vp, _vp, _vp]),
     "cbf_lattice_advance_hocbf": (C.c_int, [_P, _HP, _G, _i32, _i32, _i32, _i32, _i32, _i32, _vp, _d, _vp, _vp, _vp,
                                             _vp, _i32, _vp, _vp, _vp, _sz, _vp]),
     "cbf_mc_rollout": (C.c_int, [_P, _i32, _i32, _i32, _i32, _d, _d, _d, _d, _d, _vp, _vp, _vp, _vp, _vp]),

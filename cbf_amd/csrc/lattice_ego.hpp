@@ -251,6 +251,7 @@ void window_prep(const CellWs& Wk, const WinGeom& Q, const double2* pos, double 
 // the queued QPs are left for k_lattice_filter_hard unless `in`).
 void window_filter(const cbf_params* p, const CellWs& Wk, const WinGeom& Q, int row_begin, int row_end,
                    int cnt_begin, int cnt_end, const double2* pos, double T, double2* pos_out, double2* u,
-                   int32_t* status, int32_t* cnt, unsigned long long* stats, bool in, hipStream_t s);
+                   int32_t* status, int32_t* cnt, unsigned long long* stats, bool in, hipStream_t s,
+                   hipEvent_t t_start = nullptr, hipEvent_t t_stop = nullptr);
 
 }  // namespace cbf

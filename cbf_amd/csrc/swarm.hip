@@ -2,6 +2,7 @@
 //   graph-Laplacian consensus / cyclic pursuit   cross_and_rescue.py:108-125, meet_at_center.py:86-103
 //   Euler                                        cross_and_rescue.py:173
 //   whole timestep of a lattice swarm            SURVEY cfg3/cfg4 (cross_and_rescue.py:97-175 shape)
+#include <hip/hip_ext.h>
 #include "cbf_device.hpp"
 #include "cells.hpp"
 #include "lattice.hpp"
@@ -702,7 +703,8 @@ static int lattice_advance(const cbf_params* p, const cbf_grid* grid, int32_t W,
                            double* pos_out, double* u, int32_t* status, int32_t* nbr_count, int32_t guard_rows,
                            double* extents, uint64_t* stats, void* workspace, size_t workspace_bytes,
                            int32_t cnt_begin, int32_t cnt_end, void* stream, const ChainSpec* chain = nullptr,
-                           bool inner = false, hipEvent_t filter_done = nullptr) {
+                           bool inner = false, hipEvent_t filter_done = nullptr,
+                           hipEvent_t filter_start = nullptr) {
     int rc = check_lattice(p, grid, W, H, row_begin, row_end, win_row0, win_rows, pos, workspace, workspace_bytes);
     if (rc) return rc;
     if (!pos_out || (!inner && (!u || !status))) return CBF_EINVAL;  // inner: a cbf_lattice_run timestep
@@ -728,12 +730,19 @@ static int lattice_advance(const cbf_params* p, const cbf_grid* grid, int32_t W,
                  : (p->f_is_zero ? k_lattice_filter<true, false, true> : k_lattice_filter<false, false, true>))
            : (st ? (p->f_is_zero ? k_lattice_filter<true, true, false> : k_lattice_filter<false, true, false>)
                  : (p->f_is_zero ? k_lattice_filter<true, false, false> : k_lattice_filter<false, false, false>));
-    hipLaunchKernelGGL(filter, dim3(nb), dim3(kBlock), 0, s,
-                       kp, G, B, W, row_begin, row_end, win_row0, n, Wk.ncell, Wk.spos, Wk.svel, Wk.sidx, Wk.start,
-                       Wk.sctl, T, po, uo, status, nbr_count, ext_part, st, Wk.hardq, Wk.qrec, Wk.qcap,
-                       chain ? *chain : ChainSpec{});
-    if (filter_done)
-        if (hipError_t e = hipEventRecord(filter_done, s)) return (int)e;
+    if (filter_start) {  // the measurement hook: events carrying the filter dispatch's own start / end
+        hipExtLaunchKernelGGL(filter, dim3(nb), dim3(kBlock), 0, s, filter_start, filter_done, 0u,
+                              kp, G, B, W, row_begin, row_end, win_row0, n, Wk.ncell, Wk.spos, Wk.svel, Wk.sidx,
+                              Wk.start, Wk.sctl, T, po, uo, status, nbr_count, ext_part, st, Wk.hardq, Wk.qrec,
+                              Wk.qcap, chain ? *chain : ChainSpec{});
+    } else {
+        hipLaunchKernelGGL(filter, dim3(nb), dim3(kBlock), 0, s,
+                           kp, G, B, W, row_begin, row_end, win_row0, n, Wk.ncell, Wk.spos, Wk.svel, Wk.sidx, Wk.start,
+                           Wk.sctl, T, po, uo, status, nbr_count, ext_part, st, Wk.hardq, Wk.qrec, Wk.qcap,
+                           chain ? *chain : ChainSpec{});
+        if (filter_done)
+            if (hipError_t e = hipEventRecord(filter_done, s)) return (int)e;
+    }
     if (in) {
         if (extents) launch_extents_finalize((int)lattice_ext_waves(n), ext_part, extents, s);
         return (int)hipGetLastError();
@@ -763,6 +772,18 @@ extern "C" int cbf_lattice_advance_marked(const cbf_params* p, const cbf_grid* g
     return lattice_advance(p, grid, W, H, row_begin, row_end, win_row0, win_rows, pos, T, pos_out, u, status, nbr_count,
                            guard_rows, extents, stats, workspace, workspace_bytes, row_begin, row_end, stream, nullptr,
                            false, (hipEvent_t)filter_done);
+}
+
+extern "C" int cbf_lattice_advance_timed(const cbf_params* p, const cbf_grid* grid, int32_t W, int32_t H,
+                                         int32_t row_begin, int32_t row_end, int32_t win_row0, int32_t win_rows,
+                                         const double* pos, double T, double* pos_out, double* u, int32_t* status,
+                                         int32_t* nbr_count, int32_t guard_rows, double* extents, uint64_t* stats,
+                                         void* workspace, size_t workspace_bytes, void* filter_start,
+                                         void* filter_stop, void* stream) {
+    if (!filter_start || !filter_stop) return CBF_EINVAL;
+    return lattice_advance(p, grid, W, H, row_begin, row_end, win_row0, win_rows, pos, T, pos_out, u, status, nbr_count,
+                           guard_rows, extents, stats, workspace, workspace_bytes, row_begin, row_end, stream, nullptr,
+                           false, (hipEvent_t)filter_stop, (hipEvent_t)filter_start);
 }
 
 extern "C" int cbf_lattice_step(const cbf_params* p, const cbf_grid* grid, int32_t W, int32_t H, int32_t row_begin,
@@ -852,11 +873,11 @@ extern "C" int cbf_lattice_window_build_ex(const cbf_params* p, const cbf_grid* 
     return (int)hipGetLastError();
 }
 
-extern "C" int cbf_lattice_window_advance_ex(const cbf_params* p, const cbf_grid* grid, int32_t W, int32_t H,
-                                             int32_t row_begin, int32_t row_end, int32_t win_row0, int32_t win_rows,
-                                             const double* pos, double T, double* pos_out, double* u,
-                                             int32_t* status, int32_t* nbr_count, uint64_t* stats, void* workspace,
-                                             size_t workspace_bytes, void* filter_done, void* stream) {
+static int window_advance(const cbf_params* p, const cbf_grid* grid, int32_t W, int32_t H, int32_t row_begin,
+                          int32_t row_end, int32_t win_row0, int32_t win_rows, const double* pos, double T,
+                          double* pos_out, double* u, int32_t* status, int32_t* nbr_count, uint64_t* stats,
+                          void* workspace, size_t workspace_bytes, hipEvent_t filter_done, hipEvent_t filter_start,
+                          void* stream) {
     int rc = check_lattice(p, grid, W, H, row_begin, row_end, win_row0, win_rows, pos, workspace, workspace_bytes);
     if (rc) return rc;
     const long n = (long)W * win_rows, nown = (long)W * (row_end - row_begin);
@@ -870,13 +891,33 @@ extern "C" int cbf_lattice_window_advance_ex(const cbf_params* p, const cbf_grid
     double2* uo = reinterpret_cast<double2*>(u);
     unsigned long long* st = reinterpret_cast<unsigned long long*>(stats);
     window_filter(p, Wk, window_geom(W, H, win_row0, win_rows), row_begin, row_end, row_begin, row_end,
-                  reinterpret_cast<const double2*>(pos), T, po, uo, status, nbr_count, st, in, s);
-    if (filter_done)
-        if (hipError_t e = hipEventRecord((hipEvent_t)filter_done, s)) return (int)e;
+                  reinterpret_cast<const double2*>(pos), T, po, uo, status, nbr_count, st, in, s, filter_start,
+                  filter_start ? filter_done : nullptr);
+    if (filter_done && !filter_start)
+        if (hipError_t e = hipEventRecord(filter_done, s)) return (int)e;
     if (!in)
         launch_hard_plain(p, grid, Wk, make_win_bounds(W, win_row0, n, row_begin, row_end, row_begin, row_end, 0), n,
                           T, po, uo, status, nbr_count, st, s);
     return (int)hipGetLastError();
+}
+
+extern "C" int cbf_lattice_window_advance_ex(const cbf_params* p, const cbf_grid* grid, int32_t W, int32_t H,
+                                             int32_t row_begin, int32_t row_end, int32_t win_row0, int32_t win_rows,
+                                             const double* pos, double T, double* pos_out, double* u,
+                                             int32_t* status, int32_t* nbr_count, uint64_t* stats, void* workspace,
+                                             size_t workspace_bytes, void* filter_done, void* stream) {
+    return window_advance(p, grid, W, H, row_begin, row_end, win_row0, win_rows, pos, T, pos_out, u, status, nbr_count,
+                          stats, workspace, workspace_bytes, (hipEvent_t)filter_done, nullptr, stream);
+}
+
+extern "C" int cbf_lattice_window_advance_timed(const cbf_params* p, const cbf_grid* grid, int32_t W, int32_t H,
+                                                const double* pos, double T, double* pos_out, double* u,
+                                                int32_t* status, int32_t* nbr_count, uint64_t* stats,
+                                                void* workspace, size_t workspace_bytes, void* filter_start,
+                                                void* filter_stop, void* stream) {
+    if (!filter_start || !filter_stop) return CBF_EINVAL;
+    return window_advance(p, grid, W, H, 0, H, 0, H, pos, T, pos_out, u, status, nbr_count, stats, workspace,
+                          workspace_bytes, (hipEvent_t)filter_stop, (hipEvent_t)filter_start, stream);
 }
 
 extern "C" int cbf_lattice_window_build(const cbf_params* p, const cbf_grid* grid, int32_t W, int32_t H,

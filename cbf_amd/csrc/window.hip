@@ -23,6 +23,7 @@
 // at c -+ 2; a wave whose lanes need it scans columns c -+ 2 too (sentinels at c -+ 3); a lane
 // that still needs more walks its rows outward until every sentinel holds, with direct row
 // assembly (win_direct: any swarm, slower the less lattice-like it is).
+#include <hip/hip_ext.h>
 #include "cbf_device.hpp"
 #include "cells.hpp"
 #include "lattice.hpp"
@@ -702,7 +703,8 @@ void window_prep(const CellWs& Wk, const WinGeom& Q, const double2* pos, double 
 // unless the solve is inline).
 void window_filter(const cbf_params* p, const CellWs& Wk, const WinGeom& Q, int row_begin, int row_end,
                    int cnt_begin, int cnt_end, const double2* pos, double T, double2* pos_out, double2* u,
-                   int32_t* status, int32_t* cnt, unsigned long long* stats, bool in, hipStream_t s) {
+                   int32_t* status, int32_t* cnt, unsigned long long* stats, bool in, hipStream_t s,
+                   hipEvent_t t_start, hipEvent_t t_stop) {
     const int W = Q.W;
     const long n = (long)W * Q.rows;
     const KP kp = make_kp(p);
@@ -714,9 +716,15 @@ void window_filter(const cbf_params* p, const CellWs& Wk, const WinGeom& Q, int 
                     : (p->f_is_zero ? k_window_tile<true, false, true> : k_window_tile<false, false, true>))
            : (stats ? (p->f_is_zero ? k_window_tile<true, true, false> : k_window_tile<false, true, false>)
                     : (p->f_is_zero ? k_window_tile<true, false, false> : k_window_tile<false, false, false>));
-    hipLaunchKernelGGL(tile, dim3((unsigned)(tiles_x * tiles_y)), dim3(kTileT), 0, s, kp, B, Q, row_begin - Q.row0,
-                       tiles_x, pos, (const double2*)Wk.svel, (const float2*)win_rsp(Wk), Gd, Wk.sctl, T, pos_out,
-                       u, status, cnt, stats, Wk.hardq, Wk.qrec, Wk.qcap);
+    if (t_start)  // the measurement hook: events carrying the launch's own start / end (hip_ext.h)
+        hipExtLaunchKernelGGL(tile, dim3((unsigned)(tiles_x * tiles_y)), dim3(kTileT), 0, s, t_start, t_stop, 0u, kp, B,
+                              Q, row_begin - Q.row0, tiles_x, pos, (const double2*)Wk.svel,
+                              (const float2*)win_rsp(Wk), Gd, Wk.sctl, T, pos_out, u, status, cnt, stats, Wk.hardq,
+                              Wk.qrec, Wk.qcap);
+    else
+        hipLaunchKernelGGL(tile, dim3((unsigned)(tiles_x * tiles_y)), dim3(kTileT), 0, s, kp, B, Q, row_begin - Q.row0,
+                           tiles_x, pos, (const double2*)Wk.svel, (const float2*)win_rsp(Wk), Gd, Wk.sctl, T, pos_out,
+                           u, status, cnt, stats, Wk.hardq, Wk.qrec, Wk.qcap);
 }
 
 }  // namespace cbf

@@ -407,15 +407,26 @@ class LatticeSwarm:
                                     ptr(self.pos), self.gain, ptr(self.vel), ptr(self.ws), self.ws_bytes,
                                     stream_handle()), "cbf_lattice_build")
 
-    def advance_phase(self, mark=None, commit=True):
+    def advance_phase(self, mark=None, commit=True, timing=None):
         """filter + clip + Euler only (the dominant kernel, K4, then the queued-QP kernel K5).
         mark: a torch.cuda.Event (already recorded once) that is recorded between K4 and K5.
+        timing: (start, stop) torch.cuda.Events (already recorded once) that get the filter
+        kernel's own start and end times (cbf_lattice_*advance_timed, hipExtLaunchKernel).
         Window cull: the new positions go to a scratch tensor (the filter reads pos throughout) and
         are copied into pos unless commit=False (kernel timing)."""
+        ev = (lambda e: _lib.C.c_void_p(e.cuda_event))
         if self.cull == "window":
             torch = _lib.require_gpu()
             if getattr(self, "_pos_next", None) is None:
                 self._pos_next = torch.empty_like(self.pos)
+            if timing is not None:
+                check(lib.cbf_lattice_window_advance_timed(
+                    self.cp, _lib.C.byref(self.grid), self.W, self.H, ptr(self.pos), self.T, ptr(self._pos_next),
+                    ptr(self.u), ptr(self.status), ptr(self.nbr_count), self._st(), ptr(self.ws), self.ws_bytes,
+                    ev(timing[0]), ev(timing[1]), stream_handle()), "cbf_lattice_window_advance_timed")
+                if commit:
+                    self.pos.copy_(self._pos_next)
+                return
             check(lib.cbf_lattice_window_advance(self.cp, _lib.C.byref(self.grid), self.W, self.H, ptr(self.pos),
                                                  self.T, ptr(self._pos_next), ptr(self.u), ptr(self.status),
                                                  ptr(self.nbr_count), self._st(), ptr(self.ws), self.ws_bytes,
@@ -430,6 +441,13 @@ class LatticeSwarm:
                                                 ptr(self.u), ptr(self.status), ptr(self.nbr_count), 0, None,
                                                 self._st(), ptr(self.ws), self.ws_bytes, stream_handle()),
                   "cbf_lattice_advance_hocbf")
+            return
+        if timing is not None:
+            check(lib.cbf_lattice_advance_timed(self.cp, _lib.C.byref(self.grid), self.W, self.H, 0, self.H, 0, self.H,
+                                                ptr(self.pos), self.T, ptr(self.pos), ptr(self.u), ptr(self.status),
+                                                ptr(self.nbr_count), 0, None, self._st(), ptr(self.ws), self.ws_bytes,
+                                                ev(timing[0]), ev(timing[1]), stream_handle()),
+                  "cbf_lattice_advance_timed")
             return
         if mark is not None:
             check(lib.cbf_lattice_advance_marked(self.cp, _lib.C.byref(self.grid), self.W, self.H, 0, self.H, 0, self.H,

@@ -27,7 +27,7 @@ def test_library_loads_and_exports_every_declared_symbol():
         assert hasattr(_lib.lib, n), n
         assert n in _lib.SIGNATURES, n
     assert set(_lib.SIGNATURES) == set(names)
-    assert _lib.lib.cbf_abi_version() == _lib.ABI_VERSION == 5
+    assert _lib.lib.cbf_abi_version() == _lib.ABI_VERSION == 6
 
 
 def test_library_is_gfx950_code_object():

@@ -200,3 +200,29 @@ def test_window_guard_words_never_ready():
     for x, y in ((A.pos, B.pos), (A.u, B.u), (A.vel, B.vel), (A.status, B.status), (A.nbr_count, B.nbr_count)):
         assert torch.equal(x, y)
     assert A.stats_summary() == B.stats_summary()
+
+
+@pytest.mark.parametrize("cull", ["window", "cells"])
+def test_timed_advance_equals_marked(cull):
+    """advance_phase(timing=...) (cbf_lattice_*advance_timed: the filter launched with
+    hipExtLaunchKernel start / stop events, bench.py's kernel timing) gives the plain advance's
+    results bit for bit, and its events time the filter inside the advance call's span."""
+    W, H = 256, 192
+    pos = scenarios.lattice(W, H, seed=28)
+    A = swarm.LatticeSwarm(pos, W, H, cull=cull)
+    B = swarm.LatticeSwarm(pos, W, H, cull=cull)
+    for L in (A, B):
+        L.build_phase()
+    a, b, fs, fe, m = (torch.cuda.Event(enable_timing=True) for _ in range(5))
+    fs.record()
+    fe.record()
+    m.record()
+    A.advance_phase(mark=m)
+    a.record()
+    B.advance_phase(timing=(fs, fe))
+    b.record()
+    torch.cuda.synchronize()
+    for x, y in ((A.pos, B.pos), (A.u, B.u), (A.status, B.status), (A.nbr_count, B.nbr_count)):
+        assert torch.equal(x, y)
+    t = fs.elapsed_time(fe)
+    assert 0 < t <= a.elapsed_time(b)
