@@ -101,6 +101,21 @@ __device__ __forceinline__ float f32_up(double v) {
     return f;
 }
 
+// Minima / maxima of guard extents: the values are finite or +-inf (non-finite agents are left
+// out), never NaN, and the sign of a zero cannot change a guard test (d > 0), so the min / max
+// instruction serves as is: one VALU op instead of pmin's compare and two selects (fmin would
+// add the IEEE-mode quieting of each operand).
+__device__ __forceinline__ double gmin(double a, double b) {
+    double r;
+    asm("v_min_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+__device__ __forceinline__ double gmax(double a, double b) {
+    double r;
+    asm("v_max_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+
 // Window-cull build of one timestep: one block per candidate row.  Per agent the nominal control
 // (the lattice Laplacian of cross_and_rescue.py:121-125 shape scaled by gain, or the random walk
 // of CBF_NOMINAL_RANDOM: the scatter's arithmetic) into u0 (and vel_out), the column extents into
@@ -189,8 +204,8 @@ __global__ void __launch_bounds__(kPrepBlock) __attribute__((amdgpu_waves_per_eu
         u0[w] = a;
         if (vel_out && rl >= row_begin && rl < row_end) vel_out[(long)(rl - row_begin) * W + c] = a;
         if (isfinite(pi.x) && isfinite(pi.y)) {
-            ylo = pmin(ylo, pi.y);
-            yhi = pmax(yhi, pi.y);
+            ylo = gmin(ylo, pi.y);
+            yhi = gmax(yhi, pi.y);
         }
     }
     // column extents: suffix minimum / prefix maximum of x along the row over the finite agents,
@@ -204,7 +219,7 @@ __global__ void __launch_bounds__(kPrepBlock) __attribute__((amdgpu_waves_per_eu
     for (int j = PER - 1; j >= 0; --j) {
         if (j < m && c0 + j < W) {
             const double2 q = srow[c0 + j];
-            if (isfinite(q.x) && isfinite(q.y)) acc = pmin(acc, q.x);
+            if (isfinite(q.x) && isfinite(q.y)) acc = gmin(acc, q.x);
         }
         sm[j] = acc;
     }
@@ -213,7 +228,7 @@ __global__ void __launch_bounds__(kPrepBlock) __attribute__((amdgpu_waves_per_eu
     for (int j = 0; j < PER; ++j) {
         if (j < m && c0 + j < W) {
             const double2 q = srow[c0 + j];
-            if (isfinite(q.x) && isfinite(q.y)) acc = pmax(acc, q.x);
+            if (isfinite(q.x) && isfinite(q.y)) acc = gmax(acc, q.x);
         }
         pm[j] = acc;
     }
@@ -221,10 +236,10 @@ __global__ void __launch_bounds__(kPrepBlock) __attribute__((amdgpu_waves_per_eu
     double ss = sm[0], ps = pm[PER - 1], yl = ylo, yh = yhi;  // wave scans / reductions
     for (int o = 1; o < 64; o <<= 1) {
         const double a = __shfl_down(ss, o, 64), b = __shfl_up(ps, o, 64);
-        if (lane + o < 64) ss = pmin(ss, a);
-        if (lane >= o) ps = pmax(ps, b);
-        yl = pmin(yl, __shfl_xor(yl, o, 64));
-        yh = pmax(yh, __shfl_xor(yh, o, 64));
+        if (lane + o < 64) ss = gmin(ss, a);
+        if (lane >= o) ps = gmax(ps, b);
+        yl = gmin(yl, __shfl_xor(yl, o, 64));
+        yh = gmax(yh, __shfl_xor(yh, o, 64));
     }
     double sx = __shfl_down(ss, 1, 64), px = __shfl_up(ps, 1, 64);  // exclusive
     if (lane == 63) sx = INFINITY;
@@ -239,15 +254,15 @@ __global__ void __launch_bounds__(kPrepBlock) __attribute__((amdgpu_waves_per_eu
     double after = sx, before = px, lo = INFINITY, hi = -INFINITY;
 #pragma unroll
     for (int q = 0; q < kPrepBlock / 64; ++q) {
-        if (q > wid) after = pmin(after, red4[0][q]);
-        if (q < wid) before = pmax(before, red4[1][q]);
-        lo = pmin(lo, red4[2][q]);
-        hi = pmax(hi, red4[3][q]);
+        if (q > wid) after = gmin(after, red4[0][q]);
+        if (q < wid) before = gmax(before, red4[1][q]);
+        lo = gmin(lo, red4[2][q]);
+        hi = gmax(hi, red4[3][q]);
     }
 #pragma unroll
     for (int j = 0; j < PER; ++j) {
         const int c = c0 + j;
-        if (j < m && c < W) srsp[c] = make_float2(f32_down(pmin(sm[j], after)), f32_up(pmax(pm[j], before)));
+        if (j < m && c < W) srsp[c] = make_float2(f32_down(gmin(sm[j], after)), f32_up(gmax(pm[j], before)));
     }
     if (ext_keys) {
         // the sharded step's halo-guard extents of this build's input positions (as the cell-list
@@ -326,14 +341,14 @@ __device__ __forceinline__ void row_guard_scan(const WinGeom& Q, const WinGuard&
             lp[j] = bp + j < H ? Gd.rowy[2l * (bp + j) + 1] : -INFINITY;
         }
 #pragma unroll
-        for (int j = PER - 2; j >= 0; --j) ls[j] = pmin(ls[j], ls[j + 1]);
+        for (int j = PER - 2; j >= 0; --j) ls[j] = gmin(ls[j], ls[j + 1]);
 #pragma unroll
-        for (int j = 1; j < PER; ++j) lp[j] = pmax(lp[j], lp[j - 1]);
+        for (int j = 1; j < PER; ++j) lp[j] = gmax(lp[j], lp[j - 1]);
         double vs = ls[0], vp = lp[PER - 1];
         for (int o = 1; o < 64; o <<= 1) {  // inclusive wave scans of the thread totals
             const double a = __shfl_down(vs, o, 64), b = __shfl_up(vp, o, 64);
-            if (lane + o < 64) vs = pmin(vs, a);
-            if (lane >= o) vp = pmax(vp, b);
+            if (lane + o < 64) vs = gmin(vs, a);
+            if (lane >= o) vp = gmax(vp, b);
         }
         double xs = __shfl_down(vs, 1, 64), xp = __shfl_up(vp, 1, 64);  // exclusive
         if (lane == 63) xs = INFINITY;
@@ -343,20 +358,20 @@ __device__ __forceinline__ void row_guard_scan(const WinGeom& Q, const WinGuard&
         __syncthreads();
         double as = carry_s, bq = carry_p, ts = INFINITY, tp = -INFINITY;
         for (int q = 0; q < NW; ++q) {
-            if (q > wid) as = pmin(as, red[0][q]);
-            if (q < wid) bq = pmax(bq, red[1][q]);
-            ts = pmin(ts, red[0][q]);
-            tp = pmax(tp, red[1][q]);
+            if (q > wid) as = gmin(as, red[0][q]);
+            if (q < wid) bq = gmax(bq, red[1][q]);
+            ts = gmin(ts, red[0][q]);
+            tp = gmax(tp, red[1][q]);
         }
-        as = pmin(as, xs);
-        bq = pmax(bq, xp);
+        as = gmin(as, xs);
+        bq = gmax(bq, xp);
 #pragma unroll
         for (int j = 0; j < PER; ++j) {
-            if (bs + j < H) st_guard<PACK>(&Gd.sylo[bs + j], pmin(ls[j], as), true, token);
-            if (bp + j < H) st_guard<PACK>(&Gd.pyhi[bp + j], pmax(lp[j], bq), false, token);
+            if (bs + j < H) st_guard<PACK>(&Gd.sylo[bs + j], gmin(ls[j], as), true, token);
+            if (bp + j < H) st_guard<PACK>(&Gd.pyhi[bp + j], gmax(lp[j], bq), false, token);
         }
-        carry_s = pmin(carry_s, ts);
-        carry_p = pmax(carry_p, tp);
+        carry_s = gmin(carry_s, ts);
+        carry_p = gmax(carry_p, tp);
         if (k + 1 < nch) __syncthreads();
     }
     if (threadIdx.x == 0) st_guard<PACK>(&Gd.sylo[H], INFINITY, true, token);
