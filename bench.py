@@ -320,21 +320,24 @@ def gather_state_sha(own, ws):
     return hashlib.sha256(x.cpu().numpy().tobytes()).hexdigest()
 
 
-def lattice_cull(args, sharded):
+def lattice_cull(args, sharded, rows=None):
     """The cull of the lattice step: --cull, or auto = the lattice-window cull (CBF_RUN_WINDOW_CULL)
-    for a single-GPU lattice that stays lattice-like (the consensus nominal control of cfg4 /
-    cfg4f: 66.1-67.9 vs 71.2-72.2 us per timestep at 1 M agents, profiles/r04_row_guard_ab.txt),
-    the cell list for the random walk of cfg4r (which scrambles each row's x order: 237.7 vs 84.9
-    us, profiles/r04_cfg4r_window_vs_cells.txt), the HOCBF barrier and the sharded stripes (128-256
-    rows per sub-step window: the cell list is faster below about 384 rows,
-    profiles/r04_window_vs_cells_by_rows.txt)."""
+    for a lattice that stays lattice-like (the consensus nominal control of cfg4 / cfg4f), the
+    cell list for the random walk of cfg4r (which scrambles each row's x order: 237.7 vs 84.9 us,
+    profiles/r04_cfg4r_window_vs_cells.txt) and the HOCBF barrier.  One GPU: 66.1-67.9 vs
+    71.2-72.2 us per timestep at 1 M agents (profiles/r04_row_guard_ab.txt).  Sharded stripes of
+    rows >= 256 rows per rank (the N <= 4 strong-scaling shares and weak scaling): one rank's
+    exchange cycle 76.0 / 52.6 / 39.8 vs 87.0 / 58.1 / 42.4 us at 1024 / 512 / 256 rows; at 128
+    rows (N = 8) the cell list stays, 30.4-30.6 vs 30.8-31.1 (profiles/r04_shard_window_vs_cells.txt)."""
     if args.barrier != "reference" or not 4 <= args.width <= 2048:
         if args.cull == "window":
             raise SystemExit("--cull window: reference barrier, 4 <= width <= 2048 only")
         return "cells"
     if args.cull != "auto":
         return args.cull
-    return "window" if args.nominal is None and not sharded else "cells"
+    if args.nominal is not None:
+        return "cells"
+    return "window" if not sharded or (rows is not None and rows >= 256) else "cells"
 
 
 def bench_lattice(args, ws, rank, local):
@@ -346,11 +349,11 @@ def bench_lattice(args, ws, rank, local):
     if sharded:
         from cbf_amd.shard import ShardedLattice
         S = ShardedLattice(W, rows, seed=args.seed, halo=halo, substeps=k, spacing=args.spacing, gain=args.gain,
-                           nominal=args.nominal, exchange=args.exchange, cull=lattice_cull(args, sharded))
+                           nominal=args.nominal, exchange=args.exchange, cull=lattice_cull(args, sharded, rows))
     else:
         pos = scenarios.lattice(W, rows, seed=args.seed, spacing=args.spacing)
         S = swarm.LatticeSwarm(pos, W, rows, gain=args.gain, barrier=args.barrier, nominal=args.nominal,
-                               cull=lattice_cull(args, sharded))
+                               cull=lattice_cull(args, sharded, rows))
     progress(f"{args.config}: {W}x{rows_total} lattice built ({rows} rows on this rank)")
     use_graph = not args.eager
     # single GPU, reference barrier: the timesteps run as cbf_lattice_run calls of `chunk`

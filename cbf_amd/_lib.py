@@ -21,6 +21,7 @@ STATUS_NBR_OVERFLOW = 5
 STATUS_WORKSPACE_ERROR = 6
 RUN_OUTPUT_HISTORY = 1  # cbf_lattice_run_ex flags (include/cbf_amd.h CBF_RUN_*)
 RUN_WINDOW_CULL = 2
+LAUNCH_SEPARATE_GUARD = 1  # cbf_params.launch_flags (include/cbf_amd.h CBF_LAUNCH_*)
 # words of a lattice-step statistics slot (include/cbf_amd.h CBF_STAT_*)
 (STAT_SOLVES, STAT_OPTIMAL, STAT_RELAXED, STAT_INFEASIBLE, STAT_SEIDEL, STAT_VIOL_OPTIMAL, STAT_VIOL_ORIGINAL,
  STAT_MIN_DIST2, STAT_ERRORS, STAT_BINDING) = range(10)
@@ -31,7 +32,7 @@ class CbfParams(C.Structure):
     _fields_ = [("max_speed", C.c_double), ("dmin", C.c_double), ("k", C.c_double), ("gamma", C.c_double),
                 ("f", C.c_double * 16), ("g", C.c_double * 8), ("cull_t", C.c_double),
                 ("nrm", (C.c_double * 2) * 4), ("f_is_zero", C.c_int32), ("relax_cap", C.c_int32),
-                ("solve_inline_max", C.c_int32), ("reserved0", C.c_int32)]
+                ("solve_inline_max", C.c_int32), ("launch_flags", C.c_uint32)]
 
 
 class CbfGrid(C.Structure):

@@ -244,9 +244,12 @@ bool window_cull_ok(int W, int rows, long n_ws, const CellWs& Wk);
 // The build: nominal controls (vel_out: index (r - row_begin) W + c for rows [row_begin, row_end),
 // nullable), the guards, the halo-guard extents (ext_keys, nullable: sharded), a copy of pos
 // (copy_to, nullable).
+// the window cull's row guard formed inside the filter launch (else by a separate scan kernel
+// launched with the build): cbf_params.launch_flags
+bool window_fold(const cbf_params* p);
 void window_prep(const CellWs& Wk, const WinGeom& Q, const double2* pos, double gain, double2* vel_out,
                  double2* copy_to, unsigned long long* ext_keys, int row_begin, int row_end, ExtSpec X,
-                 hipStream_t s);
+                 bool fold, hipStream_t s);
 // The filter kernel for the egos of lattice rows [row_begin, row_end) (pos_out must not overlap pos;
 // the queued QPs are left for k_lattice_filter_hard unless `in`).
 void window_filter(const cbf_params* p, const CellWs& Wk, const WinGeom& Q, int row_begin, int row_end,

@@ -838,7 +838,7 @@ static int lattice_run_window(const cbf_params* p, const cbf_grid* grid, int32_t
         // an odd run's first build reads pos and leaves its copy in spos, which the filter then reads
         const WinGeom Q = whole_lattice(W, H);
         window_prep(Wk, Q, k == 0 && odd ? buf[0] : src, gain, out ? reinterpret_cast<double2*>(vel_out) + o : nullptr,
-                    k == 0 && odd ? buf[1] : nullptr, nullptr, 0, H, ExtSpec{0, 0, 0}, s);
+                    k == 0 && odd ? buf[1] : nullptr, nullptr, 0, H, ExtSpec{0, 0, 0}, window_fold(p), s);
         double2* uo = out ? reinterpret_cast<double2*>(u) + o : nullptr;
         int32_t* so = out ? status + o : nullptr;
         int32_t* co = out && nbr_count ? nbr_count + o : nullptr;
@@ -869,7 +869,7 @@ extern "C" int cbf_lattice_window_build_ex(const cbf_params* p, const cbf_grid* 
     if (!window_cull_ok(W, win_rows, n, Wk)) return CBF_EINVAL;
     window_prep(Wk, window_geom(W, H, win_row0, win_rows), reinterpret_cast<const double2*>(pos), gain,
                 reinterpret_cast<double2*>(vel_out), nullptr, nullptr, row_begin, row_end, ExtSpec{0, 0, 0},
-                (hipStream_t)stream);
+                window_fold(p), (hipStream_t)stream);
     return (int)hipGetLastError();
 }
 
@@ -1060,7 +1060,7 @@ static int cycle_sharded_window(const cbf_params* p, const cbf_grid* grid, int32
         // an odd call's first build reads wpos and leaves the copy its filter reads in spos
         window_prep(Wk, Q, j == 0 && odd ? buf[0] + (long)(sw0 - win_row0) * W : src, gain,
                     last ? reinterpret_cast<double2*>(wvel) + o : nullptr, j == 0 && odd ? src : nullptr, ek, a, b,
-                    ExtSpec{own_begin, own_end, guard}, st);
+                    ExtSpec{own_begin, own_end, guard}, window_fold(p), st);
         double2* uo = last ? reinterpret_cast<double2*>(wu) + o : nullptr;
         int32_t* so = last ? wstatus + o : nullptr;
         int32_t* co = last && wcnt ? wcnt + o : nullptr;

@@ -33,9 +33,6 @@ using namespace cbf;
 
 namespace {
 
-#ifndef CBF_WIN_FOLD
-#define CBF_WIN_FOLD 1  // 1: the tiled filter's first block forms the row guard (no k_window_rowscan)
-#endif
 #ifndef CBF_TILE_WPE
 #define CBF_TILE_WPE 6  // waves per SIMD the timed tile kernels (queued solve, no statistics) are fitted to
 #endif
@@ -384,10 +381,10 @@ __global__ void __launch_bounds__(kRowScanBlock) k_window_rowscan(WinGeom Q, Win
 // A row-guard value.  Packed (formed in the same launch, k_window_tile): the word is polled with
 // sc1 loads until it carries this build's token; one that never does reads as `worst` (-inf for
 // sylo, +inf for pyhi: every row a candidate row, so the windows only grow and stay complete).
-// fp32 values rounded outward (sylo down, pyhi up) are sound bounds likewise.
-template <bool PACK>
-__device__ __forceinline__ double ld_guard(const double* p, int32_t token, double worst) {
-    if (!PACK) return *p;
+// fp32 values rounded outward (sylo down, pyhi up) are sound bounds likewise.  Not packed: the
+// double k_window_rowscan wrote (an earlier launch).
+__device__ __forceinline__ double ld_guard(const double* p, bool packed, int32_t token, double worst) {
+    if (!packed) return *p;
     if (CBF_WIN_SPIN_LIMIT < 0) return worst;  // (test build tests/_lib/libcbf_winnowait.so)
     const unsigned long long* q = reinterpret_cast<const unsigned long long*>(p);
     for (long spins = 0;; ++spins) {
@@ -403,15 +400,14 @@ __device__ __forceinline__ double ld_guard(const double* p, int32_t token, doubl
 // non-increasing away from r, so the test is monotone in k and Ku counts its failures); a window
 // taller than that continues one row at a time.
 constexpr int kWinPre = 4;
-template <bool PACK = false>
 __device__ __forceinline__ void win_rows(const KP& P, const double* __restrict__ sylo,
                                          const double* __restrict__ pyhi, int r, int lo, int H, double y, int& Kd,
-                                         int& Ku, int32_t token = 0) {
+                                         int& Ku, bool packed, int32_t token) {
     double su[kWinPre], pd[kWinPre];
 #pragma unroll
     for (int k = 0; k < kWinPre; ++k) {
-        su[k] = r + k + 1 < H ? ld_guard<PACK>(sylo + r + k + 1, token, -INFINITY) : INFINITY;  // beyond: none
-        pd[k] = r - k - 1 >= lo ? ld_guard<PACK>(pyhi + r - k - 1, token, INFINITY) : -INFINITY;
+        su[k] = r + k + 1 < H ? ld_guard(sylo + r + k + 1, packed, token, -INFINITY) : INFINITY;  // beyond: none
+        pd[k] = r - k - 1 >= lo ? ld_guard(pyhi + r - k - 1, packed, token, INFINITY) : -INFINITY;
     }
     Ku = 0;
     Kd = 0;
@@ -421,9 +417,9 @@ __device__ __forceinline__ void win_rows(const KP& P, const double* __restrict__
         Kd += !(y - pd[k] > P.win_d) ? 1 : 0;
     }
     if (Ku == kWinPre)
-        while (r + Ku + 1 < H && !(ld_guard<PACK>(sylo + r + Ku + 1, token, -INFINITY) - y > P.win_d)) ++Ku;
+        while (r + Ku + 1 < H && !(ld_guard(sylo + r + Ku + 1, packed, token, -INFINITY) - y > P.win_d)) ++Ku;
     if (Kd == kWinPre)
-        while (r - Kd - 1 >= lo && !(y - ld_guard<PACK>(pyhi + r - Kd - 1, token, INFINITY) > P.win_d)) ++Kd;
+        while (r - Kd - 1 >= lo && !(y - ld_guard(pyhi + r - Kd - 1, packed, token, INFINITY) > P.win_d)) ++Kd;
 }
 
 // 32-bit byte offsets into the lattice-ordered arrays (windows of < 2^28 agents, check_lattice)
@@ -493,7 +489,7 @@ template <bool FZ, bool ST, bool IN>
 __global__ void __launch_bounds__(kTileT) __attribute__((amdgpu_waves_per_eu((IN || ST) ? 1 : CBF_TILE_WPE))) k_window_tile(KP P, WinBounds B, WinGeom Q, int er0, int tiles_x,
                                                         const double2* __restrict__ pos,
                                                         const double2* __restrict__ u0,
-                                                        const float2* __restrict__ rsp, WinGuard Gd,
+                                                        const float2* __restrict__ rsp, WinGuard Gd, bool fold,
                                                         int32_t* __restrict__ sctl, double T,
                                                         double2* __restrict__ pos_out, double2* __restrict__ u,
                                                         int32_t* __restrict__ status, int32_t* __restrict__ cnt,
@@ -518,22 +514,20 @@ __global__ void __launch_bounds__(kTileT) __attribute__((amdgpu_waves_per_eu((IN
                            status, cnt, stats, nullptr, 0, hardq);
         return;
     }
-#if CBF_WIN_FOLD
-    // The row guard without the k_window_rowscan launch: the launch's first block (dispatched
-    // first, so resident while any other block waits) forms sylo / pyhi from the build's row
-    // extents and stores each value as one 64-bit word {fp32 value rounded outward, the build's
-    // token} with an sc1 store; a reader polls the words it needs with sc1 loads until they carry
-    // the token (ld_guard), so a block that starts after the guard is formed pays no extra round
-    // trip and none waits on a done word.
+    // fold: the row guard without the k_window_rowscan launch.  The launch's first block
+    // (dispatched first, so resident while any other block waits) forms sylo / pyhi from the
+    // build's row extents and stores each value as one 64-bit word {fp32 value rounded outward,
+    // the build's token} with an sc1 store; a reader polls the words it needs with sc1 loads until
+    // they carry the token (ld_guard), so a block that starts after the guard is formed pays no
+    // extra round trip and none waits on a done word.  (Where processes time-share the GPU the
+    // first block can stall for long; cbf_params.launch_flags CBF_LAUNCH_SEPARATE_GUARD then
+    // selects the separate scan kernel: fold = false.)
     __shared__ double gred[2][kTileT / 64];
-    const int32_t token = Gd.sync[0];  // written by the build (an earlier launch)
-    if (blockIdx.x == 0) {
+    const int32_t token = fold ? Gd.sync[0] : 0;  // written by the build (an earlier launch)
+    if (fold && blockIdx.x == 0) {
         row_guard_scan<kTileT, CBF_GUARD_PER, true>(Q, Gd, gred, token);
         if (threadIdx.x == 0) Gd.sync[1] = token;  // (the next build's token follows it)
     }
-#else
-    const int32_t token = 0;
-#endif
     // stage the tile with its halo (beyond the lattice: +-inf positions, which no test passes, and
     // column extents that exclude nothing beyond the row ends)
     for (int i = threadIdx.x; i < kTileN; i += kTileT) {
@@ -553,8 +547,8 @@ __global__ void __launch_bounds__(kTileT) __attribute__((amdgpu_waves_per_eu((IN
     }
     if (threadIdx.x < kTileGuard) {
         const int a = r0 + 1 + threadIdx.x, b = r0 - kWinPre + threadIdx.x;
-        L.sy[threadIdx.x] = a < Q.cr1 ? ld_guard<CBF_WIN_FOLD>(sylo + a, token, -INFINITY) : INFINITY;
-        L.py[threadIdx.x] = b >= Q.cr0 ? ld_guard<CBF_WIN_FOLD>(pyhi + b, token, INFINITY) : -INFINITY;
+        L.sy[threadIdx.x] = a < Q.cr1 ? ld_guard(sylo + a, fold, token, -INFINITY) : INFINITY;
+        L.py[threadIdx.x] = b >= Q.cr0 ? ld_guard(pyhi + b, fold, token, INFINITY) : -INFINITY;
     }
     __syncthreads();
     const bool act = inside && w >= B.own_lo && w < B.own_hi;
@@ -674,7 +668,7 @@ __global__ void __launch_bounds__(kTileT) __attribute__((amdgpu_waves_per_eu((IN
             }
         } else if (fin) {  // the unbounded form, over the full row window (beyond the staged halo too)
             int kd, ku;
-            win_rows<CBF_WIN_FOLD>(P, sylo, pyhi, r, Q.cr0, Q.cr1, E.r1, kd, ku, token);
+            win_rows(P, sylo, pyhi, r, Q.cr0, Q.cr1, E.r1, kd, ku, fold, token);
             win_direct<FZ>(P, E, w, r, c, W, kd, ku, pos, u0, rsp, d2);
         }
         O.nbrs = E.count;
@@ -698,9 +692,11 @@ bool window_cull_ok(int W, int rows, long n_ws, const CellWs& Wk) {
     return W >= 4 && W <= kWinMaxW && rows >= 1 && win_guard_bytes(rows) <= 16 * (size_t)n_ws && Wk.cs != nullptr;
 }
 
+bool window_fold(const cbf_params* p) { return !(p->launch_flags & CBF_LAUNCH_SEPARATE_GUARD); }
+
 void window_prep(const CellWs& Wk, const WinGeom& Q, const double2* pos, double gain, double2* vel_out,
                  double2* copy_to, unsigned long long* ext_keys, int row_begin, int row_end, ExtSpec X,
-                 hipStream_t s) {
+                 bool fold, hipStream_t s) {
     const auto prep = Q.W <= 2 * kPrepBlock   ? k_window_prep<2>
                       : Q.W <= 4 * kPrepBlock ? k_window_prep<4>
                       : Q.W <= 8 * kPrepBlock ? k_window_prep<8>
@@ -708,7 +704,7 @@ void window_prep(const CellWs& Wk, const WinGeom& Q, const double2* pos, double 
     hipLaunchKernelGGL(prep, dim3(Q.cr1 - Q.cr0), dim3(kPrepBlock), 24 * (size_t)Q.W, s, Q, pos, Wk.svel,
                        win_rsp(Wk), win_guard(Wk, Q.rows), gain, vel_out, copy_to, Wk.sctl, Wk.ncell, ext_keys,
                        row_begin, row_end, X);
-    if (!CBF_WIN_FOLD)  // (else the filter's first block forms the row guard)
+    if (!fold)  // (else the filter's first block forms the row guard)
         hipLaunchKernelGGL(k_window_rowscan, dim3(1), dim3(kRowScanBlock), 0, s, Q, win_guard(Wk, Q.rows));
 }
 
@@ -734,11 +730,11 @@ void window_filter(const cbf_params* p, const CellWs& Wk, const WinGeom& Q, int 
     if (t_start)  // the measurement hook: events carrying the launch's own start / end (hip_ext.h)
         hipExtLaunchKernelGGL(tile, dim3((unsigned)(tiles_x * tiles_y)), dim3(kTileT), 0, s, t_start, t_stop, 0u, kp, B,
                               Q, row_begin - Q.row0, tiles_x, pos, (const double2*)Wk.svel,
-                              (const float2*)win_rsp(Wk), Gd, Wk.sctl, T, pos_out, u, status, cnt, stats, Wk.hardq,
+                              (const float2*)win_rsp(Wk), Gd, window_fold(p), Wk.sctl, T, pos_out, u, status, cnt, stats, Wk.hardq,
                               Wk.qrec, Wk.qcap);
     else
         hipLaunchKernelGGL(tile, dim3((unsigned)(tiles_x * tiles_y)), dim3(kTileT), 0, s, kp, B, Q, row_begin - Q.row0,
-                           tiles_x, pos, (const double2*)Wk.svel, (const float2*)win_rsp(Wk), Gd, Wk.sctl, T, pos_out,
+                           tiles_x, pos, (const double2*)Wk.svel, (const float2*)win_rsp(Wk), Gd, window_fold(p), Wk.sctl, T, pos_out,
                            u, status, cnt, stats, Wk.hardq, Wk.qrec, Wk.qcap);
 }
 

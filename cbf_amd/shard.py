@@ -244,6 +244,15 @@ class HipBackend:
         return bool(self.flag.item())
 
 
+def ranks_share_gpu(world_size):
+    """Whether this node runs more ranks than it has visible GPUs (LOCAL_WORLD_SIZE, set by
+    torchrun and by bench.py's launcher; counting devices does not initialise the GPU)."""
+    import os
+    import torch
+    local = int(os.environ.get("LOCAL_WORLD_SIZE", world_size))
+    return local > max(1, torch.cuda.device_count())
+
+
 class ShardedLattice:
     """One rank's stripe of a W x (rows_per_rank * world) lattice swarm (see module docstring)."""
 
@@ -270,7 +279,10 @@ class ShardedLattice:
             d = self.G - halo * (s + 1)
             a, b = max(0, self.rb - d), min(self.H, self.re + d)
             self.subs.append(Sub(a, b, max(0, a - halo), min(self.H, b + halo), d + halo - 1))
-        self.params = params or FilterParams()
+        # ranks time-sharing one GPU (a rehearsal on one card): the window cull's row guard from a
+        # separate kernel, since a block polling for the in-launch hand-off can wait for long there
+        # (cbf_params.launch_flags; results are identical)
+        self.params = params or FilterParams(window_guard="separate" if ranks_share_gpu(self.ws) else "in_filter")
         if pos_global is None:
             pos_global = scenarios.lattice(W, self.H, seed=seed, spacing=spacing)
         win = pos_global[self.w0 * W:self.w1 * W]

@@ -31,10 +31,18 @@ class FilterParams:
     # queued for the second kernel above), "inline" (always in the filter), "queued" (always the
     # queue kernel), or an int threshold.  Results are bit-identical; only the speed differs.
     solve_placement: object = "auto"
+    # window cull only: where its row guard is formed (cbf_params.launch_flags): "in_filter" (the
+    # filter launch's first block hands it to the others: the faster form on a GPU one process
+    # owns) or "separate" (a one-block kernel after the build: for ranks time-sharing one GPU).
+    # Results are identical.
+    window_guard: str = "in_filter"
 
     def c(self):
         p = _lib.make_params(self.max_speed, self.dmin, self.k, self.f, self.g, self.safety_distance)
         p.solve_inline_max = solve_inline_max(self.solve_placement)
+        if self.window_guard not in ("in_filter", "separate"):
+            raise ValueError(f"window_guard must be 'in_filter' or 'separate', got {self.window_guard!r}")
+        p.launch_flags = _lib.LAUNCH_SEPARATE_GUARD if self.window_guard == "separate" else 0
         return p
 
 

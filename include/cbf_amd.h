@@ -87,8 +87,14 @@ typedef struct cbf_params {
      * either way; only the speed differs.  < 0 (cbf_params_init's default): the library's own
      * threshold, 131072 agents (2 waves per SIMD on 256 CUs); 0: always queue.  ABI 4. */
     int32_t solve_inline_max;
-    int32_t reserved0;
+    /* Bit CBF_LAUNCH_SEPARATE_GUARD: the window cull (CBF_RUN_WINDOW_CULL, cbf_lattice_window_*)
+     * forms its row guard in a separate one-block kernel after the build instead of inside the
+     * filter launch, whose blocks poll for it.  The in-launch form is the faster one on a GPU one
+     * process owns; ranks that time-share one GPU should set the bit (a poll can wait for long
+     * there).  Results are identical either way.  0 from cbf_params_init.  ABI 6 (was reserved). */
+    uint32_t launch_flags;
 } cbf_params;
+#define CBF_LAUNCH_SEPARATE_GUARD 1u
 
 /* Fill *p (host).  f16 / g8 may be NULL for the callers' f = 0, g = 0.1 [I2; 0]. */
 int cbf_params_init(cbf_params* p, double max_speed, double dmin, double k, const double* f16, const double* g8,

@@ -33,7 +33,8 @@ def test_default_rank_timeout_is_bounded():
 
 
 def test_lattice_cull_policy():
-    """bench.py --cull auto: the window cull for the single-GPU consensus lattice only."""
+    """bench.py --cull auto: the window cull for the consensus lattice on one GPU and for sharded
+    stripes of >= 256 rows per rank; the cell list otherwise."""
     sys.path.insert(0, ROOT)
     import argparse
     import pytest
@@ -44,7 +45,9 @@ def test_lattice_cull_policy():
         d.update(kw)
         return argparse.Namespace(**d)
     assert bench.lattice_cull(a(), sharded=False) == "window"
-    assert bench.lattice_cull(a(), sharded=True) == "cells"
+    assert bench.lattice_cull(a(), sharded=True, rows=128) == "cells"    # N = 8 share of 1024 rows
+    assert bench.lattice_cull(a(), sharded=True, rows=256) == "window"   # N = 4
+    assert bench.lattice_cull(a(), sharded=True, rows=1024) == "window"  # weak scaling
     assert bench.lattice_cull(a(nominal=("random", 1.0, 5)), sharded=False) == "cells"
     assert bench.lattice_cull(a(barrier="euclidean_hocbf"), sharded=False) == "cells"
     assert bench.lattice_cull(a(width=4096), sharded=False) == "cells"

@@ -58,6 +58,19 @@ def test_bench_gpus2_launches_two_ranks_strong_scaling():
 
 
 @pytest.mark.gpu
+def test_bench_gpus2_window_cull_matches_one_rank():
+    """Stripes of 256 rows per rank take the window cull by default (bench.lattice_cull): the
+    2-rank split of a 256 x 512 lattice (gloo, this one GPU) ends in the 1-rank state bit for
+    bit."""
+    one = _bench("--rows", "512", steps=6)
+    two = _bench("--gpus", "2", "--backend", "gloo", "--rows", "512", n=2, steps=6)
+    assert one["config"]["cull"] == "window" and two["config"]["cull"] == "window"
+    assert two["config"]["agents_per_gpu"] == 256 * 256
+    assert two["end_state_sha256"] == one["end_state_sha256"]
+    assert two["solves_per_step"] == one["solves_per_step"]
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("n", [4, 8])
 def test_bench_gpus_n_rehearsal_matches_one_rank(n):
     """The 4- and 8-rank row splits of the strong-scaling bench (64 and 32 rows per rank of a

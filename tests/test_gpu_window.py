@@ -226,3 +226,23 @@ def test_timed_advance_equals_marked(cull):
         assert torch.equal(x, y)
     t = fs.elapsed_time(fe)
     assert 0 < t <= a.elapsed_time(b)
+
+
+def test_window_separate_guard_equals_in_filter():
+    """cbf_params.launch_flags CBF_LAUNCH_SEPARATE_GUARD (FilterParams(window_guard="separate"):
+    the row guard from the one-block scan kernel after the build, for ranks time-sharing a GPU)
+    gives the in-filter hand-off's results bit for bit, run() and step(), scrambled lattice."""
+    W, H = 64, 48
+    pos = scenarios.lattice(W, H, seed=29)
+    rng = np.random.default_rng(6)
+    a, b = rng.choice(W * H, 30, replace=False), rng.choice(W * H, 30, replace=False)
+    pos[a], pos[b] = pos[b].copy(), pos[a].copy()
+    res = []
+    for g in ("in_filter", "separate"):
+        L = swarm.LatticeSwarm(pos, W, H, gain=GAIN, params=swarm.FilterParams(window_guard=g), cull="window")
+        L.run(3)
+        L.step()
+        torch.cuda.synchronize()
+        res.append([t.cpu().numpy() for t in (L.pos, L.vel, L.u, L.status, L.nbr_count)])
+    for x, y in zip(*res):
+        assert np.array_equal(x, y)
