@@ -282,7 +282,10 @@ class ShardedLattice:
         # ranks time-sharing one GPU (a rehearsal on one card): the window cull's row guard from a
         # separate kernel, since a block polling for the in-launch hand-off can wait for long there
         # (cbf_params.launch_flags; results are identical)
-        self.params = params or FilterParams(window_guard="separate" if ranks_share_gpu(self.ws) else "in_filter")
+        self.params = params or FilterParams()
+        if self.params.window_guard == "auto" and ranks_share_gpu(self.ws):
+            import dataclasses
+            self.params = dataclasses.replace(self.params, window_guard="separate")
         if pos_global is None:
             pos_global = scenarios.lattice(W, self.H, seed=seed, spacing=spacing)
         win = pos_global[self.w0 * W:self.w1 * W]

@@ -33,15 +33,16 @@ class FilterParams:
     solve_placement: object = "auto"
     # window cull only: where its row guard is formed (cbf_params.launch_flags): "in_filter" (the
     # filter launch's first block hands it to the others: the faster form on a GPU one process
-    # owns) or "separate" (a one-block kernel after the build: for ranks time-sharing one GPU).
+    # owns), "separate" (a one-block kernel after the build: for ranks time-sharing one GPU), or
+    # "auto" (in_filter; ShardedLattice takes separate when its node runs more ranks than GPUs).
     # Results are identical.
-    window_guard: str = "in_filter"
+    window_guard: str = "auto"
 
     def c(self):
         p = _lib.make_params(self.max_speed, self.dmin, self.k, self.f, self.g, self.safety_distance)
         p.solve_inline_max = solve_inline_max(self.solve_placement)
-        if self.window_guard not in ("in_filter", "separate"):
-            raise ValueError(f"window_guard must be 'in_filter' or 'separate', got {self.window_guard!r}")
+        if self.window_guard not in ("auto", "in_filter", "separate"):
+            raise ValueError(f"window_guard must be 'auto', 'in_filter' or 'separate', got {self.window_guard!r}")
         p.launch_flags = _lib.LAUNCH_SEPARATE_GUARD if self.window_guard == "separate" else 0
         return p
 
