@@ -298,3 +298,26 @@ def test_sharded_group_swarm_equals_single_domain(name, ws):
         assert np.array_equal(r[1], pos)
     assert np.array_equal(np.concatenate([r[2] for r in res]), u)
     assert sum(r[3] for r in res) == solves
+
+
+def test_ranks_share_gpu_reads_the_local_world_size(monkeypatch):
+    """ShardedLattice takes the window cull's separate row-guard kernel when its node runs more
+    ranks than GPUs (LOCAL_WORLD_SIZE from torchrun / bench.py's launcher against the device
+    count); FilterParams validates the choice."""
+    import torch
+    from cbf_amd import shard, swarm
+    monkeypatch.setattr(torch.cuda, "device_count", lambda: 1)
+    monkeypatch.setenv("LOCAL_WORLD_SIZE", "2")
+    assert shard.ranks_share_gpu(2)
+    monkeypatch.setenv("LOCAL_WORLD_SIZE", "1")
+    assert not shard.ranks_share_gpu(8)
+    monkeypatch.setattr(torch.cuda, "device_count", lambda: 8)
+    monkeypatch.setenv("LOCAL_WORLD_SIZE", "8")
+    assert not shard.ranks_share_gpu(8)
+    monkeypatch.delenv("LOCAL_WORLD_SIZE")
+    assert not shard.ranks_share_gpu(4) and shard.ranks_share_gpu(16)
+    assert swarm.FilterParams(window_guard="separate").c().launch_flags == 1
+    assert swarm.FilterParams().c().launch_flags == 0
+    import pytest
+    with pytest.raises(ValueError):
+        swarm.FilterParams(window_guard="later").c()
