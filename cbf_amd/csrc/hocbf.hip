@@ -32,6 +32,10 @@ __device__ __forceinline__ double4 hocbf_row(const KP& P, const HP& H, double r0
 }
 
 
+#ifndef CBF_HOCBF_UNROLL
+#define CBF_HOCBF_UNROLL 8  // solve_rows' inner loops over the earlier rows, unrolled
+#endif
+
 // Plane source over rows stored in memory (workspace), relaxed in place.
 struct StoredRows {
     double4* rows;
@@ -149,7 +153,8 @@ __device__ __forceinline__ int solve_rows(const double (&bb)[4], const Src& R, d
         Interval I;
 #pragma unroll
         for (int j = 0; j < 4; ++j) I.add(ba0[j], ba1[j], bb[j], d0, d1, p0, p1);
-        for (int j = 0; j < i; ++j) {
+#pragma unroll CBF_HOCBF_UNROLL
+        for (int j = 0; j < i; ++j) {  // (unrolled: the rows' LDS loads issue together)
             double c0, c1, e;
             R.row(j, c0, c1, e);
             I.add(c0, c1, e, d0, d1, p0, p1);
@@ -161,6 +166,7 @@ __device__ __forceinline__ int solve_rows(const double (&bb)[4], const Src& R, d
 #pragma unroll
         for (int j = 0; j < 4; ++j) ok = ok && feas(ba0[j], ba1[j], bb[j], x0, x1);
         if (!ok) return 4 + i;
+#pragma unroll CBF_HOCBF_UNROLL
         for (int j = 0; j <= i; ++j) {
             double c0, c1, e;
             R.row(j, c0, c1, e);
@@ -215,6 +221,7 @@ struct LdsRows {
         b = lds[(3 * i + 2) * ks + lane];
     }
     __device__ __forceinline__ void relax() {
+#pragma unroll CBF_HOCBF_UNROLL
         for (int i = 0; i < m; ++i) {
             double& v = lds[(3 * i + 2) * ks + lane];
             v = v + 1.0;  // cbf.py:85-87
