@@ -1,0 +1,14 @@
+# GPU box, round 4: the tile's hit flush with two hits' LDS loads issued together (fb2) against the
+# restructured one-hit loop (this tree) and HEAD; window tests on fb2's source via this tree first.
+set -u
+cd "$GRAFT_REPO_ROOT"
+export TMPDIR=/tmp
+O=gpurun_out/r04al; mkdir -p $O
+for rep in 1 2; do
+  for t in tools/_abt/head . tools/_abt/fb2; do
+    timeout -k 10 120 python tools/ab_window.py $t window >> $O/ab.txt 2>&1 || { tail -20 $O/ab.txt; exit 2; }
+    timeout -k 10 120 python tools/ab_window.py $t window 0.2 >> $O/ab.txt 2>&1 || { tail -20 $O/ab.txt; exit 3; }
+  done
+done
+grep -v amdgpu.ids $O/ab.txt
+echo R04AL_OK
