@@ -48,8 +48,9 @@ def _guards(pos, W, H):
 
 
 def _tested(pos, W, H, e, G, d):
-    """The window indices the window cull tests for ego e (untiled form; the tiled one tests the
-    same set or walks)."""
+    """The window indices the window cull tests for ego e: k_window_tile's candidates (rows of the
+    row guard, columns c-1..c+1, c-+2 where a sentinel fails) or, where that is not enough, the
+    unbounded walk of win_direct."""
     sylo, pyhi, rs, rp = G
     r, c = divmod(e, W)
     xe, ye = pos[e]
