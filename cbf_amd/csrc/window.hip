@@ -40,7 +40,7 @@ namespace {
 #define CBF_GUARD_PER 2  // rows per thread of the tile launch's row-guard scan
 #endif
 #ifndef CBF_WIN_SPIN_LIMIT
-#define CBF_WIN_SPIN_LIMIT (1l << 22)  // polls of the row guard's done word before a block gives up
+#define CBF_WIN_SPIN_LIMIT (1l << 22)  // polls of a row-guard word before it reads as the worst bound
 #endif
 #ifndef CBF_PREP_BLOCK
 #define CBF_PREP_BLOCK 256  // threads of a build block (one lattice row)
