@@ -544,7 +544,7 @@ def bench_lattice(args, ws, rank, local):
         a.record()
         if timed_launch:
             S.advance_phase(timing=(fs, fe), **({"commit": False} if cull == "window" else {}))
-        elif marked and cull == "window" and not sharded:
+        elif marked and cull == "window":
             S.advance_phase(mark=m, commit=False)   # (the new positions into scratch: no copy timed)
         elif marked:
             S.advance_phase(mark=m)

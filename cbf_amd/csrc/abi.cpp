@@ -31,13 +31,16 @@ extern "C" int cbf_params_init(cbf_params* p, double max_speed, double dmin, dou
     p->cull_t = cull_threshold(safety_distance);
     p->relax_cap = 1 << 16;
     p->solve_inline_max = -1;  // the library's threshold (swarm.hip kSolveInlineDefault)
-    // L_g = -hs_p @ g per sign quadrant, numpy's pairwise order (cbf.py:56)
+    // L_g = -hs_p @ g per sign quadrant (cbf.py:56) in numpy's order: OpenBLAS dgemv_n's two-row
+    // tail, one fma per pair of columns, accumulated into a zeroed output (oracle/pyoracle.py)
     for (int q = 0; q < 4; ++q) {
         const double sx = (q & 1) ? -1.0 : 1.0, sy = (q & 2) ? -1.0 : 1.0;
         const double nh[4] = {-sx, -sy, -(k * sx), -(k * sy)};
-        for (int c = 0; c < 2; ++c)
-            p->nrm[q][c] = (nh[0] * p->g[0 * 2 + c] + nh[1] * p->g[1 * 2 + c]) +
-                           (nh[2] * p->g[2 * 2 + c] + nh[3] * p->g[3 * 2 + c]);
+        for (int c = 0; c < 2; ++c) {
+            const double t01 = fma(nh[0], p->g[0 * 2 + c], nh[1] * p->g[1 * 2 + c]);
+            const double t23 = fma(nh[2], p->g[2 * 2 + c], nh[3] * p->g[3 * 2 + c]);
+            p->nrm[q][c] = 0.0 + ((0.0 + t01) + t23);
+        }
     }
     return 0;
 }

@@ -5,8 +5,13 @@
 // uses in the reference (probed, pinned by tests/golden):
 //   hs_p @ d, np.dot(hs_p, g@u0)  -> fma chain     (cbf.py:55-59)
 //   g @ u0                        -> fma(g[r,0], u0x, g[r,1]*u0y)
+//   f @ d                         -> (f0 d0 + f2 d2) + (f1 d1 + f3 d3) per row (cbf.py:55)
 //   v @ rotation                  -> fma(v1, R[1,c], v0*R[0,c])  (cross_and_rescue.py:118)
-// so that results are bit-identical to the CPU oracle (oracle/cbf_oracle.c).
+// so that results are bit-identical to the CPU oracle (oracle/cbf_oracle.c).  BLAS accumulates
+// into a zeroed output, so numpy never returns -0.0 from these products; of them only the
+// quadrant term c can carry a zero's sign into a barrier rhs b = (gamma (H - dmin) + L_f) + c
+// (once c is +0 or nonzero, the other terms' zero signs cannot reach b), so only c is
+// canonicalised (0.0 + c) here.
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -113,6 +118,16 @@ __device__ __forceinline__ void ego_init(const KP& P, Ego& E, double px, double 
     E.count = 0;
 }
 
+// L_f = hs_p @ (f @ d) (cbf.py:55): numpy's dgemv_t row order, then the hs_p fma chain.
+__device__ __forceinline__ double lf_term(const KP& P, double d0, double d1, double d2, double d3, double sx,
+                                         double sy, double ksx, double ksy) {
+    double fd[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+        fd[i] = (P.f[4 * i] * d0 + P.f[4 * i + 2] * d2) + (P.f[4 * i + 1] * d1 + P.f[4 * i + 3] * d3);
+    return fma(ksy, fd[3], fma(ksx, fd[2], fma(sy, fd[1], sx * fd[0])));
+}
+
 // Barrier row rhs for neighbour o (cbf.py:38-59); q = sign quadrant (cbf.py:47-53, -0.0 -> +1).
 // FZ: compile-time "f == 0" (the callers' dynamics, cross_and_rescue.py:31) -> L_f = 0 with f
 // never read; otherwise the runtime flag decides.
@@ -125,14 +140,8 @@ __device__ __forceinline__ double row_b(const KP& P, const Ego& E, double o0, do
     const double ksx = P.k * sx, ksy = P.k * sy;
     const double H = fma(ksy, d3, fma(ksx, d2, fma(sy, d1, sx * d0)));
     double Lf = 0.0;
-    if (!FZ && !P.f_zero) {
-        double fd[4];
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-            fd[i] = ((P.f[4 * i] * d0 + P.f[4 * i + 1] * d1) + P.f[4 * i + 2] * d2) + P.f[4 * i + 3] * d3;
-        Lf = fma(ksy, fd[3], fma(ksx, fd[2], fma(sy, fd[1], sx * fd[0])));
-    }
-    const double c = fma(ksy, E.gu3, fma(ksx, E.gu2, fma(sy, E.gu1, sx * E.gu0)));
+    if (!FZ && !P.f_zero) Lf = lf_term(P, d0, d1, d2, d3, sx, sy, ksx, ksy);
+    const double c = 0.0 + fma(ksy, E.gu3, fma(ksx, E.gu2, fma(sy, E.gu1, sx * E.gu0)));
     q = (nx ? 1 : 0) | (ny ? 2 : 0);
     // with f == 0 the reference adds L_f = +-0, which leaves every nonzero value unchanged
     // (only the sign of an exactly-zero sum can differ); the compile-time path drops the add
@@ -144,7 +153,7 @@ __device__ __forceinline__ double row_b(const KP& P, const Ego& E, double o0, do
 __device__ __forceinline__ double quad_c(const KP& P, const Ego& E, int q) {
     const double sx = (q & 1) ? -1.0 : 1.0, sy = (q & 2) ? -1.0 : 1.0;
     const double ksx = P.k * sx, ksy = P.k * sy;
-    return fma(ksy, E.gu3, fma(ksx, E.gu2, fma(sy, E.gu1, sx * E.gu0)));
+    return 0.0 + fma(ksy, E.gu3, fma(ksx, E.gu2, fma(sy, E.gu1, sx * E.gu0)));
 }
 
 // row_b without the quadrant term c, for a neighbour whose position differs from the ego's
@@ -164,14 +173,7 @@ __device__ __forceinline__ double row_g(const KP& P, const Ego& E, double o0, do
     q = (nx ? 1 : 0) | (ny ? 2 : 0);
     if (FZ) return P.gamma * (H - P.dmin);
     double Lf = 0.0;
-    if (!P.f_zero) {
-        const double sx = nx ? -1.0 : 1.0, sy = ny ? -1.0 : 1.0;
-        double fd[4];
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-            fd[i] = ((P.f[4 * i] * d0 + P.f[4 * i + 1] * d1) + P.f[4 * i + 2] * d2) + P.f[4 * i + 3] * d3;
-        Lf = fma(ksy, fd[3], fma(ksx, fd[2], fma(sy, fd[1], sx * fd[0])));
-    }
+    if (!P.f_zero) Lf = lf_term(P, d0, d1, d2, d3, nx ? -1.0 : 1.0, ny ? -1.0 : 1.0, ksx, ksy);
     return P.gamma * (H - P.dmin) + Lf;
 }
 

@@ -52,7 +52,7 @@ inline size_t align256(size_t b) { return (b + 255) & ~size_t(255); }
 // Version of the workspace carve-up below and of its control words (cbf_workspace_layout): bump it
 // with ANY change to CellWs, HardRec, the control-word assignments or the queue header, so that a
 // saved workspace is never restored into a library that reads it differently.
-constexpr int kWorkspaceLayout = 5;
+constexpr int kWorkspaceLayout = 6;
 
 // Workspace carve-up (all segments 256-byte aligned).  The control words come first, at a fixed
 // offset, so that the shape signature they hold can be checked whatever shape a call assumes.
@@ -61,7 +61,8 @@ struct CellWs {
                       // gave up, or workspace shape mismatch), [4] n, [5] ncell: the shape the
                       // workspace is bound to (0 = fresh); [8] lattice nominal-control mode, bytes
                       // 40..55 its amplitude (double) and seed (uint64) (cbf_lattice_set_nominal);
-                      // [16] the window-cull build's block ticket (window.hip)
+                      // [16] the window cull's guard-token count, [17] the row-guard mode of
+                      // its last build (window.hip kWinTokenWord / kWinModeWord)
     int32_t* count;   // [ncell]
     int32_t* start;   // [ncell + 1]
     unsigned long long* tstate;  // [ntiles] scan tile status {epoch:30 | flag:2 | value:32}

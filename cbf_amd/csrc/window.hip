@@ -56,7 +56,6 @@ struct WinGuard {
     double* rowy;     // [2 H] {min y, max y} per row (finite agents)
     double* sylo;     // [H + 1] min over rows >= r of the row minima (sylo[H] = +inf)
     double* pyhi;     // [H] max over rows <= r of the row maxima
-    int32_t* sync;    // [2] {the build's guard token, the token of the last guard formed}
 };
 inline WinGuard win_guard(const CellWs& Wk, int H) {
     WinGuard g;
@@ -64,11 +63,21 @@ inline WinGuard win_guard(const CellWs& Wk, int H) {
     g.rowy = reinterpret_cast<double*>(p);
     g.sylo = g.rowy + 2l * H;
     g.pyhi = g.sylo + (H + 1);
-    g.sync = reinterpret_cast<int32_t*>(g.pyhi + H);
     return g;
 }
-// a build's guard token: a 24-bit count tagged in the top byte (the area is the cell list's record
-// area on other paths; its words never carry the tag)
+// Control words of the window cull in the workspace header (fixed offsets, whatever the lattice
+// shape or the cull another call used on the workspace; cells.hpp CellWs::sctl):
+//   sctl[kWinTokenWord]  the guard-token count, advanced by every window build;
+//   sctl[kWinModeWord]   how the last build's row guard is formed: kGuardInFilter (the filter
+//                        launch's first block forms it as token-tagged words) or kGuardSeparate
+//                        (k_window_rowscan wrote plain doubles).  The filter follows this word,
+//                        not its own cbf_params, so a build and an advance that disagree on
+//                        CBF_LAUNCH_SEPARATE_GUARD still read the guard the build prepared.
+constexpr int kWinTokenWord = 16, kWinModeWord = 17;
+constexpr int32_t kGuardInFilter = 1, kGuardSeparate = 2;
+// a build's guard token: a 24-bit count tagged in the top byte (the guard area is the cell list's
+// record area on other paths; its words never carry the tag).  The count lives in the header, so
+// tokens keep increasing across culls and lattice shapes sharing a workspace.
 __host__ __device__ inline int32_t guard_token(int32_t v) { return (v & 0x00FFFFFF) | 0x5A000000; }
 inline size_t win_guard_bytes(int H) { return 8 * (size_t)(4l * H + 2); }  // <= 16 W H for W >= 4
 // Geometry (WinGeom, lattice_ego.hpp): candidates are the agents of window rows [cr0, cr1).  A
@@ -126,7 +135,7 @@ __global__ void __launch_bounds__(kPrepBlock) __attribute__((amdgpu_waves_per_eu
                                                             WinGuard Gd, double gain, double2* __restrict__ vel_out,
                                                             double2* __restrict__ copy_to, int32_t* __restrict__ sctl,
                                                             long ncell, unsigned long long* __restrict__ ext_keys,
-                                                            int row_begin, int row_end, ExtSpec X) {
+                                                            int row_begin, int row_end, ExtSpec X, int32_t guard_mode) {
     extern __shared__ double2 srow[];  // [W] positions, then [W] float2 {rs, rp}
     const int W = Q.W;
     float2* srsp = reinterpret_cast<float2*>(srow + W);
@@ -138,7 +147,8 @@ __global__ void __launch_bounds__(kPrepBlock) __attribute__((amdgpu_waves_per_eu
     const long nwin = (long)W * Q.rows;
     if (r == Q.cr0 && threadIdx.x == 0) {
         build_begin(sctl, nwin, ncell);
-        Gd.sync[0] = guard_token(Gd.sync[1] + 1);  // this build's guard token (not the last one formed)
+        sctl[kWinTokenWord] = (sctl[kWinTokenWord] + 1) & 0x00FFFFFF;  // this build's guard token
+        sctl[kWinModeWord] = guard_mode;
     }
     if (ext_keys && threadIdx.x == 0) arrive = 0;
     const NominalSpec N = nominal_spec(sctl);
@@ -489,7 +499,7 @@ template <bool FZ, bool ST, bool IN>
 __global__ void __launch_bounds__(kTileT) __attribute__((amdgpu_waves_per_eu((IN || ST) ? 1 : CBF_TILE_WPE))) k_window_tile(KP P, WinBounds B, WinGeom Q, int er0, int tiles_x,
                                                         const double2* __restrict__ pos,
                                                         const double2* __restrict__ u0,
-                                                        const float2* __restrict__ rsp, WinGuard Gd, bool fold,
+                                                        const float2* __restrict__ rsp, WinGuard Gd,
                                                         int32_t* __restrict__ sctl, double T,
                                                         double2* __restrict__ pos_out, double2* __restrict__ u,
                                                         int32_t* __restrict__ status, int32_t* __restrict__ cnt,
@@ -521,13 +531,12 @@ __global__ void __launch_bounds__(kTileT) __attribute__((amdgpu_waves_per_eu((IN
     // they carry the token (ld_guard), so a block that starts after the guard is formed pays no
     // extra round trip and none waits on a done word.  (Where processes time-share the GPU the
     // first block can stall for long; cbf_params.launch_flags CBF_LAUNCH_SEPARATE_GUARD then
-    // selects the separate scan kernel: fold = false.)
+    // selects the separate scan kernel: fold = false.)  The build's choice, recorded in the
+    // workspace header, decides (kWinModeWord).
     __shared__ double gred[2][kTileT / 64];
-    const int32_t token = fold ? Gd.sync[0] : 0;  // written by the build (an earlier launch)
-    if (fold && blockIdx.x == 0) {
-        row_guard_scan<kTileT, CBF_GUARD_PER, true>(Q, Gd, gred, token);
-        if (threadIdx.x == 0) Gd.sync[1] = token;  // (the next build's token follows it)
-    }
+    const bool fold = sctl[kWinModeWord] != kGuardSeparate;
+    const int32_t token = fold ? guard_token(sctl[kWinTokenWord]) : 0;  // written by the build (an earlier launch)
+    if (fold && blockIdx.x == 0) row_guard_scan<kTileT, CBF_GUARD_PER, true>(Q, Gd, gred, token);
     // stage the tile with its halo (beyond the lattice: +-inf positions, which no test passes, and
     // column extents that exclude nothing beyond the row ends)
     for (int i = threadIdx.x; i < kTileN; i += kTileT) {
@@ -703,14 +712,14 @@ void window_prep(const CellWs& Wk, const WinGeom& Q, const double2* pos, double 
                                               : k_window_prep<16>;
     hipLaunchKernelGGL(prep, dim3(Q.cr1 - Q.cr0), dim3(kPrepBlock), 24 * (size_t)Q.W, s, Q, pos, Wk.svel,
                        win_rsp(Wk), win_guard(Wk, Q.rows), gain, vel_out, copy_to, Wk.sctl, Wk.ncell, ext_keys,
-                       row_begin, row_end, X);
+                       row_begin, row_end, X, fold ? kGuardInFilter : kGuardSeparate);
     if (!fold)  // (else the filter's first block forms the row guard)
         hipLaunchKernelGGL(k_window_rowscan, dim3(1), dim3(kRowScanBlock), 0, s, Q, win_guard(Wk, Q.rows));
 }
 
 // The filter kernel of a window-cull advance of the egos of lattice rows [row_begin, row_end)
 // (statistics over rows [cnt_begin, cnt_end)); pos_out (index (r - row_begin) W + c) must not
-// overlap pos.  The queued QPs are then solved by k_lattice_filter_hard (the caller launches it
+// overlap pos.  Where the row guard comes from is the build's choice (kWinModeWord), not p's.  The queued QPs are then solved by k_lattice_filter_hard (the caller launches it
 // unless the solve is inline).
 void window_filter(const cbf_params* p, const CellWs& Wk, const WinGeom& Q, int row_begin, int row_end,
                    int cnt_begin, int cnt_end, const double2* pos, double T, double2* pos_out, double2* u,
@@ -730,11 +739,11 @@ void window_filter(const cbf_params* p, const CellWs& Wk, const WinGeom& Q, int 
     if (t_start)  // the measurement hook: events carrying the launch's own start / end (hip_ext.h)
         hipExtLaunchKernelGGL(tile, dim3((unsigned)(tiles_x * tiles_y)), dim3(kTileT), 0, s, t_start, t_stop, 0u, kp, B,
                               Q, row_begin - Q.row0, tiles_x, pos, (const double2*)Wk.svel,
-                              (const float2*)win_rsp(Wk), Gd, window_fold(p), Wk.sctl, T, pos_out, u, status, cnt, stats, Wk.hardq,
+                              (const float2*)win_rsp(Wk), Gd, Wk.sctl, T, pos_out, u, status, cnt, stats, Wk.hardq,
                               Wk.qrec, Wk.qcap);
     else
         hipLaunchKernelGGL(tile, dim3((unsigned)(tiles_x * tiles_y)), dim3(kTileT), 0, s, kp, B, Q, row_begin - Q.row0,
-                           tiles_x, pos, (const double2*)Wk.svel, (const float2*)win_rsp(Wk), Gd, window_fold(p), Wk.sctl, T, pos_out,
+                           tiles_x, pos, (const double2*)Wk.svel, (const float2*)win_rsp(Wk), Gd, Wk.sctl, T, pos_out,
                            u, status, cnt, stats, Wk.hardq, Wk.qrec, Wk.qcap);
 }
 

@@ -196,10 +196,10 @@ class HipBackend:
                                         sub.w1 - sub.w0, P(S.wpos[(sub.w0 - S.w0) * self.W:]), self.gain, P(S.vel),
                                         P(self.wss[-1]), self.ws_bytes, L.stream_handle()), "cbf_lattice_build")
 
-    def lattice_advance(self, S, mark=None):
+    def lattice_advance(self, S, mark=None, commit=True):
         L, P = self._lib, self._lib.ptr
         sub = S.subs[-1]
-        if self.cull == "window":   # (new owned positions into scratch: kernel timing, the state stays)
+        if self.cull == "window":   # new owned positions into scratch (the filter reads the window throughout)
             if getattr(self, "_own_next", None) is None:
                 self._own_next = self.torch.empty_like(S.own)
             L.check(L.lib.cbf_lattice_window_advance_ex(
@@ -208,6 +208,8 @@ class HipBackend:
                 P(S.nbr_count), P(S.stats_ptr()), P(self.wss[-1]), self.ws_bytes,
                 L.C.c_void_p(mark.cuda_event if mark is not None else 0), L.stream_handle()),
                 "cbf_lattice_window_advance_ex")
+            if commit:
+                S.own.copy_(self._own_next)
             return
         L.check(L.lib.cbf_lattice_advance_marked(
             self.cp, L.C.byref(self.grid), self.W, self.H, S.rb, S.re, sub.w0, sub.w1 - sub.w0,
@@ -244,11 +246,24 @@ class HipBackend:
         return bool(self.flag.item())
 
 
-def ranks_share_gpu(world_size):
-    """Whether this node runs more ranks than it has visible GPUs (LOCAL_WORLD_SIZE, set by
-    torchrun and by bench.py's launcher; counting devices does not initialise the GPU)."""
+def ranks_share_gpu(world_size, group=None):
+    """Whether two ranks of the group run on one GPU.  With torch.distributed initialised and a
+    GPU visible this is decided from the real placement: every rank contributes (host, the
+    device's UUID or PCI location) once, and any repeat means time-sharing (e.g. every rank of a
+    rehearsal pinned to cuda:0).  Otherwise, from the counts: this node runs more ranks
+    (LOCAL_WORLD_SIZE, set by torchrun and by bench.py's launcher) than it has visible GPUs."""
     import os
     import torch
+    import torch.distributed as dist
+    if world_size > 1 and dist.is_available() and dist.is_initialized() and torch.cuda.is_available():
+        import socket
+        dev = torch.cuda.current_device()
+        prop = torch.cuda.get_device_properties(dev)
+        where = str(getattr(prop, "uuid", "")) or \
+            f"{getattr(prop, 'pci_domain_id', 0)}:{getattr(prop, 'pci_bus_id', 0)}:{getattr(prop, 'pci_device_id', dev)}"
+        keys = [None] * dist.get_world_size(group)
+        dist.all_gather_object(keys, (socket.gethostname(), where), group=group)
+        return len(set(keys)) < len(keys)
     local = int(os.environ.get("LOCAL_WORLD_SIZE", world_size))
     return local > max(1, torch.cuda.device_count())
 
@@ -283,7 +298,7 @@ class ShardedLattice:
         # separate kernel, since a block polling for the in-launch hand-off can wait for long there
         # (cbf_params.launch_flags; results are identical)
         self.params = params or FilterParams()
-        if self.params.window_guard == "auto" and ranks_share_gpu(self.ws):
+        if self.params.window_guard == "auto" and ranks_share_gpu(self.ws, group):
             import dataclasses
             self.params = dataclasses.replace(self.params, window_guard="separate")
         if pos_global is None:
@@ -446,8 +461,13 @@ class ShardedLattice:
     def build_phase(self):
         self.be.lattice_build(self)
 
-    def advance_phase(self, mark=None):
-        self.be.lattice_advance(self, mark)
+    def advance_phase(self, mark=None, commit=True):
+        """The last sub-step's filter + clip + Euler alone (after build_phase()), the bench's kernel
+        timing.  Both culls advance the owned positions; with the window cull the new positions go
+        to a scratch tensor first (its filter reads the window throughout) and commit=False leaves
+        them there (the state stays, as LatticeSwarm.advance_phase(commit=False)); the cell list
+        writes them in place whatever commit says."""
+        self.be.lattice_advance(self, mark, commit)
 
     def capture(self):
         """Capture each sub-step's device work (cbf_lattice_step_sharded) into its own hipGraph,

@@ -37,15 +37,25 @@ enum { ST_IDLE = 0, ST_OPTIMAL = 1, ST_RELAXED = 2, ST_BOX_INFEASIBLE = 3, ST_RE
 #define ACTIVE_TOL 1e-12
 #define RELAX_CAP (1 << 16)
 
-static double dot4(const double h[4], const double v[4]) {
-    return fma(h[3], v[3], fma(h[2], v[2], fma(h[1], v[1], h[0] * v[0])));
+/* numpy's orders (OpenBLAS 0.3.29 x86_64 kernels, pinned by tests/golden; pyoracle.py header):
+ * every BLAS result is accumulated into a zeroed output, hence the "0.0 +" (never -0.0) */
+static double dot4(const double h[4], const double v[4]) { /* ddot */
+    return 0.0 + fma(h[3], v[3], fma(h[2], v[2], fma(h[1], v[1], h[0] * v[0])));
 }
 
+/* f(4x4) @ d (dgemv_t: 4 lanes, then a horizontal add) */
+static void gemv4(const double f[16], const double d[4], double fd[4]) {
+    for (int i = 0; i < 4; ++i)
+        fd[i] = 0.0 + ((f[i * 4 + 0] * d[0] + f[i * 4 + 2] * d[2]) + (f[i * 4 + 1] * d[1] + f[i * 4 + 3] * d[3]));
+}
+
+/* -hs_p @ g (dgemv_n's two-row tail) */
 static void quadrant_normal(const orc_params* p, int q, double a[2]) {
     double sx = (q & 1) ? -1.0 : 1.0, sy = (q & 2) ? -1.0 : 1.0;
     double nh[4] = {-sx, -sy, -(p->k * sx), -(p->k * sy)};
     for (int c = 0; c < 2; ++c)
-        a[c] = (nh[0] * p->g[0 * 2 + c] + nh[1] * p->g[1 * 2 + c]) + (nh[2] * p->g[2 * 2 + c] + nh[3] * p->g[3 * 2 + c]);
+        a[c] = 0.0 + ((0.0 + fma(nh[0], p->g[0 * 2 + c], nh[1] * p->g[1 * 2 + c])) +
+                      fma(nh[2], p->g[2 * 2 + c], nh[3] * p->g[3 * 2 + c]));
 }
 
 /* cbf.py:38-59 */
@@ -56,11 +66,10 @@ static double row_b(const orc_params* p, const double r[4], const double o[4], c
     double hs[4] = {sx, sy, p->k * sx, p->k * sy};
     double H = dot4(hs, d);
     double fd[4];
-    for (int i = 0; i < 4; ++i)
-        fd[i] = ((p->f[i * 4 + 0] * d[0] + p->f[i * 4 + 1] * d[1]) + p->f[i * 4 + 2] * d[2]) + p->f[i * 4 + 3] * d[3];
+    gemv4(p->f, d, fd);
     double L_f = dot4(hs, fd);
     double gu[4];
-    for (int i = 0; i < 4; ++i) gu[i] = fma(p->g[i * 2 + 0], u0[0], p->g[i * 2 + 1] * u0[1]);
+    for (int i = 0; i < 4; ++i) gu[i] = 0.0 + fma(p->g[i * 2 + 0], u0[0], p->g[i * 2 + 1] * u0[1]);
     double c = dot4(hs, gu);
     *quad = (sx < 0 ? 1 : 0) | (sy < 0 ? 2 : 0);
     return (p->gamma * (H - p->dmin) + L_f) + c;

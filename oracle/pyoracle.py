@@ -17,13 +17,18 @@ IEEE fp64 in the exact evaluation order the reference's numpy expressions use
 (orders were probed against numpy 2.2 / OpenBLAS 0.3.29 and are pinned by the
 golden fixtures):
 
-* ``hs_p @ d``             -> fma chain fma(h3,d3,fma(h2,d2,fma(h1,d1,h0*d0)))  (cbf.py:58)
-* ``-hs_p @ g``            -> pairwise (t0+t1)+(t2+t3); pinned for exact products
-                              (k a power of two or g the callers' g), else unpinned (cbf.py:56)
+* ``hs_p @ d``             -> ddot: fma chain fma(h3,d3,fma(h2,d2,fma(h1,d1,fma(h0,d0,+0))))
+                              (cbf.py:58)
+* ``-hs_p @ g``            -> dgemv_n tail: (+0 + fma(h0,g0c,h1*g1c)) + fma(h2,g2c,h3*g3c)
+                              (cbf.py:56)
 * ``g @ u0`` (gemv)        -> fma(g[r,0], u0x, g[r,1]*u0y)         (cbf.py:59)
 * ``np.dot(hs_p, g@u0)``   -> fma chain as hs_p @ d                (cbf.py:59)
-* ``f @ d`` (gemv 4x4)     -> OpenBLAS-kernel dependent: pinned only for the callers'
-                              f = 0 (every product is a signed zero); plain order otherwise
+* ``f @ d`` (gemv 4x4)     -> dgemv_t: per row (f0 d0 + f2 d2) + (f1 d1 + f3 d3), plain products
+                              (cbf.py:55)
+* every BLAS result        -> ``+0.0 + r``: BLAS accumulates into a zeroed output, so a
+                              result is never -0.0 (only the sign of a zero differs)
+The f @ d and -hs_p @ g orders are those of OpenBLAS 0.3.29's x86_64 kernels in this image
+(numpy 2.2); the golden fixtures with random f, random g and non-integer k pin them.
 * ``np.sum(X[:,j]-X[:,i,None], 1)`` -> sequential from +0.0        (cross_and_rescue.py:118,125)
 * ``v @ rotation``         -> fma(v1, R[1,c], v0*R[0,c])           (cross_and_rescue.py:118)
 """
@@ -62,8 +67,15 @@ def fma(a: float, b: float, c: float) -> float:
 
 
 def dot4(h, v):
-    """numpy int(4,) @ float(4,[1]) as measured: a sequential fma chain."""
-    return fma(h[3], v[3], fma(h[2], v[2], fma(h[1], v[1], h[0] * v[0])))
+    """numpy (4,) @ float(4,[1]) as measured (OpenBLAS ddot's scalar tail): a sequential fma
+    chain accumulated from +0.0, so the result is never -0.0."""
+    return 0.0 + fma(h[3], v[3], fma(h[2], v[2], fma(h[1], v[1], h[0] * v[0])))
+
+
+def gemv4(f, d):
+    """numpy f(4,4) @ d(4,1) as measured (OpenBLAS dgemv_t, 4 lanes then a horizontal add):
+    per row (f0 d0 + f2 d2) + (f1 d1 + f3 d3), products rounded, into a zeroed output."""
+    return [0.0 + ((f[i, 0] * d[0] + f[i, 2] * d[2]) + (f[i, 1] * d[1] + f[i, 3] * d[3])) for i in range(4)]
 
 
 def cull_threshold(safety_distance: float) -> float:
@@ -103,12 +115,14 @@ def _hs(p: Params, d0: float, d1: float):
 
 
 def quadrant_normal(p: Params, q: int):
-    """L_g = -hs_p @ g for sign quadrant q (cbf.py:56); pairwise order."""
+    """L_g = -hs_p @ g for sign quadrant q (cbf.py:56), numpy's order (OpenBLAS dgemv_n's
+    two-row tail: pairs of columns with one fma each, accumulated from +0.0)."""
     sx = -1.0 if (q & 1) else 1.0
     sy = -1.0 if (q & 2) else 1.0
     nh = (-sx, -sy, -(p.k * sx), -(p.k * sy))
     g = p.g
-    return tuple((nh[0] * g[0, c] + nh[1] * g[1, c]) + (nh[2] * g[2, c] + nh[3] * g[3, c]) for c in range(2))
+    return tuple(0.0 + ((0.0 + fma(nh[0], g[0, c], nh[1] * g[1, c])) + fma(nh[2], g[2, c], nh[3] * g[3, c]))
+                 for c in range(2))
 
 
 def assemble_row(p: Params, r, o, u0):
@@ -116,12 +130,11 @@ def assemble_row(p: Params, r, o, u0):
     d = [float(r[i]) - float(o[i]) for i in range(4)]                 # cbf.py:39
     hs, q = _hs(p, d[0], d[1])                                          # cbf.py:47-53
     H = dot4(hs, d)                                                     # hs_p @ d
-    f = p.f
-    fd = [((f[i, 0] * d[0] + f[i, 1] * d[1]) + f[i, 2] * d[2]) + f[i, 3] * d[3] for i in range(4)]
+    fd = gemv4(p.f, d)                                                  # f @ d
     L_f = dot4(hs, fd)                                                  # cbf.py:55
     a0, a1 = quadrant_normal(p, q)                                       # cbf.py:56
     g = p.g
-    gu = [fma(g[i, 0], u0[0], g[i, 1] * u0[1]) for i in range(4)]        # g @ u0
+    gu = [0.0 + fma(g[i, 0], u0[0], g[i, 1] * u0[1]) for i in range(4)]  # g @ u0
     c = dot4(hs, gu)
     b = (p.gamma * (H - p.dmin) + L_f) + c                               # cbf.py:58-59
     return a0, a1, b, q

@@ -18,6 +18,12 @@ def pytest_configure(config):
 def golden():
     import numpy as np
 
+    cache = {}
+
     def load(name):
-        return np.load(os.path.join(GOLDEN, name))
+        # decompressed once into a dict: indexing an NpzFile re-reads the member on every access
+        if name not in cache:
+            with np.load(os.path.join(GOLDEN, name)) as z:
+                cache[name] = {k: z[k] for k in z.files}
+        return cache[name]
     return load

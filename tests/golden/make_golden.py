@@ -121,11 +121,11 @@ def call(ctrl, r, obs, f, g, u0):
 # filter cases: random + adversarial
 # ----------------------------------------------------------------------------------
 def filter_cases(mod, rng):
-    cases = []  # (r, obs, u0, max_speed, dmin, k, g, tag)
+    cases = []  # (r, obs, u0, max_speed, dmin, k, g, tag, f)
 
-    def add(r, obs, u0, ms=15, dmin=0.2, k=1, g=GX, tag=0):
+    def add(r, obs, u0, ms=15, dmin=0.2, k=1, g=GX, tag=0, f=FX):
         cases.append((np.array(r, float), np.array(obs, float).reshape(-1, 4), np.array(u0, float), ms, dmin, k,
-                      np.array(g, float), tag))
+                      np.array(g, float), tag, np.array(f, float)))
 
     # tag 0: caller-shaped random cases (robot "velocity" slot = u0, cross_and_rescue.py:133)
     for _ in range(1500):
@@ -176,13 +176,49 @@ def filter_cases(mod, rng):
         add(r, obs, u0, tag=4)
     # the worked example probed in SURVEY 8c: r=(0,0,.3,-.2), two neighbours
     add([0.0, 0.0, 0.3, -0.2], [[0.1, 0.05, 0.0, 0.0], [-0.05, 0.1, 0.2, 0.1]], [0.3, -0.2], tag=5)
+    # round 5: the constructor's and get_safe_control's other inputs at non-default values
+    # (cbf.py:6 max_speed / dmin / k, cbf.py:55-59 f and g).  Own generator, so the cases above and
+    # the rollouts / consensus vectors after them keep their draws.
+    r5 = np.random.default_rng(20261018)
+    # tag 6: random dynamics f (4x4, L_f = hs_p @ (f @ d), cbf.py:55), callers' g
+    for _ in range(250):
+        m = int(r5.integers(1, 9))
+        r = list(r5.uniform(-1, 1, 2)) + list(r5.normal(0, 0.5, 2))
+        u0 = r5.normal(0, 0.5, 2)
+        obs = [list(np.array(r[:2]) + r5.normal(0, 0.1, 2)) + list(r5.normal(0, 0.5, 2)) for _ in range(m)]
+        f = r5.normal(0, 1, (4, 4)) * (10 ** r5.uniform(-2, 0.5, (4, 4)))
+        add(r, obs, u0, ms=float(r5.choice([15, 2.0])), dmin=float(r5.choice([0.2, 0.35])), f=f, tag=6)
+    # tag 7: non-integer k (hs_p a float array, cbf.py:47-53), callers' f and g
+    for _ in range(200):
+        m = int(r5.integers(1, 9))
+        r = list(r5.uniform(-1, 1, 2)) + list(r5.normal(0, 0.5, 2))
+        u0 = r5.normal(0, 0.5, 2)
+        obs = [list(np.array(r[:2]) + r5.normal(0, 0.1, 2)) + list(r5.normal(0, 0.5, 2)) for _ in range(m)]
+        add(r, obs, u0, k=float(r5.choice([0.5, 1.5, 0.7, 2.5])), dmin=float(r5.choice([0.2, 0.1])), tag=7)
+    # tag 8: everything at once -- random f and g, k in {0.5, 1.5, 2, 2.5}, other max_speed / dmin
+    # (the FilterParams the fused-path GPU tests run), plus signed-zero offsets
+    for i in range(300):
+        m = int(r5.integers(1, 11))
+        r = list(r5.uniform(-1, 1, 2)) + list(r5.normal(0, 0.5, 2))
+        u0 = r5.normal(0, 0.5, 2)
+        obs = [list(np.array(r[:2]) + r5.normal(0, 0.1, 2)) + list(r5.normal(0, 0.5, 2)) for _ in range(m)]
+        if i % 10 == 0:
+            obs[0][0] = r[0]          # dx = +0.0
+            if m > 1:
+                obs[1][1] = r[1]      # dy = +0.0
+        f = r5.normal(0, 0.5, (4, 4))
+        g = r5.normal(0, 0.3, (4, 2))
+        add(r, obs, u0, ms=float(r5.choice([15, 2.0, 0.5])), dmin=float(r5.choice([0.2, 0.35])),
+            k=float(r5.choice([0.5, 1.5, 2.0, 2.5])), g=g, f=f, tag=8)
 
-    R, OBS_OFF, OBS, U0, MS, DMIN, KK, G, TAG = [], [0], [], [], [], [], [], [], []
+    R, OBS_OFF, OBS, U0, MS, DMIN, KK, G, TAG, FF = [], [0], [], [], [], [], [], [], [], []
     A_OFF, A, B, X, U, IT = [0], [], [], [], [], []
     kkt_max = 0.0
-    for (r, obs, u0, ms, dmin, k, g, tag) in cases:
-        ctrl = mod.ControlBarrierFunction(ms, dmin=dmin, k=k)
-        Ai, bi, xi, ui, it = call(ctrl, r, obs, FX, g, u0)
+    for (r, obs, u0, ms, dmin, k, g, tag, f) in cases:
+        # k as the caller passes it: an int (hs_p an int64 array, cbf.py:47) when integral
+        ctrl = mod.ControlBarrierFunction(ms, dmin=dmin, k=int(k) if float(k).is_integer() else k)
+        Ai, bi, xi, ui, it = call(ctrl, r, obs, f, g, u0)
+        FF.append(f)
         if it == 0:
             kkt_max = max(kkt_max, qp_bruteforce.kkt_residual(Ai, bi, xi))
         IT.append(it)
@@ -194,6 +230,7 @@ def filter_cases(mod, rng):
     assert kkt_max < 1e-9
     return dict(r=np.array(R), obs=np.vstack(OBS), obs_off=np.array(OBS_OFF), u0=np.array(U0),
                 max_speed=np.array(MS, float), dmin=np.array(DMIN), k=np.array(KK, float), g=np.array(G),
+                f=np.array(FF),
                 tag=np.array(TAG), A=np.vstack(A), b=np.concatenate(B), ab_off=np.array(A_OFF),
                 x=np.array(X), u=np.array(U), relax_iters=np.array(IT))
 

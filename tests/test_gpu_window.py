@@ -15,26 +15,29 @@ if not torch.cuda.is_available():  # collected on CPU boxes but never run there
 
 from cbf_amd import scenarios, swarm  # noqa: E402
 from oracle import coracle, pyoracle as po  # noqa: E402
+from tests import paramsets  # noqa: E402
 
 GAIN = 0.25
 
 
-def _oracle_rollout(pos, W, H, steps):
+def _oracle_rollout(pos, W, H, steps, pset="callers"):
     ref = pos.copy()
     outs = []
+    p = paramsets.oracle_params(pset)
     for _ in range(steps):
         vel = coracle.consensus_lattice(W, H, 0, H, ref, GAIN)
-        out = coracle.filter_swarm(po.Params(15), ref, vel, 0)
+        out = coracle.filter_swarm(p, ref, vel, 0)
         ref = coracle.euler(ref, out["u"], 1 / 30)
         outs.append((vel, out, ref.copy()))
     return outs
 
 
-def _check_steps(pos, W, H, steps, placement="auto", equal_nan=False):
+def _check_steps(pos, W, H, steps, placement="auto", equal_nan=False, pset="callers"):
     """step() of the window cull and of the cell list, every timestep against the oracle."""
-    runs = [swarm.LatticeSwarm(pos, W, H, gain=GAIN, params=swarm.FilterParams(solve_placement=placement), cull=c)
+    runs = [swarm.LatticeSwarm(pos, W, H, gain=GAIN, params=paramsets.filter_params(pset, solve_placement=placement),
+                               cull=c)
             for c in ("window", "cells")]
-    for t, (vel, out, ref) in enumerate(_oracle_rollout(pos, W, H, steps)):
+    for t, (vel, out, ref) in enumerate(_oracle_rollout(pos, W, H, steps, pset)):
         for L in runs:
             L.step()
             torch.cuda.synchronize()
@@ -47,11 +50,13 @@ def _check_steps(pos, W, H, steps, placement="auto", equal_nan=False):
     return runs
 
 
+@pytest.mark.parametrize("pset", paramsets.NAMES)
 @pytest.mark.parametrize("placement", ["inline", "queued"])
-def test_window_scrambled_lattice_vs_oracle(placement):
+def test_window_scrambled_lattice_vs_oracle(placement, pset):
     """Agents swapped with far-away ones (a lattice index no longer says where an agent is), so
     the row and column guards fail for their neighbours and those egos walk their rows outward;
-    plus coincident agents (s = 0: not neighbours) and an exact-cutoff pair."""
+    plus coincident agents (s = 0: not neighbours) and an exact-cutoff pair.  pset: the callers'
+    parameters or others (tests/paramsets.py; the 0.3 cull radius reaches beyond the staged tile)."""
     W, H = 64, 48
     pos = scenarios.lattice(W, H, seed=21)
     rng = np.random.default_rng(4)
@@ -60,7 +65,7 @@ def test_window_scrambled_lattice_vs_oracle(placement):
     pos[a], pos[b] = pos[b].copy(), pos[a].copy()
     pos[100] = pos[101]                        # coincident pair
     pos[300] = pos[301] + np.array([0.2, 0.0])  # s == 0.04 exactly is out (sqrt(s) < 0.2 fails)
-    _check_steps(pos, W, H, 5, placement)
+    _check_steps(pos, W, H, 5, placement, pset=pset)
 
 
 def test_window_dense_clump_overflows_hit_list():
@@ -246,3 +251,61 @@ def test_window_separate_guard_equals_in_filter():
         res.append([t.cpu().numpy() for t in (L.pos, L.vel, L.u, L.status, L.nbr_count)])
     for x, y in zip(*res):
         assert np.array_equal(x, y)
+
+
+@pytest.mark.parametrize("build_guard,advance_guard", [("in_filter", "separate"), ("separate", "in_filter")])
+def test_window_guard_mode_follows_the_build(build_guard, advance_guard):
+    """A build and an advance whose cbf_params disagree on CBF_LAUNCH_SEPARATE_GUARD: the filter
+    follows the build's choice recorded in the workspace header (window.hip kWinModeWord), so it
+    never reads the other form's words (token-tagged fp32 words left by an earlier in-filter
+    timestep read as doubles would drop neighbours).  Every timestep equals the cell list's."""
+    W, H = 64, 48
+    pos = scenarios.lattice(W, H, seed=31)
+    rng = np.random.default_rng(8)
+    a, b = rng.choice(W * H, 30, replace=False), rng.choice(W * H, 30, replace=False)
+    pos[a], pos[b] = pos[b].copy(), pos[a].copy()
+    A = swarm.LatticeSwarm(pos, W, H, gain=GAIN, params=swarm.FilterParams(window_guard=advance_guard), cull="window")
+    B = swarm.LatticeSwarm(pos, W, H, gain=GAIN, cull="cells")
+    cp_build = swarm.FilterParams(window_guard=build_guard).c()
+    cp_adv = A.cp
+    for t in range(4):
+        if t % 2 == 0:
+            A.step()                  # both phases in the advance's mode: its words stay in the area
+        else:
+            A.cp = cp_build
+            A.build_phase()
+            A.cp = cp_adv
+            A.advance_phase()
+        B.step()
+        torch.cuda.synchronize()
+        for x, y in ((A.pos, B.pos), (A.u, B.u), (A.status, B.status), (A.nbr_count, B.nbr_count)):
+            assert torch.equal(x, y), t
+
+
+@pytest.mark.parametrize("guard", ["in_filter", "separate"])
+@pytest.mark.parametrize("W,H", [(16, 1100), (2048, 6)])
+def test_window_many_rows_and_widest_rows(W, H, guard):
+    """More than 1,024 candidate rows (the row-guard scans run several chunks: 1,024 rows per
+    chunk in both the in-filter and the separate form) and the widest rows the window cull takes
+    (k_window_prep's 8-column-per-thread instantiation): every timestep equals the cell list's
+    and, for the tall lattice, the oracle's."""
+    pos = scenarios.lattice(W, H, seed=32, spacing=0.15)
+    fp = swarm.FilterParams(window_guard=guard)
+    A = swarm.LatticeSwarm(pos, W, H, gain=GAIN, params=fp, cull="window")
+    B = swarm.LatticeSwarm(pos, W, H, gain=GAIN, cull="cells")
+    ref = pos.copy()
+    for t in range(3):
+        A.step()
+        B.step()
+        torch.cuda.synchronize()
+        for x, y in ((A.pos, B.pos), (A.u, B.u), (A.status, B.status), (A.nbr_count, B.nbr_count)):
+            assert torch.equal(x, y), t
+        if W == 16:
+            vel = coracle.consensus_lattice(W, H, 0, H, ref, GAIN)
+            out = coracle.filter_swarm(po.Params(15), ref, vel, 0)
+            ref = coracle.euler(ref, out["u"], 1 / 30)
+            assert np.array_equal(A.u.cpu().numpy(), out["u"]) and np.array_equal(A.pos.cpu().numpy(), ref), t
+    A.run(3)
+    B.run(3)
+    torch.cuda.synchronize()
+    assert torch.equal(A.pos, B.pos)

@@ -10,7 +10,7 @@ from tests.golden import qp_bruteforce
 
 def _cases(F):
     for i in range(len(F["r"])):
-        p = po.Params(F["max_speed"][i], F["dmin"][i], F["k"][i], g=F["g"][i])
+        p = po.Params(F["max_speed"][i], F["dmin"][i], F["k"][i], g=F["g"][i], f=F["f"][i])
         obs = F["obs"][F["obs_off"][i]:F["obs_off"][i + 1]]
         A0 = F["A"][F["ab_off"][i]:F["ab_off"][i + 1]]
         b0 = F["b"][F["ab_off"][i]:F["ab_off"][i + 1]]
@@ -28,7 +28,22 @@ def test_assembly_bit_exact_vs_reference(golden, impl):
         assert np.array_equal(A, A0), i
         assert np.array_equal(b, b0), i
         n += 1
-    assert n == len(F["r"]) > 2000
+    assert n == len(F["r"]) > 2900
+
+
+def test_golden_covers_the_reference_parameters(golden):
+    """The fixtures exercise every input of ControlBarrierFunction (cbf.py:6) and of
+    get_safe_control's rows (cbf.py:55-59) away from the callers' defaults: random f (L_f),
+    random g, non-integer k, other dmin / max_speed -- and both at once."""
+    F = golden("golden_filter.npz")
+    fz = np.abs(F["f"]).reshape(len(F["r"]), -1).max(axis=1) == 0
+    kint = F["k"] == np.round(F["k"])
+    gdef = np.all(F["g"] == 0.1 * np.array([[1, 0], [0, 1], [0, 0], [0, 0]]), axis=(1, 2))
+    assert (~fz).sum() >= 500 and (~kint).sum() >= 400 and (~gdef).sum() >= 450
+    both = ~fz & ~kint & ~gdef & (F["dmin"] != 0.2)
+    assert both.sum() >= 100
+    # and the non-default cases include infeasible (relaxed) QPs and binding minimisers
+    assert (F["relax_iters"][~fz] > 0).sum() > 50 and (np.abs(F["x"][~fz]).max(axis=1) > 0).sum() > 50
 
 
 @pytest.mark.parametrize("impl", ["py", "c"])

@@ -51,6 +51,9 @@ def _work(rank, ws, port, W, R, steps, q, k, graph, run, nominal, exchange, plac
     S = ShardedLattice(W, R, seed=7, substeps=k, nominal=nominal, spacing=_spacing(nominal),
                        halo=4 if nominal is None else 10, exchange=exchange,
                        params=FilterParams(solve_placement=placement), cull=cull)
+    # every rank here is pinned to cuda:0 (LOCAL_WORLD_SIZE unset): the placement check sees it and
+    # picks the separate row-guard kernel for the window cull
+    assert S.params.window_guard == ("separate" if ws > 1 else "auto")
     if graph == "cycle":   # whole exchange cycles replayed as one hipGraph each
         S.capture_cycle()
     elif graph:
