@@ -258,7 +258,7 @@ def full_size_check(S, args):
             "max_relaxations": int((st >> 8).max().item())}
 
 
-def safety_report(st, steps):
+def safety_report(st, steps, agents=None):
     """The rollout's safety and parity record from the device statistics of the timed steps
     (include/cbf_amd.h CBF_STAT_*).  feasible_fraction = OPTIMAL solves / solves: the share whose
     output the reference defines (an exact QP minimiser; cvxopt's iterate for an infeasible QP is
@@ -274,6 +274,9 @@ def safety_report(st, steps):
             "max_violation_optimal": st["viol_optimal"],
             "max_violation_original_rows_relaxed": st["viol_original_relaxed"],
             "min_pairwise_distance": None if d2 is None else float(np.sqrt(d2)),
+            # the window cull's degradation (CBF_STAT_WIN_WALKS / GUARD_STALLS; 0 under the cell list)
+            "window_walk_fraction": None if not agents else st.get("win_walks", 0) / (agents * steps),
+            "window_guard_stall_words": st.get("guard_stalls", 0),
             "min_pairwise_distance_note": "over neighbour pairs the reference culls (0 < d < 0.2, "
                                           "cross_and_rescue.py:147-150); None = no pair closer than 0.2"}
 
@@ -436,7 +439,12 @@ def bench_lattice(args, ws, rank, local):
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         return float(t[0])
 
+    # the window cull's degradation counters (workspace header, counted whatever collect_stats says)
+    # around the timed steps themselves: egos that walked, guard words read at their spin limit
+    wc = hasattr(S, "window_counters") and S.cull == "window"
+    wc0 = S.window_counters() if wc else None
     elapsed = max_over_ranks(timed())
+    wc1 = S.window_counters() if wc else None
     progress(f"{args.config}: timed region done ({elapsed / args.steps * 1e6:.1f} us/step); replays")
     own = S.own if sharded else S.pos
     end_state = (own.clone(), S.u.clone(), S.status.clone())
@@ -494,7 +502,14 @@ def bench_lattice(args, ws, rank, local):
         stat.update({k: int(v) for k, v in zip(keys, c.tolist())})
         stat.update(viol_optimal=float(m[0]), viol_original_relaxed=float(m[1]),
                     min_dist2=None if not np.isfinite(m[2].item()) else -float(m[2]))
-    safety = safety_report(stat, args.steps) if args.barrier == "reference" else None
+    safety = safety_report(stat, args.steps, n_total) if args.barrier == "reference" else None
+    window_cull = None
+    if wc:
+        window_cull = {"walk_fraction": (wc1[0] - wc0[0]) / (n_local * args.steps),
+                       "guard_stall_words": wc1[1] - wc0[1],
+                       "note": "over the timed steps: egos per timestep that took the unbounded row walk, and "
+                               "row-guard words read at their spin limit (cbf_lattice_window_counters); both "
+                               "stay exact, both say the swarm has left the window cull's fast path"}
     exchange = None
     if sharded:
         # each rank's exchange (pack + collective + unpack with the guard), timed alone after the
@@ -609,6 +624,7 @@ def bench_lattice(args, ws, rank, local):
         "exchange": exchange,
         "feasible_fraction": safety["feasible_fraction"] if safety else None,
         "safety": safety,
+        "window_cull": window_cull,
         "full_size_check": check,
         "status_fraction_last_step": {"idle": codes[0] / len(status), "optimal": codes[1] / len(status),
                                       "relaxed": codes[2] / len(status),

@@ -15,7 +15,7 @@ PKG = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(PKG, "libcbf_amd.so")
 
 CBF_EINVAL = -1
-ABI_VERSION = 6  # include/cbf_amd.h CBF_ABI_VERSION
+ABI_VERSION = 7  # include/cbf_amd.h CBF_ABI_VERSION
 STATUS_IDLE, STATUS_OPTIMAL, STATUS_RELAXED, STATUS_BOX_INFEASIBLE, STATUS_RELAX_CAP = 0, 1, 2, 3, 4
 STATUS_NBR_OVERFLOW = 5
 STATUS_WORKSPACE_ERROR = 6
@@ -24,7 +24,7 @@ RUN_WINDOW_CULL = 2
 LAUNCH_SEPARATE_GUARD = 1  # cbf_params.launch_flags (include/cbf_amd.h CBF_LAUNCH_*)
 # words of a lattice-step statistics slot (include/cbf_amd.h CBF_STAT_*)
 (STAT_SOLVES, STAT_OPTIMAL, STAT_RELAXED, STAT_INFEASIBLE, STAT_SEIDEL, STAT_VIOL_OPTIMAL, STAT_VIOL_ORIGINAL,
- STAT_MIN_DIST2, STAT_ERRORS, STAT_BINDING) = range(10)
+ STAT_MIN_DIST2, STAT_ERRORS, STAT_BINDING, STAT_WIN_WALKS, STAT_GUARD_STALLS) = range(12)
 _DIST_KEY_TOP = 0x7FF0000000000000
 
 
@@ -105,6 +105,7 @@ SIGNATURES = {
     "cbf_lattice_window_advance_ex": (C.c_int, [_P, _G, _i32, _i32, _i32, _i32, _i32, _i32, _vp, _d, _vp, _vp, _vp,
                                                 _vp, _vp, _vp, _sz, _vp, _vp]),
     "cbf_lattice_window_build": (C.c_int, [_P, _G, _i32, _i32, _vp, _d, _vp, _vp, _sz, _vp]),
+    "cbf_lattice_window_counters": (C.c_int, [_vp, _sz, _vp, _vp]),
     "cbf_lattice_window_advance": (C.c_int, [_P, _G, _i32, _i32, _vp, _d, _vp, _vp, _vp, _vp, _vp, _vp, _sz, _vp,
                                              _vp]),
     "cbf_lattice_build": (C.c_int, [_P, _G, _i32, _i32, _i32, _i32, _i32, _i32, _vp, _d, _vp, _vp, _sz, _vp]),
@@ -187,7 +188,8 @@ def decode_stats(words) -> dict:
     cnt = {k: int(w[:, i].sum()) for k, i in (("solves", STAT_SOLVES), ("optimal", STAT_OPTIMAL),
                                                ("relaxed", STAT_RELAXED), ("infeasible", STAT_INFEASIBLE),
                                                ("seidel", STAT_SEIDEL), ("errors", STAT_ERRORS),
-                                               ("binding", STAT_BINDING))}
+                                               ("binding", STAT_BINDING), ("win_walks", STAT_WIN_WALKS),
+                                               ("guard_stalls", STAT_GUARD_STALLS))}
     vo = w[:, STAT_VIOL_OPTIMAL].max().reshape(1).view(np.float64)[0]
     vr = w[:, STAT_VIOL_ORIGINAL].max().reshape(1).view(np.float64)[0]
     key = int(w[:, STAT_MIN_DIST2].max())

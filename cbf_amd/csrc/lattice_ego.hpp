@@ -247,6 +247,7 @@ bool window_cull_ok(int W, int rows, long n_ws, const CellWs& Wk);
 // the window cull's row guard formed inside the filter launch (else by a separate scan kernel
 // launched with the build): cbf_params.launch_flags
 bool window_fold(const cbf_params* p);
+int window_counters(const void* workspace, size_t workspace_bytes, uint64_t* out, hipStream_t s);
 void window_prep(const CellWs& Wk, const WinGeom& Q, const double2* pos, double gain, double2* vel_out,
                  double2* copy_to, unsigned long long* ext_keys, int row_begin, int row_end, ExtSpec X,
                  bool fold, hipStream_t s);

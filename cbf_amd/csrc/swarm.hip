@@ -920,6 +920,11 @@ extern "C" int cbf_lattice_window_advance_timed(const cbf_params* p, const cbf_g
                           workspace_bytes, (hipEvent_t)filter_stop, (hipEvent_t)filter_start, stream);
 }
 
+extern "C" int cbf_lattice_window_counters(const void* workspace, size_t workspace_bytes, uint64_t* out,
+                                           void* stream) {
+    return window_counters(workspace, workspace_bytes, out, (hipStream_t)stream);
+}
+
 extern "C" int cbf_lattice_window_build(const cbf_params* p, const cbf_grid* grid, int32_t W, int32_t H,
                                         const double* pos, double gain, double* vel_out, void* workspace,
                                         size_t workspace_bytes, void* stream) {

@@ -73,7 +73,12 @@ inline WinGuard win_guard(const CellWs& Wk, int H) {
 //                        (k_window_rowscan wrote plain doubles).  The filter follows this word,
 //                        not its own cbf_params, so a build and an advance that disagree on
 //                        CBF_LAUNCH_SEPARATE_GUARD still read the guard the build prepared.
-constexpr int kWinTokenWord = 16, kWinModeWord = 17;
+//   sctl[kWinWalkWord]   (uint64) egos that took the unbounded walk (win_direct), and
+//   sctl[kWinStallWord]  (uint64) row-guard words read at their spin limit (as the worst bound),
+//                        both accumulated by every window filter since the workspace was zero-filled
+//                        (cbf_lattice_window_counters): the cull stays exact either way, these say
+//                        how far it has degraded from its lattice-neighbour fast path.
+constexpr int kWinTokenWord = 16, kWinModeWord = 17, kWinWalkWord = 20, kWinStallWord = 22;
 constexpr int32_t kGuardInFilter = 1, kGuardSeparate = 2;
 // a build's guard token: a 24-bit count tagged in the top byte (the guard area is the cell list's
 // record area on other paths; its words never carry the tag).  The count lives in the header, so
@@ -393,14 +398,21 @@ __global__ void __launch_bounds__(kRowScanBlock) k_window_rowscan(WinGeom Q, Win
 // sylo, +inf for pyhi: every row a candidate row, so the windows only grow and stay complete).
 // fp32 values rounded outward (sylo down, pyhi up) are sound bounds likewise.  Not packed: the
 // double k_window_rowscan wrote (an earlier launch).
-__device__ __forceinline__ double ld_guard(const double* p, bool packed, int32_t token, double worst) {
+// `stalls` counts the words read at the spin limit (kWinStallWord, CBF_STAT_GUARD_STALLS).
+__device__ __forceinline__ double ld_guard(const double* p, bool packed, int32_t token, double worst, int& stalls) {
     if (!packed) return *p;
-    if (CBF_WIN_SPIN_LIMIT < 0) return worst;  // (test build tests/_lib/libcbf_winnowait.so)
+    if (CBF_WIN_SPIN_LIMIT < 0) {  // (test build tests/_lib/libcbf_winnowait.so)
+        ++stalls;
+        return worst;
+    }
     const unsigned long long* q = reinterpret_cast<const unsigned long long*>(p);
     for (long spins = 0;; ++spins) {
         const unsigned long long w = __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if ((int32_t)(w >> 32) == token) return (double)__uint_as_float((unsigned)w);
-        if (spins >= CBF_WIN_SPIN_LIMIT) return worst;
+        if (spins >= CBF_WIN_SPIN_LIMIT) {
+            ++stalls;
+            return worst;
+        }
         __builtin_amdgcn_s_sleep(1);
     }
 }
@@ -412,12 +424,12 @@ __device__ __forceinline__ double ld_guard(const double* p, bool packed, int32_t
 constexpr int kWinPre = 4;
 __device__ __forceinline__ void win_rows(const KP& P, const double* __restrict__ sylo,
                                          const double* __restrict__ pyhi, int r, int lo, int H, double y, int& Kd,
-                                         int& Ku, bool packed, int32_t token) {
+                                         int& Ku, bool packed, int32_t token, int& stalls) {
     double su[kWinPre], pd[kWinPre];
 #pragma unroll
     for (int k = 0; k < kWinPre; ++k) {
-        su[k] = r + k + 1 < H ? ld_guard(sylo + r + k + 1, packed, token, -INFINITY) : INFINITY;  // beyond: none
-        pd[k] = r - k - 1 >= lo ? ld_guard(pyhi + r - k - 1, packed, token, INFINITY) : -INFINITY;
+        su[k] = r + k + 1 < H ? ld_guard(sylo + r + k + 1, packed, token, -INFINITY, stalls) : INFINITY;  // beyond: none
+        pd[k] = r - k - 1 >= lo ? ld_guard(pyhi + r - k - 1, packed, token, INFINITY, stalls) : -INFINITY;
     }
     Ku = 0;
     Kd = 0;
@@ -427,9 +439,9 @@ __device__ __forceinline__ void win_rows(const KP& P, const double* __restrict__
         Kd += !(y - pd[k] > P.win_d) ? 1 : 0;
     }
     if (Ku == kWinPre)
-        while (r + Ku + 1 < H && !(ld_guard(sylo + r + Ku + 1, packed, token, -INFINITY) - y > P.win_d)) ++Ku;
+        while (r + Ku + 1 < H && !(ld_guard(sylo + r + Ku + 1, packed, token, -INFINITY, stalls) - y > P.win_d)) ++Ku;
     if (Kd == kWinPre)
-        while (r - Kd - 1 >= lo && !(y - ld_guard(pyhi + r - Kd - 1, packed, token, INFINITY) > P.win_d)) ++Kd;
+        while (r - Kd - 1 >= lo && !(y - ld_guard(pyhi + r - Kd - 1, packed, token, INFINITY, stalls) > P.win_d)) ++Kd;
 }
 
 // 32-bit byte offsets into the lattice-ordered arrays (windows of < 2^28 agents, check_lattice)
@@ -554,10 +566,11 @@ __global__ void __launch_bounds__(kTileT) __attribute__((amdgpu_waves_per_eu((IN
             L.g[i] = make_float2(INFINITY, -INFINITY);
         }
     }
+    int stalls = 0;
     if (threadIdx.x < kTileGuard) {
         const int a = r0 + 1 + threadIdx.x, b = r0 - kWinPre + threadIdx.x;
-        L.sy[threadIdx.x] = a < Q.cr1 ? ld_guard(sylo + a, fold, token, -INFINITY) : INFINITY;
-        L.py[threadIdx.x] = b >= Q.cr0 ? ld_guard(pyhi + b, fold, token, INFINITY) : -INFINITY;
+        L.sy[threadIdx.x] = a < Q.cr1 ? ld_guard(sylo + a, fold, token, -INFINITY, stalls) : INFINITY;
+        L.py[threadIdx.x] = b >= Q.cr0 ? ld_guard(pyhi + b, fold, token, INFINITY, stalls) : -INFINITY;
     }
     __syncthreads();
     const bool act = inside && w >= B.own_lo && w < B.own_hi;
@@ -616,6 +629,7 @@ __global__ void __launch_bounds__(kTileT) __attribute__((amdgpu_waves_per_eu((IN
             }
         }
     }
+    const unsigned long long m_walk = __ballot(act && fin && slow);  // egos taking win_direct below
     EgoOut O;
     O.res = 0;
     O.w = -1;
@@ -677,13 +691,31 @@ __global__ void __launch_bounds__(kTileT) __attribute__((amdgpu_waves_per_eu((IN
             }
         } else if (fin) {  // the unbounded form, over the full row window (beyond the staged halo too)
             int kd, ku;
-            win_rows(P, sylo, pyhi, r, Q.cr0, Q.cr1, E.r1, kd, ku, fold, token);
+            win_rows(P, sylo, pyhi, r, Q.cr0, Q.cr1, E.r1, kd, ku, fold, token, stalls);
             win_direct<FZ>(P, E, w, r, c, W, kd, ku, pos, u0, rsp, d2);
         }
         O.nbrs = E.count;
         if (ST) O.d2 = d2;
         ego_finish<FZ, ST, IN>(P, E, (int)w, (int)(w - B.own_lo), (int)w, T, pos_out, u, status, cnt, hardq,
                                bx % kSubQ, qrec + (long)(bx % kSubQ) * qcap, O);
+    }
+    // degradation counters (every instantiation; rare, so one wave-aggregated atomic each when
+    // they occur): walks and guard words read at their spin limit, into the workspace header and,
+    // with statistics, the CBF_STAT_WIN_WALKS / CBF_STAT_GUARD_STALLS words
+    if (m_walk | __ballot(stalls > 0)) {
+        int ns = stalls;
+        for (int o = 32; o > 0; o >>= 1) ns += __shfl_xor(ns, o, 64);
+        if (lane == 0) {
+            const unsigned long long nw = (unsigned long long)__popcll(m_walk);
+            unsigned long long* hdr = reinterpret_cast<unsigned long long*>(sctl);
+            if (nw) atomicAdd(&hdr[kWinWalkWord / 2], nw);
+            if (ns) atomicAdd(&hdr[kWinStallWord / 2], (unsigned long long)ns);
+            if (ST && stats) {
+                unsigned long long* sl = stats + 16 * stat_slot((long)bx * kTileR + wv);
+                if (nw) atomicAdd(&sl[CBF_STAT_WIN_WALKS], nw);
+                if (ns) atomicAdd(&sl[CBF_STAT_GUARD_STALLS], (unsigned long long)ns);
+            }
+        }
     }
     if (ST && stats) {
         const bool counted = O.res != 0 && O.w >= B.cnt_lo && O.w < B.cnt_hi;
@@ -702,6 +734,14 @@ bool window_cull_ok(int W, int rows, long n_ws, const CellWs& Wk) {
 }
 
 bool window_fold(const cbf_params* p) { return !(p->launch_flags & CBF_LAUNCH_SEPARATE_GUARD); }
+
+// the two degradation counters of a workspace's header (kWinWalkWord, kWinStallWord)
+int window_counters(const void* workspace, size_t workspace_bytes, uint64_t* out, hipStream_t s) {
+    if (!workspace || workspace_bytes < 256 || !out) return CBF_EINVAL;
+    const uint64_t* hdr = reinterpret_cast<const uint64_t*>(workspace);
+    if (hipError_t e = hipMemcpyAsync(out, hdr + kWinWalkWord / 2, 8, hipMemcpyDefault, s)) return (int)e;
+    return (int)hipMemcpyAsync(out + 1, hdr + kWinStallWord / 2, 8, hipMemcpyDefault, s);
+}
 
 void window_prep(const CellWs& Wk, const WinGeom& Q, const double2* pos, double gain, double2* vel_out,
                  double2* copy_to, unsigned long long* ext_keys, int row_begin, int row_end, ExtSpec X,

@@ -282,18 +282,30 @@ class LatticeSwarm:
     cbf_lattice_step (nominal + cell list + filter + clip + Euler); optionally captured in a
     hipGraph.  Single-GPU: the window is the whole lattice."""
 
+    # cull="auto": the share of egos per timestep that took the window cull's unbounded walk above
+    # which the swarm switches to the cell list, and how many timesteps pass between looks
+    AUTO_WALK_FRACTION = 0.01
+    AUTO_CHECK_STEPS = 8
+
     def __init__(self, pos, W, H, gain=0.25, params: FilterParams = None, T=1 / 30, grid=None, margin=1.0,
                  method="cells", barrier="reference", alpha=(1.0, 1.0), nominal=None, cull="cells"):
         torch = _lib.require_gpu()
         # cull (reference barrier, cell method): "cells" = the cell-list cull rebuilt every timestep;
         # "window" = the lattice-window cull (include/cbf_amd.h CBF_RUN_WINDOW_CULL: candidates are the
         # lattice neighbours, guards prove the rest out of range; bit-identical results, no cell-list
-        # build -- fast while the swarm stays lattice-like, e.g. under consensus)
-        if cull not in ("cells", "window"):
-            raise ValueError(f"cull must be 'cells' or 'window', got {cull!r}")
-        if cull == "window" and (method != "cells" or barrier != "reference" or not 4 <= W <= 2048):
+        # build -- fast while the swarm stays lattice-like, e.g. under consensus); "auto" = the window
+        # cull while it stays on its fast path, the cell list (for the rest of the rollout) once more
+        # than AUTO_WALK_FRACTION of the egos per timestep had to walk (cbf_lattice_window_counters,
+        # read without blocking every AUTO_CHECK_STEPS timesteps).  Results are identical whichever runs.
+        if cull not in ("cells", "window", "auto"):
+            raise ValueError(f"cull must be 'cells', 'window' or 'auto', got {cull!r}")
+        window_ok = method == "cells" and barrier == "reference" and 4 <= W <= 2048
+        if cull == "window" and not window_ok:
             raise ValueError("the window cull needs the reference barrier, method='cells' and 4 <= W <= 2048")
-        self.cull = cull
+        self.cull_mode = cull
+        self.cull = "window" if cull == "window" or (cull == "auto" and window_ok) else "cells"
+        self._auto = None if cull != "auto" or self.cull != "window" else \
+            {"steps": 0, "base": (0, 0), "pending": None, "host": torch.zeros(2, dtype=torch.int64, pin_memory=True)}
         self.dev = torch.device("cuda")
         pos = np.asarray(pos, dtype=np.float64).reshape(W * H, 2)
         self.W, self.H, self.gain, self.T = W, H, float(gain), float(T)
@@ -394,11 +406,51 @@ class LatticeSwarm:
         cross_and_rescue.py:159-160) in the arrays of history(steps) instead of the last one only."""
         if self.method != "cells" or self.barrier != "reference":
             raise ValueError("run() is the fused multi-step path of the reference barrier (cell method)")
-        g = self.run_graphs.get((steps, self.collect_stats, history))
+        g = self.run_graphs.get((steps, self.collect_stats, history, self.cull))
         if g is not None:
             g.replay()
         else:
             self._launch_run(steps, history)
+        self._auto_check(steps)
+
+    def window_counters(self):
+        """(egos that took the window cull's unbounded walk, row-guard words read at their spin limit)
+        accumulated in this swarm's workspace (cbf_lattice_window_counters; synchronises the stream).
+        Both stay 0 under the cell list."""
+        torch = _lib.require_gpu()
+        out = torch.zeros(2, dtype=torch.int64, pin_memory=True)
+        check(lib.cbf_lattice_window_counters(ptr(self.ws), self.ws_bytes, ptr(out), stream_handle()),
+              "cbf_lattice_window_counters")
+        torch.cuda.current_stream().synchronize()
+        return int(out[0]), int(out[1])
+
+    def _auto_check(self, steps):
+        """cull="auto": every AUTO_CHECK_STEPS timesteps queue a copy of the window counters behind the
+        work (pinned host memory, an event); once a copy has landed (polled, never waited for), switch
+        to the cell list if the walks per ego and timestep since the previous look exceed
+        AUTO_WALK_FRACTION."""
+        A = self._auto
+        if A is None or self.cull != "window":
+            return
+        A["steps"] += steps
+        pend = A["pending"]
+        if pend is not None and pend[0].query():
+            walks, stalls = int(A["host"][0]), int(A["host"][1])
+            frac = (walks - A["base"][0]) / max(1, pend[1] * self.n)
+            A["base"], A["pending"] = (walks, stalls), None
+            A["last_fraction"] = frac
+            if frac > self.AUTO_WALK_FRACTION:
+                self.cull = "cells"
+                A["switched_after"] = A["steps"]
+                return
+        if A["pending"] is None and A["steps"] >= self.AUTO_CHECK_STEPS:
+            import torch
+            check(lib.cbf_lattice_window_counters(ptr(self.ws), self.ws_bytes, ptr(A["host"]), stream_handle()),
+                  "cbf_lattice_window_counters")
+            ev = torch.cuda.Event()
+            ev.record()
+            A["pending"] = (ev, A["steps"])
+            A["steps"] = 0
 
     def history(self, steps):
         """The per-timestep outputs of the last run(steps, history=True): (vel, u, status,
@@ -486,8 +538,9 @@ class LatticeSwarm:
 
     def capture(self, steps=None, history=False):
         """Capture one step (replayed by step()) or, with `steps`, one run(steps, history) call
-        (replayed by run(steps, history); one graph per step count) into a hipGraph.  The warm-up
-        launch outside the capture advances the swarm."""
+        (replayed by run(steps, history); one graph per step count) into a hipGraph, for the cull
+        in use (cull="auto" replays it only while that cull is).  The warm-up launch outside the
+        capture advances the swarm."""
         import torch
         launch = self._launch if steps is None else (lambda: self._launch_run(steps, history))
         s = torch.cuda.Stream()
@@ -500,9 +553,9 @@ class LatticeSwarm:
         with torch.cuda.graph(g):
             launch()
         if steps is None:
-            self.graphs[self.collect_stats] = g
+            self.graphs[(self.collect_stats, self.cull)] = g
         else:
-            self.run_graphs[(steps, self.collect_stats, history)] = g
+            self.run_graphs[(steps, self.collect_stats, history, self.cull)] = g
         return g
 
     def snapshot(self) -> list:
@@ -534,6 +587,7 @@ class LatticeSwarm:
                 "ws_bytes": int(self.ws_bytes),
                 "W": self.W, "H": self.H, "gain": self.gain, "T": self.T, "method": self.method,
                 "barrier": self.barrier, "alpha": list(self.alpha), "nominal": self.nominal, "cull": self.cull,
+                "cull_mode": self.cull_mode,
                 "grid": [self.grid.x0, self.grid.y0, self.grid.inv_h, self.grid.nx, self.grid.ny],
                 "params": {"max_speed": self.params.max_speed, "dmin": self.params.dmin, "k": self.params.k,
                            "safety_distance": self.params.safety_distance,
@@ -567,7 +621,10 @@ class LatticeSwarm:
         nominal = meta["nominal"]
         S = cls(states[0], meta["W"], meta["H"], gain=meta["gain"], params=params, T=meta["T"], grid=g,
                 method=meta["method"], barrier=meta["barrier"], alpha=tuple(meta["alpha"]),
-                nominal=tuple(nominal) if isinstance(nominal, list) else nominal, cull=meta.get("cull", "cells"))
+                nominal=tuple(nominal) if isinstance(nominal, list) else nominal,
+                # cull="auto" resumes with the cull the saved swarm had reached
+                cull="auto" if meta.get("cull_mode") == "auto" and meta.get("cull") == "window"
+                else meta.get("cull", "cells"))
         if meta.get("ws_bytes") != S.ws_bytes:
             raise ValueError(f"checkpoint {path}: workspace of {meta.get('ws_bytes')} bytes, this swarm's is "
                              f"{S.ws_bytes}")
@@ -579,11 +636,12 @@ class LatticeSwarm:
         return S
 
     def step(self):
-        g = self.graphs.get(self.collect_stats)
+        g = self.graphs.get((self.collect_stats, self.cull))
         if g is not None:
             g.replay()
         else:
             self._launch()
+        self._auto_check(1)
 
 
 def mc_rollout(params, pos, n_o, n_a, steps, T=1 / 30, theta=None, so=1.0, ga=1.0, safety=False, stats=True):

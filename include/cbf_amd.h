@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define CBF_ABI_VERSION 6
+#define CBF_ABI_VERSION 7
 
 #define CBF_EINVAL (-1)
 
@@ -68,6 +68,10 @@ extern "C" {
 #define CBF_STAT_MIN_DIST2 7     /* 0x7FF0000000000000 - bits(min neighbour distance^2); 0 = no pair */
 #define CBF_STAT_ERRORS 8        /* steps whose cell list was unusable (CBF_STATUS_WORKSPACE_ERROR) */
 #define CBF_STAT_BINDING 9       /* QPs whose minimiser is not the origin (a barrier or box row binds) */
+#define CBF_STAT_WIN_WALKS 10    /* window cull: egos whose neighbours were not lattice-near, found by the
+                                    unbounded row walk (exact, slower; ABI 7) */
+#define CBF_STAT_GUARD_STALLS 11 /* window cull: row-guard words read at their spin limit, i.e. as the
+                                    worst bound (exact, slower; ABI 7) */
 
 /* ControlBarrierFunction state (cbf.py:6-16) + the callers' dynamics and cull radius. */
 typedef struct cbf_params {
@@ -304,6 +308,14 @@ int cbf_lattice_run_ex(const cbf_params* p, const cbf_grid* grid, int32_t W, int
  * cell list: the build (nominal control into vel_out and the workspace, the guards) and the
  * advance from the same pos into pos_out (which must not overlap pos), recording filter_done
  * (nullable hipEvent_t) between the filter kernel and the queued-QP kernel. */
+/* The window cull's degradation counters of a lattice workspace, accumulated by every window-cull
+ * advance since the workspace was zero-filled (statistics or not): out[0] = egos that took the
+ * unbounded row walk, out[1] = row-guard words read at their spin limit.  Copied stream-ordered
+ * into out (host or device memory, uint64[2]); synchronise the stream before reading a host copy.
+ * A swarm that stops being lattice-like shows up here long before it shows in the timing; the cell
+ * list (the same results) costs the same for any swarm.  (ABI 7) */
+int cbf_lattice_window_counters(const void* workspace, size_t workspace_bytes, uint64_t* out, void* stream);
+
 int cbf_lattice_window_build(const cbf_params* p, const cbf_grid* grid, int32_t W, int32_t H, const double* pos,
                              double gain, double* vel_out, void* workspace, size_t workspace_bytes, void* stream);
 int cbf_lattice_window_advance(const cbf_params* p, const cbf_grid* grid, int32_t W, int32_t H, const double* pos,

@@ -27,7 +27,7 @@ def test_library_loads_and_exports_every_declared_symbol():
         assert hasattr(_lib.lib, n), n
         assert n in _lib.SIGNATURES, n
     assert set(_lib.SIGNATURES) == set(names)
-    assert _lib.lib.cbf_abi_version() == _lib.ABI_VERSION == 6
+    assert _lib.lib.cbf_abi_version() == _lib.ABI_VERSION == 7
 
 
 def test_library_is_gfx950_code_object():
@@ -117,7 +117,8 @@ def test_decode_stats():
     from cbf_amd import _lib
     w = np.zeros(1024, np.uint64)
     assert _lib.decode_stats(w.view(np.int64)) == {"solves": 0, "optimal": 0, "relaxed": 0, "infeasible": 0,
-                                                   "seidel": 0, "errors": 0, "binding": 0, "viol_optimal": 0.0,
+                                                   "seidel": 0, "errors": 0, "binding": 0, "win_walks": 0,
+                                                   "guard_stalls": 0, "viol_optimal": 0.0,
                                                    "viol_original_relaxed": 0.0, "min_dist2": None}
     s = w.reshape(64, 16)
     s[3, _lib.STAT_SOLVES] = 5
@@ -128,8 +129,10 @@ def test_decode_stats():
     s[4, _lib.STAT_VIOL_ORIGINAL] = np.array([0.25]).view(np.uint64)[0]
     for slot, d2 in ((5, 0.01), (6, 0.0049), (7, 0.03)):
         s[slot, _lib.STAT_MIN_DIST2] = np.uint64(0x7FF0000000000000) - np.array([d2]).view(np.uint64)[0]
+    s[11, _lib.STAT_WIN_WALKS] = 9
+    s[12, _lib.STAT_GUARD_STALLS] = 2
     d = _lib.decode_stats(w.view(np.int64))
-    assert d["solves"] == 12 and d["optimal"] == 4
+    assert d["solves"] == 12 and d["optimal"] == 4 and d["win_walks"] == 9 and d["guard_stalls"] == 2
     assert d["viol_optimal"] == 1e-17 and d["viol_original_relaxed"] == 0.25 and d["min_dist2"] == 0.0049
 
 

@@ -18,6 +18,11 @@ from oracle import coracle, pyoracle as po  # noqa: E402
 from tests import paramsets  # noqa: E402
 
 GAIN = 0.25
+WINDOW_ONLY = ("win_walks", "guard_stalls")   # statistics words only the window cull counts
+
+
+def _stats_row(st):
+    return np.array([st[k] for k in sorted(st) if k not in WINDOW_ONLY], dtype=object)
 
 
 def _oracle_rollout(pos, W, H, steps, pset="callers"):
@@ -133,10 +138,14 @@ def test_window_run_equals_cells_run(nominal):
         A.run(1)
         torch.cuda.synchronize()
         st = A.stats_summary()
-        res[cull] = [t.cpu().numpy() for t in (A.pos, A.vel, A.u, A.status, A.nbr_count)] + \
-            [np.array([st[k] for k in sorted(st)], dtype=object)]
+        res[cull] = [t.cpu().numpy() for t in (A.pos, A.vel, A.u, A.status, A.nbr_count)] + [_stats_row(st)]
+        if cull == "window":
+            walks = st["win_walks"]
     for a, b in zip(res["cells"], res["window"]):
         assert np.array_equal(a, b)
+    # the random walk scrambles the lattice: egos walk their rows (CBF_STAT_WIN_WALKS counts them)
+    if nominal is not None:
+        assert walks > 0
 
 
 def test_window_advance_phase_marked_equals_step():
@@ -170,8 +179,7 @@ def test_window_full_size_cfg4_equals_cells():
         A.run(12)
         torch.cuda.synchronize()
         st = A.stats_summary()
-        res[cull] = [t.cpu().numpy() for t in (A.pos, A.vel, A.u, A.status, A.nbr_count)] + \
-            [np.array([st[k] for k in sorted(st)], dtype=object)]
+        res[cull] = [t.cpu().numpy() for t in (A.pos, A.vel, A.u, A.status, A.nbr_count)] + [_stats_row(st)]
         del A
     for a, b in zip(res["cells"], res["window"]):
         assert np.array_equal(a, b)
@@ -204,7 +212,13 @@ def test_window_guard_words_never_ready():
     torch.cuda.synchronize()
     for x, y in ((A.pos, B.pos), (A.u, B.u), (A.vel, B.vel), (A.status, B.status), (A.nbr_count, B.nbr_count)):
         assert torch.equal(x, y)
-    assert A.stats_summary() == B.stats_summary()
+    sa, sb = A.stats_summary(), B.stats_summary()
+    assert _stats_row(sa).tolist() == _stats_row(sb).tolist()
+    # the degradation is visible: every word read as the worst bound, and every ego walked
+    assert sa["guard_stalls"] == 0 and sb["guard_stalls"] > 0
+    assert sb["win_walks"] == 3 * W * H > sa["win_walks"]
+    ca, cb = A.window_counters(), B.window_counters()
+    assert cb == (sb["win_walks"], sb["guard_stalls"]) and ca == (sa["win_walks"], 0)
 
 
 @pytest.mark.parametrize("cull", ["window", "cells"])
@@ -309,3 +323,29 @@ def test_window_many_rows_and_widest_rows(W, H, guard):
     B.run(3)
     torch.cuda.synchronize()
     assert torch.equal(A.pos, B.pos)
+
+
+def test_window_auto_switches_to_cells_when_the_swarm_scrambles():
+    """LatticeSwarm(cull="auto"): the window cull while the swarm stays lattice-like, the cell list
+    once the walks (CBF_STAT_WIN_WALKS, cbf_lattice_window_counters) pass AUTO_WALK_FRACTION of
+    the egos per timestep.  On cfg4r's random walk (which scrambles x along every row within a few
+    timesteps) it switches; on the consensus lattice it does not; either way the rollout equals the
+    cell list's bit for bit."""
+    W, H = 160, 128
+    for nominal, spacing, switch in ((("random", 1.0, 5), 0.22, True), (None, 0.145, False)):
+        pos = scenarios.lattice(W, H, seed=33, spacing=spacing)
+        A = swarm.LatticeSwarm(pos, W, H, gain=GAIN, nominal=nominal, cull="auto")
+        B = swarm.LatticeSwarm(pos, W, H, gain=GAIN, nominal=nominal, cull="cells")
+        assert A.cull == "window"
+        for _ in range(12):
+            A.run(4)
+            torch.cuda.synchronize()   # lets the non-blocking look see each copy
+        B.run(48)
+        torch.cuda.synchronize()
+        assert (A.cull == "cells") == switch, (nominal, A._auto)
+        for x, y in ((A.pos, B.pos), (A.u, B.u), (A.status, B.status), (A.nbr_count, B.nbr_count)):
+            assert torch.equal(x, y), nominal
+        walks, stalls = A.window_counters()
+        print(f"auto cull, nominal {nominal}: last walk fraction {A._auto.get('last_fraction')}, "
+              f"walks {walks}, stalls {stalls}, switched after {A._auto.get('switched_after')}")
+        assert stalls == 0 and (walks > 0 if switch else True)
