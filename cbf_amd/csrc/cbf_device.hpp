@@ -46,6 +46,7 @@ struct KP {
     // coordinate difference e with |e| > d makes e * e >= cull_t (rounding is monotone), i.e. the
     // candidate cannot pass the cull test s < cull_t of cross_and_rescue.py:141-150
     double win_d;
+    double win_dn;  // nextafter(win_d, +inf): x - y >= win_dn in real arithmetic proves fl(x - y) > win_d
 };
 
 inline KP make_kp(const cbf_params* p) {
@@ -66,6 +67,7 @@ inline KP make_kp(const cbf_params* p) {
     double d = sqrt(p->cull_t > 0 ? p->cull_t : 0.0);
     while (d * d < p->cull_t) d = nextafter(d, INFINITY);
     k.win_d = d;
+    k.win_dn = nextafter(d, INFINITY);
     return k;
 }
 

@@ -31,6 +31,9 @@
 
 using namespace cbf;
 
+extern "C" __device__ __attribute__((const)) double __ockl_wfred_min_f64(double);
+extern "C" __device__ __attribute__((const)) double __ockl_wfred_max_f64(double);
+
 namespace {
 
 #ifndef CBF_TILE_WPE
@@ -56,6 +59,8 @@ struct WinGuard {
     double* rowy;     // [2 H] {min y, max y} per row (finite agents)
     double* sylo;     // [H + 1] min over rows >= r of the row minima (sylo[H] = +inf)
     double* pyhi;     // [H] max over rows <= r of the row maxima
+    int32_t* srt;     // [H] 1: every agent of the row finite and x non-decreasing along it (then each
+                      // agent's own x is its column extents, and the build stores none for the row)
 };
 inline WinGuard win_guard(const CellWs& Wk, int H) {
     WinGuard g;
@@ -63,6 +68,7 @@ inline WinGuard win_guard(const CellWs& Wk, int H) {
     g.rowy = reinterpret_cast<double*>(p);
     g.sylo = g.rowy + 2l * H;
     g.pyhi = g.sylo + (H + 1);
+    g.srt = reinterpret_cast<int32_t*>(g.pyhi + H);
     return g;
 }
 // Control words of the window cull in the workspace header (fixed offsets, whatever the lattice
@@ -84,7 +90,7 @@ constexpr int32_t kGuardInFilter = 1, kGuardSeparate = 2;
 // record area on other paths; its words never carry the tag).  The count lives in the header, so
 // tokens keep increasing across culls and lattice shapes sharing a workspace.
 __host__ __device__ inline int32_t guard_token(int32_t v) { return (v & 0x00FFFFFF) | 0x5A000000; }
-inline size_t win_guard_bytes(int H) { return 8 * (size_t)(4l * H + 2); }  // <= 16 W H for W >= 4
+inline size_t win_guard_bytes(int H) { return 8 * (size_t)(4l * H + 2) + 4 * (size_t)H; }  // <= 16 W H for W >= 4
 // Geometry (WinGeom, lattice_ego.hpp): candidates are the agents of window rows [cr0, cr1).  A
 // window edge that is not a lattice edge is not a candidate row (its agents' nominal controls
 // cannot be formed there; the cell-list builds skip them likewise, and the sharded step's halo
@@ -220,39 +226,56 @@ __global__ void __launch_bounds__(kPrepBlock) __attribute__((amdgpu_waves_per_eu
             yhi = gmax(yhi, pi.y);
         }
     }
-    // column extents: suffix minimum / prefix maximum of x along the row over the finite agents,
-    // each thread over its contiguous chunk of m columns, then across the threads; one block-wide
-    // exchange carries them and the row's y extents
+    // A sorted row (every agent finite, x non-decreasing along it: a lattice row under consensus)
+    // needs no column extents -- each agent's own x is the minimum over the columns from it on and
+    // the maximum over those up to it -- so the filter reads the staged positions instead and the
+    // build skips the scans and the 8-B store per agent.  Other rows: suffix minimum / prefix
+    // maximum of x over the finite agents, each thread over its contiguous chunk of m columns, then
+    // across the threads, through one block-wide exchange with the row's y extents.
+    bool ok = true;
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+        const int c = threadIdx.x + j * kPrepBlock;
+        if (c < W) {
+            ok = ok && isfinite(p[j].x) && isfinite(p[j].y);
+            if (c + 1 < W) ok = ok && p[j].x <= srow[c + 1].x;
+        }
+    }
+    const bool sorted = __syncthreads_and(ok) != 0;
     const int m = (W + kPrepBlock - 1) / kPrepBlock;
     const int c0 = threadIdx.x * m;
     double sm[PER], pm[PER];
-    double acc = INFINITY;
-#pragma unroll
-    for (int j = PER - 1; j >= 0; --j) {
-        if (j < m && c0 + j < W) {
-            const double2 q = srow[c0 + j];
-            if (isfinite(q.x) && isfinite(q.y)) acc = gmin(acc, q.x);
-        }
-        sm[j] = acc;
-    }
-    acc = -INFINITY;
-#pragma unroll
-    for (int j = 0; j < PER; ++j) {
-        if (j < m && c0 + j < W) {
-            const double2 q = srow[c0 + j];
-            if (isfinite(q.x) && isfinite(q.y)) acc = gmax(acc, q.x);
-        }
-        pm[j] = acc;
-    }
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    double ss = sm[0], ps = pm[PER - 1], yl = ylo, yh = yhi;  // wave scans / reductions
-    for (int o = 1; o < 64; o <<= 1) {
-        const double a = __shfl_down(ss, o, 64), b = __shfl_up(ps, o, 64);
-        if (lane + o < 64) ss = gmin(ss, a);
-        if (lane >= o) ps = gmax(ps, b);
-        yl = gmin(yl, __shfl_xor(yl, o, 64));
-        yh = gmax(yh, __shfl_xor(yh, o, 64));
+    double ss = INFINITY, ps = -INFINITY, yl = ylo, yh = yhi;  // wave scans / reductions
+    if (!sorted) {
+        double acc = INFINITY;
+#pragma unroll
+        for (int j = PER - 1; j >= 0; --j) {
+            if (j < m && c0 + j < W) {
+                const double2 q = srow[c0 + j];
+                if (isfinite(q.x) && isfinite(q.y)) acc = gmin(acc, q.x);
+            }
+            sm[j] = acc;
+        }
+        acc = -INFINITY;
+#pragma unroll
+        for (int j = 0; j < PER; ++j) {
+            if (j < m && c0 + j < W) {
+                const double2 q = srow[c0 + j];
+                if (isfinite(q.x) && isfinite(q.y)) acc = gmax(acc, q.x);
+            }
+            pm[j] = acc;
+        }
+        ss = sm[0];
+        ps = pm[PER - 1];
+        for (int o = 1; o < 64; o <<= 1) {
+            const double a = __shfl_down(ss, o, 64), b = __shfl_up(ps, o, 64);
+            if (lane + o < 64) ss = gmin(ss, a);
+            if (lane >= o) ps = gmax(ps, b);
+        }
     }
+    yl = __ockl_wfred_min_f64(yl);  // DPP wave reductions (the extents are finite or +-inf)
+    yh = __ockl_wfred_max_f64(yh);
     double sx = __shfl_down(ss, 1, 64), px = __shfl_up(ps, 1, 64);  // exclusive
     if (lane == 63) sx = INFINITY;
     if (lane == 0) px = -INFINITY;
@@ -271,10 +294,12 @@ __global__ void __launch_bounds__(kPrepBlock) __attribute__((amdgpu_waves_per_eu
         lo = gmin(lo, red4[2][q]);
         hi = gmax(hi, red4[3][q]);
     }
+    if (!sorted) {
 #pragma unroll
-    for (int j = 0; j < PER; ++j) {
-        const int c = c0 + j;
-        if (j < m && c < W) srsp[c] = make_float2(f32_down(gmin(sm[j], after)), f32_up(gmax(pm[j], before)));
+        for (int j = 0; j < PER; ++j) {
+            const int c = c0 + j;
+            if (j < m && c < W) srsp[c] = make_float2(f32_down(gmin(sm[j], after)), f32_up(gmax(pm[j], before)));
+        }
     }
     if (ext_keys) {
         // the sharded step's halo-guard extents of this build's input positions (as the cell-list
@@ -306,15 +331,18 @@ __global__ void __launch_bounds__(kPrepBlock) __attribute__((amdgpu_waves_per_eu
         }
         ext_keys_flush<kPrepBlock / 64, false>(e, any, py, ext_keys, r, ered, &arrive);
     }
-    __syncthreads();
+    if (!sorted) {
+        __syncthreads();
 #pragma unroll
-    for (int j = 0; j < PER; ++j) {
-        const int c = threadIdx.x + j * kPrepBlock;
-        if (c < W) rsp[(long)r * W + c] = srsp[c];
+        for (int j = 0; j < PER; ++j) {
+            const int c = threadIdx.x + j * kPrepBlock;
+            if (c < W) rsp[(long)r * W + c] = srsp[c];
+        }
     }
     if (threadIdx.x == 0) {
         Gd.rowy[2l * r] = lo;
         Gd.rowy[2l * r + 1] = hi;
+        Gd.srt[r] = sorted ? 1 : 0;
     }
 }
 
@@ -455,7 +483,8 @@ __device__ __forceinline__ float2 ld_rsp(const float2* __restrict__ a, int t) {
 template <bool FZ>
 __device__ __forceinline__ void win_direct(const KP& P, Ego& E, long w, int r, int c, int W, int Kd, int Ku,
                                         const double2* __restrict__ pos, const double2* __restrict__ u0,
-                                        const float2* __restrict__ rsp, double& smin) {
+                                        const float2* __restrict__ rsp, const int32_t* __restrict__ srt,
+                                        double& smin) {
     E.bq0 = E.bq1 = E.bq2 = E.bq3 = INFINITY;
     E.present = 0u;
     E.count = 0;
@@ -471,13 +500,14 @@ __device__ __forceinline__ void win_direct(const KP& P, Ego& E, long w, int r, i
     };
     for (int dr = -Kd; dr <= Ku; ++dr) {
         const long b = w + (long)dr * W;
+        const bool so = srt[r + dr] != 0;  // a sorted row's column extents are its agents' own x
         for (int dc = 0; c + dc < W; ++dc) {  // the column itself, then right
             cand(b + dc);
-            if (c + dc + 1 >= W || (double)rsp[b + dc + 1].x - E.r0 > P.win_d) break;
+            if (c + dc + 1 >= W || (so ? pos[b + dc + 1].x : (double)rsp[b + dc + 1].x) - E.r0 > P.win_d) break;
         }
         for (int dc = -1; c + dc >= 0; --dc) {  // left
             cand(b + dc);
-            if (c + dc - 1 < 0 || E.r0 - (double)rsp[b + dc - 1].y > P.win_d) break;
+            if (c + dc - 1 < 0 || E.r0 - (so ? pos[b + dc - 1].x : (double)rsp[b + dc - 1].y) > P.win_d) break;
         }
     }
 }
@@ -503,7 +533,7 @@ constexpr int kTileGuard = kTileR + kWinPre - 1;  // sylo / pyhi values a tile n
 struct TileLds {
     double2 p[kTileN];
     double2 u[kTileN];
-    float2 g[kTileN];
+    float2 g[kTileN];  // column extents (fp32, outward) of the staged agents
     double sy[kTileGuard], py[kTileGuard];
 };
 
@@ -550,27 +580,58 @@ __global__ void __launch_bounds__(kTileT) __attribute__((amdgpu_waves_per_eu((IN
     const int32_t token = fold ? guard_token(sctl[kWinTokenWord]) : 0;  // written by the build (an earlier launch)
     if (fold && blockIdx.x == 0) row_guard_scan<kTileT, CBF_GUARD_PER, true>(Q, Gd, gred, token);
     // stage the tile with its halo (beyond the lattice: +-inf positions, which no test passes, and
-    // column extents that exclude nothing beyond the row ends)
-    for (int i = threadIdx.x; i < kTileN; i += kTileT) {
+    // column extents that exclude nothing beyond the row ends).  Every global load of the block --
+    // each thread's (at most kStageK) entries: position, nominal control, the row's sorted flag and
+    // the column extents, and the row-guard words' first poll -- is issued before any is waited
+    // for: one memory round trip (a loop of dependent loads took four, a third of a block's life).
+    // The extents are loaded for every row (the stale ones of a sorted row go unused).
+    constexpr int kStageK = (kTileN + kTileT - 1) / kTileT;
+    double2 sp[kStageK], su[kStageK];
+    float2 sg[kStageK];
+    int ss[kStageK];
+    bool sv[kStageK];
+#pragma unroll
+    for (int k = 0; k < kStageK; ++k) {
+        const int i = threadIdx.x + k * kTileT;
         const int lr = i / kTileCols, lc = i - lr * kTileCols;
         const int rr = r0 - kTileKS + lr, cc = c0 - kTileKC + lc;
-        if (rr >= Q.cr0 && rr < Q.cr1 && cc >= 0 && cc < W) {
-            const int t = rr * W + cc;
-            L.p[i] = ld_slot(pos, t);
-            L.u[i] = ld_slot(u0, t);
-            L.g[i] = ld_rsp(rsp, t);
+        sv[k] = i < kTileN && rr >= Q.cr0 && rr < Q.cr1 && cc >= 0 && cc < W;
+        // branch-free: an entry outside the window loads agent 0 (discarded below), so that no
+        // load waits on another's condition
+        const int t = sv[k] ? rr * W + cc : 0;
+        sp[k] = ld_slot(pos, t);
+        su[k] = ld_slot(u0, t);
+        sg[k] = ld_rsp(rsp, t);
+        ss[k] = Gd.srt[sv[k] ? rr : 0];
+    }
+    int stalls = 0;
+    const int ga = r0 + 1 + (int)threadIdx.x, gb = r0 - kWinPre + (int)threadIdx.x;
+    double gsy = INFINITY, gpy = -INFINITY;
+    if (threadIdx.x < kTileGuard) {
+        if (ga < Q.cr1) gsy = ld_guard(sylo + ga, fold, token, -INFINITY, stalls);
+        if (gb >= Q.cr0) gpy = ld_guard(pyhi + gb, fold, token, INFINITY, stalls);
+    }
+#pragma unroll
+    for (int k = 0; k < kStageK; ++k) {
+        const int i = threadIdx.x + k * kTileT;
+        if (i >= kTileN) continue;
+        if (sv[k]) {
+            L.p[i] = sp[k];
+            L.u[i] = su[k];
+            // a sorted row's column extents are its agents' own x (outward to fp32); the build
+            // stored extents for the other rows only
+            L.g[i] = ss[k] ? make_float2(f32_down(sp[k].x), f32_up(sp[k].x)) : sg[k];
         } else {
+            const int lc = i - (i / kTileCols) * kTileCols, cc = c0 - kTileKC + lc;
             const double v = cc < 0 ? -INFINITY : INFINITY;
             L.p[i] = make_double2(v, v);
             L.u[i] = make_double2(0.0, 0.0);
             L.g[i] = make_float2(INFINITY, -INFINITY);
         }
     }
-    int stalls = 0;
     if (threadIdx.x < kTileGuard) {
-        const int a = r0 + 1 + threadIdx.x, b = r0 - kWinPre + threadIdx.x;
-        L.sy[threadIdx.x] = a < Q.cr1 ? ld_guard(sylo + a, fold, token, -INFINITY, stalls) : INFINITY;
-        L.py[threadIdx.x] = b >= Q.cr0 ? ld_guard(pyhi + b, fold, token, INFINITY, stalls) : -INFINITY;
+        L.sy[threadIdx.x] = gsy;
+        L.py[threadIdx.x] = gpy;
     }
     __syncthreads();
     const bool act = inside && w >= B.own_lo && w < B.own_hi;
@@ -584,6 +645,12 @@ __global__ void __launch_bounds__(kTileT) __attribute__((amdgpu_waves_per_eu((IN
     }
     int Kd = -1, Ku = -1;
     bool slow = false;
+    // column-sentinel thresholds in fp32: a sentinel x with x > thR (x < thL) proves the columns
+    // from it on out of range, since then x - r0 >= win_dn > win_d in real arithmetic and so in
+    // fp64 (rounding is monotone); thR is r0 + win_dn rounded up (fp64, then to fp32 outward) and
+    // thL likewise down.  At most one fp32 ulp looser than the fp64 test of the extents: a looser
+    // bound only widens a window.  (Non-finite or huge coordinates give +-inf: every column needed.)
+    float thR = INFINITY, thL = -INFINITY;
     if (fin) {
         Ku = 0;
         Kd = 0;
@@ -593,39 +660,43 @@ __global__ void __launch_bounds__(kTileT) __attribute__((amdgpu_waves_per_eu((IN
             Kd += !(E.r1 - L.py[wv + kWinPre - 1 - k] > P.win_d) ? 1 : 0;
         }
         if (Ku > kTileKS || Kd > kTileKS) slow = true;  // beyond the staged rows: the unbounded form
+        const double tr = E.r0 + P.win_dn, tl = E.r0 - P.win_dn;
+        thR = f32_up(tr + (fabs(tr) * 0x1p-50 + 0x1p-1070));
+        thL = f32_down(tl - (fabs(tl) * 0x1p-50 + 0x1p-1070));
     }
-    const int KuW = wave_max_i(slow ? -1 : Ku), KdW = wave_max_i(slow ? -1 : Kd);
+    // the wave's row range (DPP reductions; -1 for lanes without a window)
+    const int KuW = (int)__ockl_wfred_max_u32((unsigned)(slow ? 0 : Ku + 1)) - 1;
+    const int KdW = (int)__ockl_wfred_max_u32((unsigned)(slow ? 0 : Kd + 1)) - 1;
     unsigned long long hm = 0;  // hit bits (dr + 3) * 8 + (dc + 2): one byte per row
     double d2 = INFINITY;
-    auto cand = [&](int off, int bit) {
+    auto cand = [&](int off) -> unsigned {
         const double2 q = L.p[off];
         const double e0 = q.x - E.r0, e1 = q.y - E.r1;
         const double s = e0 * e0 + e1 * e1;
-        if (s < P.cull_t && s > 0) {
-            hm |= 1ull << bit;
-            d2 = pmin(d2, s);
-        }
+        const bool hit = s < P.cull_t && s > 0;
+        if (ST && hit) d2 = pmin(d2, s);
+        return hit ? 1u : 0u;
     };
     unsigned pR = 0, pL = 0;  // rows (bit dr + 3) whose sentinel at c + 2 / c - 2 does not hold
     for (int dr = -KdW; dr <= KuW; ++dr) {
         if (!(fin && !slow && dr >= -Kd && dr <= Ku)) continue;
-        const int b = e + dr * kTileCols, bit = (dr + 3) * 8 + 2;
-        cand(b - 1, bit - 1);
-        cand(b, bit);
-        cand(b + 1, bit + 1);
-        if (!((double)L.g[b + 2].x - E.r0 > P.win_d)) pR |= 1u << (dr + 3);
-        if (!(E.r0 - (double)L.g[b - 2].y > P.win_d)) pL |= 1u << (dr + 3);
+        const int b = e + dr * kTileCols;
+        // the row's three hit bits (dc = -1, 0, 1 at bits 1, 2, 3 of its byte), then one shift
+        const unsigned rb = (cand(b - 1) << 1) | (dr != 0 ? cand(b) << 2 : 0u) | (cand(b + 1) << 3);  // (not itself)
+        hm |= (unsigned long long)rb << ((dr + 3) * 8);
+        if (!(L.g[b + 2].x > thR)) pR |= 1u << (dr + 3);
+        if (!(L.g[b - 2].y < thL)) pL |= 1u << (dr + 3);
     }
     if (__ballot((pR | pL) != 0)) {  // columns c -+ 2 where a sentinel did not hold
         for (int dr = -KdW; dr <= KuW; ++dr) {
-            const int b = e + dr * kTileCols, bit = (dr + 3) * 8 + 2;
+            const int b = e + dr * kTileCols, sh = (dr + 3) * 8;
             if ((pR >> (dr + 3)) & 1u) {
-                cand(b + 2, bit + 2);
-                if (!((double)L.g[b + 3].x - E.r0 > P.win_d)) slow = true;
+                hm |= (unsigned long long)(cand(b + 2) << 4) << sh;
+                if (!(L.g[b + 3].x > thR)) slow = true;
             }
             if ((pL >> (dr + 3)) & 1u) {
-                cand(b - 2, bit - 2);
-                if (!(E.r0 - (double)L.g[b - 3].y > P.win_d)) slow = true;
+                hm |= (unsigned long long)cand(b - 2) << sh;
+                if (!(L.g[b - 3].y < thL)) slow = true;
             }
         }
     }
@@ -649,33 +720,42 @@ __global__ void __launch_bounds__(kTileT) __attribute__((amdgpu_waves_per_eu((IN
             double g0 = INFINITY, g1 = INFINITY, g2 = INFINITY, g3 = INFINITY;
             if (qfin) {
                 E.count = __popcll(hm);
-                // row_g<FZ> per hit (f = 0: its H with k's sign set by bit arithmetic -- -P.k flips
-                // exactly that bit -- instead of selects; same value bit for bit)
+                // row_g<FZ> per hit (f = 0: its H with k's sign as a select of k's two high words --
+                // -P.k flips exactly that bit -- instead of a multiply; same value bit for bit).  The
+                // four quadrant minima are updated under the sign masks themselves (scalar mask logic,
+                // no quadrant index), and a quadrant's presence is read off its minimum afterwards: a
+                // present quadrant whose minimum stayed +inf (a NaN or +inf row) is a +inf plane,
+                // which no solver step can violate or bind -- the same as an absent one.
                 const unsigned long long kb = (unsigned long long)__double_as_longlong(P.k);
+                const unsigned khi = (unsigned)(kb >> 32), knhi = khi ^ 0x80000000u, klo = (unsigned)kb;
                 while (hm) {
                     const int bit = __ffsll((long long)hm) - 1;
                     hm &= hm - 1;
                     const int off = e + ((bit >> 3) - 3) * kTileCols + (bit & 7) - 2;
                     const double2 q = L.p[off], v = L.u[off];
-                    int qd;
                     double g;
+                    bool nx, ny;
                     if (FZ) {
                         const double d0 = E.r0 - q.x, d1 = E.r1 - q.y, d2 = E.r2 - v.x, d3 = E.r3 - v.y;
-                        const bool nx = d0 < 0, ny = d1 < 0;
-                        const double ksx = __longlong_as_double((long long)(kb ^ ((unsigned long long)nx << 63)));
-                        const double ksy = __longlong_as_double((long long)(kb ^ ((unsigned long long)ny << 63)));
+                        nx = d0 < 0;
+                        ny = d1 < 0;
+                        const double ksx = __hiloint2double((int)(nx ? knhi : khi), (int)klo);
+                        const double ksy = __hiloint2double((int)(ny ? knhi : khi), (int)klo);
                         const double Hh = fma(ksy, d3, fma(ksx, d2, fabs(d0) + fabs(d1)));
-                        qd = (nx ? 1 : 0) | (ny ? 2 : 0);
                         g = P.gamma * (Hh - P.dmin);
                     } else {
+                        int qd;
                         g = row_g<FZ>(P, E, q.x, q.y, v.x, v.y, qd);
+                        nx = (qd & 1) != 0;
+                        ny = (qd & 2) != 0;
                     }
-                    g0 = (qd == 0 && g < g0) ? g : g0;
-                    g1 = (qd == 1 && g < g1) ? g : g1;
-                    g2 = (qd == 2 && g < g2) ? g : g2;
-                    g3 = (qd == 3 && g < g3) ? g : g3;
-                    E.present |= 1u << qd;
+                    g0 = (!nx && !ny && g < g0) ? g : g0;
+                    g1 = (nx && !ny && g < g1) ? g : g1;
+                    g2 = (!nx && ny && g < g2) ? g : g2;
+                    g3 = (nx && ny && g < g3) ? g : g3;
                 }
+                E.present = (g0 < INFINITY ? 1u : 0u) | (g1 < INFINITY ? 2u : 0u) | (g2 < INFINITY ? 4u : 0u) |
+                            (g3 < INFINITY ? 8u : 0u);
                 E.bq0 = g0 + q0;
                 E.bq1 = g1 + q1;
                 E.bq2 = g2 + q2;
@@ -692,7 +772,7 @@ __global__ void __launch_bounds__(kTileT) __attribute__((amdgpu_waves_per_eu((IN
         } else if (fin) {  // the unbounded form, over the full row window (beyond the staged halo too)
             int kd, ku;
             win_rows(P, sylo, pyhi, r, Q.cr0, Q.cr1, E.r1, kd, ku, fold, token, stalls);
-            win_direct<FZ>(P, E, w, r, c, W, kd, ku, pos, u0, rsp, d2);
+            win_direct<FZ>(P, E, w, r, c, W, kd, ku, pos, u0, rsp, Gd.srt, d2);
         }
         O.nbrs = E.count;
         if (ST) O.d2 = d2;
