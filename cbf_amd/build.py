@@ -95,7 +95,8 @@ def build_torch_ops(verbose: bool = False) -> str:
 # up, so tests/test_gpu_parity.py can check that the failure is reported, not silent.
 TEST_VARIANTS = {"scantimeout": (["cells.hip", "swarm.hip", "hocbf.hip", "filter.hip"], ["CBF_SCAN_TEST_TIMEOUT=1"]),
                  "apwpe8": (["filter.hip"], ["CBF_AP_WPE=8"]),
-                 "winnowait": (["window.hip"], ["CBF_WIN_SPIN_LIMIT=-1"])}
+                 "winnowait": (["window.hip"], ["CBF_WIN_SPIN_LIMIT=-1"]),
+                 "evqueue": (["swarm.hip", "window.hip"], ["CBF_EVENT_IN_PLACE=64"])}
 TEST_LIB_DIR = os.path.join(ROOT, "tests", "_lib")
 
 

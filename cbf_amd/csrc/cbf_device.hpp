@@ -500,12 +500,30 @@ __device__ __forceinline__ Sol solve_ego(const KP& P, const Ego& E) {
 // event, a bound that moves x, an infeasible prefix, non-finite data) returns false and the caller
 // runs solve_ego.  Measured: 57 % (cfg4) and 89 % (cfg4f) of the QPs the origin does not solve are
 // one such event (tools).
-__device__ __forceinline__ bool solve_fast(const KP& P, const Ego& E, Sol& S) {
-    const Box B = box_rhs(P, E);
+// solve_fast in two stages: the strip pre-relaxation and solve8's test at the origin
+// (fast_origin: returns true with S set when the origin is the answer), then the one-event check
+// (fast_event).  The filter kernels that defer the second stage to a few lanes (the window tile's
+// event queue) call them apart.
+struct FastState {
+    Box B;
+    double b[8];
+    int iters, h;
+    double v0;
+};
+__device__ __forceinline__ bool fast_origin(const KP& P, const Ego& E, FastState& F, Sol& S) {
+    F.B = box_rhs(P, E);
+    const Box& B = F.B;
     const double a0[8] = {1.0, 0.0, -1.0, 0.0, P.n0[0], P.n0[1], P.n0[2], P.n0[3]};
     const double a1[8] = {0.0, 1.0, 0.0, -1.0, P.n1[0], P.n1[1], P.n1[2], P.n1[3]};
-    double b[8] = {pmin(B.S[0], B.S[4]), pmin(B.S[1], B.S[6]), pmin(B.S[2], B.S[5]), pmin(B.S[3], B.S[7]),
-                   E.bq0, E.bq1, E.bq2, E.bq3};
+    double* b = F.b;
+    b[0] = pmin(B.S[0], B.S[4]);
+    b[1] = pmin(B.S[1], B.S[6]);
+    b[2] = pmin(B.S[2], B.S[5]);
+    b[3] = pmin(B.S[3], B.S[7]);
+    b[4] = E.bq0;
+    b[5] = E.bq1;
+    b[6] = E.bq2;
+    b[7] = E.bq3;
     const unsigned mask = 0xFu | (E.present << 4);
     int iters = 0;
     if ((E.present & 9u) == 9u || (E.present & 6u) == 6u) {  // strip pre-check, as solve_ego
@@ -539,6 +557,9 @@ __device__ __forceinline__ bool solve_fast(const KP& P, const Ego& E, Sol& S) {
             if (!(d <= FEAS_TOL * pmax(1.0, fabs(b[j])))) h = j;
             if (d > v0) v0 = d;
         }
+    F.iters = iters;
+    F.h = h;
+    F.v0 = v0;
     if (h < 0) {  // solve8 returns the origin; the final check below would repeat the test above
         S.x0 = 0.0;
         S.x1 = 0.0;
@@ -548,6 +569,14 @@ __device__ __forceinline__ bool solve_fast(const KP& P, const Ego& E, Sol& S) {
         S.viol_orig = iters > 0 ? orig_violation(P, E, B, 0.0, 0.0) : v0;
         return true;
     }
+    return false;
+}
+__device__ __forceinline__ bool fast_event(const KP& P, const Ego& E, const FastState& F, Sol& S) {
+    const double a0[8] = {1.0, 0.0, -1.0, 0.0, P.n0[0], P.n0[1], P.n0[2], P.n0[3]};
+    const double a1[8] = {0.0, 1.0, 0.0, -1.0, P.n1[0], P.n1[1], P.n1[2], P.n1[3]};
+    const double* b = F.b;
+    const unsigned mask = 0xFu | (E.present << 4);
+    const int h = F.h;
     double x0 = 0.0, x1 = 0.0;
     {
         double ah0 = 0.0, ah1 = 0.0, bh = 0.0;
@@ -588,11 +617,16 @@ __device__ __forceinline__ bool solve_fast(const KP& P, const Ego& E, Sol& S) {
     if (!ok) return false;
     S.x0 = x0;
     S.x1 = x1;
-    S.iters = iters;
-    S.status = iters > 0 ? CBF_STATUS_RELAXED : CBF_STATUS_OPTIMAL;
+    S.iters = F.iters;
+    S.status = F.iters > 0 ? CBF_STATUS_RELAXED : CBF_STATUS_OPTIMAL;
     S.viol = v;
-    S.viol_orig = iters > 0 ? orig_violation(P, E, B, x0, x1) : v;
+    S.viol_orig = F.iters > 0 ? orig_violation(P, E, F.B, x0, x1) : v;
     return true;
+}
+__device__ __forceinline__ bool solve_fast(const KP& P, const Ego& E, Sol& S) {
+    FastState F;
+    if (fast_origin(P, E, F, S)) return true;
+    return fast_event(P, E, F, S);
 }
 
 // cbf.py:89-91

@@ -468,7 +468,7 @@ __global__ void __launch_bounds__(kBlock) k_lattice_filter_hocbf(
             const int m = hocbf_scan<false>(P, G, E, spos, sidx, start, keys, kBlock, threadIdx.x);
             E.count = m;
             if (m > kLdsRows && m <= kHocbfCap) {
-                qslot[(long)(bx % kSubQ) * qcap + subq_append(hardq, bx % kSubQ)] = slot;
+                qslot[subq_append(hardq, bx % kSubQ, qcap)] = slot;
             } else if (m > 0 && m <= kLdsRows) {
                 const Sol S = hocbf_solve_lds<kLdsRows, true>(P, H, E, spos, svel, keys, reinterpret_cast<double*>(keys),
                                                         kBlock, threadIdx.x, m);
@@ -502,7 +502,7 @@ __global__ void __launch_bounds__(64) k_lattice_filter_hocbf_wide(
     unsigned long long* keys = reinterpret_cast<unsigned long long*>(rows);
     double e0 = INFINITY, e1 = -INFINITY, e2 = -INFINITY, e3 = INFINITY;
     int ns = 0;
-    drain_subq(hardq, kWidePerQ, [&](int q, int i) {
+    drain_subq(hardq, kWidePerQ, qcap, [&](int q, int i) {
         const int slot = qslot[(long)q * qcap + i];
         const int w = sidx[slot];
         const int r = win_row0 + w / W, c = w % W;

@@ -130,16 +130,33 @@ __device__ __forceinline__ int run_rank(int cell, int32_t* __restrict__ count) {
     return base + lane - my_leader;
 }
 
-// This lane's entry in sub-queue q (length at hardq[32 (1 + q)]); every active lane of the wave
-// that calls it appends one entry, with one atomic per wave.
-__device__ __forceinline__ int subq_append(int32_t* hardq, int q) {
-    const unsigned long long m = __ballot(1);
+// This lane's record index in the queue area (sub-queue q at [q qcap, (q + 1) qcap), length at
+// hardq[32 (1 + q)]); every active lane of the wave that calls it appends one entry, with one
+// atomic per wave.  The capacity is sized for kBlock-lane filter blocks sharing a sub-queue; a
+// larger block (the window tile's 512 egos) can find its sub-queue full, and its remaining lanes
+// then take the next sub-queues (the counter of a full one runs past qcap: the queue kernels read
+// min(length, qcap)).  The sub-queues together hold every agent, so a slot is always found.
+__device__ __forceinline__ long subq_append(int32_t* hardq, int q, long qcap) {
     const int lane = threadIdx.x & 63;
-    const int leader = __ffsll((long long)m) - 1;
-    int base = 0;
-    if (lane == leader) base = atomicAdd(&hardq[32 * (1 + q)], __popcll(m));
-    base = __shfl(base, leader, 64);
-    return base + __popcll(m & ((1ull << lane) - 1ull));
+    long rec = -1;
+    bool need = true;
+    for (int t = 0; t < kSubQ; ++t) {
+        const unsigned long long m = __ballot(need);
+        if (!m) break;
+        const int qq = (q + t) & (kSubQ - 1);
+        const int leader = __ffsll((long long)m) - 1;
+        int base = 0;
+        if (lane == leader) base = atomicAdd(&hardq[32 * (1 + qq)], __popcll(m));
+        base = __shfl(base, leader, 64);
+        if (need) {
+            const long sl = base + __popcll(m & ((1ull << lane) - 1ull));
+            if (sl < qcap) {
+                rec = (long)qq * qcap + sl;
+                need = false;
+            }
+        }
+    }
+    return rec;
 }
 
 // The queue kernels: 64-lane blocks, block g serving sub-queue g % kSubQ as its (g / kSubQ)-th of
@@ -155,9 +172,10 @@ __device__ __forceinline__ int subq_append(int32_t* hardq, int q) {
 // length gives it no work either); a working block cannot read it after the reset, which needs
 // its own count first.
 template <class Visit>
-__device__ __forceinline__ void drain_subq(int32_t* __restrict__ hardq, int per_q, Visit&& visit) {
+__device__ __forceinline__ void drain_subq(int32_t* __restrict__ hardq, int per_q, long qcap, Visit&& visit) {
     const int q = blockIdx.x % kSubQ, k = blockIdx.x / kSubQ;
-    const int nq = hardq[32 * (1 + q)];
+    const int nq0 = hardq[32 * (1 + q)];
+    const int nq = nq0 < qcap ? nq0 : (int)qcap;  // (a full sub-queue's counter runs past qcap: subq_append)
     const int need = (nq + 63) / 64;
     const int nwork = need < per_q ? need : per_q;
     if (k >= nwork) return;
@@ -275,8 +293,9 @@ __device__ __forceinline__ void lattice_error_tail(int W, int row_begin, int row
 // Per-lane status counts and violation maxima of a queue kernel, summed over the wave (every lane
 // of the wave must call it, after its loop).
 __device__ __forceinline__ void wave_stats_counts(unsigned long long* __restrict__ st, long wave, int n_opt, int n_rel,
-                                                  int n_inf, int n_bnd, double vo, double vr) {
+                                                  int n_inf, int n_bnd, int n_sei, double vo, double vr) {
     for (int o = 32; o > 0; o >>= 1) {
+        n_sei += __shfl_xor(n_sei, o, 64);
         n_opt += __shfl_xor(n_opt, o, 64);
         n_rel += __shfl_xor(n_rel, o, 64);
         n_inf += __shfl_xor(n_inf, o, 64);
@@ -290,6 +309,7 @@ __device__ __forceinline__ void wave_stats_counts(unsigned long long* __restrict
         if (n_rel) atomicAdd(&s[CBF_STAT_RELAXED], (unsigned long long)n_rel);
         if (n_inf) atomicAdd(&s[CBF_STAT_INFEASIBLE], (unsigned long long)n_inf);
         if (n_bnd) atomicAdd(&s[CBF_STAT_BINDING], (unsigned long long)n_bnd);
+        if (n_sei) atomicAdd(&s[CBF_STAT_SEIDEL], (unsigned long long)n_sei);
         if (vo > 0.0) atomicMax(&s[CBF_STAT_VIOL_OPTIMAL], dbits(vo));
         if (vr > 0.0) atomicMax(&s[CBF_STAT_VIOL_ORIGINAL], dbits(vr));
     }

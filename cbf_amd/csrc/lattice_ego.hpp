@@ -192,25 +192,41 @@ __device__ __forceinline__ void ego_output(const KP& P, const Ego& E, const Sol&
 }
 
 // Tail of the lattice filter for one owned ego (output index k) whose QP rows are accumulated in
-// E: solve in place when solve_fast can (origin, or one Seidel event that stays put); otherwise
-// run the full solve_ego right here (IN: the small-window instantiation, below) or queue it to the
-// hard kernel (sub-queue q: header hardq, records qr).  Then clip, Euler, outputs.
+// E.  IN (the small-window instantiation): solve in place when solve_fast can (origin, or one
+// Seidel event that stays put), else run the full solve_ego right here.  Queued form: settle the
+// origin case here and queue every other QP to the hard kernel (sub-queue q: header hardq, records
+// qrec, subq_append).  Then clip, Euler, outputs.
+#ifndef CBF_EVENT_IN_PLACE
+#define CBF_EVENT_IN_PLACE 8
+#endif
+constexpr int kEventInPlace = CBF_EVENT_IN_PLACE;
 template <bool FZ, bool ST, bool IN>
 __device__ __forceinline__ void ego_finish(const KP& P, Ego& E, int w, int k, int slot, double T,
                                            double2* __restrict__ pos_out, double2* __restrict__ u,
                                            int32_t* __restrict__ status, int32_t* __restrict__ cnt,
-                                           int32_t* __restrict__ hardq, int q, HardRec* __restrict__ qr,
-                                           EgoOut& O) {
+                                           int32_t* __restrict__ hardq, int q, HardRec* __restrict__ qrec,
+                                           long qcap, EgoOut& O) {
     Sol S;
     const bool idle = E.count == 0;
-    if (!idle && !solve_fast(P, E, S)) {
-        O.seidel = true;
+    // The queued form runs solve_fast's one-event stage only in a wave where more than
+    // kEventInPlace lanes need it; the others' QPs go to the queue kernel whole, so that no filter
+    // wave runs the event stage for one lane (cfg4: 0.5 % of the egos, about one per wave), while
+    // a regime where most QPs take one event (cfg4f) does not move them all to the queue.  run(10)
+    // per timestep at 1 M agents, window cull, cfg4 / cfg4f: 63.7 / 59.2 us without deferral;
+    // threshold 4: 62.8 / 59.6; 8: 62.3 / 60.1; every event queued: 61.9 / 69.2.  The inline form
+    // (small windows, no queue kernel) keeps the one-event stage for every lane.
+    FastState F;
+    bool done = idle;
+    if (!done) done = IN ? solve_fast(P, E, S) : fast_origin(P, E, F, S);
+    if (!IN && !done && __popcll(__ballot(1)) > kEventInPlace) done = fast_event(P, E, F, S);
+    if (!done) {
+        O.seidel = IN;  // (queued: the queue kernel counts the QPs solve_fast cannot settle)
         if (IN) {
             S = solve_ego(P, E);
             ego_output<ST>(P, E, S, false, k, T, pos_out, u, status, cnt, O);
             return;
         }
-        HardRec& h = qr[subq_append(hardq, q)];
+        HardRec& h = qrec[subq_append(hardq, q, qcap)];
         h.r0 = E.r0;
         h.r1 = E.r1;
         h.r2 = E.r2;

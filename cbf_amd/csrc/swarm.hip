@@ -309,7 +309,7 @@ __device__ __forceinline__ void lattice_ego(const KP& P, const CellGrid& G, cons
                                             const int32_t* __restrict__ sidx, const int32_t* __restrict__ start,
                                             double T, double2* __restrict__ pos_out, double2* __restrict__ u,
                                             int32_t* __restrict__ status, int32_t* __restrict__ cnt,
-                                            int32_t* __restrict__ hardq, int q, HardRec* __restrict__ qr,
+                                            int32_t* __restrict__ hardq, int q, HardRec* __restrict__ qrec, long qcap,
                                             int* hit_lds, Ego& E, EgoOut& O) {
     const int w = sidx[slot];
     O.w = w;
@@ -347,7 +347,7 @@ __device__ __forceinline__ void lattice_ego(const KP& P, const CellGrid& G, cons
     }
     O.nbrs = E.count;
     if (ST) O.d2 = d2;
-    ego_finish<FZ, ST, IN>(P, E, w, w - B.own_lo, slot, T, pos_out, u, status, cnt, hardq, q, qr, O);
+    ego_finish<FZ, ST, IN>(P, E, w, w - B.own_lo, slot, T, pos_out, u, status, cnt, hardq, q, qrec, qcap, O);
 }
 
 // K4: one lane per cell-sorted slot; QPs that solve_fast settles (the origin, or one Seidel event
@@ -401,7 +401,7 @@ __global__ void __launch_bounds__(kBlock) k_lattice_filter(KP P, CellGrid G, Win
     Ego E;
     if (slot < total)  // finished (O.res == 1) or queued (O.res == 2)
         lattice_ego<FZ, ST, IN>(P, G, B, slot, spos, svel, sidx, start, T, pos_out, u, status, cnt, hardq,
-                                bx % kSubQ, qrec + (long)(bx % kSubQ) * qcap, hit_lds, E, O);
+                                bx % kSubQ, qrec, qcap, hit_lds, E, O);
     if (ext_part && O.res == 1) ext_accumulate_w(O.w, B, O.ny, e0, e1, e2, e3);
     if (C.bcs) {  // chained binning: the next build's record of this agent (queued egos: K5)
         // indexed by this advance's slot (the next scatter then reads its records in cell order and
@@ -442,7 +442,7 @@ __global__ void __launch_bounds__(64) k_lattice_filter_hard(KP P, CellGrid G, Wi
     // the last block (idle unless its sub-queue is long) refreshes the statistics snapshot
     if (stats && blockIdx.x == gridDim.x - 1) stat_snapshot(stats);
     double e0 = INFINITY, e1 = -INFINITY, e2 = -INFINITY, e3 = INFINITY;
-    int n_opt = 0, n_rel = 0, n_inf = 0, n_bnd = 0;
+    int n_opt = 0, n_rel = 0, n_inf = 0, n_bnd = 0, n_sei = 0;
     double vo = 0.0, vr = 0.0;
     // the first block of each sub-queue (the one that works whenever it is non-empty) loads its
     // lane's first entry speculatively, beside the queue length (the queue area is allocated;
@@ -450,7 +450,7 @@ __global__ void __launch_bounds__(64) k_lattice_filter_hard(KP P, CellGrid G, Wi
     const bool lead = (int)blockIdx.x < kSubQ;
     HardRec pre;
     if (lead) pre = qrec[(long)blockIdx.x * qcap + threadIdx.x];
-    drain_subq(hardq, kHardPerQ, [&](int q, int i) {
+    drain_subq(hardq, kHardPerQ, qcap, [&](int q, int i) {
         const HardRec h = (lead && i == (int)threadIdx.x) ? pre : qrec[(long)q * qcap + i];
         Ego E;
         E.r0 = h.r0;
@@ -466,6 +466,12 @@ __global__ void __launch_bounds__(64) k_lattice_filter_hard(KP P, CellGrid G, Wi
         E.present = (unsigned)h.present;
         E.count = h.count;
         const Sol S = solve_ego(P, E);
+        // CBF_STAT_SEIDEL counts the QPs that solve_fast cannot settle (the filter queues its
+        // one-event QPs here too): statistics runs only
+        if (stats && h.row >= B.cnt_lo && h.row < B.cnt_hi) {
+            Sol S1;
+            n_sei += solve_fast(P, E, S1) ? 0 : 1;
+        }
         double ux, uy;
         clip_u(P, S, E, ux, uy);
         const double2 pn = make_double2(E.r0 + T * ux, E.r1 + T * uy);
@@ -493,7 +499,7 @@ __global__ void __launch_bounds__(64) k_lattice_filter_hard(KP P, CellGrid G, Wi
             }
         }
     });
-    if (stats) wave_stats_counts(stats, blockIdx.x, n_opt, n_rel, n_inf, n_bnd, vo, vr);
+    if (stats) wave_stats_counts(stats, blockIdx.x, n_opt, n_rel, n_inf, n_bnd, n_sei, vo, vr);
     if (ext_part) wave_extents(e0, e1, e2, e3, ext_part, blockIdx.x);
 }
 

@@ -777,7 +777,7 @@ __global__ void __launch_bounds__(kTileT) __attribute__((amdgpu_waves_per_eu((IN
         O.nbrs = E.count;
         if (ST) O.d2 = d2;
         ego_finish<FZ, ST, IN>(P, E, (int)w, (int)(w - B.own_lo), (int)w, T, pos_out, u, status, cnt, hardq,
-                               bx % kSubQ, qrec + (long)(bx % kSubQ) * qcap, O);
+                               bx % kSubQ, qrec, qcap, O);
     }
     // degradation counters (every instantiation; rare, so one wave-aggregated atomic each when
     // they occur): walks and guard words read at their spin limit, into the workspace header and,

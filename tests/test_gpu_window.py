@@ -222,6 +222,40 @@ def test_window_guard_words_never_ready():
 
 
 @pytest.mark.parametrize("cull", ["window", "cells"])
+def test_queued_events_equal_in_place(cull):
+    """The queued form settles a QP's one-event stage in the filter wave only where more than
+    kEventInPlace lanes need it, and queues the others whole (lattice_ego.hpp ego_finish).  The
+    test build tests/_lib/libcbf_evqueue.so (CBF_EVENT_IN_PLACE = 64) queues every such QP: on the
+    random-walk regime, where most QPs take a Seidel event, the results and the rollout statistics
+    (CBF_STAT_SEIDEL: the QPs solve_fast cannot settle, counted by the queue kernel) are the
+    shipped library's bit for bit.  A 48-column tile queues up to 384 QPs into a sub-queue sized
+    for 256 (CellWs::subq_cap), so the full-sub-queue hand-off (subq_append) is exercised too."""
+    import ctypes as C
+    import os
+    from cbf_amd import _lib
+    V = C.CDLL(os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "libcbf_evqueue.so"))
+    fn = V.cbf_lattice_run_ex
+    fn.restype, fn.argtypes = _lib.SIGNATURES["cbf_lattice_run_ex"]
+    W, H, steps = 48, 40, 4
+    pos = scenarios.lattice(W, H, seed=5, spacing=0.22)
+    kw = dict(nominal=("random", 1.0, 3), cull=cull, params=swarm.FilterParams(solve_placement="queued"))
+    A = swarm.LatticeSwarm(pos, W, H, **kw)
+    B = swarm.LatticeSwarm(pos, W, H, **kw)
+    A.run(steps)
+    flags = _lib.RUN_WINDOW_CULL if cull == "window" else 0
+    rc = fn(B.cp, C.byref(B.grid), W, H, _lib.ptr(B.pos), B.gain, B.T, steps, _lib.ptr(B.vel), _lib.ptr(B.u),
+            _lib.ptr(B.status), _lib.ptr(B.nbr_count), B._st(), _lib.ptr(B.ws), B.ws_bytes, flags,
+            _lib.stream_handle())
+    assert rc == 0
+    torch.cuda.synchronize()
+    for x, y in ((A.pos, B.pos), (A.u, B.u), (A.vel, B.vel), (A.status, B.status), (A.nbr_count, B.nbr_count)):
+        assert torch.equal(x, y)
+    sa, sb = A.stats_summary(), B.stats_summary()
+    assert sa == sb
+    assert sa["seidel"] > 0 and sa["binding"] > 0.5 * sa["solves"]
+
+
+@pytest.mark.parametrize("cull", ["window", "cells"])
 def test_timed_advance_equals_marked(cull):
     """advance_phase(timing=...) (cbf_lattice_*advance_timed: the filter launched with
     hipExtLaunchKernel start / stop events, bench.py's kernel timing) gives the plain advance's
