@@ -468,7 +468,8 @@ __global__ void __launch_bounds__(kBlock) k_lattice_filter_hocbf(
             const int m = hocbf_scan<false>(P, G, E, spos, sidx, start, keys, kBlock, threadIdx.x);
             E.count = m;
             if (m > kLdsRows && m <= kHocbfCap) {
-                qslot[subq_append(hardq, bx % kSubQ, qcap)] = slot;
+                const long rec = subq_append(hardq, bx % kSubQ, qcap);
+                if (rec >= 0) qslot[rec] = slot;  // (always: the queue holds every agent)
             } else if (m > 0 && m <= kLdsRows) {
                 const Sol S = hocbf_solve_lds<kLdsRows, true>(P, H, E, spos, svel, keys, reinterpret_cast<double*>(keys),
                                                         kBlock, threadIdx.x, m);

@@ -226,7 +226,10 @@ __device__ __forceinline__ void ego_finish(const KP& P, Ego& E, int w, int k, in
             ego_output<ST>(P, E, S, false, k, T, pos_out, u, status, cnt, O);
             return;
         }
-        HardRec& h = qrec[subq_append(hardq, q, qcap)];
+        const long rec = subq_append(hardq, q, qcap);
+        O.res = 2;
+        if (rec < 0) return;  // (unreachable: the queue holds every agent and is emptied every advance)
+        HardRec& h = qrec[rec];
         h.r0 = E.r0;
         h.r1 = E.r1;
         h.r2 = E.r2;
@@ -242,7 +245,6 @@ __device__ __forceinline__ void ego_finish(const KP& P, Ego& E, int w, int k, in
         h.k = k;
         h.row = w;
         h.slot = slot;
-        O.res = 2;
         return;
     }
     ego_output<ST>(P, E, S, idle, k, T, pos_out, u, status, cnt, O);
