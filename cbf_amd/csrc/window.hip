@@ -52,6 +52,7 @@ namespace {
 #define CBF_PREP_WPE 1  // waves per SIMD the build kernel's registers are fitted to (1: no fit)
 #endif
 constexpr int kPrepBlock = CBF_PREP_BLOCK;
+constexpr int kPrepWideRows = 256;  // windows of at most this many rows: 2 kPrepBlock threads per row
 constexpr int kWinMaxW = 2048;                  // rows of up to 2048 agents
 
 // The guard arrays in the workspace's record area (cs, 16 B per agent, unused by this path).
@@ -140,8 +141,8 @@ __device__ __forceinline__ double gmax(double a, double b) {
 // halo-guard extents (ext_keys, nullable).  copy_to (nullable) gets a copy of the positions (the
 // run's ping-pong start).  The row is staged in LDS (dynamic, 24 B per column): every global load
 // and store is coalesced, and the row scans run over contiguous chunks of it.
-template <int PER>  // columns per thread: W <= kPrepBlock x PER (PER <= 16)
-__global__ void __launch_bounds__(kPrepBlock) __attribute__((amdgpu_waves_per_eu(CBF_PREP_WPE))) k_window_prep(WinGeom Q, const double2* __restrict__ pos,
+template <int PER, int NT>  // columns per thread (W <= NT x PER), threads of the block
+__global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(CBF_PREP_WPE))) k_window_prep(WinGeom Q, const double2* __restrict__ pos,
                                                             double2* __restrict__ u0, float2* __restrict__ rsp,
                                                             WinGuard Gd, double gain, double2* __restrict__ vel_out,
                                                             double2* __restrict__ copy_to, int32_t* __restrict__ sctl,
@@ -150,8 +151,8 @@ __global__ void __launch_bounds__(kPrepBlock) __attribute__((amdgpu_waves_per_eu
     extern __shared__ double2 srow[];  // [W] positions, then [W] float2 {rs, rp}
     const int W = Q.W;
     float2* srsp = reinterpret_cast<float2*>(srow + W);
-    __shared__ double red4[4][kPrepBlock / 64];
-    __shared__ unsigned long long ered[6][kPrepBlock / 64];
+    __shared__ double red4[4][NT / 64];
+    __shared__ unsigned long long ered[6][NT / 64];
     __shared__ int arrive;
     const int r = Q.cr0 + xcd_block();      // window row
     const int rl = Q.row0 + r;              // lattice row
@@ -170,7 +171,7 @@ __global__ void __launch_bounds__(kPrepBlock) __attribute__((amdgpu_waves_per_eu
     double2 p[PER], qu[PER], qd[PER];
 #pragma unroll
     for (int j = 0; j < PER; ++j) {
-        const int c = threadIdx.x + j * kPrepBlock;
+        const int c = threadIdx.x + j * NT;
         if (c < W) {
             p[j] = prow[c];
             if (lap && rl > 0) qu[j] = prow[c - W];
@@ -179,7 +180,7 @@ __global__ void __launch_bounds__(kPrepBlock) __attribute__((amdgpu_waves_per_eu
     }
 #pragma unroll
     for (int j = 0; j < PER; ++j) {
-        const int c = threadIdx.x + j * kPrepBlock;
+        const int c = threadIdx.x + j * NT;
         if (c < W) {
             srow[c] = p[j];
             if (copy_to) copy_to[(long)r * W + c] = p[j];
@@ -190,7 +191,7 @@ __global__ void __launch_bounds__(kPrepBlock) __attribute__((amdgpu_waves_per_eu
     double ylo = INFINITY, yhi = -INFINITY;
 #pragma unroll
     for (int j = 0; j < PER; ++j) {
-        const int c = threadIdx.x + j * kPrepBlock;
+        const int c = threadIdx.x + j * NT;
         if (c >= W) continue;
         const long w = (long)r * W + c;
         const double2 pi = p[j];
@@ -235,14 +236,14 @@ __global__ void __launch_bounds__(kPrepBlock) __attribute__((amdgpu_waves_per_eu
     bool ok = true;
 #pragma unroll
     for (int j = 0; j < PER; ++j) {
-        const int c = threadIdx.x + j * kPrepBlock;
+        const int c = threadIdx.x + j * NT;
         if (c < W) {
             ok = ok && isfinite(p[j].x) && isfinite(p[j].y);
             if (c + 1 < W) ok = ok && p[j].x <= srow[c + 1].x;
         }
     }
     const bool sorted = __syncthreads_and(ok) != 0;
-    const int m = (W + kPrepBlock - 1) / kPrepBlock;
+    const int m = (W + NT - 1) / NT;
     const int c0 = threadIdx.x * m;
     double sm[PER], pm[PER];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -288,7 +289,7 @@ __global__ void __launch_bounds__(kPrepBlock) __attribute__((amdgpu_waves_per_eu
     __syncthreads();
     double after = sx, before = px, lo = INFINITY, hi = -INFINITY;
 #pragma unroll
-    for (int q = 0; q < kPrepBlock / 64; ++q) {
+    for (int q = 0; q < NT / 64; ++q) {
         if (q > wid) after = gmin(after, red4[0][q]);
         if (q < wid) before = gmax(before, red4[1][q]);
         lo = gmin(lo, red4[2][q]);
@@ -312,7 +313,7 @@ __global__ void __launch_bounds__(kPrepBlock) __attribute__((amdgpu_waves_per_eu
         const bool comp = rl >= row_begin && rl < row_end, own = rl >= X.own_begin && rl < X.own_end;
 #pragma unroll
         for (int j = 0; j < PER; ++j) {
-            const int c = threadIdx.x + j * kPrepBlock;
+            const int c = threadIdx.x + j * NT;
             if (c >= W) continue;
             const double y = p[j].y;
             py = y;
@@ -329,13 +330,13 @@ __global__ void __launch_bounds__(kPrepBlock) __attribute__((amdgpu_waves_per_eu
                 any = 1;
             }
         }
-        ext_keys_flush<kPrepBlock / 64, false>(e, any, py, ext_keys, r, ered, &arrive);
+        ext_keys_flush<NT / 64, false>(e, any, py, ext_keys, r, ered, &arrive);
     }
     if (!sorted) {
         __syncthreads();
 #pragma unroll
         for (int j = 0; j < PER; ++j) {
-            const int c = threadIdx.x + j * kPrepBlock;
+            const int c = threadIdx.x + j * NT;
             if (c < W) rsp[(long)r * W + c] = srsp[c];
         }
     }
@@ -826,11 +827,16 @@ int window_counters(const void* workspace, size_t workspace_bytes, uint64_t* out
 void window_prep(const CellWs& Wk, const WinGeom& Q, const double2* pos, double gain, double2* vel_out,
                  double2* copy_to, unsigned long long* ext_keys, int row_begin, int row_end, ExtSpec X,
                  bool fold, hipStream_t s) {
-    const auto prep = Q.W <= 2 * kPrepBlock   ? k_window_prep<2>
-                      : Q.W <= 4 * kPrepBlock ? k_window_prep<4>
-                      : Q.W <= 8 * kPrepBlock ? k_window_prep<8>
-                                              : k_window_prep<16>;
-    hipLaunchKernelGGL(prep, dim3(Q.cr1 - Q.cr0), dim3(kPrepBlock), 24 * (size_t)Q.W, s, Q, pos, Wk.svel,
+    // one block per row; a window of few rows (one block per CU or fewer) takes 512-thread blocks,
+    // whose shorter per-thread chains end its latency-bound launch sooner (128 rows of 1,024
+    // agents: 6.2 against 7.0 us; at 1,024 rows 256 threads are faster, 11.8 against 13.9 us)
+    const bool wide = Q.cr1 - Q.cr0 <= kPrepWideRows;
+    const int nt = wide ? 2 * kPrepBlock : kPrepBlock;
+    const auto prep = wide ? (Q.W <= 2 * nt ? k_window_prep<2, 2 * kPrepBlock> : k_window_prep<4, 2 * kPrepBlock>)
+                           : (Q.W <= 2 * nt   ? k_window_prep<2, kPrepBlock>
+                              : Q.W <= 4 * nt ? k_window_prep<4, kPrepBlock>
+                                              : k_window_prep<8, kPrepBlock>);
+    hipLaunchKernelGGL(prep, dim3(Q.cr1 - Q.cr0), dim3(nt), 24 * (size_t)Q.W, s, Q, pos, Wk.svel,
                        win_rsp(Wk), win_guard(Wk, Q.rows), gain, vel_out, copy_to, Wk.sctl, Wk.ncell, ext_keys,
                        row_begin, row_end, X, fold ? kGuardInFilter : kGuardSeparate);
     if (!fold)  // (else the filter's first block forms the row guard)
