@@ -28,6 +28,9 @@ struct ExtSpec {
 // barrier at the end (it would hold every wave until the block's slowest is done), and a quarter
 // of the per-wave atomics.  ONE: each lane holds at most one agent (its e[] are y or infinite,
 // which allows a two-reduction fast path).  Every lane of the wave must call it.
+template <int NW>
+__device__ __forceinline__ void ext_keys_combine(unsigned long long (&k)[6], unsigned long long* __restrict__ ext_keys,
+                                                 long slot, unsigned long long (*red)[NW], int* arrive);
 template <int NW, bool ONE = true>
 __device__ __forceinline__ void ext_keys_flush(double (&e)[6], int any, double y,
                                                unsigned long long* __restrict__ ext_keys, long slot,
@@ -56,6 +59,34 @@ __device__ __forceinline__ void ext_keys_flush(double (&e)[6], int any, double y
 #pragma unroll
         for (int q = 0; q < 6; ++q) k[q] = ext_is_min(q) ? wave_umin64(dkey(e[q])) : wave_umax64(dkey(e[q]));
     }
+    ext_keys_combine<NW>(k, ext_keys, slot, red, arrive);
+}
+
+// The same for a block whose agents share one membership pattern (one lattice row: code bits
+// 1 computed, 2 owned below the guard, 4 owned above it, 8 owned), from each lane's minimum lo
+// (pmin) and maximum hi (NaN-propagating) over its agents: two wave reductions instead of six.
+template <int NW>
+__device__ __forceinline__ void ext_keys_flush_row(double lo, double hi, int any, unsigned code,
+                                                   unsigned long long* __restrict__ ext_keys, long slot,
+                                                   unsigned long long (*red)[NW], int* arrive) {
+    const unsigned long long kmin_id = dkey(INFINITY), kmax_id = dkey(-INFINITY);
+    const unsigned long long mn = wave_umin64(any ? dkey(lo) : kmin_id), mx = wave_umax64(any ? dkey(hi) : kmax_id);
+    unsigned long long k[6];
+    k[0] = (code & 1u) ? mn : kmin_id;
+    k[1] = (code & 1u) ? mx : kmax_id;
+    k[2] = (code & 2u) ? mx : kmax_id;
+    k[3] = (code & 4u) ? mn : kmin_id;
+    k[4] = (code & 8u) ? mn : kmin_id;
+    k[5] = (code & 8u) ? mx : kmax_id;
+    ext_keys_combine<NW>(k, ext_keys, slot, red, arrive);
+}
+
+// the block-level half of the flushes: the last wave to arrive combines the partials and issues
+// one atomic per non-identity value
+template <int NW>
+__device__ __forceinline__ void ext_keys_combine(unsigned long long (&k)[6], unsigned long long* __restrict__ ext_keys,
+                                                 long slot, unsigned long long (*red)[NW], int* arrive) {
+    const unsigned long long kmin_id = dkey(INFINITY), kmax_id = dkey(-INFINITY);
     if ((threadIdx.x & 63) != 0) return;
     const int wid = threadIdx.x >> 6;
 #pragma unroll

@@ -306,31 +306,23 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(CBF_PRE
         // the sharded step's halo-guard extents of this build's input positions (as the cell-list
         // bin kernel accumulates them, every agent of the row, non-finite ones included): {min,
         // max} over the computed rows, {max below the guard, min above it, min, max} over the owned
-        double e[6] = {INFINITY, -INFINITY, -INFINITY, INFINITY, INFINITY, -INFINITY};
+        // (the membership is the row's: each thread's minimum and maximum over its columns, then
+        // two wave reductions)
         auto nmax = [](double mm, double y) { return (y > mm || y != y) ? y : mm; };
-        int any = 0;
-        double py = 0.0;
         const bool comp = rl >= row_begin && rl < row_end, own = rl >= X.own_begin && rl < X.own_end;
+        const unsigned code = (comp ? 1u : 0u) | (own && rl < X.own_end - X.guard ? 2u : 0u) |
+                              (own && rl >= X.own_begin + X.guard ? 4u : 0u) | (own ? 8u : 0u);
+        double lo = INFINITY, hi = -INFINITY;
+        int any = 0;
 #pragma unroll
         for (int j = 0; j < PER; ++j) {
             const int c = threadIdx.x + j * NT;
             if (c >= W) continue;
-            const double y = p[j].y;
-            py = y;
-            if (comp) {
-                e[0] = pmin(e[0], y);
-                e[1] = nmax(e[1], y);
-                any = 1;
-            }
-            if (own) {
-                if (rl < X.own_end - X.guard) e[2] = nmax(e[2], y);
-                if (rl >= X.own_begin + X.guard) e[3] = pmin(e[3], y);
-                e[4] = pmin(e[4], y);
-                e[5] = nmax(e[5], y);
-                any = 1;
-            }
+            lo = pmin(lo, p[j].y);
+            hi = nmax(hi, p[j].y);
+            any = 1;
         }
-        ext_keys_flush<NT / 64, false>(e, any, py, ext_keys, r, ered, &arrive);
+        ext_keys_flush_row<NT / 64>(lo, hi, any && code != 0u, code, ext_keys, r, ered, &arrive);
     }
     if (!sorted) {
         __syncthreads();
