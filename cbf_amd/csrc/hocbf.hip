@@ -491,37 +491,232 @@ __global__ void __launch_bounds__(kBlock) k_lattice_filter_hocbf(
     if (ext_part) wave_extents(e0, e1, e2, e3, ext_part, (long)bx * (kBlock / 64) + (threadIdx.x >> 6));
 }
 
-// The queued egos (kLdsRows < m <= kHocbfCap), the sub-queues drained in full waves (drain_subq):
-// rescan, all rows in this block's LDS, same solve.
+// ---- the wide egos (kLdsRows < m <= kHocbfCap): one ego per wave, its rows across the lanes ----
+// A lane-per-ego solve of such an ego is a chain of O(m^2) dependent row steps (up to 24 rows,
+// ~90 % of the QPs solved twice for the +1 relaxation); here lane i holds row i, so the feasibility
+// tests of every row run at once and only the interval fold of solve_rows stays serial.
+
+// lane l's double, read wave-uniformly (l uniform)
+__device__ __forceinline__ double rdl(double v, int l) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readlane((int)b, l), hi = __builtin_amdgcn_readlane((int)(b >> 32), l);
+    return __hiloint2double(hi, lo);
+}
+
+// Interval::add with the row's ad and r already formed (the same expressions, in the lane)
+__device__ __forceinline__ void interval_add(Interval& I, double ad, double r) {
+    if (ad > 0) {
+        if (!I.has_hi || r * I.ah < I.rh * ad) {
+            I.rh = r;
+            I.ah = ad;
+        }
+        I.has_hi = true;
+    } else if (ad < 0) {
+        if (!I.has_lo || r * I.al > I.rl * ad) {
+            I.rl = r;
+            I.al = ad;
+        }
+        I.has_lo = true;
+    }
+}
+
+// solve_rows over the 4 box planes and the m rows held one per lane (a0, a1, b of lane i = row i):
+// the same events in the same order with the same arithmetic.  The next event is the first row
+// at or after i infeasible at the current x (one ballot: the sequential loop skips exactly the
+// feasible rows before it); its interval folds the box planes, then rows 0 .. i-1 in row order
+// (their ad and r formed in every lane at once, the fold itself serial, as the comparisons are);
+// the check after the step is one ballot over rows 0 .. i.
+__device__ __forceinline__ int solve_rows_wave(const double (&bb)[4], double a0, double a1, double b, int m, int lane,
+                                               double& xo0, double& xo1) {
+    const double ba0[4] = {1.0, 0.0, -1.0, 0.0}, ba1[4] = {0.0, 1.0, 0.0, -1.0};
+    double x0 = 0.0, x1 = 0.0;
+#pragma unroll
+    for (int h = 0; h < 4; ++h) {  // box planes: solve_rows' own code (wave-uniform)
+        if (feas(ba0[h], ba1[h], bb[h], x0, x1)) continue;
+        const double n2 = ba0[h] * ba0[h] + ba1[h] * ba1[h];
+        const double t = bb[h] / n2;
+        const double p0 = t * ba0[h], p1 = t * ba1[h];
+        const double d0 = -ba1[h], d1 = ba0[h];
+        Interval I;
+#pragma unroll
+        for (int j = 0; j < h; ++j) I.add(ba0[j], ba1[j], bb[j], d0, d1, p0, p1);
+        const double s = I.clamp0();
+        x0 = p0 + s * d0;
+        x1 = p1 + s * d1;
+        bool ok = true;
+#pragma unroll
+        for (int j = 0; j <= h; ++j) ok = ok && feas(ba0[j], ba1[j], bb[j], x0, x1);
+        if (!ok) return h;
+    }
+    const bool mine = lane < m;
+    int i = 0;
+    for (;;) {
+        const unsigned long long bad = __ballot(mine && lane >= i && !feas(a0, a1, b, x0, x1));
+        if (!bad) break;
+        const int e = __ffsll((long long)bad) - 1;
+        const double ea0 = rdl(a0, e), ea1 = rdl(a1, e), eb = rdl(b, e);
+        const double n2 = ea0 * ea0 + ea1 * ea1;
+        if (!(n2 > 0)) return 4 + e;
+        const double t = eb / n2;
+        const double p0 = t * ea0, p1 = t * ea1;
+        const double d0 = -ea1, d1 = ea0;
+        Interval I;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) I.add(ba0[j], ba1[j], bb[j], d0, d1, p0, p1);
+        const double ad = a0 * d0 + a1 * d1;
+        const double r = b - (a0 * p0 + a1 * p1);
+        for (int j = 0; j < e; ++j) interval_add(I, rdl(ad, j), rdl(r, j));
+        const double s = I.clamp0();
+        x0 = p0 + s * d0;
+        x1 = p1 + s * d1;
+        bool ok = true;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) ok = ok && feas(ba0[j], ba1[j], bb[j], x0, x1);
+        if (!ok) return 4 + e;
+        if (__ballot(mine && lane <= e && !feas(a0, a1, b, x0, x1))) return 4 + e;
+        i = e + 1;
+    }
+    xo0 = x0;
+    xo1 = x1;
+    return -1;
+}
+
+// solve_hocbf over the lanes' rows: +1 relaxation of every row while infeasible
+__device__ __forceinline__ Sol solve_hocbf_wave(const KP& P, const Ego& E, double a0, double a1, double b, int m,
+                                                int lane) {
+    const Box B = box_rhs(P, E);
+    const double bb[4] = {pmin(B.S[0], B.S[4]), pmin(B.S[1], B.S[6]), pmin(B.S[2], B.S[5]), pmin(B.S[3], B.S[7])};
+    Sol S;
+    S.status = CBF_STATUS_OPTIMAL;
+    S.iters = 0;
+    S.x0 = S.x1 = 0.0;
+    S.viol = 0.0;
+    for (;;) {
+        const int fail = solve_rows_wave(bb, a0, a1, b, m, lane, S.x0, S.x1);
+        if (fail < 0) break;
+        if (fail < 4) {
+            S.status = CBF_STATUS_BOX_INFEASIBLE;
+            S.x0 = S.x1 = 0.0;
+            break;
+        }
+        if (S.iters >= P.relax_cap) {
+            S.status = CBF_STATUS_RELAX_CAP;
+            S.x0 = S.x1 = 0.0;
+            break;
+        }
+        b = b + 1.0;  // cbf.py:85-87
+        S.iters++;
+        S.status = CBF_STATUS_RELAXED;
+    }
+    return S;
+}
+
+// 64-bit keys sorted ascending across the wave (bitonic network; lane i gets the i-th smallest)
+__device__ __forceinline__ unsigned long long wave_sort64(unsigned long long key, int lane) {
+#pragma unroll
+    for (int k = 2; k <= 64; k <<= 1)
+#pragma unroll
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            const unsigned lo = __shfl_xor((unsigned)key, j, 64), hi = __shfl_xor((unsigned)(key >> 32), j, 64);
+            const unsigned long long o = ((unsigned long long)hi << 32) | lo;
+            const bool keep_min = ((lane & j) == 0) == ((lane & k) == 0);
+            key = keep_min ? (o < key ? o : key) : (o > key ? o : key);
+        }
+    return key;
+}
+
+// The queued egos, one per 64-lane block (sub-queue q's entries k, k + nwork, ... for its k-th
+// working block): the 3x3-cell candidates tested one per lane, the hits' keys (entity << 32 |
+// slot) sorted across the lanes into the reference's row order, lane i forms row i, then the
+// wave's solve.  The same neighbour set, rows and solve as hocbf_scan + hocbf_solve_lds, bit for
+// bit.  More candidates than lanes are taken 64 at a time into LDS.
 __global__ void __launch_bounds__(64) k_lattice_filter_hocbf_wide(
     KP P, HP H, CellGrid G, int W, int row_begin, int row_end, int win_row0, const double2* __restrict__ spos,
     const double2* __restrict__ svel, const int32_t* __restrict__ sidx, const int32_t* __restrict__ start, double T,
     double2* __restrict__ pos_out, double2* __restrict__ u, int32_t* __restrict__ status, int32_t* __restrict__ cnt,
     int guard_rows, double* __restrict__ ext_part, unsigned long long* __restrict__ solves,
     int32_t* __restrict__ hardq, const int32_t* __restrict__ qslot, long qcap) {
-    __shared__ double rows[3 * kHocbfCap * 64];  // the keys live in its first third until read out
-    unsigned long long* keys = reinterpret_cast<unsigned long long*>(rows);
+    __shared__ unsigned long long hits[kHocbfCap + 64];
+    const int lane = threadIdx.x;
     double e0 = INFINITY, e1 = -INFINITY, e2 = -INFINITY, e3 = INFINITY;
     int ns = 0;
-    drain_subq(hardq, kWidePerQ, qcap, [&](int q, int i) {
-        const int slot = qslot[(long)q * qcap + i];
+    const int q = blockIdx.x % kSubQ, k = blockIdx.x / kSubQ;
+    const int nq0 = hardq[32 * (1 + q)];
+    const int nq = nq0 < qcap ? nq0 : (int)qcap;  // (a full sub-queue's counter runs past qcap: subq_append)
+    const int nwork = nq < kWidePerQ ? nq : kWidePerQ;
+    if (k >= nwork) return;
+    int done = 0;
+    if (lane == 0) done = atomicAdd(&hardq[32 * (1 + kSubQ + q)], 1);
+    for (int it = k; it < nq; it += nwork) {
+        const int slot = qslot[(long)q * qcap + it];
         const int w = sidx[slot];
         const int r = win_row0 + w / W, c = w % W;
         const double2 pe = spos[slot], ve = svel[slot];
         Ego E;
         ego_init(P, E, pe.x, pe.y, ve.x, ve.y, ve.x, ve.y);
-        const int m = hocbf_scan(P, G, E, spos, sidx, start, keys, 64, threadIdx.x);
+        // candidates: the three cell-row ranges of hocbf_scan as one sequence, a lane each
+        const int cx = cell_coord(E.r0, G.x0, G.inv_h, G.nx);
+        const int cy = cell_coord(E.r1, G.y0, G.inv_h, G.ny);
+        const int xa = cx > 0 ? cx - 1 : 0;
+        const int xb = cx < G.nx - 1 ? cx + 1 : G.nx - 1;
+        int t0[3], t1[3];
+#pragma unroll
+        for (int kk = 0; kk < 3; ++kk) {
+            const int yy = cy + kk - 1;
+            const bool in = yy >= 0 && yy < G.ny;
+            t0[kk] = in ? start[yy * G.nx + xa] : 0;
+            t1[kk] = in ? start[yy * G.nx + xb + 1] : 0;
+        }
+        const int l0 = t1[0] - t0[0], l01 = l0 + (t1[1] - t0[1]), L = l01 + (t1[2] - t0[2]);
+        int m = 0;
+        for (int v0 = 0; v0 < L; v0 += 64) {
+            const int v = v0 + lane;
+            bool hit = false;
+            unsigned long long key = 0;
+            if (v < L) {
+                const int t = v < l0 ? t0[0] + v : (v < l01 ? t0[1] + (v - l0) : t0[2] + (v - l01));
+                const double2 pq = spos[t];
+                const double q0 = pq.x - E.r0, q1 = pq.y - E.r1;
+                const double sq = q0 * q0 + q1 * q1;
+                hit = sq < P.cull_t && sq > 0;  // agents only (cross_and_rescue.py:147-150)
+                key = ((unsigned long long)(unsigned)sidx[t] << 32) | (unsigned)t;
+            }
+            const unsigned long long mk = __ballot(hit);
+            const int at = m + __popcll(mk & ((1ull << lane) - 1ull));
+            if (hit && at < kHocbfCap + 64) hits[at] = key;
+            m += __popcll(mk);
+        }
+        __syncthreads();  // (the block is this one wave: orders the hit list's writes before its reads)
         E.count = m;
-        const Sol S = hocbf_solve_lds<kHocbfCap>(P, H, E, spos, svel, keys, rows, 64, threadIdx.x, m);
-        ++ns;
-        hocbf_finish(P, &S, E, m, W, row_begin, row_end, r, c, T, pos_out, u, status, cnt, guard_rows, e0, e1, e2,
-                     e3);
-    });
-    if (solves) {
-        int t = (int)ns;
-        for (int o = 32; o > 0; o >>= 1) t += __shfl_xor(t, o, 64);
-        if (threadIdx.x == 0 && t) atomicAdd(&solves[16 * stat_slot(blockIdx.x)], (unsigned long long)t);
+        if (m > kHocbfCap) {  // (not queued by the main kernel; reported as it would be)
+            if (lane == 0)
+                hocbf_finish(P, nullptr, E, m, W, row_begin, row_end, r, c, T, pos_out, u, status, cnt, guard_rows,
+                             e0, e1, e2, e3);
+            continue;
+        }
+        // the reference's row order (ascending entity) across the lanes, then lane i's row
+        const unsigned long long key = wave_sort64(lane < m ? hits[lane] : ~0ull, lane);
+        double a0 = 0.0, a1 = 0.0, b = 0.0;
+        if (lane < m) {
+            const int sl = (int)(key & 0xFFFFFFFFull);
+            const double2 o = spos[sl], ov = svel[sl];
+            const double4 rw = hocbf_row(P, H, E.r0, E.r1, E.r2, E.r3, o.x, o.y, ov.x, ov.y, E.u0x, E.u0y);
+            a0 = rw.x;
+            a1 = rw.y;
+            b = rw.z;
+        }
+        const Sol S = solve_hocbf_wave(P, E, a0, a1, b, m, lane);
+        if (lane == 0) {
+            ++ns;
+            hocbf_finish(P, &S, E, m, W, row_begin, row_end, r, c, T, pos_out, u, status, cnt, guard_rows, e0, e1,
+                         e2, e3);
+        }
     }
+    if (lane == 0 && done == nwork - 1) {  // the last working block empties the sub-queue (drain_subq)
+        hardq[32 * (1 + q)] = 0;
+        hardq[32 * (1 + kSubQ + q)] = 0;
+    }
+    if (solves && lane == 0 && ns) atomicAdd(&solves[16 * stat_slot(blockIdx.x)], (unsigned long long)ns);
     if (ext_part) wave_extents(e0, e1, e2, e3, ext_part, blockIdx.x);
 }
 

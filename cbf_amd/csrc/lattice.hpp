@@ -341,9 +341,12 @@ void launch_extents_finalize(int nparts, const double* part, double* out, hipStr
 
 // partial extents: one record per wave of the filter grid, then one per hard-QP block
 inline long lattice_ext_waves(long win_n) { return (win_n + kBlock - 1) / kBlock * (kBlock / 64); }
-// the HOCBF wide kernel: kWidePerQ 64-lane blocks per sub-queue (~10 k queued egos at cfg4,
-// ~160 per sub-queue)
-constexpr int kWidePerQ = 4;
+// the HOCBF wide kernel: one queued ego per 64-lane block at a time, kWidePerQ blocks per
+// sub-queue (~10 k queued egos at cfg4, ~160 per sub-queue: 2-3 egos per block)
+#ifndef CBF_WIDE_PER_Q
+#define CBF_WIDE_PER_Q 64
+#endif
+constexpr int kWidePerQ = CBF_WIDE_PER_Q;
 inline int lattice_wide_blocks(long) { return kSubQ * kWidePerQ; }
 // the hard-QP kernel of the lattice step: kHardPerQ 64-lane blocks per sub-queue (2048 lanes: the
 // ~4.6 k entries per sub-queue at cfg4f in ~2 passes, the ~50 at cfg4 in one block)
