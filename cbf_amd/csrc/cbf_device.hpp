@@ -71,6 +71,19 @@ inline KP make_kp(const cbf_params* p) {
     return k;
 }
 
+#ifndef CBF_NT_STORES
+#define CBF_NT_STORES 0
+#endif
+// a streaming 16-B output store (non-temporal with CBF_NT_STORES: written through rather than left
+// dirty in L2 for the kernel's end)
+__device__ __forceinline__ void st_stream(double2* p, double2 v) {
+#if CBF_NT_STORES
+    __builtin_nontemporal_store(v.x, &p->x);
+    __builtin_nontemporal_store(v.y, &p->y);
+#else
+    *p = v;
+#endif
+}
 __device__ __forceinline__ double pmin(double a, double b) { return (b < a) ? b : a; }  // Python min(a, b)
 __device__ __forceinline__ double pmax(double a, double b) { return (b > a) ? b : a; }  // Python max(a, b)
 

@@ -213,7 +213,7 @@ __device__ __forceinline__ void ego_output(const KP& P, const Ego& E, const Sol&
         }
     }
     const double2 pn = make_double2(E.r0 + T * ux, E.r1 + T * uy);
-    pos_out[k] = pn;
+    st_stream(pos_out + k, pn);
     if (u) u[k] = make_double2(ux, uy);  // u / status / cnt: null in the inner timesteps of cbf_lattice_run
     if (status) status[k] = st;
     if (cnt) cnt[k] = E.count;

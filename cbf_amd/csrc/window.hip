@@ -220,7 +220,7 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(CBF_PRE
             }
             a = make_double2(a0 * gain, a1 * gain);
         }
-        u0[w] = a;
+        st_stream(u0 + w, a);
         if (vel_out && rl >= row_begin && rl < row_end) vel_out[(long)(rl - row_begin) * W + c] = a;
         if (isfinite(pi.x) && isfinite(pi.y)) {
             ylo = gmin(ylo, pi.y);
