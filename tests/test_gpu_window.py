@@ -37,11 +37,15 @@ def _oracle_rollout(pos, W, H, steps, pset="callers"):
     return outs
 
 
-def _check_steps(pos, W, H, steps, placement="auto", equal_nan=False, pset="callers"):
-    """step() of the window cull and of the cell list, every timestep against the oracle."""
+def _check_steps(pos, W, H, steps, placement="auto", equal_nan=False, pset="callers", stats=True):
+    """step() of the window cull and of the cell list, every timestep against the oracle.  stats=False:
+    the statistics-free kernels (with queued QPs, the window filter's timed instantiation, the one
+    the bench runs)."""
     runs = [swarm.LatticeSwarm(pos, W, H, gain=GAIN, params=paramsets.filter_params(pset, solve_placement=placement),
                                cull=c)
             for c in ("window", "cells")]
+    for L in runs:
+        L.collect_stats = stats
     for t, (vel, out, ref) in enumerate(_oracle_rollout(pos, W, H, steps, pset)):
         for L in runs:
             L.step()
@@ -56,8 +60,8 @@ def _check_steps(pos, W, H, steps, placement="auto", equal_nan=False, pset="call
 
 
 @pytest.mark.parametrize("pset", paramsets.NAMES)
-@pytest.mark.parametrize("placement", ["inline", "queued"])
-def test_window_scrambled_lattice_vs_oracle(placement, pset):
+@pytest.mark.parametrize("placement,stats", [("inline", True), ("queued", True), ("queued", False)])
+def test_window_scrambled_lattice_vs_oracle(placement, stats, pset):
     """Agents swapped with far-away ones (a lattice index no longer says where an agent is), so
     the row and column guards fail for their neighbours and those egos walk their rows outward;
     plus coincident agents (s = 0: not neighbours) and an exact-cutoff pair.  pset: the callers'
@@ -70,7 +74,9 @@ def test_window_scrambled_lattice_vs_oracle(placement, pset):
     pos[a], pos[b] = pos[b].copy(), pos[a].copy()
     pos[100] = pos[101]                        # coincident pair
     pos[300] = pos[301] + np.array([0.2, 0.0])  # s == 0.04 exactly is out (sqrt(s) < 0.2 fails)
-    _check_steps(pos, W, H, 5, placement, pset=pset)
+    runs = _check_steps(pos, W, H, 5, placement, pset=pset, stats=stats)
+    walks, _ = runs[0].window_counters()
+    assert walks > 0
 
 
 def test_window_dense_clump_overflows_hit_list():
