@@ -470,41 +470,6 @@ __device__ __forceinline__ float2 ld_rsp(const float2* __restrict__ a, int t) {
     return *reinterpret_cast<const float2*>(reinterpret_cast<const char*>(a) + ((uint32_t)t << 3));
 }
 
-// The unbounded form for one lane (rare): every row of [r - Kd, r + Ku] walked outward from the
-// ego's column until its sentinels hold, hits assembled row by row (ego_add: the overflow path of
-// the cell-list filter, same rows, same minima).
-template <bool FZ>
-__device__ __forceinline__ void win_direct(const KP& P, Ego& E, long w, int r, int c, int W, int Kd, int Ku,
-                                        const double2* __restrict__ pos, const double2* __restrict__ u0,
-                                        const float2* __restrict__ rsp, const int32_t* __restrict__ srt,
-                                        double& smin) {
-    E.bq0 = E.bq1 = E.bq2 = E.bq3 = INFINITY;
-    E.present = 0u;
-    E.count = 0;
-    smin = INFINITY;
-    auto cand = [&](long j) {
-        const double2 p = pos[j];
-        const double e0 = p.x - E.r0, e1 = p.y - E.r1;
-        const double s = e0 * e0 + e1 * e1;
-        if (!(s < P.cull_t && s > 0)) return;
-        smin = pmin(smin, s);
-        const double2 v = u0[j];
-        ego_add<FZ>(P, E, p.x, p.y, v.x, v.y);
-    };
-    for (int dr = -Kd; dr <= Ku; ++dr) {
-        const long b = w + (long)dr * W;
-        const bool so = srt[r + dr] != 0;  // a sorted row's column extents are its agents' own x
-        for (int dc = 0; c + dc < W; ++dc) {  // the column itself, then right
-            cand(b + dc);
-            if (c + dc + 1 >= W || (so ? pos[b + dc + 1].x : (double)rsp[b + dc + 1].x) - E.r0 > P.win_d) break;
-        }
-        for (int dc = -1; c + dc >= 0; --dc) {  // left
-            cand(b + dc);
-            if (c + dc - 1 < 0 || E.r0 - (so ? pos[b + dc - 1].x : (double)rsp[b + dc - 1].y) > P.win_d) break;
-        }
-    }
-}
-
 // ---- the window filter: LDS tiles -----------------------------------
 // A block is a tile of kTileR lattice rows x kTileW columns (one wave per tile row).  It stages
 // the tile plus kTileKS halo rows and kTileKC halo columns of positions, nominal controls and
@@ -529,6 +494,57 @@ struct TileLds {
     float2 g[kTileN];  // column extents (fp32, outward) of the staged agents
     double sy[kTileGuard], py[kTileGuard];
 };
+
+// The unbounded form for one lane (rare): every row of [r - Kd, r + Ku] walked outward from the
+// ego's column until its sentinels hold, hits assembled row by row (ego_add: the overflow path of
+// the cell-list filter, same rows, same minima).  With f = 0 (FZ), candidates and sentinels inside
+// the block's staged tile (rows tr0 .., columns tc0 .., kTileRows x kTileCols) are read from LDS,
+// the rest from memory: the walk is one lane's chain of dependent reads, and from LDS it no longer holds
+// its block into the launch's tail.  A staged sentinel is the fp32 column extent (a sorted row's:
+// its own x rounded outward), at most one ulp looser than the exact x: a walk stops at the same
+// column or one later, whose candidates then fail the cull test, so the hits are the same.
+template <bool FZ>
+__device__ __forceinline__ void win_direct(const KP& P, Ego& E, long w, int r, int c, int W, int Kd, int Ku,
+                                        const double2* __restrict__ pos, const double2* __restrict__ u0,
+                                        const float2* __restrict__ rsp, const int32_t* __restrict__ srt,
+                                        double& smin, const double2* lp, const double2* lu, const float2* lg,
+                                        int tr0, int tc0) {
+    E.bq0 = E.bq1 = E.bq2 = E.bq3 = INFINITY;
+    E.present = 0u;
+    E.count = 0;
+    smin = INFINITY;
+    auto cand = [&](long j, bool st, int li) {
+        const double2 p = st ? lp[li] : pos[j];
+        const double e0 = p.x - E.r0, e1 = p.y - E.r1;
+        const double s = e0 * e0 + e1 * e1;
+        if (!(s < P.cull_t && s > 0)) return;
+        smin = pmin(smin, s);
+        const double2 v = st ? lu[li] : u0[j];
+        ego_add<FZ>(P, E, p.x, p.y, v.x, v.y);
+    };
+    for (int dr = -Kd; dr <= Ku; ++dr) {
+        const long b = w + (long)dr * W;
+        const bool so = srt[r + dr] != 0;  // a sorted row's column extents are its agents' own x
+        const int lr = r + dr - tr0, lb = lr * kTileCols - tc0;
+        const bool srow = (unsigned)lr < (unsigned)kTileRows;
+        // (f = 0 only: the general instantiation's walk has no registers to spare for it)
+        auto staged = [&](int cc) { return FZ && srow && (unsigned)(cc - tc0) < (unsigned)kTileCols; };
+        for (int dc = 0; c + dc < W; ++dc) {  // the column itself, then right
+            const int cc = c + dc;
+            cand(b + dc, staged(cc), lb + cc);
+            if (cc + 1 >= W) break;
+            const double sx = staged(cc + 1) ? (double)lg[lb + cc + 1].x : (so ? pos[b + dc + 1].x : (double)rsp[b + dc + 1].x);
+            if (sx - E.r0 > P.win_d) break;
+        }
+        for (int dc = -1; c + dc >= 0; --dc) {  // left
+            const int cc = c + dc;
+            cand(b + dc, staged(cc), lb + cc);
+            if (cc - 1 < 0) break;
+            const double sx = staged(cc - 1) ? (double)lg[lb + cc - 1].y : (so ? pos[b + dc - 1].x : (double)rsp[b + dc - 1].y);
+            if (E.r0 - sx > P.win_d) break;
+        }
+    }
+}
 
 template <bool FZ, bool ST, bool IN>
 __global__ void __launch_bounds__(kTileT) __attribute__((amdgpu_waves_per_eu((IN || ST) ? 1 : CBF_TILE_WPE))) k_window_tile(KP P, WinBounds B, WinGeom Q, int er0, int tiles_x,
@@ -765,7 +781,7 @@ __global__ void __launch_bounds__(kTileT) __attribute__((amdgpu_waves_per_eu((IN
         } else if (fin) {  // the unbounded form, over the full row window (beyond the staged halo too)
             int kd, ku;
             win_rows(P, sylo, pyhi, r, Q.cr0, Q.cr1, E.r1, kd, ku, fold, token, stalls);
-            win_direct<FZ>(P, E, w, r, c, W, kd, ku, pos, u0, rsp, Gd.srt, d2);
+            win_direct<FZ>(P, E, w, r, c, W, kd, ku, pos, u0, rsp, Gd.srt, d2, L.p, L.u, L.g, r0 - kTileKS, c0 - kTileKC);
         }
         O.nbrs = E.count;
         if (ST) O.d2 = d2;
