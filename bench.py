@@ -323,6 +323,13 @@ def gather_state_sha(own, ws):
     return hashlib.sha256(x.cpu().numpy().tobytes()).hexdigest()
 
 
+def solves_inline(cp, n):
+    """Where a window of n agents solves its full QPs under the params cp actually passed
+    (include/cbf_amd_measure.h cbf_lattice_solves_inline): the filter kernel, or the queue kernel."""
+    from cbf_amd import _lib
+    return bool(_lib.lib.cbf_lattice_solves_inline(_lib.C.byref(cp), int(n)))
+
+
 def lattice_cull(args, sharded, rows=None):
     """The cull of the lattice step: --cull, or auto = the lattice-window cull (CBF_RUN_WINDOW_CULL)
     for a lattice that stays lattice-like (the consensus nominal control of cfg4 / cfg4f), the
@@ -616,7 +623,8 @@ def bench_lattice(args, ws, rank, local):
                                       if args.exchange == "neighbour" else "all-gather of ghost-row slabs")
                                    + f" per {k} steps ({halo * k} ghost rows per side)") if sharded else "single GPU",
                    "exchange_bytes_per_rank": S.exchange_bytes() if sharded else 0,
-                   "solve_placement": "inline in the filter" if rows * W <= 131072 else "queued (k_lattice_filter_hard)",
+                   "solve_placement": "inline in the filter" if solves_inline(S.cp, rows * W) else
+                                      "queued (k_lattice_filter_hard)",
                    "graph": use_graph,
                    "timesteps_per_call": max(plan) if chunk > 1 else 1},
         "timesteps_per_s": args.steps / elapsed,

@@ -70,6 +70,7 @@ _HP = C.POINTER(CbfHocbf)
 _CP, _UP = C.POINTER(CbfCertParams), C.POINTER(CbfUnicycleParams)
 SIGNATURES = {
     "cbf_abi_version": (C.c_int, []),
+    "cbf_lattice_solves_inline": (C.c_int, [_P, C.c_int64]),  # (include/cbf_amd_measure.h)
     "cbf_workspace_layout": (C.c_int, []),
     "cbf_params_init": (C.c_int, [_P, _d, _d, _d, _vp, _vp, _d]),
     "cbf_get_safe_control_batch": (C.c_int, [_P, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),

@@ -62,7 +62,11 @@ struct CellWs {
                       // workspace is bound to (0 = fresh); [8] lattice nominal-control mode, bytes
                       // 40..55 its amplitude (double) and seed (uint64) (cbf_lattice_set_nominal);
                       // [16] the window cull's guard-token count, [17] the row-guard mode of
-                      // its last build (window.hip kWinTokenWord / kWinModeWord)
+                      // its last build (window.hip kWinTokenWord / kWinModeWord); [20..21]
+                      // (uint64) egos that took the window cull's unbounded walk and [22..23]
+                      // (uint64) row-guard words read at their spin limit, both accumulated for
+                      // the workspace's life and checkpointed with it (window.hip kWinWalkWord /
+                      // kWinStallWord, cbf_lattice_window_counters)
     int32_t* count;   // [ncell]
     int32_t* start;   // [ncell + 1]
     unsigned long long* tstate;  // [ntiles] scan tile status {epoch:30 | flag:2 | value:32}

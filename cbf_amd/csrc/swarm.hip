@@ -7,6 +7,7 @@
 #include "cells.hpp"
 #include "lattice.hpp"
 #include "lattice_ego.hpp"
+#include "cbf_amd_measure.h"
 
 using namespace cbf;
 
@@ -768,6 +769,10 @@ extern "C" int cbf_lattice_advance(const cbf_params* p, const cbf_grid* grid, in
                                    void* workspace, size_t workspace_bytes, void* stream) {
     return lattice_advance(p, grid, W, H, row_begin, row_end, win_row0, win_rows, pos, T, pos_out, u, status, nbr_count,
                            guard_rows, extents, stats, workspace, workspace_bytes, row_begin, row_end, stream);
+}
+
+extern "C" int cbf_lattice_solves_inline(const cbf_params* p, int64_t n) {
+    return p && solve_inline(p, (long)n) ? 1 : 0;
 }
 
 extern "C" int cbf_lattice_advance_marked(const cbf_params* p, const cbf_grid* grid, int32_t W, int32_t H,

@@ -434,17 +434,17 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(FU ? 4 
         const bool comp = rl >= row_begin && rl < row_end, own = rl >= X.own_begin && rl < X.own_end;
         const unsigned code = (comp ? 1u : 0u) | (own && rl < X.own_end - X.guard ? 2u : 0u) |
                               (own && rl >= X.own_begin + X.guard ? 4u : 0u) | (own ? 8u : 0u);
-        double lo = INFINITY, hi = -INFINITY;
+        double elo = INFINITY, ehi = -INFINITY;  // (not the row's y extents lo / hi the row guard stores)
         int any = 0;
 #pragma unroll
         for (int j = 0; j < PER; ++j) {
             const int c = threadIdx.x + j * NT;
             if (c >= W) continue;
-            lo = pmin(lo, p[j].y);
-            hi = nmax(hi, p[j].y);
+            elo = pmin(elo, p[j].y);
+            ehi = nmax(ehi, p[j].y);
             any = 1;
         }
-        ext_keys_flush_row<NT / 64>(lo, hi, any && code != 0u, code, ext_keys, r, ered, &arrive);
+        ext_keys_flush_row<NT / 64>(elo, ehi, any && code != 0u, code, ext_keys, r, ered, &arrive);
     }
     if (!sorted) {
         __syncthreads();

@@ -444,8 +444,11 @@ class LatticeSwarm:
         pend = A["pending"]
         if pend is not None and pend[0].query():
             walks, stalls = int(A["host"][0]), int(A["host"][1])
-            frac = (walks - A["base"][0]) / max(1, pend[1] * self.n)
+            base = A["base"]
             A["base"], A["pending"] = (walks, stalls), None
+            if base is None:  # a baseline look only (after a restore or a capture: _auto_rebase)
+                return
+            frac = (walks - base[0]) / max(1, pend[1] * self.n)
             A["last_fraction"] = frac
             if frac > self.AUTO_WALK_FRACTION:
                 self.cull = "cells"
@@ -459,6 +462,13 @@ class LatticeSwarm:
             ev.record()
             A["pending"] = (ev, A["steps"])
             A["steps"] = 0
+
+    def _auto_rebase(self):
+        """cull="auto": the workspace counters hold walks of launches _auto_check never counted (a
+        restored workspace's whole history, a capture's warm-up launch), so the next look that lands
+        only sets the baseline and the decision waits for the one after it."""
+        if self._auto is not None:
+            self._auto["base"], self._auto["pending"] = None, None
 
     def history(self, steps):
         """The per-timestep outputs of the last run(steps, history=True): (vel, u, status,
@@ -557,6 +567,7 @@ class LatticeSwarm:
             launch()  # warm-up outside capture
         torch.cuda.current_stream().wait_stream(s)
         torch.cuda.synchronize()
+        self._auto_rebase()
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
             launch()
@@ -641,6 +652,7 @@ class LatticeSwarm:
                 raise ValueError(f"checkpoint {path}: state{i} does not fit this swarm ({a.shape}, {a.dtype} vs "
                                  f"{tuple(t.shape)}, {t.dtype})")
             t.copy_(_lib.require_gpu().from_numpy(a))
+        S._auto_rebase()  # the restored workspace carries the saved rollout's walk counts
         return S
 
     def step(self):

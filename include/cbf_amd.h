@@ -327,14 +327,6 @@ int cbf_lattice_window_advance(const cbf_params* p, const cbf_grid* grid, int32_
                                double T, double* pos_out, double* u, int32_t* status, int32_t* nbr_count,
                                uint64_t* stats, void* workspace, size_t workspace_bytes, void* filter_done,
                                void* stream);
-/* cbf_lattice_window_advance with the filter kernel launched so that filter_start / filter_stop
- * (hipEvent_t, both required, created beforehand) carry that dispatch's own start and end times
- * (hipExtLaunchKernel): the bench's measurement of the dominant kernel, free of the launch's
- * dispatch and end-of-kernel cache flush, as a kernel trace measures it.  (ABI 6) */
-int cbf_lattice_window_advance_timed(const cbf_params* p, const cbf_grid* grid, int32_t W, int32_t H,
-                                     const double* pos, double T, double* pos_out, double* u, int32_t* status,
-                                     int32_t* nbr_count, uint64_t* stats, void* workspace, size_t workspace_bytes,
-                                     void* filter_start, void* filter_stop, void* stream);
 /* The same for the owned rows [row_begin, row_end) of a window of win_rows lattice rows from
  * win_row0 (one sub-step of a sharded stripe); pos holds the window, pos_out the owned rows. */
 int cbf_lattice_window_build_ex(const cbf_params* p, const cbf_grid* grid, int32_t W, int32_t H, int32_t row_begin,
@@ -353,25 +345,14 @@ int cbf_lattice_advance(const cbf_params* p, const cbf_grid* grid, int32_t W, in
                         int32_t row_end, int32_t win_row0, int32_t win_rows, const double* pos, double T,
                         double* pos_out, double* u, int32_t* status, int32_t* nbr_count, int32_t guard_rows,
                         double* extents, uint64_t* solves, void* workspace, size_t workspace_bytes, void* stream);
-/* cbf_lattice_advance, recording `filter_done` (a hipEvent_t, nullable) on `stream` between the
- * filter kernel and the queued-QP kernel: the measurement hook for the dominant kernel alone. */
-int cbf_lattice_advance_marked(const cbf_params* p, const cbf_grid* grid, int32_t W, int32_t H, int32_t row_begin,
-                               int32_t row_end, int32_t win_row0, int32_t win_rows, const double* pos, double T,
-                               double* pos_out, double* u, int32_t* status, int32_t* nbr_count, int32_t guard_rows,
-                               double* extents, uint64_t* solves, void* workspace, size_t workspace_bytes,
-                               void* filter_done, void* stream);
-/* cbf_lattice_advance with the filter's own start / end times in filter_start / filter_stop (as
- * cbf_lattice_window_advance_timed).  (ABI 6) */
-int cbf_lattice_advance_timed(const cbf_params* p, const cbf_grid* grid, int32_t W, int32_t H, int32_t row_begin,
-                              int32_t row_end, int32_t win_row0, int32_t win_rows, const double* pos, double T,
-                              double* pos_out, double* u, int32_t* status, int32_t* nbr_count, int32_t guard_rows,
-                              double* extents, uint64_t* solves, void* workspace, size_t workspace_bytes,
-                              void* filter_start, void* filter_stop, void* stream);
 
 /* cbf_lattice_advance with Euclidean HOCBF rows (cbf_hocbf above): after cbf_lattice_build, the
  * filter of every owned agent over its 3x3-cell neighbours in ascending entity order, the HOCBF
  * QP, clip and Euler; same outputs, extents and solve counter as cbf_lattice_advance.  More than
  * 24 neighbours: CBF_STATUS_NBR_OVERFLOW (u = u0). */
+/* Measurement hooks (the bench's timed launches of the filter kernel alone) are declared in
+ * include/cbf_amd_measure.h: they are not part of the drop-in surface. */
+
 int cbf_lattice_advance_hocbf(const cbf_params* p, const cbf_hocbf* hp, const cbf_grid* grid, int32_t W, int32_t H,
                               int32_t row_begin, int32_t row_end, int32_t win_row0, int32_t win_rows,
                               const double* pos, double T, double* pos_out, double* u, int32_t* status,

@@ -13,10 +13,33 @@ from oracle import pyoracle as po
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def _declared():
-    src = open(os.path.join(ROOT, "include", "cbf_amd.h")).read()
-    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
-    return sorted(set(re.findall(r"^\s*(?:int|int64_t|size_t)\s+(cbf_\w+)\s*\(", src, flags=re.M)))
+HEADERS = ("cbf_amd.h", "cbf_amd_measure.h")  # the drop-in surface; the bench's measurement hooks
+
+
+def _declared(headers=HEADERS):
+    names = set()
+    for h in headers:
+        src = open(os.path.join(ROOT, "include", h)).read()
+        src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+        names |= set(re.findall(r"^\s*(?:int|int64_t|size_t)\s+(cbf_\w+)\s*\(", src, flags=re.M))
+    return sorted(names)
+
+
+def test_measurement_hooks_are_not_in_the_public_header():
+    public, hooks = set(_declared(("cbf_amd.h",))), set(_declared(("cbf_amd_measure.h",)))
+    assert hooks == {"cbf_lattice_advance_marked", "cbf_lattice_advance_timed", "cbf_lattice_window_advance_timed",
+                     "cbf_lattice_solves_inline"}
+    assert not public & hooks
+
+
+def test_solves_inline_query_follows_the_params():
+    from cbf_amd import _lib, swarm
+    for placement, n, want in (("inline", 1 << 30, 1), ("queued", 16, 0), (4096, 4096, 1), (4096, 4097, 0)):
+        cp = swarm.FilterParams(solve_placement=placement).c()
+        assert _lib.lib.cbf_lattice_solves_inline(C.byref(cp), n) == want, (placement, n)
+    cp = swarm.FilterParams().c()   # "auto": the library's threshold, inline for small windows only
+    assert _lib.lib.cbf_lattice_solves_inline(C.byref(cp), 1024) == 1
+    assert _lib.lib.cbf_lattice_solves_inline(C.byref(cp), 1 << 20) == 0
 
 
 def test_library_loads_and_exports_every_declared_symbol():

@@ -108,17 +108,24 @@ def test_window_edge_shapes(W, H):
     _check_steps(pos, W, H, 3)
 
 
-def test_window_nonfinite_positions_match_cells():
+@pytest.mark.parametrize("placement,stats", [("auto", True), ("inline", False), ("queued", True), ("queued", False)])
+def test_window_nonfinite_positions_match_cells(placement, stats):
     """Non-finite positions (NaN, +-inf) never pass the cull test and are left out of the guards'
     extents; the window cull then gives the cell list's results bit for bit (NaNs compared as
-    equal)."""
+    equal), with the QPs solved inline and queued.  The tile forms a quadrant's presence from its
+    minimum (a NaN or +inf row leaves it absent) where the cell list's assembly marks every hit
+    present; the solve is the same either way (a +inf plane never binds), so the egos next to a
+    non-finite neighbour -- a NaN nominal control makes their rows NaN -- must agree exactly."""
     W, H = 48, 32
     pos = scenarios.lattice(W, H, seed=25)
     pos[10] = [np.nan, 0.3]
     pos[500] = [np.inf, pos[500, 1]]
     pos[900] = [pos[900, 0], -np.inf]
-    A = swarm.LatticeSwarm(pos, W, H, gain=GAIN, cull="window")
-    B = swarm.LatticeSwarm(pos, W, H, gain=GAIN, cull="cells")
+    fp = paramsets.filter_params("callers", solve_placement=placement)
+    A = swarm.LatticeSwarm(pos, W, H, gain=GAIN, params=fp, cull="window")
+    B = swarm.LatticeSwarm(pos, W, H, gain=GAIN, params=fp, cull="cells")
+    A.collect_stats = B.collect_stats = stats
+    near = [9, 11, 10 + W, 499, 501, 500 - W, 899, 901, 900 + W]
     for _ in range(3):
         A.step()
         B.step()
@@ -126,6 +133,8 @@ def test_window_nonfinite_positions_match_cells():
         for x, y in ((A.pos, B.pos), (A.u, B.u), (A.vel, B.vel)):
             assert np.array_equal(x.cpu().numpy(), y.cpu().numpy(), equal_nan=True)
         assert torch.equal(A.status, B.status) and torch.equal(A.nbr_count, B.nbr_count)
+        assert np.array_equal(A.u[near].cpu().numpy(), B.u[near].cpu().numpy(), equal_nan=True)
+        assert torch.equal(A.status[near], B.status[near])
 
 
 @pytest.mark.parametrize("nominal", [None, ("random", 1.0, 5)])
@@ -389,3 +398,36 @@ def test_window_auto_switches_to_cells_when_the_swarm_scrambles():
         print(f"auto cull, nominal {nominal}: last walk fraction {A._auto.get('last_fraction')}, "
               f"walks {walks}, stalls {stalls}, switched after {A._auto.get('switched_after')}")
         assert stalls == 0 and (walks > 0 if switch else True)
+
+
+def test_window_auto_baseline_after_checkpoint_and_capture(tmp_path):
+    """cull="auto" after a restore and a capture: the workspace header's walk counter (kWinWalkWord,
+    word 20) carries walks _auto_check never counted -- the saved rollout's whole history, the
+    capture's warm-up launch -- so the first look after either only sets the baseline.  A consensus
+    lattice whose restored header claims 10^9 earlier walks must stay on the window cull, and its
+    rollout equals the cell list's bit for bit."""
+    W, H = 160, 128
+    pos = scenarios.lattice(W, H, seed=34, spacing=0.145)
+    A = swarm.LatticeSwarm(pos, W, H, gain=GAIN, cull="auto")
+    B = swarm.LatticeSwarm(pos, W, H, gain=GAIN, cull="cells")
+    A.run(4)
+    torch.cuda.synchronize()
+    A.ws[80:88] = torch.tensor([10 ** 9], dtype=torch.int64).view(torch.uint8).to(A.ws.device)
+    path = str(tmp_path / "auto.npz")
+    A.save_checkpoint(path)
+    R = swarm.LatticeSwarm.from_checkpoint(path)
+    assert R.cull_mode == "auto" and R.cull == "window" and R._auto["base"] is None
+    for _ in range(6):
+        R.run(4)
+        torch.cuda.synchronize()
+    R.collect_stats = False
+    R.capture(steps=4)  # the warm-up launch adds 4 timesteps outside _auto_check
+    for _ in range(6):
+        R.run(4)
+        torch.cuda.synchronize()
+    assert R.cull == "window", R._auto
+    B.run(4 + 24 + 4 + 24)
+    torch.cuda.synchronize()
+    for x, y in ((R.pos, B.pos), (R.u, B.u), (R.status, B.status)):
+        assert torch.equal(x, y)
+    assert R._auto.get("last_fraction") is not None and R._auto["last_fraction"] < R.AUTO_WALK_FRACTION
