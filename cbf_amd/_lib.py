@@ -21,7 +21,7 @@ STATUS_NBR_OVERFLOW = 5
 STATUS_WORKSPACE_ERROR = 6
 RUN_OUTPUT_HISTORY = 1  # cbf_lattice_run_ex flags (include/cbf_amd.h CBF_RUN_*)
 RUN_WINDOW_CULL = 2
-LAUNCH_SEPARATE_GUARD, LAUNCH_QUEUE_KERNEL = 1, 2  # cbf_params.launch_flags (include/cbf_amd.h CBF_LAUNCH_*)
+LAUNCH_SEPARATE_GUARD = 1  # cbf_params.launch_flags (include/cbf_amd.h CBF_LAUNCH_*)
 # words of a lattice-step statistics slot (include/cbf_amd.h CBF_STAT_*)
 (STAT_SOLVES, STAT_OPTIMAL, STAT_RELAXED, STAT_INFEASIBLE, STAT_SEIDEL, STAT_VIOL_OPTIMAL, STAT_VIOL_ORIGINAL,
  STAT_MIN_DIST2, STAT_ERRORS, STAT_BINDING, STAT_WIN_WALKS, STAT_GUARD_STALLS) = range(12)

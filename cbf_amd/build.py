@@ -38,7 +38,7 @@ def _compile(src: str, variant: str = "", defines=()) -> str:
     stamp = out + ".cmd"
     key = hashlib.sha256("\0".join(cmd).encode()).hexdigest()
     deps = [path] + [os.path.join(CSRC, h) for h in os.listdir(CSRC) if h.endswith(".hpp")] + \
-        [os.path.join(ROOT, "include", "cbf_amd.h")]
+        [os.path.join(ROOT, "include", h) for h in os.listdir(os.path.join(ROOT, "include")) if h.endswith(".h")]
     if os.path.exists(out) and os.path.getmtime(out) >= max(os.path.getmtime(d) for d in deps):
         try:
             with open(stamp) as f:

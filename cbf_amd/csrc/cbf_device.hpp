@@ -397,80 +397,9 @@ __device__ __forceinline__ int solve_planes_reg(const double (&a0)[N], const dou
     return -1;
 }
 
-// solve_planes_reg with the outer loop (the planes in slot order) rolled: one copy of the step
-// body instead of N, for kernels fitted to ~80 VGPRs (the window tile's own exact solves).  Same
-// arithmetic in the same order, so bit-identical: the plane of the step is selected by its slot
-// (exact copies), and the inner loops still run over the earlier slots in order with the same
-// predicates (a slot j >= h takes no part, as in the unrolled form's shorter loops).
-template <int N>
-__device__ __forceinline__ int solve_planes_rolled(const double (&a0)[N], const double (&a1)[N], const double (&b)[N],
-                                                   unsigned mask, double& xo0, double& xo1) {
-    // the tolerances formed where they are used (the same values), not held in registers
-    auto tb = [&](int j) { return FEAS_TOL * pmax(1.0, fabs(b[j])); };
-    double x0 = 0.0, x1 = 0.0;
-#pragma unroll 1
-    for (int h = 0; h < N; ++h) {
-        if (!((mask >> h) & 1u)) continue;
-        double ah0 = 0.0, ah1 = 0.0, bh = 0.0;
-#pragma unroll
-        for (int j = 0; j < N; ++j)
-            if (j == h) {
-                ah0 = a0[j];
-                ah1 = a1[j];
-                bh = b[j];
-            }
-        if ((ah0 * x0 + ah1 * x1) - bh <= FEAS_TOL * pmax(1.0, fabs(bh))) continue;
-        const double n2 = ah0 * ah0 + ah1 * ah1;
-        if (!(n2 > 0)) return h;
-        const double t = bh / n2;
-        const double p0 = t * ah0, p1 = t * ah1;
-        const double d0 = -ah1, d1 = ah0;
-        double rh = 0.0, ah = 0.0, rl = 0.0, al = 0.0;
-        bool has_hi = false, has_lo = false;
-#pragma unroll
-        for (int j = 0; j < N; ++j) {
-            if (j >= h || !((mask >> j) & 1u)) continue;
-            const double ad = a0[j] * d0 + a1[j] * d1;
-            const double r = b[j] - (a0[j] * p0 + a1[j] * p1);
-            if (ad > 0) {
-                if (!has_hi || r * ah < rh * ad) {
-                    rh = r;
-                    ah = ad;
-                }
-                has_hi = true;
-            } else if (ad < 0) {
-                if (!has_lo || r * al > rl * ad) {
-                    rl = r;
-                    al = ad;
-                }
-                has_lo = true;
-            }
-        }
-        double s = 0.0;
-        bool s_hi = false;
-        if (has_hi && rh < 0) {
-            s = rh / ah;
-            s_hi = true;
-        }
-        if (has_lo && (s_hi ? (rh * al > rl * ah) : (rl < 0))) s = rl / al;
-        x0 = p0 + s * d0;
-        x1 = p1 + s * d1;
-        bool ok = true;
-#pragma unroll
-        for (int j = 0; j < N; ++j)
-            if (j <= h && ((mask >> j) & 1u)) ok = ok && ((a0[j] * x0 + a1[j] * x1) - b[j] <= tb(j));
-        if (!ok) return h;
-    }
-    xo0 = x0;
-    xo1 = x1;
-    return -1;
-}
-
 // slots 0..3: merged box rows, 4..7: the CBF quadrants
-template <bool LEAN = false>
 __device__ __forceinline__ int solve8(const double (&a0)[8], const double (&a1)[8], const double (&b)[8],
                                       unsigned mask, double& xo0, double& xo1) {
-    if (LEAN) return solve_planes_rolled<8>(a0, a1, b, mask, xo0, xo1);
     return solve_planes_reg<8>(a0, a1, b, mask, xo0, xo1);
 }
 
@@ -500,9 +429,7 @@ __device__ __forceinline__ double orig_violation(const KP& P, const Ego& E, cons
 }
 
 // The QP of cbf.py:62-87 for an ego: merged box rows + per-quadrant CBF rows, with the
-// reference's +1 relaxation (cbf.py:84-87) applied while infeasible.  LEAN: the rolled plane loop
-// (solve_planes_rolled; bit-identical) for kernels that cannot spare the unrolled form's registers.
-template <bool LEAN = false>
+// reference's +1 relaxation (cbf.py:84-87) applied while infeasible.
 __device__ __forceinline__ Sol solve_ego(const KP& P, const Ego& E) {
     const Box B = box_rhs(P, E);
     double a0[8] = {1.0, 0.0, -1.0, 0.0, P.n0[0], P.n0[1], P.n0[2], P.n0[3]};
@@ -541,7 +468,7 @@ __device__ __forceinline__ Sol solve_ego(const KP& P, const Ego& E) {
         }
     }
     for (;;) {
-        const int fail = solve8<LEAN>(a0, a1, b, mask, S.x0, S.x1);
+        const int fail = solve8(a0, a1, b, mask, S.x0, S.x1);
         if (fail < 0) break;
         if (fail < 4) {  // reported as at the first solve: no relaxation applied
             S.status = CBF_STATUS_BOX_INFEASIBLE;

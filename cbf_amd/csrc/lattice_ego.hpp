@@ -231,15 +231,12 @@ __device__ __forceinline__ void ego_output(const KP& P, const Ego& E, const Sol&
 #define CBF_EVENT_IN_PLACE 8
 #endif
 constexpr int kEventInPlace = CBF_EVENT_IN_PLACE;
-// wrec >= 0 (the window tile's per-wave form, solved by the next build: k_window_prep FUSED):
-// the queued QPs of a wave go to records wrec, wrec + 1, ... in lane order, one per queueing lane,
-// with no atomic; else to sub-queue q.
 template <bool FZ, bool ST, bool IN>
 __device__ __forceinline__ void ego_finish(const KP& P, Ego& E, int w, int k, int slot, double T,
                                            double2* __restrict__ pos_out, double2* __restrict__ u,
                                            int32_t* __restrict__ status, int32_t* __restrict__ cnt,
                                            int32_t* __restrict__ hardq, int q, HardRec* __restrict__ qrec,
-                                           long qcap, EgoOut& O, long wrec = -1) {
+                                           long qcap, EgoOut& O) {
     Sol S;
     const bool idle = E.count == 0;
     // The queued form runs solve_fast's one-event stage only in a wave where more than
@@ -260,8 +257,7 @@ __device__ __forceinline__ void ego_finish(const KP& P, Ego& E, int w, int k, in
             ego_output<ST>(P, E, S, false, k, T, pos_out, u, status, cnt, O);
             return;
         }
-        const long rec = wrec >= 0 ? wrec + __popcll(__ballot(1) & ((1ull << (threadIdx.x & 63)) - 1ull))
-                                   : subq_append(hardq, q, qcap);
+        const long rec = subq_append(hardq, q, qcap);
         O.res = 2;
         if (rec < 0) return;  // (unreachable: the queue holds every agent and is emptied every advance)
         HardRec& h = qrec[rec];
@@ -301,28 +297,14 @@ bool window_cull_ok(int W, int rows, long n_ws, const CellWs& Wk);
 // launched with the build): cbf_params.launch_flags
 bool window_fold(const cbf_params* p);
 int window_counters(const void* workspace, size_t workspace_bytes, uint64_t* out, hipStream_t s);
-// The previous advance's queued QPs solved by the build (window_filter per_wave, then window_prep
-// with F): the advance's parameters, the positions it wrote (= the ones the build reads) and its
-// outputs (nullable).  Whole-lattice windows of W <= 4 x the build's threads (window_fusable).
-struct FusedHard {
-    KP P;
-    double T;
-    const HardRec* qrec;
-    double2* pos;     // the positions the build reads; the queued egos' new ones are written here
-    double2* u;       // the previous advance's outputs (nullable: an inner timestep of a run)
-    int32_t* status;
-    int32_t* cnt;
-};
-bool window_fusable(int W, int rows);
 void window_prep(const CellWs& Wk, const WinGeom& Q, const double2* pos, double gain, double2* vel_out,
                  double2* copy_to, unsigned long long* ext_keys, int row_begin, int row_end, ExtSpec X,
-                 bool fold, hipStream_t s, const FusedHard* F = nullptr);
+                 bool fold, hipStream_t s);
 // The filter kernel for the egos of lattice rows [row_begin, row_end) (pos_out must not overlap pos;
-// the queued QPs are left for k_lattice_filter_hard unless `in`; per_wave: left as per-wave records
-// for the next build, window_prep's FusedHard, instead).
+// the queued QPs are left for k_lattice_filter_hard unless `in`).
 void window_filter(const cbf_params* p, const CellWs& Wk, const WinGeom& Q, int row_begin, int row_end,
                    int cnt_begin, int cnt_end, const double2* pos, double T, double2* pos_out, double2* u,
                    int32_t* status, int32_t* cnt, unsigned long long* stats, bool in, hipStream_t s,
-                   hipEvent_t t_start = nullptr, hipEvent_t t_stop = nullptr, bool per_wave = false);
+                   hipEvent_t t_start = nullptr, hipEvent_t t_stop = nullptr);
 
 }  // namespace cbf

@@ -830,9 +830,6 @@ static void launch_hard_plain(const cbf_params* p, const cbf_grid* grid, const C
 // kernel.  The filter reads its input positions while writing new ones, so timesteps alternate
 // between pos and the workspace's spos: with an odd count the first build also copies pos to spos
 // and the first filter reads that copy, so the last timestep always writes pos.
-#ifndef CBF_FUSE_HARD
-#define CBF_FUSE_HARD 0  // (in development: the fused build measured slower than the queue kernel)
-#endif
 static int lattice_run_window(const cbf_params* p, const cbf_grid* grid, int32_t W, int32_t H, double* pos,
                               double gain, double T, int32_t steps, double* vel_out, double* u, int32_t* status,
                               int32_t* nbr_count, uint64_t* stats, void* workspace, bool hist, void* stream) {
@@ -841,11 +838,6 @@ static int lattice_run_window(const cbf_params* p, const cbf_grid* grid, int32_t
     CellWs Wk(workspace, n, (long)grid->nx * grid->ny);
     if (!window_cull_ok(W, H, n, Wk)) return CBF_EINVAL;
     const bool in = solve_inline(p, n);
-    // The queued QPs of every timestep but the last are solved by the next timestep's build
-    // (window_prep FusedHard: no queue-kernel launch per timestep) unless the statistics are on
-    // (the queue kernel counts them) or CBF_LAUNCH_QUEUE_KERNEL asks for the queue kernel.
-    const bool fuse = CBF_FUSE_HARD && !in && !stats && !(p->launch_flags & CBF_LAUNCH_QUEUE_KERNEL) &&
-                      window_fusable(W, H);
     double2* buf[2] = {reinterpret_cast<double2*>(pos), Wk.spos};
     const int odd = steps & 1;
     unsigned long long* st = reinterpret_cast<unsigned long long*>(stats);
@@ -854,26 +846,15 @@ static int lattice_run_window(const cbf_params* p, const cbf_grid* grid, int32_t
         double2* dst = buf[(k + 1 + odd) & 1];
         const bool last = k + 1 == steps, out = last || hist;
         const long o = hist ? (long)k * n : 0;
-        // the previous timestep's queued QPs, left for this build (its outputs are stored only with
-        // a history: an inner timestep's are overwritten)
-        FusedHard F;
-        const bool fused_in = fuse && k > 0;
-        if (fused_in) {
-            const long op = (long)(k - 1) * n;
-            F = FusedHard{make_kp(p), T, Wk.qrec, src, hist ? reinterpret_cast<double2*>(u) + op : nullptr,
-                          hist ? status + op : nullptr, hist && nbr_count ? nbr_count + op : nullptr};
-        }
         // an odd run's first build reads pos and leaves its copy in spos, which the filter then reads
         const WinGeom Q = whole_lattice(W, H);
         window_prep(Wk, Q, k == 0 && odd ? buf[0] : src, gain, out ? reinterpret_cast<double2*>(vel_out) + o : nullptr,
-                    k == 0 && odd ? buf[1] : nullptr, nullptr, 0, H, ExtSpec{0, 0, 0}, window_fold(p), s,
-                    fused_in ? &F : nullptr);
+                    k == 0 && odd ? buf[1] : nullptr, nullptr, 0, H, ExtSpec{0, 0, 0}, window_fold(p), s);
         double2* uo = out ? reinterpret_cast<double2*>(u) + o : nullptr;
         int32_t* so = out ? status + o : nullptr;
         int32_t* co = out && nbr_count ? nbr_count + o : nullptr;
-        const bool per_wave = fuse && !last;
-        window_filter(p, Wk, Q, 0, H, 0, H, src, T, dst, uo, so, co, st, in, s, nullptr, nullptr, per_wave);
-        if (!in && !per_wave) launch_hard_plain(p, grid, Wk, W, H, T, dst, uo, so, co, st, s);
+        window_filter(p, Wk, Q, 0, H, 0, H, src, T, dst, uo, so, co, st, in, s);
+        if (!in) launch_hard_plain(p, grid, Wk, W, H, T, dst, uo, so, co, st, s);
         if (int rc = (int)hipGetLastError()) return rc;
     }
     return 0;

@@ -62,7 +62,6 @@ struct WinGuard {
     double* pyhi;     // [H] max over rows <= r of the row maxima
     int32_t* srt;     // [H] 1: every agent of the row finite and x non-decreasing along it (then each
                       // agent's own x is its column extents, and the build stores none for the row)
-    int32_t* wq;      // [H tiles_x] queued QPs per tile wave (the fused form: k_window_tile -> k_window_prep)
 };
 inline WinGuard win_guard(const CellWs& Wk, int H) {
     WinGuard g;
@@ -71,7 +70,6 @@ inline WinGuard win_guard(const CellWs& Wk, int H) {
     g.sylo = g.rowy + 2l * H;
     g.pyhi = g.sylo + (H + 1);
     g.srt = reinterpret_cast<int32_t*>(g.pyhi + H);
-    g.wq = g.srt + H;
     return g;
 }
 // Control words of the window cull in the workspace header (fixed offsets, whatever the lattice
@@ -93,11 +91,7 @@ constexpr int32_t kGuardInFilter = 1, kGuardSeparate = 2;
 // record area on other paths; its words never carry the tag).  The count lives in the header, so
 // tokens keep increasing across culls and lattice shapes sharing a workspace.
 __host__ __device__ inline int32_t guard_token(int32_t v) { return (v & 0x00FFFFFF) | 0x5A000000; }
-constexpr int kTileWidth = 64;  // columns of a window-filter tile (one wave per tile row)
-__host__ __device__ inline int win_tiles_x(int W) { return (W + kTileWidth - 1) / kTileWidth; }
-inline size_t win_guard_bytes(int W, int H) {  // <= 16 W H for W >= 4
-    return 8 * (size_t)(4l * H + 2) + 4 * (size_t)H + 4 * (size_t)H * win_tiles_x(W);
-}
+inline size_t win_guard_bytes(int H) { return 8 * (size_t)(4l * H + 2) + 4 * (size_t)H; }  // <= 16 W H for W >= 4
 // Geometry (WinGeom, lattice_ego.hpp): candidates are the agents of window rows [cr0, cr1).  A
 // window edge that is not a lattice edge is not a candidate row (its agents' nominal controls
 // cannot be formed there; the cell-list builds skip them likewise, and the sharded step's halo
@@ -147,22 +141,13 @@ __device__ __forceinline__ double gmax(double a, double b) {
 // halo-guard extents (ext_keys, nullable).  copy_to (nullable) gets a copy of the positions (the
 // run's ping-pong start).  The row is staged in LDS (dynamic, 24 B per column): every global load
 // and store is coalesced, and the row scans run over contiguous chunks of it.
-// The previous timestep's queued QPs, solved by the build that follows it instead of a queue
-// kernel (FU, whole-lattice window runs): k_window_tile left each wave's QPs as records r W + c0 ..
-// (HardRec, lane order) with their count in Gd.wq.  Block r solves the QPs of rows r - 1, r, r + 1
-// (each one by three blocks, the same arithmetic: bit-identical), patches those positions into the
-// ones it read, and writes the new positions (and, when given, u / status / neighbour count) of
-// its own row's.  No hand-off inside a launch: the kernel boundary orders the records before it.
-constexpr int kFuseE = 3 * (kWinMaxW / kTileWidth);  // (row, tile column) entries of three rows
-
-template <int PER, int NT, bool FU>  // columns per thread (W <= NT x PER), threads of the block, fused solve
-__global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(FU ? 4 : CBF_PREP_WPE))) k_window_prep(WinGeom Q, const double2* pos,
+template <int PER, int NT>  // columns per thread (W <= NT x PER), threads of the block
+__global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(CBF_PREP_WPE))) k_window_prep(WinGeom Q, const double2* __restrict__ pos,
                                                             double2* __restrict__ u0, float2* __restrict__ rsp,
                                                             WinGuard Gd, double gain, double2* __restrict__ vel_out,
                                                             double2* __restrict__ copy_to, int32_t* __restrict__ sctl,
                                                             long ncell, unsigned long long* __restrict__ ext_keys,
-                                                            int row_begin, int row_end, ExtSpec X, int32_t guard_mode,
-                                                            FusedHard F) {
+                                                            int row_begin, int row_end, ExtSpec X, int32_t guard_mode) {
     extern __shared__ double2 srow[];  // [W] positions, then [W] float2 {rs, rp}
     const int W = Q.W;
     float2* srsp = reinterpret_cast<float2*>(srow + W);
@@ -181,20 +166,6 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(FU ? 4 
     const NominalSpec N = nominal_spec(sctl);
     const bool lap = N.mode != CBF_NOMINAL_RANDOM;
     const double2* prow = pos + (long)r * W;
-    // FU: the queued-QP counts of rows r - 1 .. r + 1 (entry e: row r - 1 + e / tiles_x, tile column
-    // e % tiles_x), loaded with the positions
-    const int tiles_x = win_tiles_x(W), ne = 3 * tiles_x;
-    __shared__ int s_off[FU ? kFuseE + 1 : 1];
-    __shared__ int s_wt[FU ? NT / 64 : 1];
-    __shared__ unsigned s_bm[FU ? 2 : 1][FU ? kWinMaxW / 32 : 1];  // rows r -+ 1: columns patched
-    __shared__ double2 s_pv[FU ? NT : 1];                           // a chunk's new positions, rows r -+ 1
-    __shared__ int s_pc[FU ? NT : 1];                               // ... their columns
-    int wc = 0;
-    if (FU) {
-        const int e = threadIdx.x, rr = r - 1 + e / (tiles_x > 0 ? tiles_x : 1);
-        if (e < ne && rr >= Q.cr0 && rr < Q.cr1) wc = Gd.wq[(long)rr * tiles_x + e % tiles_x];
-        for (int i = threadIdx.x; i < 2 * (kWinMaxW / 32); i += NT) s_bm[i / (kWinMaxW / 32)][i % (kWinMaxW / 32)] = 0u;
-    }
     // every load of the block in one round trip: the row (coalesced: column c = thread + j * block)
     // and, for the Laplacian, the rows above and below
     double2 p[PER], qu[PER], qd[PER];
@@ -207,16 +178,6 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(FU ? 4 
             if (lap && rl < Q.Hl - 1) qd[j] = prow[c + W];
         }
     }
-    const int lane0 = threadIdx.x & 63, wid0 = threadIdx.x >> 6;
-    int wincl = 0;
-    if (FU) {  // exclusive scan of the counts: the wave's part here, the waves' totals after the barrier
-        wincl = wc;
-        for (int o = 1; o < 64; o <<= 1) {
-            const int y = __shfl_up(wincl, o, 64);
-            if (lane0 >= o) wincl += y;
-        }
-        if (lane0 == 63) s_wt[wid0] = wincl;
-    }
 #pragma unroll
     for (int j = 0; j < PER; ++j) {
         const int c = threadIdx.x + j * NT;
@@ -226,89 +187,6 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(FU ? 4 
         }
     }
     __syncthreads();
-    if (FU) {
-        int base = 0, m = 0;
-        for (int q = 0; q < NT / 64; ++q) {
-            base += q < wid0 ? s_wt[q] : 0;
-            m += s_wt[q];
-        }
-        if ((int)threadIdx.x < ne) s_off[threadIdx.x] = base + wincl - wc;
-        if ((int)threadIdx.x == 0) s_off[ne] = m;
-        __syncthreads();
-        const int lo_u = s_off[0], hi_u = s_off[tiles_x], lo_d = s_off[2 * tiles_x];  // rows r - 1 / r + 1
-        for (int g0 = 0; g0 < m; g0 += NT) {  // chunks of NT records (one per thread)
-            const int g = g0 + (int)threadIdx.x;
-            int sel = -1;
-            if (g < m) {
-                int a = 0, b = ne;  // the entry holding record g: s_off[a] <= g < s_off[a + 1]
-                while (b - a > 1) {
-                    const int mid = (a + b) >> 1;
-                    if (s_off[mid] <= g) a = mid;
-                    else b = mid;
-                }
-                sel = a / tiles_x;
-                const int rr = r - 1 + sel;
-                const HardRec h = F.qrec[(long)rr * W + (a % tiles_x) * kTileWidth + (g - s_off[a])];
-                Ego E;
-                E.r0 = h.r0;
-                E.r1 = h.r1;
-                E.r2 = h.r2;
-                E.r3 = h.r3;
-                E.u0x = h.u0x;
-                E.u0y = h.u0y;
-                E.bq0 = h.bq0;
-                E.bq1 = h.bq1;
-                E.bq2 = h.bq2;
-                E.bq3 = h.bq3;
-                E.present = (unsigned)h.present;
-                E.count = h.count;
-                const Sol S = solve_ego<true>(F.P, E);
-                double ux, uy;
-                clip_u(F.P, S, E, ux, uy);
-                const double2 pn = make_double2(E.r0 + F.T * ux, E.r1 + F.T * uy);
-                const int col = h.row - rr * W;
-                if (sel == 1) {  // this block's row: its new position, patched and stored
-                    srow[col] = pn;
-                    F.pos[h.row] = pn;
-                    if (F.u) F.u[h.k] = make_double2(ux, uy);
-                    if (F.status) F.status[h.k] = pack_status(S);
-                    if (F.cnt) F.cnt[h.k] = E.count;
-                } else {
-                    s_pv[threadIdx.x] = pn;
-                    s_pc[threadIdx.x] = col;
-                    atomicOr(&s_bm[sel >> 1][col >> 5], 1u << (col & 31));
-                }
-            }
-            __syncthreads();
-            // rows r -+ 1: each patched column's value from the chunk's records of that row, which are in
-            // column order (entries by tile column, records by lane)
-#pragma unroll
-            for (int j = 0; j < PER; ++j) {
-                const int c = threadIdx.x + j * NT;
-                if (c >= W) continue;
-                p[j] = srow[c];
-#pragma unroll
-                for (int t = 0; t < 2; ++t) {
-                    if (!((s_bm[t][c >> 5] >> (c & 31)) & 1u)) continue;
-                    int a = (t == 0 ? lo_u : lo_d) - g0, b = (t == 0 ? hi_u : m) - g0;
-                    a = a < 0 ? 0 : a;
-                    b = b > NT ? NT : b;
-                    while (b - a > 1) {  // the last record of the range with column <= c
-                        const int mid = (a + b) >> 1;
-                        if (s_pc[mid] <= c) a = mid;
-                        else b = mid;
-                    }
-                    if (t == 0) qu[j] = s_pv[a];
-                    else qd[j] = s_pv[a];
-                }
-            }
-            if (g0 + NT < m) {  // another chunk: clear the marks once every thread has read them
-                __syncthreads();
-                for (int i = threadIdx.x; i < 2 * (kWinMaxW / 32); i += NT) s_bm[i / (kWinMaxW / 32)][i % (kWinMaxW / 32)] = 0u;
-                __syncthreads();
-            }
-        }
-    }
     // nominal controls and the row's y extents
     double ylo = INFINITY, yhi = -INFINITY;
 #pragma unroll
@@ -600,7 +478,7 @@ __device__ __forceinline__ float2 ld_rsp(const float2* __restrict__ a, int t) {
 // are bits of a register mask over the (7 rows x 5 columns) window, assembled from LDS after the
 // scan.  An ego whose row window or column walk leaves the staged halo takes win_direct (global
 // memory, unbounded), as in the untiled form.
-constexpr int kTileW = kTileWidth;
+constexpr int kTileW = 64;  // columns of a tile (one wave per tile row)
 #ifndef CBF_TILE_R
 #define CBF_TILE_R 8  // lattice rows (waves) per tile (4: 43.0 us, 8: 41.3 us per launch at 1 M agents)
 #endif
@@ -687,7 +565,7 @@ __global__ void __launch_bounds__(kTileT) __attribute__((amdgpu_waves_per_eu((IN
                                                         int32_t* __restrict__ status, int32_t* __restrict__ cnt,
                                                         unsigned long long* __restrict__ stats,
                                                         int32_t* __restrict__ hardq, HardRec* __restrict__ qrec,
-                                                        long qcap, int32_t* __restrict__ wq) {
+                                                        long qcap) {
     __shared__ TileLds L;
     const double* __restrict__ sylo = Gd.sylo;
     const double* __restrict__ pyhi = Gd.pyhi;
@@ -708,7 +586,6 @@ __global__ void __launch_bounds__(kTileT) __attribute__((amdgpu_waves_per_eu((IN
     if (sctl[2] != 0) {  // the workspace is bound to another shape: report, touch nothing else
         lattice_error_tail(W, Q.row0 + B.own_lo / W, Q.row0 + B.own_hi / W, Q.row0, nwin, inside ? w : nwin, u,
                            status, cnt, stats, nullptr, 0, hardq);
-        if (wq && lane == 0 && r < Q.rows) wq[(long)r * tiles_x + tx] = 0;  // (nothing queued)
         return;
     }
     // fold: the row guard without the k_window_rowscan launch.  The launch's first block
@@ -925,14 +802,7 @@ __global__ void __launch_bounds__(kTileT) __attribute__((amdgpu_waves_per_eu((IN
         O.nbrs = E.count;
         if (ST) O.d2 = d2;
         ego_finish<FZ, ST, IN>(P, E, (int)w, (int)(w - B.own_lo), (int)w, T, pos_out, u, status, cnt, hardq,
-                               bx % kSubQ, qrec, qcap, O, wq ? (long)r * W + c0 : -1l);
-    }
-    // the per-wave form (wq: the next build solves them, k_window_prep FUSED): the wave's queued
-    // QPs are records r W + c0 .. in lane order, and their count goes to wq[r tiles_x + tile column]
-    // (every wave of the window writes its count, so no reset is needed)
-    if (wq) {
-        const unsigned long long mq = __ballot(O.res == 2);
-        if (lane == 0 && r < Q.rows) wq[(long)r * tiles_x + tx] = __popcll(mq);
+                               bx % kSubQ, qrec, qcap, O);
     }
     // degradation counters (every instantiation; rare, so one wave-aggregated atomic each when
     // they occur): walks and guard words read at their spin limit, into the workspace header and,
@@ -965,7 +835,7 @@ namespace cbf {
 
 // window-cull geometry a call can use: whole lattice (no halo), rows of 4 .. 2048 agents
 bool window_cull_ok(int W, int rows, long n_ws, const CellWs& Wk) {
-    return W >= 4 && W <= kWinMaxW && rows >= 1 && win_guard_bytes(W, rows) <= 16 * (size_t)n_ws && Wk.cs != nullptr;
+    return W >= 4 && W <= kWinMaxW && rows >= 1 && win_guard_bytes(rows) <= 16 * (size_t)n_ws && Wk.cs != nullptr;
 }
 
 bool window_fold(const cbf_params* p) { return !(p->launch_flags & CBF_LAUNCH_SEPARATE_GUARD); }
@@ -984,22 +854,18 @@ int window_counters(const void* workspace, size_t workspace_bytes, uint64_t* out
 // against 13.9 us)
 static int prep_threads(int rows) { return rows <= kPrepWideRows ? 2 * kPrepBlock : kPrepBlock; }
 
-bool window_fusable(int W, int rows) { return W <= 4 * prep_threads(rows); }
-
 void window_prep(const CellWs& Wk, const WinGeom& Q, const double2* pos, double gain, double2* vel_out,
                  double2* copy_to, unsigned long long* ext_keys, int row_begin, int row_end, ExtSpec X,
-                 bool fold, hipStream_t s, const FusedHard* F) {
+                 bool fold, hipStream_t s) {
     const int nt = prep_threads(Q.cr1 - Q.cr0);
     const bool wide = nt != kPrepBlock;
-    const auto prep = F ? (wide ? (Q.W <= 2 * nt ? k_window_prep<2, 2 * kPrepBlock, true> : k_window_prep<4, 2 * kPrepBlock, true>)
-                                : (Q.W <= 2 * nt ? k_window_prep<2, kPrepBlock, true> : k_window_prep<4, kPrepBlock, true>))
-                        : wide ? (Q.W <= 2 * nt ? k_window_prep<2, 2 * kPrepBlock, false> : k_window_prep<4, 2 * kPrepBlock, false>)
-                               : (Q.W <= 2 * nt   ? k_window_prep<2, kPrepBlock, false>
-                                  : Q.W <= 4 * nt ? k_window_prep<4, kPrepBlock, false>
-                                                  : k_window_prep<8, kPrepBlock, false>);
+    const auto prep = wide ? (Q.W <= 2 * nt ? k_window_prep<2, 2 * kPrepBlock> : k_window_prep<4, 2 * kPrepBlock>)
+                           : (Q.W <= 2 * nt   ? k_window_prep<2, kPrepBlock>
+                              : Q.W <= 4 * nt ? k_window_prep<4, kPrepBlock>
+                                              : k_window_prep<8, kPrepBlock>);
     hipLaunchKernelGGL(prep, dim3(Q.cr1 - Q.cr0), dim3(nt), 24 * (size_t)Q.W, s, Q, pos, Wk.svel,
                        win_rsp(Wk), win_guard(Wk, Q.rows), gain, vel_out, copy_to, Wk.sctl, Wk.ncell, ext_keys,
-                       row_begin, row_end, X, fold ? kGuardInFilter : kGuardSeparate, F ? *F : FusedHard{});
+                       row_begin, row_end, X, fold ? kGuardInFilter : kGuardSeparate);
     if (!fold)  // (else the filter's first block forms the row guard)
         hipLaunchKernelGGL(k_window_rowscan, dim3(1), dim3(kRowScanBlock), 0, s, Q, win_guard(Wk, Q.rows));
 }
@@ -1011,7 +877,7 @@ void window_prep(const CellWs& Wk, const WinGeom& Q, const double2* pos, double 
 void window_filter(const cbf_params* p, const CellWs& Wk, const WinGeom& Q, int row_begin, int row_end,
                    int cnt_begin, int cnt_end, const double2* pos, double T, double2* pos_out, double2* u,
                    int32_t* status, int32_t* cnt, unsigned long long* stats, bool in, hipStream_t s,
-                   hipEvent_t t_start, hipEvent_t t_stop, bool per_wave) {
+                   hipEvent_t t_start, hipEvent_t t_stop) {
     const int W = Q.W;
     const long n = (long)W * Q.rows;
     const KP kp = make_kp(p);
@@ -1027,11 +893,11 @@ void window_filter(const cbf_params* p, const CellWs& Wk, const WinGeom& Q, int 
         hipExtLaunchKernelGGL(tile, dim3((unsigned)(tiles_x * tiles_y)), dim3(kTileT), 0, s, t_start, t_stop, 0u, kp, B,
                               Q, row_begin - Q.row0, tiles_x, pos, (const double2*)Wk.svel,
                               (const float2*)win_rsp(Wk), Gd, Wk.sctl, T, pos_out, u, status, cnt, stats, Wk.hardq,
-                              Wk.qrec, Wk.qcap, per_wave ? Gd.wq : nullptr);
+                              Wk.qrec, Wk.qcap);
     else
         hipLaunchKernelGGL(tile, dim3((unsigned)(tiles_x * tiles_y)), dim3(kTileT), 0, s, kp, B, Q, row_begin - Q.row0,
                            tiles_x, pos, (const double2*)Wk.svel, (const float2*)win_rsp(Wk), Gd, Wk.sctl, T, pos_out,
-                           u, status, cnt, stats, Wk.hardq, Wk.qrec, Wk.qcap, per_wave ? Gd.wq : nullptr);
+                           u, status, cnt, stats, Wk.hardq, Wk.qrec, Wk.qcap);
 }
 
 }  // namespace cbf

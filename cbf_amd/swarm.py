@@ -37,21 +37,13 @@ class FilterParams:
     # "auto" (in_filter; ShardedLattice takes separate when its node runs more ranks than GPUs).
     # Results are identical.
     window_guard: str = "auto"
-    # window-cull runs only: who solves the queued QPs of a timestep that is not a run's last
-    # (cbf_params.launch_flags CBF_LAUNCH_QUEUE_KERNEL): "auto" / "next_build" (the next timestep's
-    # build, no queue-kernel launch per timestep; runs without statistics) or "queue_kernel" (the
-    # queue kernel after every filter).  Results are identical.
-    hard_solve: str = "auto"
 
     def c(self):
         p = _lib.make_params(self.max_speed, self.dmin, self.k, self.f, self.g, self.safety_distance)
         p.solve_inline_max = solve_inline_max(self.solve_placement)
         if self.window_guard not in ("auto", "in_filter", "separate"):
             raise ValueError(f"window_guard must be 'auto', 'in_filter' or 'separate', got {self.window_guard!r}")
-        if self.hard_solve not in ("auto", "next_build", "queue_kernel"):
-            raise ValueError(f"hard_solve must be 'auto', 'next_build' or 'queue_kernel', got {self.hard_solve!r}")
-        p.launch_flags = (_lib.LAUNCH_SEPARATE_GUARD if self.window_guard == "separate" else 0) | \
-            (_lib.LAUNCH_QUEUE_KERNEL if self.hard_solve == "queue_kernel" else 0)
+        p.launch_flags = _lib.LAUNCH_SEPARATE_GUARD if self.window_guard == "separate" else 0
         return p
 
 

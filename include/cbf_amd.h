@@ -95,15 +95,10 @@ typedef struct cbf_params {
      * forms its row guard in a separate one-block kernel after the build instead of inside the
      * filter launch, whose blocks poll for it.  The in-launch form is the faster one on a GPU one
      * process owns; ranks that time-share one GPU should set the bit (a poll can wait for long
-     * there).  Results are identical either way.  0 from cbf_params_init.  ABI 6 (was reserved).
-     * Bit CBF_LAUNCH_QUEUE_KERNEL: in a window-cull run (cbf_lattice_run_ex, CBF_RUN_WINDOW_CULL)
-     * every timestep's queued QPs are solved by the queue kernel, as in a single step, instead of by
-     * the next timestep's build (the default for the timesteps but the last of a run without
-     * statistics: no queue-kernel launch per timestep).  Results are identical either way. */
+     * there).  Results are identical either way.  0 from cbf_params_init.  ABI 6 (was reserved). */
     uint32_t launch_flags;
 } cbf_params;
 #define CBF_LAUNCH_SEPARATE_GUARD 1u
-#define CBF_LAUNCH_QUEUE_KERNEL 2u
 
 /* Fill *p (host).  f16 / g8 may be NULL for the callers' f = 0, g = 0.1 [I2; 0]. */
 int cbf_params_init(cbf_params* p, double max_speed, double dmin, double k, const double* f16, const double* g8,
