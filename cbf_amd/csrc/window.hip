@@ -187,17 +187,18 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(CBF_PRE
         }
     }
     __syncthreads();
-    // nominal controls and the row's y extents
+    // nominal controls and the row's y extents: every column's value first, then all the stores
+    // together, so that no later wait for a load result also waits for a store in flight (a wait
+    // between the columns' stores serialised their round trips: 11.8 against 8.8 us per build at
+    // 1 M agents)
     double ylo = INFINITY, yhi = -INFINITY;
+    double2 a[PER];
 #pragma unroll
     for (int j = 0; j < PER; ++j) {
         const int c = threadIdx.x + j * NT;
-        if (c >= W) continue;
-        const long w = (long)r * W + c;
         const double2 pi = p[j];
-        double2 a;
         if (!lap) {
-            a = random_nominal(N, (long)Q.row0 * W + w, pi);
+            a[j] = random_nominal(N, (long)Q.row0 * W + (long)r * W + c, pi);
         } else {  // lattice_sum's neighbour order and arithmetic: (r-1, c), (r, c-1), (r, c+1), (r+1, c)
             double a0 = 0.0, a1 = 0.0;
             if (rl > 0) {
@@ -218,14 +219,20 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(CBF_PRE
                 a0 = a0 + (qd[j].x - pi.x);
                 a1 = a1 + (qd[j].y - pi.y);
             }
-            a = make_double2(a0 * gain, a1 * gain);
+            a[j] = make_double2(a0 * gain, a1 * gain);
         }
-        st_stream(u0 + w, a);
-        if (vel_out && rl >= row_begin && rl < row_end) vel_out[(long)(rl - row_begin) * W + c] = a;
-        if (isfinite(pi.x) && isfinite(pi.y)) {
-            ylo = gmin(ylo, pi.y);
-            yhi = gmax(yhi, pi.y);
-        }
+        const bool f = c < W && isfinite(pi.x) && isfinite(pi.y);  // (a column beyond W: no agent)
+        const double lo = gmin(ylo, pi.y), hi = gmax(yhi, pi.y);
+        ylo = f ? lo : ylo;
+        yhi = f ? hi : yhi;
+    }
+    const bool vo = vel_out && rl >= row_begin && rl < row_end;
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+        const int c = threadIdx.x + j * NT;
+        if (c >= W) continue;
+        st_stream(u0 + (long)r * W + c, a[j]);
+        if (vo) vel_out[(long)(rl - row_begin) * W + c] = a[j];
     }
     // A sorted row (every agent finite, x non-decreasing along it: a lattice row under consensus)
     // needs no column extents -- each agent's own x is the minimum over the columns from it on and
@@ -242,7 +249,17 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(CBF_PRE
             if (c + 1 < W) ok = ok && p[j].x <= srow[c + 1].x;
         }
     }
-    const bool sorted = __syncthreads_and(ok) != 0;
+    // block-wide AND: a vote per wave, one barrier (__syncthreads_and took three and LDS atomics:
+    // 11.1 against 11.5 us per build at 1 M agents)
+    __shared__ int s_ok[NT / 64];
+    {
+        const bool wok = __all(ok) != 0;
+        if ((threadIdx.x & 63) == 0) s_ok[threadIdx.x >> 6] = wok ? 1 : 0;
+    }
+    __syncthreads();
+    bool sorted = true;
+#pragma unroll
+    for (int q = 0; q < NT / 64; ++q) sorted = sorted && s_ok[q] != 0;
     const int m = (W + NT - 1) / NT;
     const int c0 = threadIdx.x * m;
     double sm[PER], pm[PER];

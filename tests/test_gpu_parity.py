@@ -1046,10 +1046,12 @@ def test_cell_starts_full_size_equal_host_scan(steps):
     assert np.array_equal(cells[sidx], slot_cell)
 
 
-def test_window_full_size_driver_timesteps_vs_oracle():
+@pytest.mark.parametrize("spacing", [0.145, 0.2], ids=["cfg4", "cfg4f"])
+def test_window_full_size_driver_timesteps_vs_oracle(spacing):
     """The driver's headline path at its own size and timesteps: the 1024 x 1024 lattice under the
     window cull through cbf_lattice_run with statistics off (bench.py cfg4 times timesteps 6-25 of
-    this rollout).  One run(25, history=True) stores every timestep's nominal control, filtered
+    this rollout), and cfg4f's (spacing 0.2: most QPs feasible, the branch of cbf.py:75-87 whose
+    answer the reference defines; bench.py's feasible_regime record).  One run(25, history=True) stores every timestep's nominal control, filtered
     control, status and neighbour count; the input positions of every timestep follow from them by
     the Euler update (the device's own arithmetic, p + T u), and the plain run(25) -- the bench's
     form -- must end in the same positions.  At timesteps 6, 15 and 25, 512 sampled egos are
@@ -1057,7 +1059,7 @@ def test_window_full_size_driver_timesteps_vs_oracle():
     controls, statuses and neighbour counts bit for bit, nominal controls over the whole lattice."""
     W = H = 1024
     steps = 25
-    pos = scenarios.lattice(W, H, seed=0)
+    pos = scenarios.lattice(W, H, seed=0, spacing=spacing)
     A = swarm.LatticeSwarm(pos, W, H, cull="window")
     A.collect_stats = False
     A.run(steps, history=True)
@@ -1073,6 +1075,7 @@ def test_window_full_size_driver_timesteps_vs_oracle():
     del B
     p = pos.copy()
     rng = np.random.default_rng(25)
+    optimal = 0
     for t in range(steps):
         if t + 1 in (6, 15, 25):
             vel = coracle.consensus_lattice(W, H, 0, H, p, scenarios.LATTICE_GAIN)
@@ -1080,5 +1083,9 @@ def test_window_full_size_driver_timesteps_vs_oracle():
             idx = rng.choice(W * H, 512, replace=False)
             for e, (ru, rst, rc) in zip(idx, _sample_oracle(p, vel, idx)):
                 assert np.array_equal(hu[t][e], ru) and hs[t][e] == rst and hc[t][e] == rc, (t + 1, e)
+                optimal += (rst & 0xFF) == 1
         p = coracle.euler(p, hu[t], 1 / 30)
     assert np.array_equal(p, end_a)
+    if spacing == 0.2:  # the sample exercises the feasible (OPTIMAL) branch, not only the relaxation
+        print(f"cfg4f sample: {optimal} of {3 * 512} sampled egos OPTIMAL")
+        assert optimal >= 256, optimal
