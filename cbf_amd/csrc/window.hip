@@ -500,6 +500,9 @@ constexpr int kTileW = 64;  // columns of a tile (one wave per tile row)
 #define CBF_TILE_R 8  // lattice rows (waves) per tile (4: 43.0 us, 8: 41.3 us per launch at 1 M agents)
 #endif
 constexpr int kTileR = CBF_TILE_R;
+// (the launch's first block forms the row guard with a block scan over power-of-two waves: a tile of
+// 6 or 7 rows left every guard word unformed, read at its spin limit -- exact, 0.78 s per launch)
+static_assert(kTileR >= 2 && (kTileR & (kTileR - 1)) == 0, "tile rows: a power of two");
 constexpr int kTileT = kTileR * 64;  // threads per tile block
 constexpr int kTileKS = 3;  // rows each side (the row guard's window up to +-3)
 constexpr int kTileKC = 3;  // columns each side (candidates to +-2, sentinels to +-3)
