@@ -40,6 +40,7 @@ struct KP {
     double g[8];
     double cull_t;
     double n0[4], n1[4];  // quadrant normals L_g (host-computed with the reference's order)
+    double z[4];          // n0[q] * 0.0 + n1[q] * 0.0: the CBF planes' a.x at the origin (solve_fast)
     int f_zero;
     int relax_cap;
     // window cull (CBF_RUN_WINDOW_CULL): the smallest double d with d * d >= cull_t, so that a
@@ -61,6 +62,7 @@ inline KP make_kp(const cbf_params* p) {
     for (int q = 0; q < 4; ++q) {
         k.n0[q] = p->nrm[q][0];
         k.n1[q] = p->nrm[q][1];
+        k.z[q] = k.n0[q] * 0.0 + k.n1[q] * 0.0;
     }
     k.f_zero = p->f_is_zero;
     k.relax_cap = p->relax_cap;
@@ -86,6 +88,14 @@ __device__ __forceinline__ void st_stream(double2* p, double2 v) {
 }
 __device__ __forceinline__ double pmin(double a, double b) { return (b < a) ? b : a; }  // Python min(a, b)
 __device__ __forceinline__ double pmax(double a, double b) { return (b > a) ? b : a; }  // Python max(a, b)
+// pmax(1.0, fabs(b)) as one v_max_f64 (the compiler's form canonicalises |b| first: two
+// instructions).  The same value for every b the solvers see: arithmetic results, so never a
+// signalling NaN, and IEEE-mode max returns 1.0 for a quiet NaN as the compare-select does.
+__device__ __forceinline__ double max1abs(double b) {
+    double r;
+    asm("v_max_f64 %0, 1.0, |%1|" : "=v"(r) : "v"(b));
+    return r;
+}
 
 // fp32 screen of the cull test.  A candidate can pass the exact fp64 test s = e0^2 + e1^2 < cull_t
 // (cross_and_rescue.py:141-150) only if S = the fp32 distance^2 of the fp32-rounded coordinates
@@ -342,7 +352,7 @@ __device__ __forceinline__ int solve_planes_reg(const double (&a0)[N], const dou
                                                 unsigned mask, double& xo0, double& xo1) {
     double tb[N];
 #pragma unroll
-    for (int h = 0; h < N; ++h) tb[h] = FEAS_TOL * pmax(1.0, fabs(b[h]));
+    for (int h = 0; h < N; ++h) tb[h] = FEAS_TOL * max1abs(b[h]);
     double x0 = 0.0, x1 = 0.0;
 #pragma unroll
     for (int h = 0; h < N; ++h) {
@@ -451,12 +461,12 @@ __device__ __forceinline__ Sol solve_ego(const KP& P, const Ego& E) {
             bool dead = false;
             if ((E.present & 9u) == 9u) {
                 const double s = b[4] + b[7];
-                const double tb = FEAS_TOL * (pmax(1.0, fabs(b[4])) + pmax(1.0, fabs(b[7])));
+                const double tb = FEAS_TOL * (max1abs(b[4]) + max1abs(b[7]));
                 dead = dead || (s < -tb - 1e-9 * (1.0 + fabs(b[4]) + fabs(b[7])));
             }
             if ((E.present & 6u) == 6u) {
                 const double s = b[5] + b[6];
-                const double tb = FEAS_TOL * (pmax(1.0, fabs(b[5])) + pmax(1.0, fabs(b[6])));
+                const double tb = FEAS_TOL * (max1abs(b[5]) + max1abs(b[6]));
                 dead = dead || (s < -tb - 1e-9 * (1.0 + fabs(b[5]) + fabs(b[6])));
             }
             if (!dead || S.iters >= P.relax_cap) break;
@@ -544,12 +554,12 @@ __device__ __forceinline__ bool fast_origin(const KP& P, const Ego& E, FastState
             bool dead = false;
             if ((E.present & 9u) == 9u) {
                 const double s = b[4] + b[7];
-                const double tb = FEAS_TOL * (pmax(1.0, fabs(b[4])) + pmax(1.0, fabs(b[7])));
+                const double tb = FEAS_TOL * (max1abs(b[4]) + max1abs(b[7]));
                 dead = dead || (s < -tb - 1e-9 * (1.0 + fabs(b[4]) + fabs(b[7])));
             }
             if ((E.present & 6u) == 6u) {
                 const double s = b[5] + b[6];
-                const double tb = FEAS_TOL * (pmax(1.0, fabs(b[5])) + pmax(1.0, fabs(b[6])));
+                const double tb = FEAS_TOL * (max1abs(b[5]) + max1abs(b[6]));
                 dead = dead || (s < -tb - 1e-9 * (1.0 + fabs(b[5]) + fabs(b[6])));
             }
             if (!dead || iters >= P.relax_cap) break;
@@ -566,8 +576,9 @@ __device__ __forceinline__ bool fast_origin(const KP& P, const Ego& E, FastState
 #pragma unroll
     for (int j = 7; j >= 0; --j)
         if ((mask >> j) & 1u) {
-            const double d = (a0[j] * 0.0 + a1[j] * 0.0) - b[j];
-            if (!(d <= FEAS_TOL * pmax(1.0, fabs(b[j])))) h = j;
+            // a.0 for the CBF planes from the host (P.z: the same products and sum, uniform)
+            const double d = (j < 4 ? (a0[j] * 0.0 + a1[j] * 0.0) : P.z[j - 4]) - b[j];
+            if (!(d <= FEAS_TOL * max1abs(b[j]))) h = j;
             if (d > v0) v0 = d;
         }
     F.iters = iters;
@@ -624,7 +635,7 @@ __device__ __forceinline__ bool fast_event(const KP& P, const Ego& E, const Fast
     for (int j = 0; j < 8; ++j)
         if ((mask >> j) & 1u) {
             const double d = (a0[j] * x0 + a1[j] * x1) - b[j];
-            ok = ok && (d <= FEAS_TOL * pmax(1.0, fabs(b[j])));
+            ok = ok && (d <= FEAS_TOL * max1abs(b[j]));
             if (d > v) v = d;
         }
     if (!ok) return false;
