@@ -623,8 +623,10 @@ def bench_lattice(args, ws, rank, local):
                                       if args.exchange == "neighbour" else "all-gather of ghost-row slabs")
                                    + f" per {k} steps ({halo * k} ghost rows per side)") if sharded else "single GPU",
                    "exchange_bytes_per_rank": S.exchange_bytes() if sharded else 0,
-                   "solve_placement": "inline in the filter" if solves_inline(S.cp, rows * W) else
-                                      "queued (k_lattice_filter_hard)",
+                   "solve_placement": ("inline in the filter" if solves_inline(S.params.c() if sharded else S.cp, rows * W)
+                                       else "queued (k_lattice_filter_hard)")
+                                      + (" (sharded: decided per sub-step window, its ghost rows included)"
+                                         if sharded else ""),
                    "graph": use_graph,
                    "timesteps_per_call": max(plan) if chunk > 1 else 1},
         "timesteps_per_s": args.steps / elapsed,

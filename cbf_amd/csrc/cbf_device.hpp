@@ -88,6 +88,15 @@ __device__ __forceinline__ void st_stream(double2* p, double2 v) {
 }
 __device__ __forceinline__ double pmin(double a, double b) { return (b < a) ? b : a; }  // Python min(a, b)
 __device__ __forceinline__ double pmax(double a, double b) { return (b > a) ? b : a; }  // Python max(a, b)
+// v_min_f64 (volatile: kept under its branch, not speculated into a select).  For the per-quadrant
+// minima of barrier rows g it equals `g < m ? g : m` (m the running minimum, never NaN): g is never
+// -0 (H - dmin of a hit is +0 at worst, and L_f only adds to it) nor a signalling NaN (arithmetic
+// results), and IEEE-mode min returns m for a quiet-NaN g, as the compare skips it.
+__device__ __forceinline__ double vmin_f64(double a, double b) {
+    double r;
+    asm volatile("v_min_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
 // pmax(1.0, fabs(b)) as one v_max_f64 (the compiler's form canonicalises |b| first: two
 // instructions).  The same value for every b the solvers see: arithmetic results, so never a
 // signalling NaN, and IEEE-mode max returns 1.0 for a quiet NaN as the compare-select does.
@@ -258,8 +267,7 @@ struct HitList {
                     int qd;
                     const double g = row_g<FZ>(P, E, pj[q].x, pj[q].y, vj[q].x, vj[q].y, qd);
                     double* slot = gq + qd * kBlock + threadIdx.x;
-                    const double cur = *slot;
-                    *slot = (g < cur) ? g : cur;
+                    *slot = vmin_f64(*slot, g);  // = (g < cur ? g : cur): see vmin_f64
                     E.present |= 1u << qd;
                 }
             }

@@ -102,13 +102,6 @@ inline float2* win_rsp(const CellWs& Wk) { return reinterpret_cast<float2*>(Wk.w
 
 // fp32 bounds of a double: the largest float <= v / the smallest float >= v (outward rounding, so
 // the column guard built from them stays sound)
-// v_min_f64 that stays under its branch (volatile: not speculated into a select), for the tile's
-// exec-masked quadrant minima
-__device__ __forceinline__ double vmin_f64(double a, double b) {
-    double r;
-    asm volatile("v_min_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
-    return r;
-}
 __device__ __forceinline__ float f32_down(double v) {
     float f = (float)v;
     if ((double)f > v) {
@@ -799,10 +792,8 @@ __global__ void __launch_bounds__(kTileT) __attribute__((amdgpu_waves_per_eu((IN
                         ny = (qd & 2) != 0;
                     }
                     // the hit's quadrant minimum, one v_min_f64 under that quadrant's lanes (exec-masked:
-                    // the compare-and-select form took a compare and two selects per quadrant).  The
-                    // same value as `g < gq ? g : gq`: g is never -0 (H - dmin of a hit is +0 at
-                    // worst, and L_f only adds to it) nor a signalling NaN (arithmetic results), and
-                    // IEEE-mode min returns gq for a quiet-NaN g, as the compare skips it
+                    // the compare-and-select form took a compare and two selects per quadrant; the
+                    // same value, see vmin_f64)
                     if (!nx && !ny) g0 = vmin_f64(g0, g);
                     if (nx && !ny) g1 = vmin_f64(g1, g);
                     if (!nx && ny) g2 = vmin_f64(g2, g);
