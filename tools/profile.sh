@@ -13,7 +13,7 @@ for C in ${CONFIGS:-cfg4 cfg4f cfg5}; do
     B="python3 bench.py --config cfg5 --steps 3 --warmup 1"
     SQ="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_ACTIVE_INST_VALU SQ_BUSY_CYCLES SQ_WAIT_INST_ANY"
   else
-    B="python3 bench.py --config $C --steps 60 --warmup 20 --no-cpu-baseline --kernel-iters 10"
+    B="python3 bench.py --config $C --steps 60 --warmup 20 --no-cpu-baseline --no-exact-qp --kernel-iters 10"
     SQ="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_ACTIVE_INST_VALU SQ_WAIT_INST_ANY SQ_INSTS_VMEM_RD SQ_BUSY_CYCLES"
   fi
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d $D/trace -o run -- $B > $D/trace.log 2>&1 || exit 1
