@@ -371,7 +371,8 @@ def bench_lattice(args, ws, rank, local):
     # timestep, so the bin pass runs once per call), each call one hipGraph.  Sharded: one
     # hipGraph per exchange cycle (cbf_lattice_cycle_sharded) replayed after each exchange, whose
     # pack / collective / unpack stay eager.
-    chunk = args.chunk if (use_graph and not sharded and args.barrier == "reference" and args.chunk > 1) else 1
+    # (the HOCBF barrier: `chunk` single-timestep launches captured as one graph)
+    chunk = args.chunk if (use_graph and not sharded and args.chunk > 1) else 1
     plan = [chunk] * (args.steps // chunk) + ([args.steps % chunk] if args.steps % chunk else [])
 
     def advance(n):
@@ -400,7 +401,8 @@ def bench_lattice(args, ws, rank, local):
                     S.capture(steps=n)
             else:
                 S.capture()
-        if chunk > 1 and not args.timed_stats:   # the per-step-outputs variant (history), statistics off
+        if chunk > 1 and not args.timed_stats and args.barrier == "reference":
+            # the per-step-outputs variant (history), statistics off
             S.collect_stats = False
             for n in set(plan):
                 S.capture(steps=n, history=True)
@@ -473,7 +475,7 @@ def bench_lattice(args, ws, rank, local):
             raise RuntimeError("the statistics replay did not repeat the timed rollout bit for bit")
     state_sha = gather_state_sha(own, ws)
     elapsed_hist = None
-    if snap is not None and chunk > 1:
+    if snap is not None and chunk > 1 and args.barrier == "reference":
         # the same timed steps again with every timestep's outputs stored (u, status, nominal
         # control, neighbour count: the reference's per-step si_velocities), statistics off
         stats_keep = S.stats.clone()

@@ -36,6 +36,9 @@ extern "C" __device__ __attribute__((const)) double __ockl_wfred_max_f64(double)
 
 namespace {
 
+#ifndef CBF_TILE_FUSED_FLUSH
+#define CBF_TILE_FUSED_FLUSH 1  // 0: the hits' rows formed after the scan, from the hit mask (round 6)
+#endif
 #ifndef CBF_TILE_WPE
 #define CBF_TILE_WPE 6  // waves per SIMD the timed tile kernels (queued solve, no statistics) are fitted to
 #endif
@@ -711,12 +714,32 @@ __global__ void __launch_bounds__(kTileT) __attribute__((amdgpu_waves_per_eu((IN
     const int KdW = (int)__ockl_wfred_max_u32((unsigned)(slow ? 0 : Kd + 1)) - 1;
     unsigned long long hm = 0;  // hit bits (dr + 3) * 8 + (dc + 2): one byte per row
     double d2 = INFINITY;
+    // FZ (f = 0) and CBF_TILE_FUSED_FLUSH: each hit's row_g goes into its quadrant minimum as the
+    // candidate is tested (the coordinate differences reused: e = -d exactly up to the sign of a
+    // zero, which neither |d0| + |d1| nor the d < 0 tests see); the minima are used where the
+    // quadrant terms are finite (else the hits are taken row by row from hm, below)
+    constexpr bool kFused = FZ && CBF_TILE_FUSED_FLUSH;
+    double g0 = INFINITY, g1 = INFINITY, g2 = INFINITY, g3 = INFINITY;
+    const unsigned long long kb = (unsigned long long)__double_as_longlong(P.k);
+    const unsigned khi = (unsigned)(kb >> 32), knhi = khi ^ 0x80000000u, klo = (unsigned)kb;
     auto cand = [&](int off) -> unsigned {
         const double2 q = L.p[off];
         const double e0 = q.x - E.r0, e1 = q.y - E.r1;
         const double s = e0 * e0 + e1 * e1;
         const bool hit = s < P.cull_t && s > 0;
         if (ST && hit) d2 = pmin(d2, s);
+        if (kFused && hit) {
+            const double2 v = L.u[off];
+            const bool nx = e0 > 0, ny = e1 > 0;  // d0 < 0, d1 < 0
+            const double ksx = __hiloint2double((int)(nx ? knhi : khi), (int)klo);
+            const double ksy = __hiloint2double((int)(ny ? knhi : khi), (int)klo);
+            const double Hh = fma(ksy, E.r3 - v.y, fma(ksx, E.r2 - v.x, fabs(e0) + fabs(e1)));
+            const double g = P.gamma * (Hh - P.dmin);
+            if (!nx && !ny) g0 = vmin_f64(g0, g);
+            if (nx && !ny) g1 = vmin_f64(g1, g);
+            if (!nx && ny) g2 = vmin_f64(g2, g);
+            if (nx && ny) g3 = vmin_f64(g3, g);
+        }
         return hit ? 1u : 0u;
     };
     unsigned pR = 0, pL = 0;  // rows (bit dr + 3) whose sentinel at c + 2 / c - 2 does not hold
@@ -759,7 +782,6 @@ __global__ void __launch_bounds__(kTileT) __attribute__((amdgpu_waves_per_eu((IN
         if (fin && !slow) {
             // the hits from LDS: per-quadrant minima of row_g plus the quadrant terms, or row by row
             // (row_b) when a quadrant term is not finite -- the cell-list filter's two forms
-            double g0 = INFINITY, g1 = INFINITY, g2 = INFINITY, g3 = INFINITY;
             if (qfin) {
                 E.count = __popcll(hm);
                 // row_g<FZ> per hit (f = 0: its H with k's sign as a select of k's two high words --
@@ -768,9 +790,7 @@ __global__ void __launch_bounds__(kTileT) __attribute__((amdgpu_waves_per_eu((IN
                 // no quadrant index), and a quadrant's presence is read off its minimum afterwards: a
                 // present quadrant whose minimum stayed +inf (a NaN or +inf row) is a +inf plane,
                 // which no solver step can violate or bind -- the same as an absent one.
-                const unsigned long long kb = (unsigned long long)__double_as_longlong(P.k);
-                const unsigned khi = (unsigned)(kb >> 32), knhi = khi ^ 0x80000000u, klo = (unsigned)kb;
-                while (hm) {
+                while (!kFused && hm) {
                     const int bit = __ffsll((long long)hm) - 1;
                     hm &= hm - 1;
                     const int off = e + ((bit >> 3) - 3) * kTileCols + (bit & 7) - 2;

@@ -387,6 +387,12 @@ class LatticeSwarm:
         return h
 
     def _launch_run(self, steps, history=False):
+        if self.barrier == "euclidean_hocbf":  # no fused multi-step launch: `steps` single timesteps
+            if history:
+                raise ValueError("run(history=True) is the reference barrier's (cbf_lattice_run_ex)")
+            for _ in range(steps):
+                self._launch()
+            return
         if history:
             vel, u, st, cnt = self._history(steps)
             flags = _lib.RUN_OUTPUT_HISTORY
@@ -401,11 +407,13 @@ class LatticeSwarm:
     def run(self, steps, history=False):
         """`steps` timesteps through cbf_lattice_run (bit-identical to `steps` step() calls; the
         bin pass runs once, later timesteps are binned by the previous advance).  Reference
-        barrier, cell method only.  history=True stores every timestep's nominal control, filtered
+        barrier, cell method.  history=True stores every timestep's nominal control, filtered
         control, status and neighbour count (the reference's per-step si_velocities,
-        cross_and_rescue.py:159-160) in the arrays of history(steps) instead of the last one only."""
-        if self.method != "cells" or self.barrier != "reference":
-            raise ValueError("run() is the fused multi-step path of the reference barrier (cell method)")
+        cross_and_rescue.py:159-160) in the arrays of history(steps) instead of the last one only.
+        The Euclidean HOCBF barrier (cell method, no history): `steps` step() launches, replayed as
+        one hipGraph once capture(steps) has recorded them (no per-timestep graph launch)."""
+        if self.method != "cells":
+            raise ValueError("run() is the multi-step path of the cell method")
         g = self.run_graphs.get((steps, self.collect_stats, history, self.cull))
         if g is not None:
             g.replay()

@@ -180,3 +180,33 @@ def test_lattice_advance_twice_without_build(barrier):
     for o in outs[1:]:
         for a, b in zip(outs[0], o):
             assert np.array_equal(a, b)
+
+
+def test_lattice_hocbf_run_graph_equals_steps():
+    """HOCBF mode's run(steps): `steps` timesteps captured as one hipGraph (capture(steps)) give
+    the same positions, controls, statuses and solve count as as many step() calls, and as the
+    eager run(steps); the per-step-outputs form is the reference barrier's only."""
+    from cbf_amd import scenarios
+    W = H = 40
+    pos = scenarios.lattice(W, H, seed=11, spacing=0.1)  # some egos take the wide kernel
+    A = swarm.LatticeSwarm(pos, W, H, gain=scenarios.LATTICE_GAIN, barrier="euclidean_hocbf")
+    B = swarm.LatticeSwarm(pos, W, H, gain=scenarios.LATTICE_GAIN, barrier="euclidean_hocbf")
+    C = swarm.LatticeSwarm(pos, W, H, gain=scenarios.LATTICE_GAIN, barrier="euclidean_hocbf")
+    for _ in range(7):
+        A.step()
+    snap = B.snapshot()
+    B.capture(steps=5)   # its warm-up launch advances B: rewind
+    B.restore(snap)
+    B.reset_solves()
+    B.run(5)
+    B.run(2)             # (no graph of 2 steps: eager)
+    C.run(7)
+    torch.cuda.synchronize()
+    for S in (B, C):
+        assert np.array_equal(A.pos.cpu().numpy(), S.pos.cpu().numpy())
+        assert np.array_equal(A.u.cpu().numpy(), S.u.cpu().numpy())
+        assert np.array_equal(A.status.cpu().numpy(), S.status.cpu().numpy())
+        assert A.solves_total() == S.solves_total()
+    assert int((A.nbr_count > 8).sum()) > 0
+    with pytest.raises(ValueError):
+        B.run(3, history=True)

@@ -2,6 +2,7 @@
 # Profiling recipe run on the GPU box (gpurun): per config, a kernel-trace pass and separate PMC
 # passes (FETCH_SIZE and WRITE_SIZE never share a pass; MI355X_MICROARCH.md "rocprofv3 PMC slots").
 #   CONFIGS="cfg4 cfg4f cfg5" bash tools/profile.sh      -> gpurun_out/prof/<config>/...
+#   (cfg4_hocbf: the cfg4 shape with --barrier euclidean_hocbf)
 # then, back in the container: python tools/summarize_profile.py gpurun_out/prof r02
 set -o pipefail
 export TMPDIR=/tmp
@@ -11,6 +12,9 @@ for C in ${CONFIGS:-cfg4 cfg4f cfg5}; do
   mkdir -p $D
   if [ $C = cfg5 ]; then
     B="python3 bench.py --config cfg5 --steps 3 --warmup 1"
+    SQ="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_ACTIVE_INST_VALU SQ_BUSY_CYCLES SQ_WAIT_INST_ANY"
+  elif [ $C = cfg4_hocbf ]; then
+    B="python3 bench.py --config cfg4 --barrier euclidean_hocbf --steps 40 --warmup 10 --no-cpu-baseline --no-exact-qp"
     SQ="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_ACTIVE_INST_VALU SQ_BUSY_CYCLES SQ_WAIT_INST_ANY"
   else
     B="python3 bench.py --config $C --steps 60 --warmup 20 --no-cpu-baseline --no-exact-qp --kernel-iters 10"
