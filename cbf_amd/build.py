@@ -92,11 +92,13 @@ def build_torch_ops(verbose: bool = False) -> str:
 
 # Test-only builds of the library with a compile switch flipped in some sources (never loaded by
 # the package): name -> (sources, defines).  CBF_SCAN_TEST_TIMEOUT makes every scan look-back give
-# up, so tests/test_gpu_parity.py can check that the failure is reported, not silent.
+# up, so tests/test_gpu_parity.py can check that the failure is reported, not silent; hocbfnocert
+# runs every HOCBF relaxation pass (no infeasibility certificate), for tests/test_gpu_hocbf.py.
 TEST_VARIANTS = {"scantimeout": (["cells.hip", "swarm.hip", "hocbf.hip", "filter.hip"], ["CBF_SCAN_TEST_TIMEOUT=1"]),
                  "apwpe8": (["filter.hip"], ["CBF_AP_WPE=8"]),
                  "winnowait": (["window.hip"], ["CBF_WIN_SPIN_LIMIT=-1"]),
-                 "evqueue": (["swarm.hip", "window.hip"], ["CBF_EVENT_IN_PLACE=64"])}
+                 "evqueue": (["swarm.hip", "window.hip"], ["CBF_EVENT_IN_PLACE=64"]),
+                 "hocbfnocert": (["hocbf.hip"], ["CBF_HOCBF_CERT=0"])}
 TEST_LIB_DIR = os.path.join(ROOT, "tests", "_lib")
 
 

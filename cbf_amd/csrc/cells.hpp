@@ -23,7 +23,8 @@ constexpr int kScanTile = 256 * CBF_SCAN_PER;  // 256 threads x CBF_SCAN_PER cel
 // them in full waves.  One chip-wide counter serialised ~16 k wave atomics a step at the memory
 // side (the filter ran 200 us instead of 43 at cfg4f); 64 counters on separate 128-B lines take
 // ~256 each, in parallel.  Header: [2..7] the cell-order state of the last build; [32 (1 + q)]
-// sub-queue q's length; [32 (1 + kSubQ + q)] its done counter (queue kernel).
+// sub-queue q's length; [32 (1 + kSubQ + q)] its done counter (queue kernel); the same words + 16:
+// the HOCBF step's second queue (hocbf.hip kHardQ2).
 constexpr int kSubQ = 64;
 constexpr int kHardHeader = 32 * (1 + 2 * kSubQ);
 // A QP the filter kernel could not solve at the origin, queued with its assembled state.
@@ -52,7 +53,7 @@ inline size_t align256(size_t b) { return (b + 255) & ~size_t(255); }
 // Version of the workspace carve-up below and of its control words (cbf_workspace_layout): bump it
 // with ANY change to CellWs, HardRec, the control-word assignments or the queue header, so that a
 // saved workspace is never restored into a library that reads it differently.
-constexpr int kWorkspaceLayout = 6;
+constexpr int kWorkspaceLayout = 7;
 
 // Workspace carve-up (all segments 256-byte aligned).  The control words come first, at a fixed
 // offset, so that the shape signature they hold can be checked whatever shape a call assumes.

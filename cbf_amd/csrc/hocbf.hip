@@ -14,6 +14,8 @@
 
 using namespace cbf;
 
+extern "C" __device__ __attribute__((const)) double __ockl_wfred_min_f64(double);
+
 namespace {
 
 struct HP {
@@ -32,6 +34,9 @@ __device__ __forceinline__ double4 hocbf_row(const KP& P, const HP& H, double r0
 }
 
 
+#ifndef CBF_HOCBF_CERT
+#define CBF_HOCBF_CERT 1  // 0: every relaxation pass run in the main kernel, no infeasibility certificate
+#endif
 #ifndef CBF_HOCBF_UNROLL
 #define CBF_HOCBF_UNROLL 8  // solve_rows' inner loops over the earlier rows, unrolled
 #endif
@@ -117,11 +122,12 @@ struct Interval {
 // oracle/cbf_oracle.c:solve_planes_n over the 4 merged box planes (static, in registers) then the
 // m barrier rows of R (dynamic), in that order; same arithmetic.  The box planes are never
 // selected by a runtime index (that would be lowered to scratch).
-template <class Src>
-__device__ __forceinline__ int solve_rows(const double (&bb)[4], const Src& R, double& xo0, double& xo1) {
+// The box planes' part of solve_rows (h = 0..3, from x = 0): the failing plane, or -1 with x set.
+// It depends on the box alone, so it is the same in every pass of the relaxation loop.
+__device__ __forceinline__ int box_phase(const double (&bb)[4], double& x0, double& x1) {
     const double ba0[4] = {1.0, 0.0, -1.0, 0.0}, ba1[4] = {0.0, 1.0, 0.0, -1.0};
-    double x0 = 0.0, x1 = 0.0;
-    // box planes h = 0..3
+    x0 = 0.0;
+    x1 = 0.0;
 #pragma unroll
     for (int h = 0; h < 4; ++h) {
         if (feas(ba0[h], ba1[h], bb[h], x0, x1)) continue;
@@ -140,6 +146,16 @@ __device__ __forceinline__ int solve_rows(const double (&bb)[4], const Src& R, d
         for (int j = 0; j <= h; ++j) ok = ok && feas(ba0[j], ba1[j], bb[j], x0, x1);
         if (!ok) return h;
     }
+    return -1;
+}
+
+template <class Src>
+__device__ __forceinline__ int solve_rows(const double (&bb)[4], const Src& R, double& xo0, double& xo1) {
+    const double ba0[4] = {1.0, 0.0, -1.0, 0.0}, ba1[4] = {0.0, 1.0, 0.0, -1.0};
+    double x0, x1;
+    // box planes h = 0..3
+    const int hb = box_phase(bb, x0, x1);
+    if (hb >= 0) return hb;
     // barrier rows h = 4 + i
     for (int i = 0; i < R.m; ++i) {
         double a0, a1, b;
@@ -176,6 +192,45 @@ __device__ __forceinline__ int solve_rows(const double (&bb)[4], const Src& R, d
     xo0 = x0;
     xo1 = x1;
     return -1;
+}
+
+// Infeasibility certificate for the unrelaxed rows (Farkas, three rows): if it holds, the first
+// pass of solve_hocbf is certain to fail at a barrier row, so the caller may start at one
+// relaxation -- the same state the failed pass leaves (iters 1, RELAXED; box phase checked apart).
+// Proof: a pass that succeeds ends at an x meeting every plane within feas' tolerance, i.e. (real
+// arithmetic) a_t.x - b_t <= tau_t with tau_t <= 1.01e-12 max(1, |b_t|) + 4u (|a_t0||x0| +
+// |a_t1||x1| + |b_t|), and the box planes likewise, so |x0| <= X0, |x1| <= X1 below.  For any
+// lambda >= 0 summing the rows gives R.x - sum lambda b <= sum lambda tau with R = sum lambda a, and
+// R.x >= -(|R0| X0 + |R1| X1); so sum lambda b + |R0| X0 + |R1| X1 + sum lambda tau < 0 rules every
+// such x out.  The test below asks that sum, evaluated in fp64, to be below -1e-9 mag (mag = sum
+// lambda (1 + |b| + |a0| X0 + |a1| X1)), which bounds every tau and every rounding error of the
+// evaluation (each <= 1e-11 mag) with room to spare.  lambda: the cross products of the three rows
+// (sum lambda a = 0 in real arithmetic; used only when all share a sign).  Non-finite data never
+// passes (a NaN or inf comparison is false).
+struct CertRow {
+    double a0, a1, b, mg;  // the row and its share of mag per unit lambda
+};
+__device__ __forceinline__ bool cert_triple(const CertRow& I, const CertRow& J, const CertRow& K, double X0,
+                                            double X1) {
+    double li = J.a0 * K.a1 - J.a1 * K.a0, lj = K.a0 * I.a1 - K.a1 * I.a0, lk = I.a0 * J.a1 - I.a1 * J.a0;
+    const bool pos = li >= 0.0 && lj >= 0.0 && lk >= 0.0, neg = li <= 0.0 && lj <= 0.0 && lk <= 0.0;
+    if (neg) {
+        li = -li;
+        lj = -lj;
+        lk = -lk;
+    }
+    const double sb = (li * I.b + lj * J.b) + lk * K.b;
+    const double r0 = (li * I.a0 + lj * J.a0) + lk * K.a0, r1 = (li * I.a1 + lj * J.a1) + lk * K.a1;
+    const double mag = (li * I.mg + lj * J.mg) + lk * K.mg;
+    const double q = (sb + fabs(r0) * X0) + fabs(r1) * X1;
+    return (pos || neg) && q < -1e-9 * mag;
+}
+__device__ __forceinline__ CertRow cert_row(double a0, double a1, double b, double X0, double X1) {
+    return CertRow{a0, a1, b, 1.0 + fabs(b) + fabs(a0) * X0 + fabs(a1) * X1};
+}
+__device__ __forceinline__ void cert_bounds(const double (&bb)[4], double& X0, double& X1) {
+    X0 = pmax(fabs(bb[0]), fabs(bb[2])) * (1.0 + 1e-11) + 1e-11;
+    X1 = pmax(fabs(bb[1]), fabs(bb[3])) * (1.0 + 1e-11) + 1e-11;
 }
 
 // oracle/cbf_oracle.c:solve_hocbf -- +1 relaxation of every barrier row while infeasible
@@ -413,6 +468,158 @@ __device__ __forceinline__ Sol hocbf_solve_lds(const KP& P, const HP& H, const E
     return solve_hocbf(P, E, R);
 }
 
+// hocbf_cert for the main kernel, in fp32 on register copies of the <= 8 rows (every loop unrolled,
+// no LDS re-reads): the same rows chosen (i the most violated, its two best opposite partners, every
+// other row as the third) and the same proof, with the fp32 rounding in the bound -- rows rounded
+// to fp32 (relative 2^-24 each, an underflow below 2^-126 absolute), every sum and product of the
+// test (a dozen roundings of 2^-24 each), all below 1e-6 mag, so the test asks q < -1e-4 mag (on the
+// cfg4 lattice q / mag is about -3e-3).  X0, X1 are fp64 upper bounds rounded up into fp32.
+struct CertRowF {
+    float a0, a1, b, mg;
+};
+__device__ __forceinline__ bool cert_triple_f(const CertRowF& I, const CertRowF& J, const CertRowF& K, float X0,
+                                              float X1) {
+    float li = J.a0 * K.a1 - J.a1 * K.a0, lj = K.a0 * I.a1 - K.a1 * I.a0, lk = I.a0 * J.a1 - I.a1 * J.a0;
+    const bool pos = li >= 0.0f && lj >= 0.0f && lk >= 0.0f, neg = li <= 0.0f && lj <= 0.0f && lk <= 0.0f;
+    if (neg) {
+        li = -li;
+        lj = -lj;
+        lk = -lk;
+    }
+    const float sb = (li * I.b + lj * J.b) + lk * K.b;
+    const float r0 = (li * I.a0 + lj * J.a0) + lk * K.a0, r1 = (li * I.a1 + lj * J.a1) + lk * K.a1;
+    const float mag = (li * I.mg + lj * J.mg) + lk * K.mg;
+    const float q = (sb + fabsf(r0) * X0) + fabsf(r1) * X1;
+    return (pos || neg) && q < -1e-4f * mag;
+}
+template <int CAP>
+__device__ __forceinline__ bool hocbf_cert_f32(const float (&fa0)[CAP], const float (&fa1)[CAP], const float (&fb)[CAP],
+                                               int m, const double (&bb)[4]) {
+    if (m < 3) return false;
+    double X0d, X1d;
+    cert_bounds(bb, X0d, X1d);
+    const float X0 = (float)(X0d * (1.0 + 1e-6)), X1 = (float)(X1d * (1.0 + 1e-6));
+    int i = 0;
+    float bi = fb[0], ai0 = fa0[0], ai1 = fa1[0];
+#pragma unroll
+    for (int k = 1; k < CAP; ++k) {
+        const bool t = k < m && fb[k] < bi;
+        bi = t ? fb[k] : bi;
+        ai0 = t ? fa0[k] : ai0;
+        ai1 = t ? fa1[k] : ai1;
+        i = t ? k : i;
+    }
+    if (!(bi < 0.0f)) return false;
+    const float n2 = ai0 * ai0 + ai1 * ai1;
+    int j1 = -1, j2 = -1;
+    float s1 = INFINITY, s2 = INFINITY;
+    CertRowF J1{0.0f, 0.0f, 0.0f, 0.0f}, J2{0.0f, 0.0f, 0.0f, 0.0f};
+    float mg[CAP];
+#pragma unroll
+    for (int k = 0; k < CAP; ++k) {
+        mg[k] = 1.0f + fabsf(fb[k]) + fabsf(fa0[k]) * X0 + fabsf(fa1[k]) * X1;
+        const float dt = ai0 * fa0[k] + ai1 * fa1[k];
+        const float sc = fb[k] * n2 - bi * dt;
+        const bool ok = k < m && k != i && dt < 0.0f;
+        const bool t1 = ok && sc < s1, t2 = ok && !t1 && sc < s2;
+        const CertRowF Kr{fa0[k], fa1[k], fb[k], mg[k]};
+        if (t1) {
+            s2 = s1;
+            j2 = j1;
+            J2 = J1;
+            s1 = sc;
+            j1 = k;
+            J1 = Kr;
+        }
+        if (t2) {
+            s2 = sc;
+            j2 = k;
+            J2 = Kr;
+        }
+    }
+    if (j1 < 0) return false;
+    const CertRowF I{ai0, ai1, bi, 1.0f + fabsf(bi) + fabsf(ai0) * X0 + fabsf(ai1) * X1};
+    bool cert = false;
+#pragma unroll
+    for (int k = 0; k < CAP; ++k) {
+        const CertRowF K{fa0[k], fa1[k], fb[k], mg[k]};
+        const bool in = k < m && k != i;
+        cert = cert || (in && k != j1 && cert_triple_f(I, J1, K, X0, X1)) ||
+               (in && j2 >= 0 && k != j2 && cert_triple_f(I, J2, K, X0, X1));
+    }
+    return cert;
+}
+
+// The main lattice kernel's part of the solve (CBF_HOCBF_CERT): the QPs settled without one
+// Seidel event.  After the box phase (solve_rows' first part; a failure there is solve_hocbf's
+// BOX_INFEASIBLE), the first pass has no event exactly when every row holds at its point xb, and
+// then returns xb (OPTIMAL); when hocbf_cert_f32 proves the unrelaxed rows infeasible (so the first
+// pass fails at a row) and a relaxation is allowed, the second pass likewise returns xb (RELAXED,
+// one relaxation) when every row + 1 holds there.  Everything else -- about one ego in ten at cfg4
+// -- goes whole, with its sorted neighbour slots, to k_lattice_filter_hocbf_hard: a lane-per-ego
+// loop runs as many Seidel passes as its slowest lane needs, so the egos that take events are
+// gathered into full waves of their own.  True with S set when settled; nb: the row order's slots.
+struct HocbfHardRec {
+    int slot, m;
+    int nb[8];
+};
+constexpr int kHardQ2 = 16;  // the hard queue's counters: word 16 of each of the header's queue lines
+// its records: after the wide queue's slots in the queue area (CellWs::qrec holds kSubQ qcap
+// HardRecs of 104 B; slots 4 B + these 40 B per entry fit)
+__device__ __host__ inline HocbfHardRec* hocbf_hard_rec(int32_t* qslot, long qcap) {
+    return reinterpret_cast<HocbfHardRec*>(reinterpret_cast<char*>(qslot) +
+                                            ((4 * (size_t)kSubQ * qcap + 255) & ~(size_t)255));
+}
+static_assert(sizeof(HocbfHardRec) + 4 <= sizeof(HardRec), "the queue area holds both HOCBF queues");
+__device__ __forceinline__ bool hocbf_settle(const KP& P, const HP& H, const Ego& E, const double2* __restrict__ spos,
+                                             const double2* __restrict__ svel, const unsigned long long* keys, int ks,
+                                             int lane, int m, Sol& S, int (&nb)[kLdsRows]) {
+    S.status = CBF_STATUS_OPTIMAL;
+    S.iters = 0;
+    S.x0 = S.x1 = 0.0;
+    S.viol = 0.0;
+    const Box B = box_rhs(P, E);
+    const double bb[4] = {pmin(B.S[0], B.S[4]), pmin(B.S[1], B.S[6]), pmin(B.S[2], B.S[5]), pmin(B.S[3], B.S[7])};
+    double xb0, xb1;
+    if (box_phase(bb, xb0, xb1) >= 0) {  // solve_hocbf's first pass fails in its box phase
+        S.status = CBF_STATUS_BOX_INFEASIBLE;
+        return true;
+    }
+    unsigned long long kr[kLdsRows];
+#pragma unroll
+    for (int i = 0; i < kLdsRows; ++i) kr[i] = i < m ? keys[i * ks + lane] : ~0ull;
+    hocbf_sort8(kr);
+    float fa0[kLdsRows], fa1[kLdsRows], fb[kLdsRows];  // the certificate's fp32 copies
+    bool ok0 = true, ok1 = true;
+#pragma unroll
+    for (int i = 0; i < kLdsRows; ++i) {
+        fa0[i] = fa1[i] = fb[i] = 0.0f;
+        nb[i] = (int)(kr[i] & 0xFFFFFFFFull);
+        if (i < m) {
+            const double2 o = spos[nb[i]], ov = svel[nb[i]];
+            const double4 rw = hocbf_row(P, H, E.r0, E.r1, E.r2, E.r3, o.x, o.y, ov.x, ov.y, E.u0x, E.u0y);
+            ok0 = ok0 && feas(rw.x, rw.y, rw.z, xb0, xb1);
+            ok1 = ok1 && feas(rw.x, rw.y, rw.z + 1.0, xb0, xb1);  // (the relaxed row: cbf.py:85-87)
+            fa0[i] = (float)rw.x;
+            fa1[i] = (float)rw.y;
+            fb[i] = (float)rw.z;
+        }
+    }
+    if (ok0) {
+        S.x0 = xb0;
+        S.x1 = xb1;
+        return true;
+    }
+    if (ok1 && P.relax_cap >= 1 && hocbf_cert_f32<kLdsRows>(fa0, fa1, fb, m, bb)) {
+        S.status = CBF_STATUS_RELAXED;
+        S.iters = 1;
+        S.x0 = xb0;
+        S.x1 = xb1;
+        return true;
+    }
+    return false;
+}
+
 // Outputs of an owned ego (clip, Euler, status, count) and its guard extents.
 __device__ __forceinline__ void hocbf_finish(const KP& P, const Sol* S, const Ego& E, int m, int W, int row_begin,
                                              int row_end, int r, int c, double T, double2* __restrict__ pos_out,
@@ -447,7 +654,11 @@ __global__ void __launch_bounds__(kBlock) k_lattice_filter_hocbf(
     int32_t* __restrict__ status, int32_t* __restrict__ cnt, int guard_rows, double* __restrict__ ext_part,
     unsigned long long* __restrict__ solves, int32_t* __restrict__ hardq, int32_t* __restrict__ qslot, long qcap,
     const int32_t* __restrict__ sctl) {
-    __shared__ unsigned long long keys[kHocbfCap * kBlock];
+#if CBF_HOCBF_CERT
+    __shared__ unsigned long long keys[kLdsRows * kBlock];
+#else
+    __shared__ unsigned long long keys[kHocbfCap * kBlock];  // the keys, then the rows (3 doubles each)
+#endif
     const int bx = xcd_block();
     const int slot = bx * kBlock + threadIdx.x;
     if (sctl[2] != 0) {  // unusable cell list (build_begin / scan timeout): touch none of it
@@ -470,6 +681,23 @@ __global__ void __launch_bounds__(kBlock) k_lattice_filter_hocbf(
             if (m > kLdsRows && m <= kHocbfCap) {
                 const long rec = subq_append(hardq, bx % kSubQ, qcap);
                 if (rec >= 0) qslot[rec] = slot;  // (always: the queue holds every agent)
+            } else if (CBF_HOCBF_CERT && m > 0 && m <= kLdsRows) {
+                Sol S;
+                int nb[kLdsRows];
+                if (hocbf_settle(P, H, E, spos, svel, keys, kBlock, threadIdx.x, m, S, nb)) {
+                    solved = true;
+                    hocbf_finish(P, &S, E, m, W, row_begin, row_end, r, c, T, pos_out, u, status, cnt, guard_rows,
+                                 e0, e1, e2, e3);
+                } else {  // the Seidel events: k_lattice_filter_hocbf_hard
+                    const long rec = subq_append(hardq + kHardQ2, bx % kSubQ, qcap);
+                    if (rec >= 0) {  // (always: the queue holds every agent)
+                        HocbfHardRec& h = hocbf_hard_rec(qslot, qcap)[rec];
+                        h.slot = slot;
+                        h.m = m;
+#pragma unroll
+                        for (int i = 0; i < kLdsRows; ++i) h.nb[i] = nb[i];
+                    }
+                }
             } else if (m > 0 && m <= kLdsRows) {
                 const Sol S = hocbf_solve_lds<kLdsRows, true>(P, H, E, spos, svel, keys, reinterpret_cast<double*>(keys),
                                                         kBlock, threadIdx.x, m);
@@ -491,7 +719,8 @@ __global__ void __launch_bounds__(kBlock) k_lattice_filter_hocbf(
     if (ext_part) wave_extents(e0, e1, e2, e3, ext_part, (long)bx * (kBlock / 64) + (threadIdx.x >> 6));
 }
 
-// ---- the wide egos (kLdsRows < m <= kHocbfCap): one ego per wave, its rows across the lanes ----
+// ---- the wide egos (kLdsRows < m <= kHocbfCap, and those the main kernel's one pass left unsolved):
+// one ego per wave, its rows across the lanes ----
 // A lane-per-ego solve of such an ego is a chain of O(m^2) dependent row steps (up to 24 rows,
 // ~90 % of the QPs solved twice for the +1 relaxation); here lane i holds row i, so the feasibility
 // tests of every row run at once and only the interval fold of solve_rows stays serial.
@@ -581,7 +810,33 @@ __device__ __forceinline__ int solve_rows_wave(const double (&bb)[4], double a0,
     return -1;
 }
 
-// solve_hocbf over the lanes' rows: +1 relaxation of every row while infeasible
+// hocbf_cert over the rows held one per lane (lane t < m: row t): i and j found by wave
+// reductions, every lane's row tried as the third; the same test and proof (any i, j, k do).
+__device__ __forceinline__ bool hocbf_cert_wave(double a0, double a1, double b, int m, int lane,
+                                                const double (&bb)[4]) {
+    if (m < 3) return false;
+    const bool mine = lane < m;
+    const double bmin = __ockl_wfred_min_f64(mine ? b : INFINITY);
+    if (!(bmin < 0.0)) return false;
+    const unsigned long long mi_ = __ballot(mine && b == bmin);
+    const int i = __ffsll((long long)mi_) - 1;
+    const double ai0 = rdl(a0, i), ai1 = rdl(a1, i), bi = rdl(b, i);
+    const double dt = ai0 * a0 + ai1 * a1;
+    const double sc = b * (ai0 * ai0 + ai1 * ai1) - bi * dt;
+    const bool cand = mine && lane != i && dt < 0.0;
+    const double smin = __ockl_wfred_min_f64(cand ? sc : INFINITY);
+    const unsigned long long mj_ = __ballot(cand && sc == smin);
+    if (!mj_) return false;
+    const int j = __ffsll((long long)mj_) - 1;
+    double X0, X1;
+    cert_bounds(bb, X0, X1);
+    const CertRow I = cert_row(ai0, ai1, bi, X0, X1), J = cert_row(rdl(a0, j), rdl(a1, j), rdl(b, j), X0, X1);
+    const CertRow K = cert_row(a0, a1, b, X0, X1);
+    return __ballot(mine && lane != i && lane != j && cert_triple(I, J, K, X0, X1)) != 0;
+}
+
+// solve_hocbf over the lanes' rows: +1 relaxation of every row while infeasible (CBF_HOCBF_CERT:
+// a first pass hocbf_cert_wave proves infeasible is skipped, as solve_hocbf does)
 __device__ __forceinline__ Sol solve_hocbf_wave(const KP& P, const Ego& E, double a0, double a1, double b, int m,
                                                 int lane) {
     const Box B = box_rhs(P, E);
@@ -591,6 +846,14 @@ __device__ __forceinline__ Sol solve_hocbf_wave(const KP& P, const Ego& E, doubl
     S.iters = 0;
     S.x0 = S.x1 = 0.0;
     S.viol = 0.0;
+    if (CBF_HOCBF_CERT && P.relax_cap >= 1) {
+        double xb0, xb1;
+        if (box_phase(bb, xb0, xb1) < 0 && hocbf_cert_wave(a0, a1, b, m, lane, bb)) {
+            b = b + 1.0;  // cbf.py:85-87
+            S.iters = 1;
+            S.status = CBF_STATUS_RELAXED;
+        }
+    }
     for (;;) {
         const int fail = solve_rows_wave(bb, a0, a1, b, m, lane, S.x0, S.x1);
         if (fail < 0) break;
@@ -630,17 +893,86 @@ __device__ __forceinline__ unsigned long long wave_sort64(unsigned long long key
 // slot) sorted across the lanes into the reference's row order, lane i forms row i, then the
 // wave's solve.  The same neighbour set, rows and solve as hocbf_scan + hocbf_solve_lds, bit for
 // bit.  More candidates than lanes are taken 64 at a time into LDS.
-__global__ void __launch_bounds__(64) k_lattice_filter_hocbf_wide(
-    KP P, HP H, CellGrid G, int W, int row_begin, int row_end, int win_row0, const double2* __restrict__ spos,
-    const double2* __restrict__ svel, const int32_t* __restrict__ sidx, const int32_t* __restrict__ start, double T,
+// blocks per sub-queue of the hard role: ~10 % of the egos at cfg4 (~2 k per sub-queue) in one
+// round of lanes
+#ifndef CBF_HOCBF_HARD_PER_Q
+#define CBF_HOCBF_HARD_PER_Q 64
+#endif
+constexpr int kHocbfHardPerQ = CBF_HOCBF_HARD_PER_Q;
+static_assert(kHocbfHardPerQ <= 128, "lattice_ext_bytes reserves 128 blocks per sub-queue");
+
+// The egos hocbf_settle left (CBF_HOCBF_CERT): solve_hocbf whole, one lane per ego, rows formed
+// from the queued neighbour slots into LDS, the sub-queue drained in full waves as drain_subq does
+// -- the main kernel's own solve (hocbf_solve_lds), on waves made only of such egos.
+// (block bid of the hard role; rl: 3 kLdsRows 64 doubles of LDS)
+__device__ __forceinline__ void hocbf_hard_block(
+    int bid, double* rl, const KP& P, const HP& H, int W, int row_begin, int row_end, int win_row0,
+    const double2* __restrict__ spos, const double2* __restrict__ svel, const int32_t* __restrict__ sidx, double T,
     double2* __restrict__ pos_out, double2* __restrict__ u, int32_t* __restrict__ status, int32_t* __restrict__ cnt,
     int guard_rows, double* __restrict__ ext_part, unsigned long long* __restrict__ solves,
-    int32_t* __restrict__ hardq, const int32_t* __restrict__ qslot, long qcap) {
-    __shared__ unsigned long long hits[kHocbfCap + 64];
+    int32_t* __restrict__ hardq, int32_t* __restrict__ qslot, long qcap) {
+    const int lane = threadIdx.x;
+    const HocbfHardRec* __restrict__ hrec = hocbf_hard_rec(qslot, qcap);
+    int32_t* __restrict__ hq = hardq + kHardQ2;
+    double e0 = INFINITY, e1 = -INFINITY, e2 = -INFINITY, e3 = INFINITY;
+    int ns = 0;
+    // drain_subq for block bid
+    const int q = bid % kSubQ, kb = bid / kSubQ;
+    const int nq0 = hq[32 * (1 + q)];
+    const int nq = nq0 < qcap ? nq0 : (int)qcap;
+    const int need = (nq + 63) / 64;
+    const int nwork = need < kHocbfHardPerQ ? need : kHocbfHardPerQ;
+    if (kb >= nwork) return;
+    int done = 0;
+    if (lane == 0) done = atomicAdd(&hq[32 * (1 + kSubQ + q)], 1);
+    for (int i = kb * 64 + lane; i < nq; i += nwork * 64) {
+        const HocbfHardRec h = hrec[(long)q * qcap + i];
+        const int w = sidx[h.slot];
+        const int r = win_row0 + w / W, c = w % W;
+        const double2 pe = spos[h.slot], ve = svel[h.slot];
+        Ego E;
+        ego_init(P, E, pe.x, pe.y, ve.x, ve.y, ve.x, ve.y);
+        E.count = h.m;
+#pragma unroll
+        for (int k = 0; k < kLdsRows; ++k) {
+            if (k < h.m) {
+                const double2 o = spos[h.nb[k]], ov = svel[h.nb[k]];
+                const double4 rw = hocbf_row(P, H, E.r0, E.r1, E.r2, E.r3, o.x, o.y, ov.x, ov.y, E.u0x, E.u0y);
+                rl[(3 * k) * 64 + lane] = rw.x;
+                rl[(3 * k + 1) * 64 + lane] = rw.y;
+                rl[(3 * k + 2) * 64 + lane] = rw.z;
+            }
+        }
+        LdsRows R{rl, 64, lane, h.m};
+        const Sol S = solve_hocbf(P, E, R);
+        hocbf_finish(P, &S, E, h.m, W, row_begin, row_end, r, c, T, pos_out, u, status, cnt, guard_rows, e0, e1, e2,
+                     e3);
+        ++ns;
+    }
+    if (lane == 0 && done == nwork - 1) {  // the last working block empties the sub-queue
+        hq[32 * (1 + q)] = 0;
+        hq[32 * (1 + kSubQ + q)] = 0;
+    }
+    if (solves) {
+        int tot = ns;
+        for (int o = 32; o > 0; o >>= 1) tot += __shfl_xor(tot, o, 64);
+        if (lane == 0 && tot) atomicAdd(&solves[16 * stat_slot(bid)], (unsigned long long)tot);
+    }
+    if (ext_part) wave_extents(e0, e1, e2, e3, ext_part, bid);
+}
+
+// (block bid of the wide role; hits: kHocbfCap + 64 words of LDS)
+__device__ __forceinline__ void hocbf_wide_block(
+    int bid, unsigned long long* hits, const KP& P, const HP& H, const CellGrid& G, int W, int row_begin,
+    int row_end, int win_row0, const double2* __restrict__ spos, const double2* __restrict__ svel,
+    const int32_t* __restrict__ sidx, const int32_t* __restrict__ start, double T, double2* __restrict__ pos_out,
+    double2* __restrict__ u, int32_t* __restrict__ status, int32_t* __restrict__ cnt, int guard_rows,
+    double* __restrict__ ext_part, unsigned long long* __restrict__ solves, int32_t* __restrict__ hardq,
+    const int32_t* __restrict__ qslot, long qcap) {
     const int lane = threadIdx.x;
     double e0 = INFINITY, e1 = -INFINITY, e2 = -INFINITY, e3 = INFINITY;
     int ns = 0;
-    const int q = blockIdx.x % kSubQ, k = blockIdx.x / kSubQ;
+    const int q = bid % kSubQ, k = bid / kSubQ;
     const int nq0 = hardq[32 * (1 + q)];
     const int nq = nq0 < qcap ? nq0 : (int)qcap;  // (a full sub-queue's counter runs past qcap: subq_append)
     const int nwork = nq < kWidePerQ ? nq : kWidePerQ;
@@ -716,8 +1048,41 @@ __global__ void __launch_bounds__(64) k_lattice_filter_hocbf_wide(
         hardq[32 * (1 + q)] = 0;
         hardq[32 * (1 + kSubQ + q)] = 0;
     }
-    if (solves && lane == 0 && ns) atomicAdd(&solves[16 * stat_slot(blockIdx.x)], (unsigned long long)ns);
-    if (ext_part) wave_extents(e0, e1, e2, e3, ext_part, blockIdx.x);
+    if (solves && lane == 0 && ns) atomicAdd(&solves[16 * stat_slot(bid)], (unsigned long long)ns);
+    if (ext_part) wave_extents(e0, e1, e2, e3, ext_part, bid);
+}
+
+__global__ void __launch_bounds__(64) k_lattice_filter_hocbf_wide(
+    KP P, HP H, CellGrid G, int W, int row_begin, int row_end, int win_row0, const double2* __restrict__ spos,
+    const double2* __restrict__ svel, const int32_t* __restrict__ sidx, const int32_t* __restrict__ start, double T,
+    double2* __restrict__ pos_out, double2* __restrict__ u, int32_t* __restrict__ status, int32_t* __restrict__ cnt,
+    int guard_rows, double* __restrict__ ext_part, unsigned long long* __restrict__ solves,
+    int32_t* __restrict__ hardq, const int32_t* __restrict__ qslot, long qcap) {
+    __shared__ unsigned long long hits[kHocbfCap + 64];
+    hocbf_wide_block(blockIdx.x, hits, P, H, G, W, row_begin, row_end, win_row0, spos, svel, sidx, start, T, pos_out,
+                     u, status, cnt, guard_rows, ext_part, solves, hardq, qslot, qcap);
+}
+
+// The rest of a HOCBF advance in one launch (CBF_HOCBF_CERT): blocks [0, hh) drain the hard queue
+// (hocbf_hard_block), the others the wide queue (hocbf_wide_block) -- two latency-bound sets of
+// chains side by side instead of one launch after the other.  Extents records: the hard blocks',
+// then the wide blocks'.
+__global__ void __launch_bounds__(64) k_lattice_filter_hocbf_rest(
+    KP P, HP H, CellGrid G, int W, int row_begin, int row_end, int win_row0, const double2* __restrict__ spos,
+    const double2* __restrict__ svel, const int32_t* __restrict__ sidx, const int32_t* __restrict__ start, double T,
+    double2* __restrict__ pos_out, double2* __restrict__ u, int32_t* __restrict__ status, int32_t* __restrict__ cnt,
+    int guard_rows, double* __restrict__ ext_part, unsigned long long* __restrict__ solves,
+    int32_t* __restrict__ hardq, int32_t* __restrict__ qslot, long qcap, int hh) {
+    __shared__ double lds[3 * kLdsRows * 64];
+    static_assert(sizeof(lds) >= 8 * (kHocbfCap + 64), "the wide role's hit list fits the hard role's rows");
+    const int b = blockIdx.x;
+    if (b < hh)
+        hocbf_hard_block(b, lds, P, H, W, row_begin, row_end, win_row0, spos, svel, sidx, T, pos_out, u, status, cnt,
+                         guard_rows, ext_part, solves, hardq, qslot, qcap);
+    else
+        hocbf_wide_block(b - hh, reinterpret_cast<unsigned long long*>(lds), P, H, G, W, row_begin, row_end, win_row0,
+                         spos, svel, sidx, start, T, pos_out, u, status, cnt, guard_rows,
+                         ext_part ? ext_part + 4l * hh : nullptr, solves, hardq, qslot, qcap);
 }
 
 inline int nblocks(long n) { return (int)((n + kBlock - 1) / kBlock); }
@@ -784,13 +1149,25 @@ extern "C" int cbf_lattice_advance_hocbf(const cbf_params* p, const cbf_hocbf* h
                        reinterpret_cast<double2*>(pos_out), reinterpret_cast<double2*>(u), status, nbr_count,
                        guard_rows, ext_part, reinterpret_cast<unsigned long long*>(solves), Wk.hardq,
                        reinterpret_cast<int32_t*>(Wk.qrec), Wk.qcap, Wk.sctl);
+    const long nw = lattice_ext_waves(n);
     const int hb = lattice_wide_blocks(n);
-    hipLaunchKernelGGL(k_lattice_filter_hocbf_wide, dim3(hb), dim3(64), 0, s, make_kp(p), make_hp(hp), G, W,
-                       row_begin, row_end, win_row0, Wk.spos, Wk.svel, Wk.sidx, Wk.start, T,
-                       reinterpret_cast<double2*>(pos_out), reinterpret_cast<double2*>(u), status, nbr_count,
-                       guard_rows, ext_part ? ext_part + 4l * lattice_ext_waves(n) : nullptr,
-                       reinterpret_cast<unsigned long long*>(solves), Wk.hardq,
-                       reinterpret_cast<const int32_t*>(Wk.qrec), Wk.qcap);
-    if (extents) launch_extents_finalize((int)lattice_ext_waves(n) + hb, ext_part, extents, s);
+    int hh = 0;  // the hard role's blocks (their extents records follow the main kernel's waves)
+    if (CBF_HOCBF_CERT) {
+        hh = kSubQ * kHocbfHardPerQ;
+        hipLaunchKernelGGL(k_lattice_filter_hocbf_rest, dim3(hh + hb), dim3(64), 0, s, make_kp(p), make_hp(hp), G, W,
+                           row_begin, row_end, win_row0, Wk.spos, Wk.svel, Wk.sidx, Wk.start, T,
+                           reinterpret_cast<double2*>(pos_out), reinterpret_cast<double2*>(u), status, nbr_count,
+                           guard_rows, ext_part ? ext_part + 4l * nw : nullptr,
+                           reinterpret_cast<unsigned long long*>(solves), Wk.hardq,
+                           reinterpret_cast<int32_t*>(Wk.qrec), Wk.qcap, hh);
+    } else {
+        hipLaunchKernelGGL(k_lattice_filter_hocbf_wide, dim3(hb), dim3(64), 0, s, make_kp(p), make_hp(hp), G, W,
+                           row_begin, row_end, win_row0, Wk.spos, Wk.svel, Wk.sidx, Wk.start, T,
+                           reinterpret_cast<double2*>(pos_out), reinterpret_cast<double2*>(u), status, nbr_count,
+                           guard_rows, ext_part ? ext_part + 4l * nw : nullptr,
+                           reinterpret_cast<unsigned long long*>(solves), Wk.hardq,
+                           reinterpret_cast<const int32_t*>(Wk.qrec), Wk.qcap);
+    }
+    if (extents) launch_extents_finalize((int)(nw + hh) + hb, ext_part, extents, s);
     return (int)hipGetLastError();
 }

@@ -356,9 +356,11 @@ inline int lattice_wide_blocks(long) { return kSubQ * kWidePerQ; }
 #endif
 constexpr int kHardPerQ = CBF_HARD_PER_Q;
 inline int lattice_hard_blocks(long) { return kSubQ * kHardPerQ; }
+// (the HOCBF step has both: its hard kernel's blocks -- up to 128 per sub-queue -- then the wide
+// kernel's)
 inline size_t lattice_ext_bytes(long win_n) {
-    const long hb = lattice_hard_blocks(win_n), wb = lattice_wide_blocks(win_n);
-    return align256(32 * (size_t)(lattice_ext_waves(win_n) + (hb > wb ? hb : wb)));
+    const long hb = lattice_hard_blocks(win_n), wb = lattice_wide_blocks(win_n), hh = kSubQ * 128l;
+    return align256(32 * (size_t)(lattice_ext_waves(win_n) + (hb > hh ? hb : hh) + wb));
 }
 
 inline int check_lattice(const cbf_params* p, const cbf_grid* grid, int32_t W, int32_t H, int32_t row_begin,

@@ -210,3 +210,41 @@ def test_lattice_hocbf_run_graph_equals_steps():
     assert int((A.nbr_count > 8).sum()) > 0
     with pytest.raises(ValueError):
         B.run(3, history=True)
+
+
+@pytest.mark.parametrize("spacing", [0.145, 0.1])
+def test_lattice_hocbf_certificate_skip_is_bit_identical(spacing):
+    """The HOCBF kernels skip a first relaxation pass that a three-row Farkas certificate proves
+    infeasible (hocbf_cert / hocbf_cert_wave).  Against the test build that runs every pass
+    (tests/_lib/libcbf_hocbfnocert.so, CBF_HOCBF_CERT=0), advance by advance on the same cell list:
+    positions, controls, statuses (relaxation counts included) and neighbour counts bit for bit,
+    on the cfg4 spacing (most egos certified) and a denser one (wide-kernel egos too)."""
+    import ctypes as C
+    import os
+    from cbf_amd import _lib, scenarios
+    V = C.CDLL(os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "libcbf_hocbfnocert.so"))
+    adv = V.cbf_lattice_advance_hocbf
+    adv.restype, adv.argtypes = _lib.SIGNATURES["cbf_lattice_advance_hocbf"]
+    W = H = 96
+    L = swarm.LatticeSwarm(scenarios.lattice(W, H, seed=4, spacing=spacing), W, H, gain=scenarios.LATTICE_GAIN,
+                           barrier="euclidean_hocbf")
+    relaxed = wide = 0
+    for _ in range(6):
+        L.build_phase()
+        p0 = L.pos.clone()
+        L.advance_phase()
+        torch.cuda.synchronize()
+        got = [t.clone() for t in (L.pos, L.u, L.status, L.nbr_count)]
+        L.pos.copy_(p0)
+        assert adv(L.cp, C.byref(L.hp), C.byref(L.grid), W, H, 0, H, 0, H, _lib.ptr(L.pos), L.T, _lib.ptr(L.pos),
+                   _lib.ptr(L.u), _lib.ptr(L.status), _lib.ptr(L.nbr_count), 0, None, None, _lib.ptr(L.ws),
+                   L.ws_bytes, _lib.stream_handle()) == 0
+        torch.cuda.synchronize()
+        for a, b in zip(got, (L.pos, L.u, L.status, L.nbr_count)):
+            assert torch.equal(a, b)
+        st = L.status.cpu().numpy()
+        relaxed += int(((st & 0xFF) == cbf_amd.STATUS_RELAXED).sum())
+        wide += int((L.nbr_count > 8).sum())
+    assert relaxed > 0
+    if spacing < 0.12:
+        assert wide > 0
