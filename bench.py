@@ -587,7 +587,7 @@ def bench_lattice(args, ws, rank, local):
     achieved_adv = FILTER_BYTES_PER_AGENT * n_local / (k_ms * 1e-3) / 1e9
     adv_kernels = WINDOW_KERNELS if cull == "window" else ADVANCE_KERNELS
     traffic = load_pmc_traffic(args.config, adv_kernels[:1]) if args.barrier == "reference" else \
-        load_pmc_traffic(args.config + "_hocbf", ("k_lattice_filter_hocbf", "k_lattice_filter_hocbf_wide"))
+        load_pmc_traffic(args.config + "_hocbf", ("k_lattice_filter_hocbf", "k_lattice_filter_hocbf_rest"))
     traffic_adv = load_pmc_traffic(args.config, adv_kernels) if args.barrier == "reference" else traffic
     res = {
         "metric": METRIC,
@@ -649,7 +649,7 @@ def bench_lattice(args, ws, rank, local):
                                    "times it" if own else "HIP events on its launch stream, the end event recorded "
                                    "by the advance call between it and the queued-QP kernel") + ")")
                      if args.barrier == "reference"
-                     else "advance phase: k_lattice_filter_hocbf + k_lattice_filter_hocbf_wide",
+                     else "advance phase: k_lattice_filter_hocbf + k_lattice_filter_hocbf_rest",
                      "kernel_ms": f_ms,
                      "kernel_ms_stream_events": f_stream_ms,
                      "advance_phase": {"kernels": " + ".join(k.split("<")[0] for k in adv_kernels), "ms": k_ms,
