@@ -37,6 +37,9 @@ __device__ __forceinline__ double4 hocbf_row(const KP& P, const HP& H, double r0
 #ifndef CBF_HOCBF_CERT
 #define CBF_HOCBF_CERT 1  // 0: every relaxation pass run in the main kernel, no infeasibility certificate
 #endif
+#ifndef CBF_HOCBF_HARD_BATCHED
+#define CBF_HOCBF_HARD_BATCHED 1  // the hard role's solve with batched row loads (0: solve_hocbf's loops)
+#endif
 #ifndef CBF_HOCBF_CERT_J
 #define CBF_HOCBF_CERT_J 1  // partners j tried with every third row (2: the best two; main kernel
                             // 80.9 against 73.3 us at cfg4, the hard role 42.3 against 43.1)
@@ -901,6 +904,82 @@ __device__ __forceinline__ unsigned long long wave_sort64(unsigned long long key
 // slot) sorted across the lanes into the reference's row order, lane i forms row i, then the
 // wave's solve.  The same neighbour set, rows and solve as hocbf_scan + hocbf_solve_lds, bit for
 // bit.  More candidates than lanes are taken 64 at a time into LDS.
+// solve_rows for rows staged in LDS (LdsRows) with the loops over earlier rows unrolled over all
+// CAP slots and predicated (j < i), so that each event's row loads issue together instead of one
+// guarded round trip per row; the same events, arithmetic and order.  The checks after an event
+// return 4 + i whichever plane fails first, so they are one conjunction.
+template <int CAP>
+__device__ __forceinline__ int solve_rows_batched(const double (&bb)[4], const LdsRows& R, double& xo0,
+                                                  double& xo1) {
+    const double ba0[4] = {1.0, 0.0, -1.0, 0.0}, ba1[4] = {0.0, 1.0, 0.0, -1.0};
+    double x0, x1;
+    const int hb = box_phase(bb, x0, x1);
+    if (hb >= 0) return hb;
+    for (int i = 0; i < R.m; ++i) {
+        double a0, a1, b;
+        R.row(i, a0, a1, b);
+        if (feas(a0, a1, b, x0, x1)) continue;
+        const double n2 = a0 * a0 + a1 * a1;
+        if (!(n2 > 0)) return 4 + i;
+        const double t = b / n2;
+        const double p0 = t * a0, p1 = t * a1;
+        const double d0 = -a1, d1 = a0;
+        Interval I;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) I.add(ba0[j], ba1[j], bb[j], d0, d1, p0, p1);
+#pragma unroll
+        for (int j = 0; j < CAP; ++j) {
+            double c0, c1, e;
+            R.row(j, c0, c1, e);
+            if (j < i) I.add(c0, c1, e, d0, d1, p0, p1);
+        }
+        const double s = I.clamp0();
+        x0 = p0 + s * d0;
+        x1 = p1 + s * d1;
+        bool ok = true;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) ok = ok & feas(ba0[j], ba1[j], bb[j], x0, x1);
+#pragma unroll
+        for (int j = 0; j < CAP; ++j) {
+            double c0, c1, e;
+            R.row(j, c0, c1, e);
+            ok = ok & (j > i || feas(c0, c1, e, x0, x1));
+        }
+        if (!ok) return 4 + i;
+    }
+    xo0 = x0;
+    xo1 = x1;
+    return -1;
+}
+// solve_hocbf over solve_rows_batched
+__device__ __forceinline__ Sol solve_hocbf_batched(const KP& P, const Ego& E, LdsRows& R) {
+    const Box B = box_rhs(P, E);
+    const double bb[4] = {pmin(B.S[0], B.S[4]), pmin(B.S[1], B.S[6]), pmin(B.S[2], B.S[5]), pmin(B.S[3], B.S[7])};
+    Sol S;
+    S.status = CBF_STATUS_OPTIMAL;
+    S.iters = 0;
+    S.x0 = S.x1 = 0.0;
+    S.viol = 0.0;
+    for (;;) {  // oracle/cbf_oracle.c:solve_hocbf
+        const int fail = solve_rows_batched<kLdsRows>(bb, R, S.x0, S.x1);
+        if (fail < 0) break;
+        if (fail < 4) {
+            S.status = CBF_STATUS_BOX_INFEASIBLE;
+            S.x0 = S.x1 = 0.0;
+            break;
+        }
+        if (S.iters >= P.relax_cap) {
+            S.status = CBF_STATUS_RELAX_CAP;
+            S.x0 = S.x1 = 0.0;
+            break;
+        }
+        R.relax();
+        S.iters++;
+        S.status = CBF_STATUS_RELAXED;
+    }
+    return S;
+}
+
 // blocks per sub-queue of the hard role: ~10 % of the egos at cfg4 (~2 k per sub-queue) in one
 // round of lanes
 #ifndef CBF_HOCBF_HARD_PER_Q
@@ -952,7 +1031,11 @@ __device__ __forceinline__ void hocbf_hard_block(
             }
         }
         LdsRows R{rl, 64, lane, h.m};
+#if CBF_HOCBF_HARD_BATCHED
+        const Sol S = solve_hocbf_batched(P, E, R);
+#else
         const Sol S = solve_hocbf(P, E, R);
+#endif
         hocbf_finish(P, &S, E, h.m, W, row_begin, row_end, r, c, T, pos_out, u, status, cnt, guard_rows, e0, e1, e2,
                      e3);
         ++ns;
