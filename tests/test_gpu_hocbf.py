@@ -212,8 +212,8 @@ def test_lattice_hocbf_run_graph_equals_steps():
         B.run(3, history=True)
 
 
-@pytest.mark.parametrize("spacing", [0.145, 0.1])
-def test_lattice_hocbf_certificate_skip_is_bit_identical(spacing):
+@pytest.mark.parametrize("spacing,poison", [(0.145, False), (0.1, False), (0.145, True)])
+def test_lattice_hocbf_certificate_skip_is_bit_identical(spacing, poison):
     """The HOCBF kernels skip a first relaxation pass that a three-row Farkas certificate proves
     infeasible (hocbf_cert / hocbf_cert_wave).  Against the test build that runs every pass
     (tests/_lib/libcbf_hocbfnocert.so, CBF_HOCBF_CERT=0), advance by advance on the same cell list:
@@ -226,8 +226,11 @@ def test_lattice_hocbf_certificate_skip_is_bit_identical(spacing):
     adv = V.cbf_lattice_advance_hocbf
     adv.restype, adv.argtypes = _lib.SIGNATURES["cbf_lattice_advance_hocbf"]
     W = H = 96
-    L = swarm.LatticeSwarm(scenarios.lattice(W, H, seed=4, spacing=spacing), W, H, gain=scenarios.LATTICE_GAIN,
-                           barrier="euclidean_hocbf")
+    pos = scenarios.lattice(W, H, seed=4, spacing=spacing)
+    if poison:  # non-finite agents: their neighbours' rows are NaN / inf (never settled by the certificate)
+        pos[W * 40 + 40] = (np.nan, 0.5)
+        pos[W * 60 + 20] = (np.inf, -np.inf)
+    L = swarm.LatticeSwarm(pos, W, H, gain=scenarios.LATTICE_GAIN, barrier="euclidean_hocbf")
     relaxed = wide = 0
     for _ in range(6):
         L.build_phase()
@@ -241,7 +244,8 @@ def test_lattice_hocbf_certificate_skip_is_bit_identical(spacing):
                    L.ws_bytes, _lib.stream_handle()) == 0
         torch.cuda.synchronize()
         for a, b in zip(got, (L.pos, L.u, L.status, L.nbr_count)):
-            assert torch.equal(a, b)
+            assert torch.equal(a.cpu().view(torch.int64) if a.dtype == torch.float64 else a.cpu(),
+                               b.cpu().view(torch.int64) if b.dtype == torch.float64 else b.cpu())  # (NaN bits too)
         st = L.status.cpu().numpy()
         relaxed += int(((st & 0xFF) == cbf_amd.STATUS_RELAXED).sum())
         wide += int((L.nbr_count > 8).sum())
