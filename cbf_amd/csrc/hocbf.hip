@@ -374,7 +374,7 @@ constexpr int kHScan = 6;  // candidates in flight per lane in the HOCBF scan
 // list keys[i * ks + lane] (first kHocbfCap of them).  Returns the hit count m.
 // SORTED: keep the list sorted by insertion (all kHocbfCap slots); otherwise append the first
 // kLdsRows hits unsorted (the main kernel sorts them in registers, hocbf_sort8; egos with more
-// hits are queued and rescanned sorted by the wide kernel).
+// hits are queued and rescanned sorted by the wide role).
 template <bool SORTED = true>
 __device__ __forceinline__ int hocbf_scan(const KP& P, const CellGrid& G, const Ego& E, const double2* __restrict__ spos,
                                           const int32_t* __restrict__ sidx, const int32_t* __restrict__ start,
@@ -655,9 +655,11 @@ __device__ __forceinline__ void hocbf_finish(const KP& P, const Sol* S, const Eg
 // Lattice step K4 in HOCBF mode: one lane per cell-sorted slot (owned agents); exact cull over
 // the 3x3 cells; hits kept as LDS keys (entity << 32 | slot) in ascending entity order (the
 // oracle's reference-order row sequence, independent of the atomic arrival order inside a cell);
-// rows computed into LDS, solve, clip, Euler, outputs as k_lattice_filter.  Egos with more than
-// kLdsRows neighbours are queued (their slot, hardq) for k_lattice_filter_hocbf_wide, so the
-// long tail does not hold whole waves; more than kHocbfCap: CBF_STATUS_NBR_OVERFLOW, u = u0.
+// the QP settled here when it needs no Seidel event (hocbf_settle, CBF_HOCBF_CERT), else queued
+// whole for the hard role of k_lattice_filter_hocbf_rest (without CBF_HOCBF_CERT: the rows in LDS and
+// the full solve here); clip, Euler, outputs as k_lattice_filter.  Egos with more than kLdsRows
+// neighbours are queued (their slot, hardq) for the wide role, so the long tail does not hold
+// whole waves; more than kHocbfCap: CBF_STATUS_NBR_OVERFLOW, u = u0.
 __global__ void __launch_bounds__(kBlock) k_lattice_filter_hocbf(
     KP P, HP H, CellGrid G, int W, int row_begin, int row_end, int win_row0, long nwin, long ncell,
     const double2* __restrict__ spos, const double2* __restrict__ svel, const int32_t* __restrict__ sidx,
