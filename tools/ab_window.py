@@ -1,6 +1,7 @@
 """A/B timing of the lattice step for a source tree (tools/_ab/<tree> or .): hipGraphs of run(10),
 per-timestep time, and the build / filter / advance kernels by HIP events (the filter's end event
 recorded by the advance call).  Usage: python tools/ab_window.py <tree-root> <cull> [spacing] [rows] [placement]"""
+import os
 import sys
 import time
 
@@ -15,9 +16,9 @@ from cbf_amd import scenarios, swarm  # noqa: E402
 
 W = 1024
 L = swarm.LatticeSwarm(scenarios.lattice(W, H, seed=0, spacing=spacing), W, H, gain=0.25, cull=cull,
-                       params=swarm.FilterParams(solve_placement=placement))
+                       params=swarm.FilterParams(solve_placement=placement,
+                                                 window_guard=os.environ.get("AB_GUARD", "auto")))
 L.collect_stats = False
-import os  # noqa: E402
 if os.environ.get("AB_DRIVER"):
     # the driver's timed span: timesteps 6-25 (bench.py --steps 20 --warmup 5), as two run(10) graph
     # replays from the state after 5 timesteps, repeated from a snapshot
