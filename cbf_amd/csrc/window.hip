@@ -36,6 +36,9 @@ extern "C" __device__ __attribute__((const)) double __ockl_wfred_max_f64(double)
 
 namespace {
 
+#ifndef CBF_TILE_EARLY_ROWS
+#define CBF_TILE_EARLY_ROWS 1  // rows -1..+1 tested before the row guard is read (0: after)
+#endif
 #ifndef CBF_TILE_FUSED_FLUSH
 #define CBF_TILE_FUSED_FLUSH 1  // 0: the hits' rows formed after the scan, from the hit mask (round 6)
 #endif
@@ -652,10 +655,13 @@ __global__ void __launch_bounds__(kTileT) __attribute__((amdgpu_waves_per_eu((IN
     int stalls = 0;
     const int ga = r0 + 1 + (int)threadIdx.x, gb = r0 - kWinPre + (int)threadIdx.x;
     double gsy = INFINITY, gpy = -INFINITY;
-    if (threadIdx.x < kTileGuard) {
-        if (ga < Q.cr1) gsy = ld_guard(sylo + ga, fold, token, -INFINITY, stalls);
-        if (gb >= Q.cr0) gpy = ld_guard(pyhi + gb, fold, token, INFINITY, stalls);
-    }
+    auto poll_guard = [&]() {
+        if (threadIdx.x < kTileGuard) {
+            if (ga < Q.cr1) gsy = ld_guard(sylo + ga, fold, token, -INFINITY, stalls);
+            if (gb >= Q.cr0) gpy = ld_guard(pyhi + gb, fold, token, INFINITY, stalls);
+        }
+    };
+    if (!CBF_TILE_EARLY_ROWS) poll_guard();
 #pragma unroll
     for (int k = 0; k < kStageK; ++k) {
         const int i = threadIdx.x + k * kTileT;
@@ -674,7 +680,7 @@ __global__ void __launch_bounds__(kTileT) __attribute__((amdgpu_waves_per_eu((IN
             L.g[i] = make_float2(INFINITY, -INFINITY);
         }
     }
-    if (threadIdx.x < kTileGuard) {
+    if (!CBF_TILE_EARLY_ROWS && threadIdx.x < kTileGuard) {
         L.sy[threadIdx.x] = gsy;
         L.py[threadIdx.x] = gpy;
     }
@@ -688,30 +694,6 @@ __global__ void __launch_bounds__(kTileT) __attribute__((amdgpu_waves_per_eu((IN
         ego_init(P, E, pe.x, pe.y, ve.x, ve.y, ve.x, ve.y);
         fin = isfinite(pe.x) && isfinite(pe.y);
     }
-    int Kd = -1, Ku = -1;
-    bool slow = false;
-    // column-sentinel thresholds in fp32: a sentinel x with x > thR (x < thL) proves the columns
-    // from it on out of range, since then x - r0 >= win_dn > win_d in real arithmetic and so in
-    // fp64 (rounding is monotone); thR is r0 + win_dn rounded up (fp64, then to fp32 outward) and
-    // thL likewise down.  At most one fp32 ulp looser than the fp64 test of the extents: a looser
-    // bound only widens a window.  (Non-finite or huge coordinates give +-inf: every column needed.)
-    float thR = INFINITY, thL = -INFINITY;
-    if (fin) {
-        Ku = 0;
-        Kd = 0;
-#pragma unroll
-        for (int k = 0; k < kWinPre; ++k) {
-            Ku += !(L.sy[wv + k] - E.r1 > P.win_d) ? 1 : 0;
-            Kd += !(E.r1 - L.py[wv + kWinPre - 1 - k] > P.win_d) ? 1 : 0;
-        }
-        if (Ku > kTileKS || Kd > kTileKS) slow = true;  // beyond the staged rows: the unbounded form
-        const double tr = E.r0 + P.win_dn, tl = E.r0 - P.win_dn;
-        thR = f32_up(tr + (fabs(tr) * 0x1p-50 + 0x1p-1070));
-        thL = f32_down(tl - (fabs(tl) * 0x1p-50 + 0x1p-1070));
-    }
-    // the wave's row range (DPP reductions; -1 for lanes without a window)
-    const int KuW = (int)__ockl_wfred_max_u32((unsigned)(slow ? 0 : Ku + 1)) - 1;
-    const int KdW = (int)__ockl_wfred_max_u32((unsigned)(slow ? 0 : Kd + 1)) - 1;
     unsigned long long hm = 0;  // hit bits (dr + 3) * 8 + (dc + 2): one byte per row
     double d2 = INFINITY;
     // FZ (f = 0) and CBF_TILE_FUSED_FLUSH: each hit's row_g goes into its quadrant minimum as the
@@ -742,13 +724,57 @@ __global__ void __launch_bounds__(kTileT) __attribute__((amdgpu_waves_per_eu((IN
         }
         return hit ? 1u : 0u;
     };
+    auto row_bits = [&](int dr) {  // the row's three hit bits (dc = -1, 0, 1 at bits 1, 2, 3 of its byte)
+        const int b = e + dr * kTileCols;
+        const unsigned rb = (cand(b - 1) << 1) | (dr != 0 ? cand(b) << 2 : 0u) | (cand(b + 1) << 3);  // (not itself)
+        hm |= (unsigned long long)rb << ((dr + 3) * 8);
+    };
+    // CBF_TILE_EARLY_ROWS: rows -1, 0, +1 are tested before the row guard is read (so that a block
+    // of the launch's first round does this work while the first block forms the guard).  Rows the
+    // guard would have left out yield no hit: it proves their agents out of range, so hm, the
+    // quadrant minima and d2 come out the same.
+    if (CBF_TILE_EARLY_ROWS) {
+        if (fin) {
+            row_bits(-1);
+            row_bits(0);
+            row_bits(1);
+        }
+        poll_guard();
+        if (threadIdx.x < kTileGuard) {
+            L.sy[threadIdx.x] = gsy;
+            L.py[threadIdx.x] = gpy;
+        }
+        __syncthreads();
+    }
+    int Kd = -1, Ku = -1;
+    bool slow = false;
+    // column-sentinel thresholds in fp32: a sentinel x with x > thR (x < thL) proves the columns
+    // from it on out of range, since then x - r0 >= win_dn > win_d in real arithmetic and so in
+    // fp64 (rounding is monotone); thR is r0 + win_dn rounded up (fp64, then to fp32 outward) and
+    // thL likewise down.  At most one fp32 ulp looser than the fp64 test of the extents: a looser
+    // bound only widens a window.  (Non-finite or huge coordinates give +-inf: every column needed.)
+    float thR = INFINITY, thL = -INFINITY;
+    if (fin) {
+        Ku = 0;
+        Kd = 0;
+#pragma unroll
+        for (int k = 0; k < kWinPre; ++k) {
+            Ku += !(L.sy[wv + k] - E.r1 > P.win_d) ? 1 : 0;
+            Kd += !(E.r1 - L.py[wv + kWinPre - 1 - k] > P.win_d) ? 1 : 0;
+        }
+        if (Ku > kTileKS || Kd > kTileKS) slow = true;  // beyond the staged rows: the unbounded form
+        const double tr = E.r0 + P.win_dn, tl = E.r0 - P.win_dn;
+        thR = f32_up(tr + (fabs(tr) * 0x1p-50 + 0x1p-1070));
+        thL = f32_down(tl - (fabs(tl) * 0x1p-50 + 0x1p-1070));
+    }
+    // the wave's row range (DPP reductions; -1 for lanes without a window)
+    const int KuW = (int)__ockl_wfred_max_u32((unsigned)(slow ? 0 : Ku + 1)) - 1;
+    const int KdW = (int)__ockl_wfred_max_u32((unsigned)(slow ? 0 : Kd + 1)) - 1;
     unsigned pR = 0, pL = 0;  // rows (bit dr + 3) whose sentinel at c + 2 / c - 2 does not hold
     for (int dr = -KdW; dr <= KuW; ++dr) {
         if (!(fin && !slow && dr >= -Kd && dr <= Ku)) continue;
         const int b = e + dr * kTileCols;
-        // the row's three hit bits (dc = -1, 0, 1 at bits 1, 2, 3 of its byte), then one shift
-        const unsigned rb = (cand(b - 1) << 1) | (dr != 0 ? cand(b) << 2 : 0u) | (cand(b + 1) << 3);  // (not itself)
-        hm |= (unsigned long long)rb << ((dr + 3) * 8);
+        if (!CBF_TILE_EARLY_ROWS || dr < -1 || dr > 1) row_bits(dr);
         if (!(L.g[b + 2].x > thR)) pR |= 1u << (dr + 3);
         if (!(L.g[b - 2].y < thL)) pL |= 1u << (dr + 3);
     }
