@@ -733,11 +733,27 @@ __global__ void __launch_bounds__(kTileT) __attribute__((amdgpu_waves_per_eu((IN
     // of the launch's first round does this work while the first block forms the guard).  Rows the
     // guard would have left out yield no hit: it proves their agents out of range, so hm, the
     // quadrant minima and d2 come out the same.
+    // column-sentinel thresholds in fp32: a sentinel x with x > thR (x < thL) proves the columns
+    // from it on out of range, since then x - r0 >= win_dn > win_d in real arithmetic and so in
+    // fp64 (rounding is monotone); thR is r0 + win_dn rounded up (fp64, then to fp32 outward) and
+    // thL likewise down.  At most one fp32 ulp looser than the fp64 test of the extents: a looser
+    // bound only widens a window.  (Non-finite or huge coordinates give +-inf: every column needed.)
+    float thR = INFINITY, thL = -INFINITY;
+    if (fin) {
+        const double tr = E.r0 + P.win_dn, tl = E.r0 - P.win_dn;
+        thR = f32_up(tr + (fabs(tr) * 0x1p-50 + 0x1p-1070));
+        thL = f32_down(tl - (fabs(tl) * 0x1p-50 + 0x1p-1070));
+    }
+    unsigned pR0 = 0, pL0 = 0;  // rows -1..+1 whose sentinel does not hold (EARLY_ROWS: masked below)
     if (CBF_TILE_EARLY_ROWS) {
         if (fin) {
-            row_bits(-1);
-            row_bits(0);
-            row_bits(1);
+#pragma unroll
+            for (int dr = -1; dr <= 1; ++dr) {
+                row_bits(dr);
+                const int b = e + dr * kTileCols;
+                if (!(L.g[b + 2].x > thR)) pR0 |= 1u << (dr + 3);
+                if (!(L.g[b - 2].y < thL)) pL0 |= 1u << (dr + 3);
+            }
         }
         poll_guard();
         if (threadIdx.x < kTileGuard) {
@@ -748,12 +764,6 @@ __global__ void __launch_bounds__(kTileT) __attribute__((amdgpu_waves_per_eu((IN
     }
     int Kd = -1, Ku = -1;
     bool slow = false;
-    // column-sentinel thresholds in fp32: a sentinel x with x > thR (x < thL) proves the columns
-    // from it on out of range, since then x - r0 >= win_dn > win_d in real arithmetic and so in
-    // fp64 (rounding is monotone); thR is r0 + win_dn rounded up (fp64, then to fp32 outward) and
-    // thL likewise down.  At most one fp32 ulp looser than the fp64 test of the extents: a looser
-    // bound only widens a window.  (Non-finite or huge coordinates give +-inf: every column needed.)
-    float thR = INFINITY, thL = -INFINITY;
     if (fin) {
         Ku = 0;
         Kd = 0;
@@ -763,18 +773,21 @@ __global__ void __launch_bounds__(kTileT) __attribute__((amdgpu_waves_per_eu((IN
             Kd += !(E.r1 - L.py[wv + kWinPre - 1 - k] > P.win_d) ? 1 : 0;
         }
         if (Ku > kTileKS || Kd > kTileKS) slow = true;  // beyond the staged rows: the unbounded form
-        const double tr = E.r0 + P.win_dn, tl = E.r0 - P.win_dn;
-        thR = f32_up(tr + (fabs(tr) * 0x1p-50 + 0x1p-1070));
-        thL = f32_down(tl - (fabs(tl) * 0x1p-50 + 0x1p-1070));
     }
     // the wave's row range (DPP reductions; -1 for lanes without a window)
     const int KuW = (int)__ockl_wfred_max_u32((unsigned)(slow ? 0 : Ku + 1)) - 1;
     const int KdW = (int)__ockl_wfred_max_u32((unsigned)(slow ? 0 : Kd + 1)) - 1;
     unsigned pR = 0, pL = 0;  // rows (bit dr + 3) whose sentinel at c + 2 / c - 2 does not hold
+    if (CBF_TILE_EARLY_ROWS && fin && !slow) {  // the early rows' sentinels, within the row window
+        const unsigned win = ((2u << (Ku + 3)) - 1u) & ~((1u << (3 - Kd)) - 1u);  // bits -Kd .. Ku
+        pR = pR0 & win;
+        pL = pL0 & win;
+    }
     for (int dr = -KdW; dr <= KuW; ++dr) {
         if (!(fin && !slow && dr >= -Kd && dr <= Ku)) continue;
+        if (CBF_TILE_EARLY_ROWS && dr >= -1 && dr <= 1) continue;
         const int b = e + dr * kTileCols;
-        if (!CBF_TILE_EARLY_ROWS || dr < -1 || dr > 1) row_bits(dr);
+        row_bits(dr);
         if (!(L.g[b + 2].x > thR)) pR |= 1u << (dr + 3);
         if (!(L.g[b - 2].y < thL)) pL |= 1u << (dr + 3);
     }
